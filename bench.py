@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Headline benchmark: U-Net train imgs/sec at 256x256 (BASELINE.json metric, config 2/3).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched under
+torch.distributed.run, one rank per GPU. W untimed warm-up steps, then exactly K timed steps
+bracketed by barrier + device sync on both sides; the time is the MAX over ranks; rank 0 prints one
+JSON line. ``value`` is the whole-job aggregate (images/s over all ranks).
+
+The step is the full reference training step (``scripts/train_segmenter.py:156-165``): forward,
+BCEWithLogits loss, backward, Adam(lr=1e-4) -- on random-init weights of the reference
+architecture (``UNet(3, 1)``, bilinear decoder) and synthetic 256x256 RGB images / binary masks.
+
+Implementations:
+  * ``--impl native`` (default): the framework's HIP/CDNA4 kernels (NHWC bf16 implicit-GEMM convs,
+    fused BN/ReLU/pool/upsample/loss kernels, flat fused Adam), optional hipGraph capture, RCCL
+    bucketed gradient all-reduce.
+  * ``--impl eager``: the reference execution model on the same GPU (torch eager + MIOpen,
+    bf16 autocast, channels_last) -- the comparison baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# reference training throughput (bs4 256^2 fp32, measured on the sandbox CPU).
+BASELINE_TRAIN_IMGS_PER_S = 2.14
+METRIC = "U-Net train imgs/sec at 256×256 (1/2/4/8 GPU); e2e frames/sec + p50 latency"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=32, help="per-GPU batch")
+    p.add_argument("--size", type=int, default=256)
+    p.add_argument("--impl", choices=["native", "eager"], default="native")
+    p.add_argument("--decoder", choices=["bilinear", "transposed"], default="bilinear")
+    p.add_argument("--graph", type=int, default=1, help="capture the native step in a hipGraph")
+    p.add_argument("--bucket-mb", type=float, default=16.0)
+    p.add_argument("--loss", choices=["bce", "bce_dice"], default="bce")
+    p.add_argument("--serve", type=int, default=0, help="also measure e2e serving FPS / p50 latency")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if dev.type == "cuda" else "gloo"
+        dist.init_process_group(backend=backend, device_id=dev if dev.type == "cuda" else None)
+    return rank, world, dev
+
+
+def sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def barrier(world, dev):
+    if world > 1:
+        dist.barrier()
+    sync(dev)
+
+
+def make_eager_step(args, dev, world):
+    from robotic_discovery_platform_amd.models.unet_ref import UNet
+    model = UNet(3, 1, bilinear=(args.decoder == "bilinear")).to(dev).to(memory_format=torch.channels_last)
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if dev.type == "cuda" else None,
+                                                          bucket_cap_mb=args.bucket_mb)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    crit = torch.nn.BCEWithLogitsLoss()
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x = torch.rand(args.batch, 3, args.size, args.size, generator=g).to(dev).to(memory_format=torch.channels_last)
+    y = (torch.rand(args.batch, 1, args.size, args.size, generator=g) > 0.5).float().to(dev)
+    amp = dev.type == "cuda"
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
+            out = model(x)
+        loss = crit(out.float(), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    return step
+
+
+def make_native_step(args, dev, world):
+    from robotic_discovery_platform_amd.train.engine import build_bench_step
+    return build_bench_step(batch=args.batch, size=args.size, decoder=args.decoder, device=dev,
+                            world=world, graph=bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss)
+
+
+def main():
+    args = parse()
+    rank, world, dev = setup_dist(args)
+    step = make_eager_step(args, dev, world) if args.impl == "eager" else make_native_step(args, dev, world)
+    for _ in range(args.warmup):
+        step()
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier(world, dev)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if world > 1 and dev.type == "cuda" else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    imgs = args.batch * world * args.steps / dt
+    extra = {}
+    if args.serve and rank == 0:
+        from robotic_discovery_platform_amd.serve.bench_serve import measure_serving
+        extra = measure_serving(dev)
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(imgs, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(imgs / BASELINE_TRAIN_IMGS_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic (random 256x256 RGB + binary masks), random-init weights",
+            "config": {
+                "model": f"UNet(3,1) {args.decoder} decoder, 17.26M params" if args.decoder == "bilinear"
+                else "UNet(3,1) transposed decoder (fixed), 31.04M params",
+                "global_batch": args.batch * world,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "image_size": args.size,
+                "parallelism": f"dp{world}",
+                "impl": args.impl,
+                "optimizer": "Adam(lr=1e-4)",
+                "loss": args.loss,
+                "hipgraph": bool(args.graph) if args.impl == "native" else False,
+            },
+            "baseline_note": "vs_baseline = value / 2.14 img/s (BASELINE.md: reference bs4 fp32 on CPU; "
+                             "no published GPU number exists)",
+        }
+        out.update(extra)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,305 @@
+// Python bindings for the rdp HIP kernels (built in-tree as robotic_discovery_platform_amd/_C.so).
+//
+// Activations are NHWC bf16 torch tensors ([N,H,W,C], channel stride 1, possibly a channel slice
+// of a wider tensor: pixel pitch = stride(2)). Every launcher validates shapes/strides here so a
+// kernel never sees an inconsistent view; the kernels themselves use buffer descriptors sized from
+// these views (out-of-range = zero / dropped, never a fault).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
+                   long, int, int, int, float*, int, int, int, int, int, int, int, hipStream_t);
+int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
+                   float*, int, int, int, int, int, int, int, int, int, hipStream_t);
+long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
+int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
+                    float*, hipStream_t);
+int rdp_bn_eval_coef(int, const float*, const float*, const float*, const float*, float, float*, hipStream_t);
+int rdp_bn_relu_apply(const void*, int, void*, int, const float*, int, int, int, hipStream_t);
+int rdp_bn_relu_bwd_reduce(const void*, int, const void*, int, const float*, int, int, int, float*, int, hipStream_t);
+int rdp_bn_bwd_finalize(const float*, int, int, long, const float*, const float*, float*, float*, float*, hipStream_t);
+int rdp_bn_relu_bwd_apply(const void*, int, const void*, int, const float*, const float*, void*, int, int, int, int,
+                          hipStream_t);
+int rdp_maxpool2_fwd(const void*, int, void*, int, int, int, int, int, hipStream_t);
+int rdp_maxpool2_bwd(const void*, int, const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
+int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_head_partial_blocks(long);
+int rdp_head_fwd(const void*, int, const float*, const float*, const float*, float*, float*, float*, float*, int, float,
+                 float, hipStream_t);
+int rdp_head_bwd(const void*, int, const float*, const float*, const float*, const float*, void*, int, float*, float*,
+                 float*, int, float, float, float, hipStream_t);
+int rdp_head_mask(const void*, int, const float*, const float*, float, void*, int, hipStream_t);
+int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, int*,
+             hipStream_t);
+int rdp_cast_bf16(const float*, void*, long, hipStream_t);
+int rdp_wprep(const float*, void*, const void*, int, hipStream_t);
+int rdp_wseg_size();
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+struct Act {
+  void* ptr = nullptr;
+  int N = 0, H = 0, W = 0, C = 0, pitch = 0;
+  long bytes = 0;
+};
+
+Act act(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, ": must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, ": must be bf16");
+  TORCH_CHECK(t.dim() == 4, name, ": must be NHWC 4-D");
+  Act a;
+  a.N = t.size(0); a.H = t.size(1); a.W = t.size(2); a.C = t.size(3);
+  TORCH_CHECK(t.stride(3) == 1, name, ": channel stride must be 1");
+  a.pitch = t.stride(2);
+  TORCH_CHECK(a.pitch >= a.C, name, ": pixel pitch < C");
+  TORCH_CHECK(t.stride(1) == (long)a.W * a.pitch && t.stride(0) == (long)a.H * a.W * a.pitch, name,
+              ": pixels must be densely packed (only channel slicing allowed)");
+  TORCH_CHECK(a.pitch % 8 == 0 && ((uintptr_t)t.data_ptr() % 16) == 0, name, ": pitch/base must be 16-B aligned");
+  a.ptr = t.data_ptr();
+  a.bytes = ((long)a.N * a.H * a.W - 1) * a.pitch * 2 + (long)a.C * 2;
+  return a;
+}
+
+void check_f32(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), name,
+              ": must be a contiguous fp32 GPU tensor");
+}
+
+int conv_stats_rows(long M, int Cout, int bm_pref) {
+  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return (M + 127) / 128;
+  return (M + 255) / 256;
+}
+
+// y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)
+int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, int taps, int packed,
+             torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref) {
+  Act a1 = act(x1, "x1"), a2;
+  if (x2) {
+    a2 = act(*x2, "x2");
+    TORCH_CHECK(a2.N == a1.N && a2.H == a1.H && a2.W == a1.W, "x2 spatial mismatch");
+  }
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
+  Act o1 = act(y1, "y1"), o2;
+  int Cout = o1.C;
+  if (y2) { o2 = act(*y2, "y2"); Cout += o2.C; }
+  TORCH_CHECK(o1.N == a1.N && o1.H == a1.H && o1.W == a1.W, "y spatial mismatch");
+  TORCH_CHECK(w.size(0) == Cout, "w rows != Cout");
+  float* sp = nullptr;
+  if (stats) {
+    check_f32(*stats, "stats");
+    const long M = (long)a1.N * a1.H * a1.W;
+    const long rows = conv_stats_rows(M, Cout, bm_pref);
+    TORCH_CHECK(stats->numel() >= rows * 2 * Cout, "stats slab too small");
+    sp = stats->data_ptr<float>();
+  }
+  const int r = rdp_conv_igemm(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
+                               a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1), o1.ptr,
+                               y2 ? o2.ptr : nullptr, o1.bytes, y2 ? o2.bytes : 0, o1.C, o1.pitch, y2 ? o2.pitch : 0,
+                               sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, cur_stream());
+  TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
+  return r;
+}
+
+
+int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor dy, int taps, int packed, int cin_real,
+               torch::Tensor slab, torch::Tensor out, int accumulate, int splits) {
+  Act a1 = act(x1, "x1"), a2;
+  if (x2) a2 = act(*x2, "x2");
+  Act d = act(dy, "dy");
+  TORCH_CHECK(d.N == a1.N && d.H == a1.H && d.W == a1.W, "dy spatial mismatch");
+  check_f32(slab, "slab");
+  check_f32(out, "out");
+  const int Cin = packed ? cin_real : a1.C + (x2 ? a2.C : 0);
+  TORCH_CHECK(out.numel() == (long)d.C * taps * Cin, "wgrad out numel mismatch");
+  const int r = rdp_conv_wgrad(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
+                               a1.pitch, x2 ? a2.pitch : 0, d.ptr, d.bytes, d.pitch, slab.data_ptr<float>(),
+                               slab.numel(), out.data_ptr<float>(), accumulate, a1.N, a1.H, a1.W, d.C, taps, packed,
+                               cin_real, splits, cur_stream());
+  TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
+  return r;
+}
+
+long wgrad_slab_elems(int N, int H, int W, int Cin, int Cout, int taps, int packed, int splits) {
+  return rdp_conv_wgrad_slab_elems(N, H, W, Cin, Cout, taps, packed, splits);
+}
+
+void bn_finalize(torch::Tensor stats, int T, long count, torch::Tensor gamma, torch::Tensor beta,
+                 c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
+                 c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor coef) {
+  const int C = gamma.numel();
+  check_f32(stats, "stats"); check_f32(gamma, "gamma"); check_f32(beta, "beta"); check_f32(coef, "coef");
+  TORCH_CHECK(stats.numel() >= (long)T * 2 * C && coef.numel() >= 4 * C, "bn_finalize sizes");
+  float* rm = nullptr; float* rv = nullptr; long long* nb = nullptr;
+  if (rmean) { check_f32(*rmean, "rmean"); rm = rmean->data_ptr<float>(); }
+  if (rvar) { check_f32(*rvar, "rvar"); rv = rvar->data_ptr<float>(); }
+  if (nbt) { TORCH_CHECK(nbt->scalar_type() == torch::kInt64 && nbt->is_cuda(), "nbt int64"); nb = (long long*)nbt->data_ptr(); }
+  rdp_bn_finalize(stats.data_ptr<float>(), T, C, count, gamma.data_ptr<float>(), beta.data_ptr<float>(), rm, rv, nb,
+                  (float)momentum, (float)eps, coef.data_ptr<float>(), cur_stream());
+}
+
+void bn_eval_coef(torch::Tensor gamma, torch::Tensor beta, torch::Tensor rmean, torch::Tensor rvar, double eps,
+                  torch::Tensor coef) {
+  const int C = gamma.numel();
+  check_f32(coef, "coef");
+  rdp_bn_eval_coef(C, gamma.data_ptr<float>(), beta.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                   (float)eps, coef.data_ptr<float>(), cur_stream());
+}
+
+void bn_relu_apply(torch::Tensor y, torch::Tensor out, torch::Tensor coef, int relu) {
+  Act a = act(y, "y"), o = act(out, "out");
+  TORCH_CHECK(a.N == o.N && a.H == o.H && a.W == o.W && a.C == o.C, "bn_relu_apply shape");
+  TORCH_CHECK(coef.numel() >= 4 * a.C, "coef");
+  TORCH_CHECK(rdp_bn_relu_apply(a.ptr, a.pitch, o.ptr, o.pitch, coef.data_ptr<float>(), a.N * a.H * a.W, a.C, relu,
+                                cur_stream()) == 0, "bn_relu_apply");
+}
+
+int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, int relu, torch::Tensor partial) {
+  Act d = act(da, "da"), a = act(y, "y");
+  TORCH_CHECK(d.N == a.N && d.H == a.H && d.W == a.W && d.C == a.C, "bn bwd shape");
+  check_f32(partial, "partial");
+  const int maxb = partial.numel() / (2 * a.C);
+  const int T = rdp_bn_relu_bwd_reduce(d.ptr, d.pitch, a.ptr, a.pitch, coef.data_ptr<float>(), a.N * a.H * a.W, a.C,
+                                       relu, partial.data_ptr<float>(), maxb, cur_stream());
+  TORCH_CHECK(T > 0, "bn_relu_bwd_reduce");
+  return T;
+}
+
+void bn_bwd_finalize(torch::Tensor partial, int T, long count, torch::Tensor gamma, torch::Tensor coef,
+                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor coef2) {
+  const int C = gamma.numel();
+  rdp_bn_bwd_finalize(partial.data_ptr<float>(), T, C, count, gamma.data_ptr<float>(), coef.data_ptr<float>(),
+                      dgamma ? dgamma->data_ptr<float>() : nullptr, dbeta ? dbeta->data_ptr<float>() : nullptr,
+                      coef2.data_ptr<float>(), cur_stream());
+}
+
+void bn_relu_bwd_apply(torch::Tensor da, torch::Tensor y, torch::Tensor coef, torch::Tensor coef2, torch::Tensor dy,
+                       int relu) {
+  Act d = act(da, "da"), a = act(y, "y"), o = act(dy, "dy");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && o.C == a.C, "bn bwd apply shape");
+  TORCH_CHECK(rdp_bn_relu_bwd_apply(d.ptr, d.pitch, a.ptr, a.pitch, coef.data_ptr<float>(), coef2.data_ptr<float>(),
+                                    o.ptr, o.pitch, a.N * a.H * a.W, a.C, relu, cur_stream()) == 0, "bn bwd apply");
+}
+
+void maxpool2_fwd(torch::Tensor x, torch::Tensor out) {
+  Act a = act(x, "x"), o = act(out, "out");
+  TORCH_CHECK(o.N == a.N && o.H == a.H / 2 && o.W == a.W / 2 && o.C == a.C, "maxpool shape");
+  TORCH_CHECK(rdp_maxpool2_fwd(a.ptr, a.pitch, o.ptr, o.pitch, a.N, a.H, a.W, a.C, cur_stream()) == 0, "maxpool");
+}
+
+void maxpool2_bwd(torch::Tensor dp, torch::Tensor x, c10::optional<torch::Tensor> dskip, torch::Tensor dx) {
+  Act p = act(dp, "dp"), a = act(x, "x"), o = act(dx, "dx"), s;
+  if (dskip) { s = act(*dskip, "dskip"); TORCH_CHECK(s.N == a.N && s.H == a.H && s.W == a.W && s.C == a.C, "dskip shape"); }
+  TORCH_CHECK(p.N == a.N && p.H == a.H / 2 && p.W == a.W / 2 && p.C == a.C, "maxpool bwd shape");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && o.C == a.C, "maxpool bwd dx shape");
+  TORCH_CHECK(rdp_maxpool2_bwd(p.ptr, p.pitch, a.ptr, a.pitch, dskip ? s.ptr : nullptr, dskip ? s.pitch : 0, o.ptr,
+                               o.pitch, a.N, a.H, a.W, a.C, cur_stream()) == 0, "maxpool bwd");
+}
+
+void upsample2_fwd(torch::Tensor x, torch::Tensor out, int oy, int ox) {
+  Act a = act(x, "x"), o = act(out, "out");
+  TORCH_CHECK(o.N == a.N && o.C == a.C, "upsample shape");
+  TORCH_CHECK(rdp_upsample2_fwd(a.ptr, a.pitch, o.ptr, o.pitch, a.N, a.H, a.W, o.H, o.W, oy, ox, a.C, cur_stream()) == 0,
+              "upsample fwd");
+}
+
+void upsample2_bwd(torch::Tensor dout, torch::Tensor dx, int oy, int ox) {
+  Act d = act(dout, "dout"), o = act(dx, "dx");
+  TORCH_CHECK(o.N == d.N && o.C == d.C, "upsample bwd shape");
+  TORCH_CHECK(rdp_upsample2_bwd(d.ptr, d.pitch, o.ptr, o.pitch, o.N, o.H, o.W, d.H, d.W, oy, ox, o.C, cur_stream()) == 0,
+              "upsample bwd");
+}
+
+int head_partial_blocks(long M) { return rdp_head_partial_blocks(M); }
+
+void head_fwd(torch::Tensor a, torch::Tensor w, torch::Tensor b, torch::Tensor target, torch::Tensor logits,
+              torch::Tensor partial, torch::Tensor sums, torch::Tensor loss, double dice_w, double dice_eps) {
+  Act x = act(a, "a");
+  TORCH_CHECK(x.C == 64, "head expects 64 channels");
+  const long M = (long)x.N * x.H * x.W;
+  TORCH_CHECK(target.numel() == M && logits.numel() == M, "head target/logits numel");
+  TORCH_CHECK(partial.numel() >= (long)rdp_head_partial_blocks(M) * 65, "head partial too small");
+  rdp_head_fwd(x.ptr, x.pitch, w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<float>(),
+               logits.data_ptr<float>(), partial.data_ptr<float>(), sums.data_ptr<float>(), loss.data_ptr<float>(), M,
+               (float)dice_w, (float)dice_eps, cur_stream());
+}
+
+void head_bwd(torch::Tensor a, torch::Tensor w, torch::Tensor logits, torch::Tensor target, torch::Tensor sums,
+              torch::Tensor da, torch::Tensor partial, torch::Tensor gw, torch::Tensor gb, double dice_w,
+              double dice_eps, double gscale) {
+  Act x = act(a, "a"), d = act(da, "da");
+  const long M = (long)x.N * x.H * x.W;
+  TORCH_CHECK(d.C == 64 && x.C == 64, "head bwd channels");
+  TORCH_CHECK(partial.numel() >= (long)rdp_head_partial_blocks(M) * 65, "head partial too small");
+  rdp_head_bwd(x.ptr, x.pitch, w.data_ptr<float>(), logits.data_ptr<float>(), target.data_ptr<float>(),
+               sums.data_ptr<float>(), d.ptr, d.pitch, partial.data_ptr<float>(), gw.data_ptr<float>(),
+               gb.data_ptr<float>(), M, (float)dice_w, (float)dice_eps, (float)gscale, cur_stream());
+}
+
+void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_thr, torch::Tensor mask) {
+  Act x = act(a, "a");
+  TORCH_CHECK(mask.scalar_type() == torch::kUInt8 && mask.numel() == (long)x.N * x.H * x.W, "mask u8 numel");
+  rdp_head_mask(x.ptr, x.pitch, w.data_ptr<float>(), b.data_ptr<float>(), (float)logit_thr, mask.data_ptr(),
+                x.N * x.H * x.W, cur_stream());
+}
+
+void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+          double lr, double b1, double b2, double eps, double wd, double gscale, torch::Tensor step) {
+  check_f32(p, "p"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam numel");
+  TORCH_CHECK(step.scalar_type() == torch::kInt32 && step.is_cuda(), "step int32");
+  void* sh = nullptr;
+  if (shadow) {
+    TORCH_CHECK(shadow->scalar_type() == torch::kBFloat16 && shadow->numel() == p.numel(), "shadow");
+    sh = shadow->data_ptr();
+  }
+  TORCH_CHECK(rdp_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sh, p.numel(),
+                       (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale,
+                       (int*)step.data_ptr(), cur_stream()) == 0, "adam: numel must be a multiple of 4");
+}
+
+void cast_bf16(torch::Tensor p, torch::Tensor out) {
+  check_f32(p, "p");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.numel() == p.numel(), "cast out");
+  rdp_cast_bf16(p.data_ptr<float>(), out.data_ptr(), p.numel(), cur_stream());
+}
+
+void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg) {
+  check_f32(master, "master");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16, "wprep out bf16");
+  TORCH_CHECK(segs.is_cuda() && segs.numel() * segs.element_size() >= (long)nseg * rdp_wseg_size(), "segs");
+  rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "rdp MI355X (gfx950) HIP kernels";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_stats_rows", &conv_stats_rows);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("wgrad_slab_elems", &wgrad_slab_elems);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_eval_coef", &bn_eval_coef);
+  m.def("bn_relu_apply", &bn_relu_apply);
+  m.def("bn_relu_bwd_reduce", &bn_relu_bwd_reduce);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_relu_bwd_apply", &bn_relu_bwd_apply);
+  m.def("maxpool2_fwd", &maxpool2_fwd);
+  m.def("maxpool2_bwd", &maxpool2_bwd);
+  m.def("upsample2_fwd", &upsample2_fwd);
+  m.def("upsample2_bwd", &upsample2_bwd);
+  m.def("head_partial_blocks", &head_partial_blocks);
+  m.def("head_fwd", &head_fwd);
+  m.def("head_bwd", &head_bwd);
+  m.def("head_mask", &head_mask);
+  m.def("adam", &adam);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("wprep", &wprep);
+  m.def("wseg_size", &rdp_wseg_size);
+}

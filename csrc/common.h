@@ -1,0 +1,103 @@
+// Common CDNA4 (gfx950) helpers for the rdp kernels.
+//
+// Every global access in the hot kernels goes through a buffer resource (SRD): reads outside
+// `num_records` return 0 and writes outside it are dropped, so a wrong index can corrupt an
+// output but never fault the GPU (and zero-padding of convolution halos is free: an out-of-range
+// voffset reads zeros, also for the LDS-DMA form `buffer_load ... lds`).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RDP_DEV __device__ __forceinline__
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// Offset used for "this lane reads zeros": >= num_records of every descriptor we build (<2 GiB).
+#define RDP_OOB 0x80000000u
+
+RDP_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  // wave-uniform by construction: only kernel arguments feed it (cdna_hip_programming.md T8/T20)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// ---- bf16 <-> f32 (round-to-nearest-even; NaN-preserving via the compiler's cvt) ----
+RDP_DEV float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
+RDP_DEV u16 f2bf(float f) {
+  __bf16 b = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 at -O3 (keeps NaN a NaN)
+  return __builtin_bit_cast(u16, b);
+}
+RDP_DEV uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// ---- 16/8-byte buffer loads/stores ----
+RDP_DEV uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return *reinterpret_cast<uint4*>(&v);
+}
+RDP_DEV uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+  return *reinterpret_cast<uint2*>(&v);
+}
+RDP_DEV uint32_t bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0);
+}
+RDP_DEV void bstore16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(&v), r, voff, 0, 0);
+}
+RDP_DEV void bstore8(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<__attribute__((ext_vector_type(2))) uint32_t*>(&v), r, voff, 0, 0);
+}
+RDP_DEV void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+}
+
+// LDS-DMA: 16 bytes per lane, LDS destination = wave-uniform base + lane*16.
+RDP_DEV void dma16(__amdgpu_buffer_rsrc_t r, lds_void* lds_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_base, 16, voff, 0, 0, 0);
+}
+
+RDP_DEV void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+RDP_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+RDP_DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); }
+
+// ---- XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective") ----
+// Blocks are dealt round-robin over 8 XCDs; remap so each XCD gets a contiguous range of logical ids.
+RDP_DEV uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
+  const uint32_t q = nwg >> 3, r = nwg & 7, xcd = orig & 7, idx = orig >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// ---- fast unsigned division by a runtime-invariant divisor (magic multiply) ----
+struct FastDiv {
+  uint32_t d, m, s;  // n / d = (umulhi(n, m) + n) >> s   for n < 2^31
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << s) - d)) / d + 1);
+  return f;
+}
+RDP_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+RDP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+RDP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}

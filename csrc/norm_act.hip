@@ -1,0 +1,272 @@
+// Training/eval BatchNorm2d + ReLU kernels on NHWC bf16 activations.
+//
+// Reference semantics: nn.BatchNorm2d + nn.ReLU(inplace=True) inside DoubleConv
+// (/root/reference/pkg/segmentation_model.py:32-36): batch statistics over N*H*W (biased variance
+// for normalisation, unbiased for running_var), momentum 0.1, eps 1e-5; eval uses running stats.
+//
+// Forward statistics arrive as per-M-tile (sum, sumsq) slabs from the conv epilogue
+// (conv_igemm.hip); bn_finalize reduces them in fp64, updates running stats and emits the
+// per-channel affine (scale, shift) applied by bn_relu_apply. Backward is a two-pass
+// reduce (sum g, sum g*xhat) -> finalize (dgamma, dbeta, 3 apply coefficients) -> apply.
+#include "common.h"
+#include <algorithm>
+
+// coef layout: [0:C) mean, [C:2C) invstd, [2C:3C) scale = gamma*invstd, [3C:4C) shift = beta - mean*scale
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int T, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, long long* nbt,
+                                   float momentum, float eps, float* __restrict__ coef) {
+  __shared__ double red[2][4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int t = ty; t < T; t += 4) {
+      s += (double)stats[(size_t)t * 2 * C + c];
+      q += (double)stats[(size_t)t * 2 * C + C + c];
+    }
+  }
+  red[0][ty][tx] = s;
+  red[1][ty][tx] = q;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    s = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
+    q = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    const double mean = s / count;
+    double var = q / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * invstd;
+    coef[c] = (float)mean;
+    coef[C + c] = invstd;
+    coef[2 * C + c] = sc;
+    coef[3 * C + c] = beta[c] - (float)mean * sc;
+    if (rmean) {
+      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+}
+
+// eval-mode coefficients from running stats
+__global__ void bn_eval_coef_kernel(int C, const float* gamma, const float* beta, const float* rmean,
+                                    const float* rvar, float eps, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.0f / sqrtf(rvar[c] + eps);
+  const float sc = gamma[c] * invstd;
+  coef[c] = rmean[c];
+  coef[C + c] = invstd;
+  coef[2 * C + c] = sc;
+  coef[3 * C + c] = beta[c] - rmean[c] * sc;
+}
+
+RDP_DEV void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(w[k] << 16);
+    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+RDP_DEV uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]);
+  v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+// a = relu(y*scale + shift), 8 channels per thread
+__global__ void bn_relu_apply_kernel(const u16* __restrict__ y, int ypitch, u16* __restrict__ out, int opitch,
+                                     const float* __restrict__ coef, int M, int C, int relu) {
+  const int CG = C >> 3;
+  const long total = (long)M * CG;
+  const float* sc = coef + 2 * C;
+  const float* sh = coef + 3 * C;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int p = it / CG, g = it - (long)p * CG;
+    const int c = g * 8;
+    float f[8];
+    unpack8(*(const uint4*)(y + (size_t)p * ypitch + c), f);
+    const float4 s0 = *(const float4*)(sc + c), s1 = *(const float4*)(sc + c + 4);
+    const float4 h0 = *(const float4*)(sh + c), h1 = *(const float4*)(sh + c + 4);
+    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float z = fmaf(f[k], ss[k], hh[k]);
+      f[k] = relu ? fmaxf(z, 0.f) : z;
+    }
+    *(uint4*)(out + (size_t)p * opitch + c) = pack8(f);
+  }
+}
+
+// Backward reduce: partial[blk][0][c] = sum g, partial[blk][1][c] = sum g*xhat,
+// g = da * (y*scale+shift > 0), xhat = (y-mean)*invstd.
+__global__ __launch_bounds__(256) void bn_relu_bwd_reduce_kernel(const u16* __restrict__ da, int dapitch,
+                                                                 const u16* __restrict__ y, int ypitch,
+                                                                 const float* __restrict__ coef, int M, int C,
+                                                                 int relu, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [rows][C][2]
+  const int CG = C >> 3;
+  const int rows = 256 / CG;  // pixel rows processed in parallel by the block
+  const int g = threadIdx.x % CG, r = threadIdx.x / CG;
+  const int c = g * 8;
+  float mean[8], inv[8], ss[8], hh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = coef[c + k];
+    inv[k] = coef[C + c + k];
+    ss[k] = coef[2 * C + c + k];
+    hh[k] = coef[3 * C + c + k];
+  }
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sg[k] = 0.f; sgx[k] = 0.f; }
+  if (r < rows) {
+    for (long p = blockIdx.x * (long)rows + r; p < M; p += (long)gridDim.x * rows) {
+      float fd[8], fy[8];
+      unpack8(*(const uint4*)(da + (size_t)p * dapitch + c), fd);
+      unpack8(*(const uint4*)(y + (size_t)p * ypitch + c), fy);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = (!relu || fmaf(fy[k], ss[k], hh[k]) > 0.f) ? fd[k] : 0.f;
+        sg[k] += gg;
+        sgx[k] += gg * (fy[k] - mean[k]) * inv[k];
+      }
+    }
+  }
+  const int R = rows;
+  if (r < R) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sred[(r * C + c + k) * 2] = sg[k];
+      sred[(r * C + c + k) * 2 + 1] = sgx[k];
+    }
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int q = 0; q < R; ++q) { a0 += sred[(q * C + cc) * 2]; a1 += sred[(q * C + cc) * 2 + 1]; }
+    partial[(size_t)blockIdx.x * 2 * C + cc] = a0;
+    partial[(size_t)blockIdx.x * 2 * C + C + cc] = a1;
+  }
+}
+
+// Backward finalize: dgamma, dbeta (written or accumulated into fp32 grads) and the apply
+// coefficients coef2 = [A | B | Cc]: dy = A*g + B*y + Cc.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int T, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ coef,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coef2) {
+  __shared__ double red[2][4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int t = ty; t < T; t += 4) {
+      s += (double)partial[(size_t)t * 2 * C + c];
+      q += (double)partial[(size_t)t * 2 * C + C + c];
+    }
+  }
+  red[0][ty][tx] = s;
+  red[1][ty][tx] = q;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    s = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
+    q = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    if (dbeta) dbeta[c] = (float)s;
+    if (dgamma) dgamma[c] = (float)q;
+    const double mean = coef[c], inv = coef[C + c], gm = gamma[c];
+    const double A = gm * inv;
+    const double mg = s / count, mgx = q / count;
+    coef2[c] = (float)A;
+    coef2[C + c] = (float)(-A * inv * mgx);
+    coef2[2 * C + c] = (float)(-A * mg + A * inv * mgx * mean);
+  }
+}
+
+__global__ void bn_relu_bwd_apply_kernel(const u16* __restrict__ da, int dapitch, const u16* __restrict__ y,
+                                         int ypitch, const float* __restrict__ coef,
+                                         const float* __restrict__ coef2, u16* __restrict__ dy, int dypitch,
+                                         int M, int C, int relu) {
+  const int CG = C >> 3;
+  const long total = (long)M * CG;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int p = it / CG, g = it - (long)p * CG;
+    const int c = g * 8;
+    float fd[8], fy[8], o[8];
+    unpack8(*(const uint4*)(da + (size_t)p * dapitch + c), fd);
+    unpack8(*(const uint4*)(y + (size_t)p * ypitch + c), fy);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float ss = coef[2 * C + c + k], hh = coef[3 * C + c + k];
+      const float gg = (!relu || fmaf(fy[k], ss, hh) > 0.f) ? fd[k] : 0.f;
+      o[k] = fmaf(coef2[c + k], gg, fmaf(coef2[C + c + k], fy[k], coef2[2 * C + c + k]));
+    }
+    *(uint4*)(dy + (size_t)p * dypitch + c) = pack8(o);
+  }
+}
+
+static int grid_for(long items, int block = 256, int cap = 2048) {
+  long g = (items + block - 1) / block;
+  return (int)std::max<long>(1, std::min<long>(g, cap));
+}
+
+extern "C" {
+
+int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* gamma, const float* beta,
+                    float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, stats, T, C, (double)count, gamma,
+                     beta, rmean, rvar, nbt, momentum, eps, coef);
+  return 0;
+}
+
+int rdp_bn_eval_coef(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                     float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 63) / 64), dim3(64), 0, s, C, gamma, beta, rmean, rvar, eps, coef);
+  return 0;
+}
+
+int rdp_bn_relu_apply(const void* y, int ypitch, void* out, int opitch, const float* coef, int M, int C, int relu,
+                      hipStream_t s) {
+  if (C % 8 || ypitch % 8 || opitch % 8) return -1;
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 0, s, (const u16*)y, ypitch,
+                     (u16*)out, opitch, coef, M, C, relu);
+  return 0;
+}
+
+// returns the number of partial rows written (T for bn_bwd_finalize)
+int rdp_bn_relu_bwd_reduce(const void* da, int dapitch, const void* y, int ypitch, const float* coef, int M, int C,
+                           int relu, float* partial, int max_blocks, hipStream_t s) {
+  if (C % 8 || C > 2048) return -1;
+  const int rows = 256 / (C / 8);
+  int blocks = (int)std::min<long>(max_blocks, ((long)M + rows * 8 - 1) / (rows * 8));
+  if (blocks < 1) blocks = 1;
+  const size_t lds = (size_t)rows * C * 2 * sizeof(float);
+  hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel, dim3(blocks), dim3(256), lds, s, (const u16*)da, dapitch,
+                     (const u16*)y, ypitch, coef, M, C, relu, partial);
+  return blocks;
+}
+
+int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const float* gamma, const float* coef,
+                        float* dgamma, float* dbeta, float* coef2, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, partial, T, C, (double)count, gamma,
+                     coef, dgamma, dbeta, coef2);
+  return 0;
+}
+
+int rdp_bn_relu_bwd_apply(const void* da, int dapitch, const void* y, int ypitch, const float* coef,
+                          const float* coef2, void* dy, int dypitch, int M, int C, int relu, hipStream_t s) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 0, s, (const u16*)da,
+                     dapitch, (const u16*)y, ypitch, coef, coef2, (u16*)dy, dypitch, M, C, relu);
+  return 0;
+}
+
+}  // extern "C"

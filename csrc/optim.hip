@@ -1,0 +1,109 @@
+// Fused Adam over ONE flat fp32 master buffer + bf16 weight shadows for the conv kernels.
+//
+// Reference: torch.optim.Adam(model.parameters(), lr=1e-4) (/root/reference/scripts/train_segmenter.py:144,163),
+// default betas (0.9, 0.999), eps 1e-8, no weight decay, bias correction. Math mirrors torch's:
+//   m = lerp(m, g, 1-b1); v = b2*v + (1-b2)*g*g;
+//   p -= (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+// The step counter lives on the device (hipGraph-replayable); `gscale` folds the 1/world DDP
+// average into the update. Each updated value is also written as bf16 into the flat shadow
+// (identity layout = the forward conv weights, OHWI).
+// wprep builds the derived bf16 layouts from the fp32 masters in one launch (segment table):
+//   kind 0: dgrad weights  Wt[cin][8-tap][cout] = W[cout][tap][cin]   (flip + transpose)
+//   kind 1: packed first layer  Wp[cout][16][8] (taps 0..8, channels 0..cin-1, zeros elsewhere)
+#include "common.h"
+#include <algorithm>
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, u16* __restrict__ shadow, long n, float lr, float b1, float b2,
+                            float eps, float wd, float gscale, const int* __restrict__ step) {
+  const int t = step[0] + 1;
+  const float bc1 = 1.f - (float)pow((double)b1, (double)t);
+  const float bc2 = 1.f - (float)pow((double)b2, (double)t);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const long n4 = n >> 2;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pp = ((float4*)p)[i], gg = ((const float4*)g)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = ga[k] * gscale;
+      if (wd != 0.f) gk = fmaf(wd, pa[k], gk);
+      ma[k] = ma[k] + (1.f - b1) * (gk - ma[k]);
+      va[k] = va[k] * b2 + (1.f - b2) * gk * gk;
+      const float den = sqrtf(va[k]) / bc2s + eps;
+      pa[k] = pa[k] - step_size * ma[k] / den;
+    }
+    ((float4*)p)[i] = pp;
+    ((float4*)m)[i] = mm;
+    ((float4*)v)[i] = vv;
+    if (shadow) {
+      uint2 o;
+      o.x = pack2bf(pp.x, pp.y);
+      o.y = pack2bf(pp.z, pp.w);
+      ((uint2*)shadow)[i] = o;
+    }
+  }
+}
+
+__global__ void step_inc_kernel(int* step) { step[0] += 1; }
+
+__global__ void cast_bf16_kernel(const float* __restrict__ p, u16* __restrict__ out, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) out[i] = f2bf(p[i]);
+}
+
+struct WSeg {
+  long src;  // element offset in the fp32 master
+  long dst;  // element offset in the bf16 derived buffer
+  int kind, cout, cin, taps;
+};
+
+__global__ void wprep_kernel(const float* __restrict__ master, u16* __restrict__ out, const WSeg* __restrict__ segs) {
+  const WSeg sg = segs[blockIdx.y];
+  if (sg.kind == 0) {
+    const long n = (long)sg.cout * sg.taps * sg.cin;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+      // destination-major so the bf16 writes are coalesced: i -> (ci, tp, co)
+      const int co = i % sg.cout;
+      const long r = i / sg.cout;
+      const int tp = r % sg.taps, ci = r / sg.taps;
+      const int tap = sg.taps - 1 - tp;
+      out[sg.dst + i] = f2bf(master[sg.src + ((long)co * sg.taps + tap) * sg.cin + ci]);
+    }
+  } else {
+    const long n = (long)sg.cout * 128;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+      const int c = i % 8, tap = (i / 8) % 16, co = i / 128;
+      float val = 0.f;
+      if (tap < sg.taps && c < sg.cin) val = master[sg.src + ((long)co * sg.taps + tap) * sg.cin + c];
+      out[sg.dst + i] = f2bf(val);
+    }
+  }
+}
+
+extern "C" {
+int rdp_adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2,
+             float eps, float wd, float gscale, int* step, hipStream_t s) {
+  if (n % 4) return -1;
+  const long n4 = n / 4;
+  const int grid = (int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 8192));
+  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, s, p, g, m, v, (u16*)shadow, n, lr, b1, b2, eps, wd, gscale,
+                     step);
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  return 0;
+}
+
+int rdp_cast_bf16(const float* p, void* out, long n, hipStream_t s) {
+  const int grid = (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid), dim3(256), 0, s, p, (u16*)out, n);
+  return 0;
+}
+
+// segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps} (32 bytes each)
+int rdp_wprep(const float* master, void* out, const void* segs, int nseg, hipStream_t s) {
+  if (nseg <= 0) return 0;
+  hipLaunchKernelGGL(wprep_kernel, dim3(64, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs);
+  return 0;
+}
+int rdp_wseg_size() { return (int)sizeof(WSeg); }
+}

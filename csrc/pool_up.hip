@@ -1,0 +1,247 @@
+// MaxPool2d(2) and bilinear x2 upsampling (align_corners=True) with zero-pad placement, NHWC bf16.
+//
+// Reference ops: nn.MaxPool2d(2) in Down (/root/reference/pkg/segmentation_model.py:47) and
+// nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True) + F.pad in Up.forward (:61,68-74).
+// Semantics preserved:
+//   * maxpool: floor mode; backward routes the gradient to the FIRST maximum of each 2x2 window in
+//     row-major order (NaN wins), as torch does; the skip-connection gradient is added in the same
+//     pass (d a = pool_bwd(d p) + d skip), so the encoder activation's gradient is written once.
+//   * upsample: src = dst * (in-1)/(out-1) in fp32 (torch area_pixel_compute_source_index),
+//     i1 = i0 + (i0 < in-1); the x2 output is placed at offset (oy, ox) inside the skip's H2 x W2
+//     (F.pad with [dx//2, dx-dx//2, dy//2, dy-dy//2]); the rest is zero. Backward is a
+//     deterministic gather (no atomics) that re-derives the forward's exact index/weight arithmetic.
+#include "common.h"
+#include <algorithm>
+
+RDP_DEV void unpack8f(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(w[k] << 16);
+    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+RDP_DEV uint4 pack8f(const float* f) {
+  uint4 v;
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]);
+  v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+__global__ void maxpool2_fwd_kernel(const u16* __restrict__ x, int xpitch, u16* __restrict__ out, int opitch, int N,
+                                    int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, CG = C >> 3;
+  const long total = (long)N * Ho * Wo * CG;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int g = it % CG;
+    const long po = it / CG;
+    const int wo = po % Wo;
+    const long t = po / Wo;
+    const int ho = t % Ho, n = t / Ho;
+    const long p00 = ((long)n * H + 2 * ho) * W + 2 * wo;
+    const int c = g * 8;
+    float v[4][8];
+    unpack8f(*(const uint4*)(x + p00 * xpitch + c), v[0]);
+    unpack8f(*(const uint4*)(x + (p00 + 1) * xpitch + c), v[1]);
+    unpack8f(*(const uint4*)(x + (p00 + W) * xpitch + c), v[2]);
+    unpack8f(*(const uint4*)(x + (p00 + W + 1) * xpitch + c), v[3]);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float m = v[0][k];
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (v[q][k] > m || isnan(v[q][k])) m = v[q][k];
+      o[k] = m;
+    }
+    *(uint4*)(out + po * opitch + c) = pack8f(o);
+  }
+}
+
+// dx[2x2 window] = (argmax ? dp : 0) + dskip ; pixels outside every window get dskip only.
+__global__ void maxpool2_bwd_kernel(const u16* __restrict__ dp, int dppitch, const u16* __restrict__ x, int xpitch,
+                                    const u16* __restrict__ dskip, int dspitch, u16* __restrict__ dx, int dxpitch,
+                                    int N, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, CG = C >> 3;
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;  // windows covering every pixel
+  const long total = (long)N * Hc * Wc * CG;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int g = it % CG;
+    const long pw = it / CG;
+    const int wc = pw % Wc;
+    const long t = pw / Wc;
+    const int hc = t % Hc, n = t / Hc;
+    const int c = g * 8;
+    const bool pooled = hc < Ho && wc < Wo;
+    float v[4][8], d[8], o[4][8];
+    int idx[8];
+    if (pooled) {
+      const long p00 = ((long)n * H + 2 * hc) * W + 2 * wc;
+      unpack8f(*(const uint4*)(x + p00 * xpitch + c), v[0]);
+      unpack8f(*(const uint4*)(x + (p00 + 1) * xpitch + c), v[1]);
+      unpack8f(*(const uint4*)(x + (p00 + W) * xpitch + c), v[2]);
+      unpack8f(*(const uint4*)(x + (p00 + W + 1) * xpitch + c), v[3]);
+      const long po = ((long)n * Ho + hc) * Wo + wc;
+      unpack8f(*(const uint4*)(dp + po * dppitch + c), d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float m = v[0][k];
+        int id = 0;
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (v[q][k] > m || isnan(v[q][k])) { m = v[q][k]; id = q; }
+        idx[k] = id;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int hh = 2 * hc + (q >> 1), ww = 2 * wc + (q & 1);
+      if (hh >= H || ww >= W) continue;
+      const long p = ((long)n * H + hh) * W + ww;
+      float s[8];
+      if (dskip) unpack8f(*(const uint4*)(dskip + p * dspitch + c), s);
+      else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[q][k] = s[k] + ((pooled && idx[k] == q) ? d[k] : 0.f);
+      *(uint4*)(dx + p * dxpitch + c) = pack8f(o[q]);
+    }
+  }
+}
+
+struct UpGeom {
+  int N, hin, win, Hout, Wout, oy, ox, C;
+  float rh, rw;
+};
+
+RDP_DEV void up_src(int u, int in, float r, int& i0, int& i1, float& l1) {
+  const float s = r * (float)u;
+  i0 = (int)s;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+}
+
+__global__ void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch, u16* __restrict__ out, int opitch,
+                                     UpGeom g) {
+  const int CG = g.C >> 3;
+  const long total = (long)g.N * g.Hout * g.Wout * CG;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int cg = it % CG;
+    const long po = it / CG;
+    const int X = po % g.Wout;
+    const long t = po / g.Wout;
+    const int Y = t % g.Hout, n = t / g.Hout;
+    const int c = cg * 8;
+    const int uy = Y - g.oy, ux = X - g.ox;
+    float o[8];
+    if (uy < 0 || ux < 0 || uy >= 2 * g.hin || ux >= 2 * g.win) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = 0.f;
+    } else {
+      int y0, y1, x0, x1;
+      float ly, lx;
+      up_src(uy, g.hin, g.rh, y0, y1, ly);
+      up_src(ux, g.win, g.rw, x0, x1, lx);
+      const long base = (long)n * g.hin;
+      float a[8], b[8], cc[8], d[8];
+      unpack8f(*(const uint4*)(x + ((base + y0) * g.win + x0) * xpitch + c), a);
+      unpack8f(*(const uint4*)(x + ((base + y0) * g.win + x1) * xpitch + c), b);
+      unpack8f(*(const uint4*)(x + ((base + y1) * g.win + x0) * xpitch + c), cc);
+      unpack8f(*(const uint4*)(x + ((base + y1) * g.win + x1) * xpitch + c), d);
+      const float hy = 1.f - ly, hx = 1.f - lx;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = hy * (hx * a[k] + lx * b[k]) + ly * (hx * cc[k] + lx * d[k]);
+    }
+    *(uint4*)(out + po * opitch + c) = pack8f(o);
+  }
+}
+
+RDP_DEV float up_weight(int u, int in, float r, int i) {
+  int i0, i1;
+  float l1;
+  up_src(u, in, r, i0, i1, l1);
+  return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+__global__ void upsample2_bwd_kernel(const u16* __restrict__ dout, int dpitch, u16* __restrict__ dx, int xpitch,
+                                     UpGeom g) {
+  const int CG = g.C >> 3;
+  const long total = (long)g.N * g.hin * g.win * CG;
+  const int uh = 2 * g.hin, uw = 2 * g.win;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int cg = it % CG;
+    const long pi = it / CG;
+    const int j = pi % g.win;
+    const long t = pi / g.win;
+    const int i = t % g.hin, n = t / g.hin;
+    const int c = cg * 8;
+    // candidate u ranges: floor(u*r) in {i-1, i}
+    int ylo = 0, yhi = uh - 1, xlo = 0, xhi = uw - 1;
+    if (g.rh > 0.f) { ylo = max(0, (int)floorf((i - 1) / g.rh) - 1); yhi = min(uh - 1, (int)ceilf((i + 1) / g.rh) + 1); }
+    if (g.rw > 0.f) { xlo = max(0, (int)floorf((j - 1) / g.rw) - 1); xhi = min(uw - 1, (int)ceilf((j + 1) / g.rw) + 1); }
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int uy = ylo; uy <= yhi; ++uy) {
+      const int Y = uy + g.oy;
+      if (Y < 0 || Y >= g.Hout) continue;
+      const float wy = up_weight(uy, g.hin, g.rh, i);
+      if (wy == 0.f) continue;
+      for (int ux = xlo; ux <= xhi; ++ux) {
+        const int X = ux + g.ox;
+        if (X < 0 || X >= g.Wout) continue;
+        const float wx = up_weight(ux, g.win, g.rw, j);
+        if (wx == 0.f) continue;
+        float d[8];
+        unpack8f(*(const uint4*)(dout + (((long)n * g.Hout + Y) * g.Wout + X) * dpitch + c), d);
+        const float w = wy * wx;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, d[k], acc[k]);
+      }
+    }
+    *(uint4*)(dx + pi * xpitch + c) = pack8f(acc);
+  }
+}
+
+static int gridN(long items) {
+  long g = (items + 255) / 256;
+  return (int)std::max<long>(1, std::min<long>(g, 4096));
+}
+static float ac_scale(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
+
+extern "C" {
+int rdp_maxpool2_fwd(const void* x, int xpitch, void* out, int opitch, int N, int H, int W, int C, hipStream_t s) {
+  if (C % 8 || xpitch % 8 || opitch % 8) return -1;
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(gridN((long)N * (H / 2) * (W / 2) * (C / 8))), dim3(256), 0, s,
+                     (const u16*)x, xpitch, (u16*)out, opitch, N, H, W, C);
+  return 0;
+}
+int rdp_maxpool2_bwd(const void* dp, int dppitch, const void* x, int xpitch, const void* dskip, int dspitch, void* dx,
+                     int dxpitch, int N, int H, int W, int C, hipStream_t s) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(gridN((long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8))), dim3(256),
+                     0, s, (const u16*)dp, dppitch, (const u16*)x, xpitch, (const u16*)dskip, dspitch, (u16*)dx,
+                     dxpitch, N, H, W, C);
+  return 0;
+}
+int rdp_upsample2_fwd(const void* x, int xpitch, void* out, int opitch, int N, int hin, int win, int Hout, int Wout,
+                      int oy, int ox, int C, hipStream_t s) {
+  if (C % 8) return -1;
+  UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
+  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(gridN((long)N * Hout * Wout * (C / 8))), dim3(256), 0, s,
+                     (const u16*)x, xpitch, (u16*)out, opitch, g);
+  return 0;
+}
+int rdp_upsample2_bwd(const void* dout, int dpitch, void* dx, int xpitch, int N, int hin, int win, int Hout, int Wout,
+                      int oy, int ox, int C, hipStream_t s) {
+  if (C % 8) return -1;
+  UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
+  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(gridN((long)N * hin * win * (C / 8))), dim3(256), 0, s,
+                     (const u16*)dout, dpitch, (u16*)dx, xpitch, g);
+  return 0;
+}
+}

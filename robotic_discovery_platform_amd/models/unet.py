@@ -1,0 +1,544 @@
+"""MI355X-native U-Net: flat parameter store + static-shape executor over the HIP kernels.
+
+Architecture and state_dict are those of the reference ``UNet(3, 1)``
+(``/root/reference/pkg/segmentation_model.py:86-120``, mirrored by :class:`UNetRef`), but the
+execution model is MI355X-first:
+
+* **Parameters** live in ONE flat fp32 master buffer (grads, Adam moments and a bf16 shadow share
+  its layout). Each reference-named parameter is a view into it; conv weights are stored
+  channels_last (physical OHWI = the [Cout][tap][Cin] K-contiguous layout the implicit-GEMM kernels
+  read), so ``state_dict()`` has the reference's 110 keys / shapes while the kernels read weights
+  with zero re-layout. Derived bf16 layouts (dgrad's flipped/transposed weights, the packed first
+  layer) are rebuilt by one ``wprep`` launch after each optimizer step.
+* **Activations** are NHWC bf16, preallocated once per (batch, H, W): every launch is static, so
+  the whole train step (forward, backward, Adam) is capturable in one hipGraph.
+* **Kernels**: implicit-GEMM MFMA convs with BN statistics fused in the epilogue; the Up block's
+  concat is never materialised (dual-source conv operand; dual-destination dgrad);
+  maxpool backward fuses the skip-gradient add; head + BCE(+Dice) are fused.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .unet_ref import UNetRef, unet_widths
+
+ALIGN = 64  # elements; keeps every parameter 256-B aligned in fp32, 128-B in bf16
+
+
+@dataclass
+class ConvSpec:
+    name: str  # reference module path of the conv, e.g. "down1.maxpool_conv.1.double_conv.0"
+    bn: str  # reference module path of its BatchNorm
+    cin: int
+    cout: int
+    taps: int = 9
+    packed: bool = False  # first layer: Cin padded to 8, 8 taps per K step
+    cin_real: int = 0
+
+
+class ParamStore:
+    """Flat fp32 master/grad/Adam buffers + bf16 shadow, with reference-named parameter views."""
+
+    def __init__(self, ref: nn.Module, device: torch.device):
+        self.device = device
+        self.names: List[str] = []
+        self.offsets: Dict[str, int] = {}
+        self.shapes: Dict[str, torch.Size] = {}
+        off = 0
+        for name, p in ref.named_parameters():
+            self.names.append(name)
+            self.offsets[name] = off
+            self.shapes[name] = p.shape
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        self.exp_avg = torch.zeros(off, dtype=torch.float32, device=device)
+        self.exp_avg_sq = torch.zeros(off, dtype=torch.float32, device=device)
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=device)
+        self.step = torch.zeros(1, dtype=torch.int32, device=device)
+        with torch.no_grad():
+            for name, p in ref.named_parameters():
+                self.view(name).copy_(p.detach().to(device))
+
+    def _phys(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        o, shp = self.offsets[name], self.shapes[name]
+        n = 1
+        for s in shp:
+            n *= s
+        return buf[o:o + n]
+
+    def view(self, name: str, buf: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Logical (reference-shaped) view; 4-D conv weights are channels_last (physical OHWI)."""
+        buf = self.flat if buf is None else buf
+        t = self._phys(buf, name)
+        shp = self.shapes[name]
+        if len(shp) == 4:
+            co, ci, kh, kw = shp
+            return t.view(co, kh, kw, ci).permute(0, 3, 1, 2)
+        return t.view(shp)
+
+    def flat_slice(self, name: str, buf: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self._phys(self.flat if buf is None else buf, name)
+
+
+def unet_conv_specs(depth: int, base: int, in_ch: int, bilinear: bool) -> List[ConvSpec]:
+    """Conv layers in forward order with reference module paths."""
+    f = 2 if bilinear else 1
+    enc = unet_widths(base, depth, bilinear)
+    specs: List[ConvSpec] = []
+
+    def dc(prefix: str, cin: int, cout: int, cmid: Optional[int] = None, first: bool = False):
+        cmid = cmid or cout
+        specs.append(ConvSpec(f"{prefix}.double_conv.0", f"{prefix}.double_conv.1", cin, cmid,
+                              packed=first, cin_real=cin if first else 0))
+        specs.append(ConvSpec(f"{prefix}.double_conv.3", f"{prefix}.double_conv.4", cmid, cout))
+
+    dc("inc", in_ch, enc[0], first=True)
+    for i in range(1, depth + 1):
+        dc(f"down{i}.maxpool_conv.1", enc[i - 1], enc[i])
+    for i in range(1, depth + 1):
+        lvl = depth - i
+        cin = base * (2 ** (lvl + 1))
+        cout = base * (2 ** lvl) // (f if i < depth else 1)
+        dc(f"up{i}.conv", cin, cout, cin // 2 if bilinear else None)
+    return specs
+
+
+class UNetNative(nn.Module):
+    """Reference-keyed U-Net whose compute runs on the native HIP kernels (training + inference)."""
+
+    def __init__(self, n_channels: int = 3, n_classes: int = 1, bilinear: bool = True, base_width: int = 64,
+                 depth: int = 4, device: Optional[torch.device] = None, init_from: Optional[nn.Module] = None):
+        super().__init__()
+        if n_classes != 1:
+            raise NotImplementedError("native head supports n_classes == 1 (reference: UNet(3, 1))")
+        if not bilinear:
+            raise NotImplementedError("native transposed-conv decoder not built yet; use UNetRef")
+        if n_channels > 8:
+            raise NotImplementedError("native first layer packs <= 8 input channels")
+        if base_width != 64:
+            raise NotImplementedError("native head assumes 64 channels")
+        self.n_channels, self.n_classes, self.bilinear = n_channels, n_classes, bilinear
+        self.depth, self.base_width = depth, base_width
+        device = device or torch.device("cuda")
+        ref = init_from if init_from is not None else UNetRef(n_channels, n_classes, bilinear, base_width, depth)
+        self.store = ParamStore(ref, device)
+        # reference-named parameters (views into the flat master) and BN buffers
+        self._pnames = list(self.store.names)
+        self._bn_names: List[str] = []
+        for name in self.store.names:
+            self._register_view(name, nn.Parameter(self.store.view(name), requires_grad=False))
+        for name, buf in ref.named_buffers():
+            self._register_buffer_path(name, buf.detach().clone().to(device))
+        self.specs = unet_conv_specs(depth, base_width, n_channels, bilinear)
+        self._derived_built = False
+        self._build_derived()
+
+    # ---- module plumbing: keep reference key names ("inc.double_conv.0.weight", ...) ----
+    def _holder(self, path: str) -> Tuple[nn.Module, str]:
+        parts = path.split(".")
+        mod: nn.Module = self
+        for p in parts[:-1]:
+            if p not in mod._modules:
+                mod._modules[p] = nn.Module()
+            mod = mod._modules[p]
+        return mod, parts[-1]
+
+    def _register_view(self, path: str, param: nn.Parameter):
+        mod, leaf = self._holder(path)
+        mod._parameters[leaf] = param
+
+    def _register_buffer_path(self, path: str, t: torch.Tensor):
+        mod, leaf = self._holder(path)
+        mod._buffers[leaf] = t
+
+    def buf(self, path: str) -> torch.Tensor:
+        mod, leaf = self._holder(path)
+        return mod._buffers[leaf]
+
+    def load_state_dict(self, sd, strict: bool = True):  # keep flat-buffer views intact
+        own = dict(self.named_parameters())
+        ownb = dict(self.named_buffers())
+        missing = [k for k in list(own) + list(ownb) if k not in sd]
+        unexpected = [k for k in sd if k not in own and k not in ownb]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"state_dict mismatch: missing={missing} unexpected={unexpected}")
+        with torch.no_grad():
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(v.to(own[k].device))
+                elif k in ownb:
+                    ownb[k].copy_(v.to(ownb[k].device))
+        self._build_derived()
+        return missing, unexpected
+
+    # ---- derived bf16 weight layouts ----
+    def _build_derived(self):
+        C = _native()
+        st = self.store
+        segs = []
+        off = 0
+        self._dw: Dict[str, Tuple[int, int]] = {}  # name -> (offset, numel) in derived
+        for sp in self.specs:
+            wname = sp.name + ".weight"
+            if sp.packed:
+                n = sp.cout * 128
+                segs.append((st.offsets[wname], off, 1, sp.cout, sp.cin_real, sp.taps))
+            else:
+                n = sp.cout * sp.taps * sp.cin
+                segs.append((st.offsets[wname], off, 0, sp.cout, sp.cin, sp.taps))
+            self._dw[sp.name] = (off, n)
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.derived = torch.zeros(max(off, 1), dtype=torch.bfloat16, device=st.device)
+        seg_size = C.wseg_size()
+        raw = bytearray()
+        import struct
+        for s in segs:
+            rec = struct.pack("<qqiiii", *s)
+            raw += rec + b"\0" * (seg_size - len(rec))
+        self._segs = torch.tensor(list(raw), dtype=torch.uint8).to(st.device)
+        self._nseg = len(segs)
+        self.refresh_weights()
+
+    def refresh_weights(self):
+        """Rebuild the bf16 shadow + derived layouts from the fp32 master (after load / manual edits)."""
+        C = _native()
+        C.cast_bf16(self.store.flat, self.store.shadow)
+        C.wprep(self.store.flat, self.derived, self._segs, self._nseg)
+
+    def fwd_weight(self, sp: ConvSpec) -> torch.Tensor:
+        if sp.packed:
+            o, n = self._dw[sp.name]
+            return self.derived[o:o + n].view(sp.cout, 128)
+        return self.store.flat_slice(sp.name + ".weight", self.store.shadow).view(sp.cout, sp.taps * sp.cin)
+
+    def dgrad_weight(self, sp: ConvSpec) -> torch.Tensor:
+        o, n = self._dw[sp.name]
+        return self.derived[o:o + n].view(sp.cin, sp.taps * sp.cout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """NCHW float input -> NCHW fp32 logits (inference helper; training uses UNetExecutor)."""
+        ex = self.executor(x.shape[0], x.shape[2], x.shape[3], training=False)
+        ex.set_input(x)
+        ex.forward()
+        return ex.logits_nchw()
+
+    def executor(self, batch: int, h: int, w: int, training: bool = True, loss: str = "bce",
+                 dice_weight: float = 1.0) -> "UNetExecutor":
+        key = (batch, h, w, training, loss, dice_weight)
+        cache = self.__dict__.setdefault("_executors", {})
+        if key not in cache:
+            cache[key] = UNetExecutor(self, batch, h, w, training, loss, dice_weight)
+        return cache[key]
+
+
+def _native():
+    from ..ops import native
+    return native()
+
+
+@dataclass
+class _Layer:
+    spec: ConvSpec
+    x1: torch.Tensor
+    x2: Optional[torch.Tensor]
+    y: torch.Tensor
+    a: torch.Tensor
+    coef: torch.Tensor
+    coef2: torch.Tensor
+    da: Optional[torch.Tensor] = None  # gradient w.r.t. a (filled by the consumer)
+    dy: Optional[torch.Tensor] = None
+    dx1: Optional[torch.Tensor] = None  # dgrad destinations (None => no dgrad)
+    dx2: Optional[torch.Tensor] = None
+    splits: int = 1
+
+
+class UNetExecutor:
+    """Static-shape forward/backward/step program for one (batch, H, W)."""
+
+    def __init__(self, model: UNetNative, N: int, H: int, W: int, training: bool, loss: str, dice_weight: float):
+        self.m, self.N, self.H, self.W = model, N, H, W
+        self.training = training
+        self.dice_w = float(dice_weight) if loss == "bce_dice" else 0.0
+        self.dice_eps = 1.0
+        dev = model.store.device
+        self.dev = dev
+        C = _native()
+        D = model.depth
+        bf = torch.bfloat16
+        specs = model.specs
+        enc = unet_widths(model.base_width, D, model.bilinear)
+        sizes = [(H, W)]
+        for _ in range(D):
+            h, w = sizes[-1]
+            sizes.append((h // 2, w // 2))
+        self.sizes = sizes
+
+        def t(h, w, c):
+            return torch.zeros(N, h, w, c, dtype=bf, device=dev)
+
+        self.x_in = t(H, W, 8)
+        self.target = torch.zeros(N * H * W, dtype=torch.float32, device=dev)
+        self.layers: List[_Layer] = []
+        it = iter(specs)
+
+        def mk(spec, x1, x2, h, w):
+            L = _Layer(spec, x1, x2, t(h, w, spec.cout), t(h, w, spec.cout),
+                       torch.zeros(4 * spec.cout, device=dev), torch.zeros(3 * spec.cout, device=dev))
+            self.layers.append(L)
+            return L
+
+        # encoder
+        h, w = sizes[0]
+        l0 = mk(next(it), self.x_in, None, h, w)
+        l1 = mk(next(it), l0.a, None, h, w)
+        self.skips = [l1.a]
+        self.pools: List[torch.Tensor] = []
+        self.down_layers: List[Tuple[_Layer, _Layer]] = [(l0, l1)]
+        for i in range(1, D + 1):
+            h, w = sizes[i]
+            p = t(h, w, enc[i - 1])
+            self.pools.append(p)
+            la = mk(next(it), p, None, h, w)
+            lb = mk(next(it), la.a, None, h, w)
+            self.down_layers.append((la, lb))
+            self.skips.append(lb.a)
+        # decoder
+        self.ups: List[torch.Tensor] = []
+        self.up_layers: List[Tuple[_Layer, _Layer]] = []
+        low = self.skips[D]
+        for i in range(1, D + 1):
+            lv = D - i
+            h, w = sizes[lv]
+            u = t(h, w, low.shape[3])
+            self.ups.append(u)
+            la = mk(next(it), self.skips[lv], u, h, w)
+            lb = mk(next(it), la.a, None, h, w)
+            self.up_layers.append((la, lb))
+            low = lb.a
+        self.final = low
+        M = N * H * W
+        self.M = M
+        self.logits = torch.zeros(M, dtype=torch.float32, device=dev)
+        self.head_partial = torch.zeros(C.head_partial_blocks(M) * 65, dtype=torch.float32, device=dev)
+        self.loss_sums = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(2, dtype=torch.float32, device=dev)
+        # stats slab (reused by every conv; finalize runs right after each conv)
+        max_rows = max(C.conv_stats_rows(L.x1.shape[0] * L.x1.shape[1] * L.x1.shape[2], L.spec.cout, 0) * 2 * L.spec.cout
+                       for L in self.layers)
+        self.stats = torch.zeros(max_rows, dtype=torch.float32, device=dev)
+        if training:
+            self._alloc_backward(C)
+        else:
+            self._eval_coef_ready = False
+
+    # ------------------------------------------------------------------ backward buffers
+    def _alloc_backward(self, C):
+        dev, bf = self.dev, torch.bfloat16
+        N = self.N
+        D = self.m.depth
+
+        def like(x):
+            return torch.zeros_like(x)
+
+        for L in self.layers:
+            L.da = like(L.a)
+            L.dy = like(L.y)
+        # dgrad destinations
+        enc_layers = self.down_layers
+        # inc: conv1 has no dgrad; conv2 -> inc conv1 da
+        (l0, l1) = enc_layers[0]
+        l1.dx1 = l0.da
+        self.dpools: List[torch.Tensor] = []
+        self.dskips: List[torch.Tensor] = [like(s) for s in self.skips[:D]]  # grads from the decoder concat
+        for i in range(1, D + 1):
+            la, lb = enc_layers[i]
+            lb.dx1 = la.da
+            dp = like(self.pools[i - 1])
+            self.dpools.append(dp)
+            la.dx1 = dp
+        self.dups: List[torch.Tensor] = []
+        for i in range(1, D + 1):
+            lv = D - i
+            la, lb = self.up_layers[i - 1]
+            lb.dx1 = la.da
+            du = like(self.ups[i - 1])
+            self.dups.append(du)
+            la.dx1 = self.dskips[lv]
+            la.dx2 = du
+        # wgrad split-K choice + shared slab
+        slab = 0
+        for L in self.layers:
+            n, h, w, _ = L.x1.shape
+            M = n * h * w
+            cin = L.spec.cin if not L.spec.packed else 8
+            ncols = 72 if L.spec.packed else L.spec.taps * cin
+            tiles = ((ncols + 255) // 256) * (L.spec.cout // 64)
+            L.splits = int(max(1, min((1024 + tiles - 1) // tiles, M // 2048)))
+            slab = max(slab, C.wgrad_slab_elems(n, h, w, cin, L.spec.cout, L.spec.taps, int(L.spec.packed), L.splits))
+        self.slab = torch.zeros(slab, dtype=torch.float32, device=dev)
+        maxc = max(L.spec.cout for L in self.layers)
+        self.bn_partial = torch.zeros(1024 * 2 * maxc, dtype=torch.float32, device=dev)
+
+    # ------------------------------------------------------------------ data
+    def set_input(self, x: torch.Tensor, target: Optional[torch.Tensor] = None):
+        """x: [N,C,H,W] (float, values in [0,1]) or NHWC8 bf16; target: [N,1,H,W] float masks."""
+        with torch.no_grad():
+            if x.dim() == 4 and x.shape[-1] == 8 and x.dtype == torch.bfloat16:
+                self.x_in.copy_(x)
+            else:
+                self.x_in.zero_()
+                self.x_in[..., : x.shape[1]].copy_(x.permute(0, 2, 3, 1))
+            if target is not None:
+                self.target.copy_(target.reshape(-1))
+
+    # ------------------------------------------------------------------ forward
+    def _conv_bn_relu(self, C, L: _Layer):
+        sp = L.spec
+        m = self.m
+        w = m.fwd_weight(sp)
+        rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats if self.training else None, 0)
+        g = m.store.view(sp.bn + ".weight")
+        b = m.store.view(sp.bn + ".bias")
+        if self.training:
+            M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
+            C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
+                          m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef)
+        C.bn_relu_apply(L.y, L.a, L.coef, 1)
+
+    def prepare_eval(self):
+        C = _native()
+        m = self.m
+        for L in self.layers:
+            sp = L.spec
+            C.bn_eval_coef(m.store.view(sp.bn + ".weight"), m.store.view(sp.bn + ".bias"),
+                           m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"), 1e-5, L.coef)
+
+    def forward(self):
+        C = _native()
+        D = self.m.depth
+        if not self.training:
+            self.prepare_eval()
+        l0, l1 = self.down_layers[0]
+        self._conv_bn_relu(C, l0)
+        self._conv_bn_relu(C, l1)
+        for i in range(1, D + 1):
+            C.maxpool2_fwd(self.skips[i - 1], self.pools[i - 1])
+            la, lb = self.down_layers[i]
+            self._conv_bn_relu(C, la)
+            self._conv_bn_relu(C, lb)
+        low = self.skips[D]
+        for i in range(1, D + 1):
+            lv = D - i
+            u = self.ups[i - 1]
+            oy = (u.shape[1] - 2 * low.shape[1]) // 2
+            ox = (u.shape[2] - 2 * low.shape[2]) // 2
+            C.upsample2_fwd(low, u, oy, ox)
+            la, lb = self.up_layers[i - 1]
+            self._conv_bn_relu(C, la)
+            self._conv_bn_relu(C, lb)
+            low = lb.a
+        head_w = self.m.store.view("outc.conv.weight").reshape(-1)
+        head_b = self.m.store.view("outc.conv.bias")
+        C.head_fwd(self.final, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums, self.loss,
+                   self.dice_w, self.dice_eps)
+
+    def logits_nchw(self) -> torch.Tensor:
+        return self.logits.view(self.N, 1, self.H, self.W)
+
+    # ------------------------------------------------------------------ backward
+    def _bn_bwd(self, C, L: _Layer):
+        sp = L.spec
+        st = self.m.store
+        M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
+        T = C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
+        C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
+                          st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2)
+        C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
+
+    def _conv_bwd(self, C, L: _Layer, hooks=None):
+        sp = L.spec
+        st = self.m.store
+        self._bn_bwd(C, L)
+        gw = st.flat_slice(sp.name + ".weight", st.grad)
+        C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw, 0, L.splits)
+        if L.dx1 is not None:
+            C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0)
+        if hooks is not None:
+            hooks(sp)
+
+    def backward(self, grad_hook=None, gscale: float = 1.0):
+        """Full backward; ``grad_hook(spec)`` fires after each conv layer's grads are final."""
+        C = _native()
+        D = self.m.depth
+        st = self.m.store
+        head_w = st.view("outc.conv.weight").reshape(-1)
+        C.head_bwd(self.final, head_w, self.logits, self.target, self.loss_sums, self.up_layers[-1][1].da,
+                   self.head_partial, st.flat_slice("outc.conv.weight", st.grad), st.flat_slice("outc.conv.bias", st.grad),
+                   self.dice_w, self.dice_eps, gscale)
+        for i in range(D, 0, -1):
+            la, lb = self.up_layers[i - 1]
+            self._conv_bwd(C, lb, grad_hook)
+            self._conv_bwd(C, la, grad_hook)
+            # d(low) = upsample backward of du
+            low_layer = self.down_layers[D][1] if i == 1 else self.up_layers[i - 2][1]
+            du = self.dups[i - 1]
+            oy = (du.shape[1] - 2 * low_layer.a.shape[1]) // 2
+            ox = (du.shape[2] - 2 * low_layer.a.shape[2]) // 2
+            C.upsample2_bwd(du, low_layer.da, oy, ox)
+        for i in range(D, 0, -1):
+            la, lb = self.down_layers[i]
+            self._conv_bwd(C, lb, grad_hook)
+            self._conv_bwd(C, la, grad_hook)
+            prev = self.down_layers[i - 1][1]
+            C.maxpool2_bwd(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1], prev.da)
+        l0, l1 = self.down_layers[0]
+        self._conv_bwd(C, l1, grad_hook)
+        self._conv_bwd(C, l0, grad_hook)
+
+    def backward_order(self) -> List[ConvSpec]:
+        """Conv layers in the order their gradients become final during backward()."""
+        D = self.m.depth
+        out = []
+        for i in range(D, 0, -1):
+            la, lb = self.up_layers[i - 1]
+            out += [lb.spec, la.spec]
+        for i in range(D, 0, -1):
+            la, lb = self.down_layers[i]
+            out += [lb.spec, la.spec]
+        l0, l1 = self.down_layers[0]
+        return out + [l1.spec, l0.spec]
+
+
+class NativeAdam:
+    """torch.optim.Adam semantics over the flat store, one fused launch (+ derived-weight rebuild)."""
+
+    def __init__(self, model: UNetNative, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0):
+        self.m = model
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+
+    def step(self, gscale: float = 1.0):
+        C = _native()
+        st = self.m.store
+        C.adam(st.flat, st.grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr, self.betas[0], self.betas[1], self.eps,
+               self.wd, gscale, st.step)
+        C.wprep(st.flat, self.m.derived, self.m._segs, self.m._nseg)
+
+    def state_dict(self):
+        st = self.m.store
+        return {"step": st.step.clone(), "exp_avg": st.exp_avg.clone(), "exp_avg_sq": st.exp_avg_sq.clone(),
+                "lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.wd}
+
+    def load_state_dict(self, sd):
+        st = self.m.store
+        with torch.no_grad():
+            st.step.copy_(sd["step"])
+            st.exp_avg.copy_(sd["exp_avg"])
+            st.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.lr, self.betas, self.eps, self.wd = sd["lr"], tuple(sd["betas"]), sd["eps"], sd["weight_decay"]

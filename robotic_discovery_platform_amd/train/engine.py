@@ -1,0 +1,179 @@
+"""Training engines: the native (HIP kernel) step and the eager (plain torch) step.
+
+Both implement the reference step (``/root/reference/scripts/train_segmenter.py:156-165``):
+zero_grad -> forward -> BCEWithLogits (optionally + Dice) -> backward -> Adam(lr 1e-4), and
+optionally DDP over RCCL with flat-buffer gradient buckets (``parallel/ddp.py``).
+
+``NativeTrainer`` runs everything on the hand-written gfx950 kernels. On a single GPU the whole
+step (forward + backward + Adam + weight re-layout) is captured once into a hipGraph
+(``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replayed: ~250 launches become one graph
+launch, so the step is never host-bound. With world > 1 the step runs as eager launches so the
+bucketed all-reduces can overlap backward on RCCL's stream (RCCL calls are not captured).
+
+``EagerTrainer`` is the reference execution model (torch autograd + MIOpen) used for the CPU path,
+CPU/gloo DDP tests and as the measured comparison baseline.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from ..models.unet import NativeAdam, UNetNative
+from ..models.unet_ref import UNetRef
+from ..parallel.ddp import FlatBucketer, broadcast_module_state, dist_info
+
+
+class NativeTrainer:
+    def __init__(self, model: UNetNative, batch: int, h: int, w: int, lr: float = 1e-4, loss: str = "bce",
+                 dice_weight: float = 1.0, graph: bool = True, bucket_mb: float = 16.0):
+        self.model = model
+        self.ex = model.executor(batch, h, w, training=True, loss=loss, dice_weight=dice_weight)
+        self.opt = NativeAdam(model, lr=lr)
+        self.rank, self.world = dist_info()
+        self.bucketer = None
+        if self.world > 1:
+            st = model.store
+            broadcast_module_state([st.flat] + [b for _, b in model.named_buffers()])
+            model.refresh_weights()
+            ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
+            self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb)
+            self._layer_params = {sp.name: [sp.name + ".weight", sp.bn + ".weight", sp.bn + ".bias"]
+                                  for sp in model.specs}
+        self.use_graph = graph and self.world == 1 and torch.cuda.is_available()
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.steps = 0
+
+    def _hook(self, spec):
+        self.bucketer.mark_ready(self._layer_params[spec.name])
+
+    def _step_body(self):
+        ex = self.ex
+        ex.forward()
+        if self.bucketer is not None:
+            self.bucketer.reset()
+            ex.backward(grad_hook=self._hook)
+            self.bucketer.mark_ready(["outc.conv.weight", "outc.conv.bias"])
+            self.bucketer.finish()
+            self.opt.step(gscale=1.0 / self.world)
+        else:
+            ex.backward()
+            self.opt.step()
+
+    def set_batch(self, x: torch.Tensor, target: torch.Tensor):
+        self.ex.set_input(x, target)
+
+    def step(self) -> torch.Tensor:
+        """One training step on the current input buffers; returns the (device) loss tensor."""
+        if self.use_graph:
+            if self.graph is None:
+                if self.steps < 2:  # warm up eagerly (allocator, first-launch costs) before capture
+                    self._step_body()
+                    self.steps += 1
+                    return self.ex.loss
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=s):
+                        self._step_body()
+                torch.cuda.current_stream().wait_stream(s)
+                self.graph = g
+            self.graph.replay()
+        else:
+            self._step_body()
+        self.steps += 1
+        return self.ex.loss
+
+    def eval_loss(self) -> torch.Tensor:
+        """Validation forward (batch statistics are NOT updated: eval-mode BN)."""
+        ev = self.model.executor(self.ex.N, self.ex.H, self.ex.W, training=False)
+        ev.target.copy_(self.ex.target)
+        ev.x_in.copy_(self.ex.x_in)
+        ev.dice_w = self.ex.dice_w
+        ev.forward()
+        return ev.loss
+
+
+def _numel(shape):
+    n = 1
+    for s in shape:
+        n *= s
+    return n
+
+
+class EagerTrainer:
+    """Plain-torch trainer (reference execution model) with the same flat-bucket DDP."""
+
+    def __init__(self, model: nn.Module, lr: float = 1e-4, loss: str = "bce", dice_weight: float = 1.0,
+                 bucket_mb: float = 16.0, amp: Optional[torch.dtype] = None):
+        self.model = model
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr)
+        self.loss_kind, self.dice_w = loss, dice_weight
+        self.amp = amp
+        self.rank, self.world = dist_info()
+        self.bucketer = None
+        if self.world > 1:
+            params = list(model.named_parameters())
+            broadcast_module_state([p.data for _, p in params] + [b for _, b in model.named_buffers()])
+            # flat grad buffer; each param.grad is a view into it (autograd accumulates in place)
+            total = sum(p.numel() for _, p in params)
+            dev = params[0][1].device
+            self.flat_grad = torch.zeros(total, dtype=params[0][1].dtype, device=dev)
+            ranges, off = [], 0
+            for n, p in params:
+                p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+                ranges.append((n, off, off + p.numel()))
+                off += p.numel()
+            self.bucketer = FlatBucketer(self.flat_grad, ranges, bucket_mb)
+            for n, p in params:
+                p.register_post_accumulate_grad_hook(lambda _p, n=n: self.bucketer.mark_ready([n]))
+
+    def compute_loss(self, logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        logits = logits.float()
+        loss = nn.functional.binary_cross_entropy_with_logits(logits, target)
+        if self.loss_kind == "bce_dice":
+            p = torch.sigmoid(logits)
+            dice = 1 - (2 * (p * target).sum() + 1.0) / (p.sum() + target.sum() + 1.0)
+            loss = loss + self.dice_w * dice
+        return loss
+
+    def step(self, x: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        if self.bucketer is not None:
+            self.flat_grad.zero_()
+            self.bucketer.reset()
+        else:
+            self.opt.zero_grad(set_to_none=True)
+        ctx = torch.autocast(device_type=x.device.type, dtype=self.amp) if self.amp else contextlib.nullcontext()
+        with ctx:
+            out = self.model(x)
+        loss = self.compute_loss(out, target)
+        loss.backward()
+        if self.bucketer is not None:
+            self.bucketer.finish()
+            self.flat_grad /= self.world
+        self.opt.step()
+        return loss.detach()
+
+
+def build_bench_step(batch: int, size: int, decoder: str, device: torch.device, world: int, graph: bool,
+                     bucket_mb: float, loss: str = "bce"):
+    """bench.py hook: returns a zero-arg callable running one full native training step."""
+    if decoder != "bilinear":
+        raise NotImplementedError("native bench runs the reference (bilinear) decoder")
+    torch.manual_seed(0)
+    ref = UNetRef(3, 1, bilinear=True)
+    model = UNetNative(3, 1, bilinear=True, device=device, init_from=ref)
+    tr = NativeTrainer(model, batch, size, size, loss=loss, graph=graph, bucket_mb=bucket_mb)
+    g = torch.Generator(device="cpu").manual_seed(1234 + tr.rank)
+    x = torch.rand(batch, 3, size, size, generator=g).to(device)
+    y = (torch.rand(batch, 1, size, size, generator=g) > 0.5).float().to(device)
+    tr.set_batch(x, y)
+
+    def step():
+        return tr.step()
+
+    step.trainer = tr
+    return step

@@ -1,0 +1,273 @@
+"""Numerics of every native HIP kernel vs a plain-PyTorch fp32 reference of the same op (GPU only).
+
+Inputs are rounded to bf16 first, so the references see exactly the kernel's operands; tolerances
+cover bf16 output rounding and fp32-vs-MFMA accumulation order.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def C():
+    from robotic_discovery_platform_amd.ops import native
+    return native()
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def relerr(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def ohwi(w):  # [Cout,Cin,kh,kw] -> [Cout, kh*kw*Cin]
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [
+    (2, 16, 16, 64, 0, 64), (1, 32, 32, 128, 0, 128), (2, 9, 13, 64, 64, 128),
+    (1, 8, 8, 256, 256, 256), (3, 7, 5, 64, 0, 64), (1, 16, 16, 512, 0, 512)])
+def test_conv_fwd_and_stats(C, N, H, W, C1, C2, Cout):
+    torch.manual_seed(0)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    rows = C.conv_stats_rows(N * H * W, Cout, 0)
+    stats = torch.zeros(rows * 2 * Cout, device=dev)
+    r = C.conv_fwd(x1, x2, ohwi(w).contiguous(), 9, 0, y, None, stats, 0)
+    assert r == rows
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.conv2d(xin, w.float(), padding=1)
+    assert relerr(nchw(y), ref) < 1e-2
+    yq = nchw(y).float()
+    s = stats.view(rows, 2, Cout).sum(0)
+    assert torch.allclose(s[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+def test_conv_fwd_asymmetric_identity(C):
+    """A = I style check with an asymmetric weight: catches row/col swaps in the MFMA C-write."""
+    dev = "cuda"
+    N, H, W, Cin, Cout = 1, 4, 4, 64, 64
+    x = torch.zeros(N, H, W, Cin, device=dev)
+    for c in range(Cin):
+        x[0, c // 16, (c // 4) % 4, c] = 1.0
+    w = torch.zeros(Cout, Cin, 3, 3, device=dev)
+    for co in range(Cout):
+        for ci in range(Cin):
+            w[co, ci, 1, 1] = float((co * 7 + ci * 3) % 11) - 5  # asymmetric, small ints (exact in bf16)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(bf(x), None, ohwi(bf(w)).contiguous(), 9, 0, y, None, None, 0)
+    ref = F.conv2d(nchw(x), w, padding=1)
+    assert torch.equal(nchw(y).float(), ref)
+
+
+def test_conv_packed_first_layer(C):
+    torch.manual_seed(1)
+    dev = "cuda"
+    N, H, W, Cout = 2, 20, 12, 64
+    x = torch.rand(N, 3, H, W, device=dev)
+    x8 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device=dev)
+    x8[..., :3] = bf(nhwc(x))
+    w = bf(torch.randn(Cout, 3, 3, 3, device=dev) * 0.3)
+    wp = torch.zeros(Cout, 16, 8, dtype=torch.bfloat16, device=dev)
+    wp[:, :9, :3] = w.permute(0, 2, 3, 1).reshape(Cout, 9, 3)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x8, None, wp.view(Cout, 128), 9, 1, y, None, None, 0)
+    ref = F.conv2d(nchw(x8[..., :3]).float(), w.float(), padding=1)
+    assert relerr(nchw(y), ref) < 1e-2
+
+
+def test_conv_dgrad_split_output(C):
+    """dgrad = conv(dy, flip(W)^T) written into two destinations (the Up-block concat split)."""
+    torch.manual_seed(2)
+    dev = "cuda"
+    N, H, W, Cs, Cu, Cout = 2, 12, 10, 64, 64, 64
+    x = torch.randn(N, Cs + Cu, H, W, device=dev, requires_grad=True)
+    w = bf(torch.randn(Cout, Cs + Cu, 3, 3, device=dev) / 30)
+    dy = bf(torch.randn(N, Cout, H, W, device=dev))
+    y = F.conv2d(x, w.float(), padding=1)
+    y.backward(dy.float())
+    wt = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cs + Cu, 9 * Cout).contiguous()  # [cin][tap'][cout]
+    d1 = torch.empty(N, H, W, Cs, dtype=torch.bfloat16, device=dev)
+    d2 = torch.empty(N, H, W, Cu, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(nhwc(dy), None, wt, 9, 0, d1, d2, None, 0)
+    got = torch.cat([nchw(d1), nchw(d2)], 1)
+    assert relerr(got, x.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,splits", [
+    (2, 16, 16, 64, 0, 64, 3), (1, 32, 32, 128, 0, 128, 4), (2, 9, 13, 64, 64, 128, 2), (1, 8, 8, 256, 0, 512, 1)])
+def test_conv_wgrad(C, N, H, W, C1, C2, Cout, splits):
+    torch.manual_seed(3)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    dy = bf(torch.randn(N, H, W, Cout, device=dev))
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    w = torch.zeros(Cout, C1 + C2, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(xin, w, padding=1).backward(nchw(dy).float())
+    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, C1 + C2, Cout, 9, 0, splits), device=dev)
+    out = torch.zeros(Cout * 9 * (C1 + C2), device=dev)
+    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits)
+    ref = w.grad.permute(0, 2, 3, 1).reshape(-1)
+    assert relerr(out, ref) < 2e-3
+
+
+def test_conv_wgrad_packed(C):
+    torch.manual_seed(4)
+    dev = "cuda"
+    N, H, W, Cout = 2, 18, 14, 64
+    x = bf(torch.rand(N, H, W, 3, device=dev))
+    x8 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device=dev)
+    x8[..., :3] = x
+    dy = bf(torch.randn(N, H, W, Cout, device=dev))
+    w = torch.zeros(Cout, 3, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(nchw(x).float(), w, padding=1).backward(nchw(dy).float())
+    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 8, Cout, 9, 1, 5), device=dev)
+    out = torch.zeros(Cout * 27, device=dev)
+    C.conv_wgrad(x8, None, dy, 9, 1, 3, slab, out, 0, 5)
+    assert relerr(out, w.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
+
+
+def test_bn_relu_train_fwd_bwd(C):
+    torch.manual_seed(5)
+    dev = "cuda"
+    N, H, W, Ch = 4, 16, 16, 128
+    y = bf(torch.randn(N, H, W, Ch, device=dev) * 2 + 0.5)
+    gamma = torch.rand(Ch, device=dev) + 0.5
+    beta = torch.randn(Ch, device=dev) * 0.1
+    M = N * H * W
+    stats = torch.stack([y.float().sum((0, 1, 2)), (y.float() ** 2).sum((0, 1, 2))]).reshape(-1).contiguous()
+    rm, rv = torch.zeros(Ch, device=dev), torch.ones(Ch, device=dev)
+    nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+    coef = torch.zeros(4 * Ch, device=dev)
+    C.bn_finalize(stats, 1, M, gamma, beta, rm, rv, nbt, 0.1, 1e-5, coef)
+    a = torch.empty_like(y)
+    C.bn_relu_apply(y, a, coef, 1)
+    bn = torch.nn.BatchNorm2d(Ch).to(dev)
+    with torch.no_grad():
+        bn.weight.copy_(gamma); bn.bias.copy_(beta)
+    yin = nchw(y).float().detach().requires_grad_(True)
+    ref = torch.relu(bn(yin))
+    assert relerr(nchw(a), ref) < 1e-2
+    assert torch.allclose(rm, bn.running_mean, atol=1e-4) and torch.allclose(rv, bn.running_var, rtol=1e-3)
+    assert nbt.item() == 1
+    da = bf(torch.randn(N, H, W, Ch, device=dev))
+    ref.backward(nchw(da).float())
+    part = torch.zeros(1024 * 2 * Ch, device=dev)
+    T = C.bn_relu_bwd_reduce(da, y, coef, 1, part)
+    dg, db, coef2 = torch.zeros(Ch, device=dev), torch.zeros(Ch, device=dev), torch.zeros(3 * Ch, device=dev)
+    C.bn_bwd_finalize(part, T, M, gamma, coef, dg, db, coef2)
+    dy = torch.empty_like(y)
+    C.bn_relu_bwd_apply(da, y, coef, coef2, dy, 1)
+    assert relerr(nchw(dy), yin.grad) < 2e-2
+    assert relerr(dg, bn.weight.grad) < 1e-3 and relerr(db, bn.bias.grad) < 1e-3
+
+
+def test_maxpool_fwd_bwd_with_skip(C):
+    torch.manual_seed(6)
+    dev = "cuda"
+    for (N, H, W, Ch) in [(2, 16, 16, 64), (1, 9, 7, 128)]:
+        x = bf(torch.randn(N, H, W, Ch, device=dev))
+        x[0, 0, 0, :8] = x[0, 0, 1, :8]  # ties: first max wins
+        p = torch.empty(N, H // 2, W // 2, Ch, dtype=torch.bfloat16, device=dev)
+        C.maxpool2_fwd(x, p)
+        xr = nchw(x).float().requires_grad_(True)
+        pr = F.max_pool2d(xr, 2)
+        assert torch.equal(nchw(p).float(), pr)
+        dp = bf(torch.randn_like(pr))
+        ds = bf(torch.randn(N, Ch, H, W, device=dev))
+        pr.backward(dp.float())
+        dx = torch.empty_like(x)
+        C.maxpool2_bwd(nhwc(dp), x, nhwc(ds), dx)
+        assert relerr(nchw(dx), xr.grad + ds.float()) < 1e-2
+
+
+@pytest.mark.parametrize("hin,win,H2,W2", [(8, 8, 16, 16), (5, 7, 11, 14), (16, 16, 32, 32), (1, 1, 2, 2)])
+def test_upsample_fwd_bwd(C, hin, win, H2, W2):
+    torch.manual_seed(7)
+    dev = "cuda"
+    N, Ch = 2, 64
+    x = bf(torch.randn(N, hin, win, Ch, device=dev))
+    xr = nchw(x).float().requires_grad_(True)
+    up = F.interpolate(xr, scale_factor=2, mode="bilinear", align_corners=True)
+    dY, dX = H2 - up.shape[2], W2 - up.shape[3]
+    ref = F.pad(up, [dX // 2, dX - dX // 2, dY // 2, dY - dY // 2])
+    out = torch.empty(N, H2, W2, Ch, dtype=torch.bfloat16, device=dev)
+    C.upsample2_fwd(x, out, dY // 2, dX // 2)
+    assert relerr(nchw(out), ref) < 1e-2
+    g = bf(torch.randn_like(ref))
+    ref.backward(g.float())
+    dx = torch.empty_like(x)
+    C.upsample2_bwd(nhwc(g), dx, dY // 2, dX // 2)
+    assert relerr(nchw(dx), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("dice_w", [0.0, 1.0])
+def test_head_loss(C, dice_w):
+    torch.manual_seed(8)
+    dev = "cuda"
+    N, H, W = 2, 24, 20
+    a = bf(torch.randn(N, H, W, 64, device=dev))
+    wt = torch.randn(64, device=dev) * 0.1
+    b = torch.randn(1, device=dev) * 0.1
+    t = (torch.rand(N, 1, H, W, device=dev) > 0.5).float()
+    M = N * H * W
+    logits = torch.zeros(M, device=dev)
+    part = torch.zeros(C.head_partial_blocks(M) * 65, device=dev)
+    sums, loss = torch.zeros(4, device=dev), torch.zeros(2, device=dev)
+    C.head_fwd(a, wt, b, t.reshape(-1).contiguous(), logits, part, sums, loss, dice_w, 1.0)
+    ar = nchw(a).float().requires_grad_(True)
+    wr = wt.clone().view(1, 64, 1, 1).requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    lg = F.conv2d(ar, wr, br)
+    L = F.binary_cross_entropy_with_logits(lg, t)
+    if dice_w:
+        p = torch.sigmoid(lg)
+        L = L + dice_w * (1 - (2 * (p * t).sum() + 1) / (p.sum() + t.sum() + 1))
+    assert torch.allclose(logits.view_as(lg), lg, atol=1e-4)
+    assert abs(loss[0].item() - L.item()) < 1e-4
+    L.backward()
+    da = torch.empty_like(a)
+    gw, gb = torch.zeros(64, device=dev), torch.zeros(1, device=dev)
+    C.head_bwd(a, wt, logits, t.reshape(-1).contiguous(), sums, da, part, gw, gb, dice_w, 1.0, 1.0)
+    assert relerr(nchw(da), ar.grad) < 1e-2
+    assert relerr(gw, wr.grad.view(-1)) < 1e-4 and relerr(gb, br.grad) < 1e-4
+
+
+def test_adam_matches_torch(C):
+    torch.manual_seed(9)
+    dev = "cuda"
+    n = 4096
+    p0 = torch.randn(n, device=dev)
+    p = p0.clone()
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    sh = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=1e-3)
+    for _ in range(5):
+        g = torch.randn(n, device=dev)
+        C.adam(p, g, m, v, sh, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, step)
+        ref.grad = g.clone()
+        opt.step()
+    assert step.item() == 5
+    assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5)
+    assert torch.equal(sh, p.to(torch.bfloat16))
