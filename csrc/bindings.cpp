@@ -15,11 +15,12 @@ int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, con
                    float*, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
 int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
-                    float*, hipStream_t);
+                    float*, float*, hipStream_t);
 int rdp_bn_eval_coef(int, const float*, const float*, const float*, const float*, float, float*, hipStream_t);
 int rdp_bn_relu_apply(const void*, int, void*, int, const float*, int, int, int, hipStream_t);
 int rdp_bn_relu_bwd_reduce(const void*, int, const void*, int, const float*, int, int, int, float*, int, hipStream_t);
-int rdp_bn_bwd_finalize(const float*, int, int, long, const float*, const float*, float*, float*, float*, hipStream_t);
+int rdp_bn_bwd_finalize(const float*, int, int, long, const float*, const float*, float*, float*, float*, float*,
+                        hipStream_t);
 int rdp_bn_relu_bwd_apply(const void*, int, const void*, int, const float*, const float*, void*, int, int, int, int,
                           hipStream_t);
 int rdp_maxpool2_fwd(const void*, int, void*, int, int, int, int, int, hipStream_t);
@@ -69,6 +70,14 @@ Act act(const torch::Tensor& t, const char* name) {
 void check_f32(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), name,
               ": must be a contiguous fp32 GPU tensor");
+}
+
+// reduction workspace for the two-stage BN finalize (>= 64 rows x K floats), or nullptr
+float* ws_ptr(const c10::optional<torch::Tensor>& ws, int K) {
+  if (!ws) return nullptr;
+  check_f32(*ws, "ws");
+  TORCH_CHECK(ws->numel() >= 64l * K, "workspace too small");
+  return ws->data_ptr<float>();
 }
 
 int conv_stats_rows(long M, int Cout, int bm_pref) {
@@ -131,7 +140,8 @@ long wgrad_slab_elems(int N, int H, int W, int Cin, int Cout, int taps, int pack
 
 void bn_finalize(torch::Tensor stats, int T, long count, torch::Tensor gamma, torch::Tensor beta,
                  c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
-                 c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor coef) {
+                 c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor coef,
+                 c10::optional<torch::Tensor> ws) {
   const int C = gamma.numel();
   check_f32(stats, "stats"); check_f32(gamma, "gamma"); check_f32(beta, "beta"); check_f32(coef, "coef");
   TORCH_CHECK(stats.numel() >= (long)T * 2 * C && coef.numel() >= 4 * C, "bn_finalize sizes");
@@ -140,7 +150,7 @@ void bn_finalize(torch::Tensor stats, int T, long count, torch::Tensor gamma, to
   if (rvar) { check_f32(*rvar, "rvar"); rv = rvar->data_ptr<float>(); }
   if (nbt) { TORCH_CHECK(nbt->scalar_type() == torch::kInt64 && nbt->is_cuda(), "nbt int64"); nb = (long long*)nbt->data_ptr(); }
   rdp_bn_finalize(stats.data_ptr<float>(), T, C, count, gamma.data_ptr<float>(), beta.data_ptr<float>(), rm, rv, nb,
-                  (float)momentum, (float)eps, coef.data_ptr<float>(), cur_stream());
+                  (float)momentum, (float)eps, coef.data_ptr<float>(), ws_ptr(ws, 2 * C), cur_stream());
 }
 
 void bn_eval_coef(torch::Tensor gamma, torch::Tensor beta, torch::Tensor rmean, torch::Tensor rvar, double eps,
@@ -171,11 +181,12 @@ int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, in
 }
 
 void bn_bwd_finalize(torch::Tensor partial, int T, long count, torch::Tensor gamma, torch::Tensor coef,
-                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor coef2) {
+                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor coef2,
+                     c10::optional<torch::Tensor> ws) {
   const int C = gamma.numel();
   rdp_bn_bwd_finalize(partial.data_ptr<float>(), T, C, count, gamma.data_ptr<float>(), coef.data_ptr<float>(),
                       dgamma ? dgamma->data_ptr<float>() : nullptr, dbeta ? dbeta->data_ptr<float>() : nullptr,
-                      coef2.data_ptr<float>(), cur_stream());
+                      coef2.data_ptr<float>(), ws_ptr(ws, 2 * C), cur_stream());
 }
 
 void bn_relu_bwd_apply(torch::Tensor da, torch::Tensor y, torch::Tensor coef, torch::Tensor coef2, torch::Tensor dy,

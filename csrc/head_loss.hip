@@ -167,14 +167,20 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
   }
 }
 
-// grad[0..63] = dW, grad_b[0] = db (sum of block partials)
+// grad[0..63] = dW, grad_b[0] = db: one block per column, 256 threads reduce the T block partials
 __global__ void head_grad_finalize_kernel(const float* __restrict__ partial, int T, float* __restrict__ gw,
                                           float* __restrict__ gbias) {
-  const int c = threadIdx.x;
-  if (c > HEAD_C) return;
-  double s = 0.0;
-  for (int t = 0; t < T; ++t) s += (double)partial[t * (HEAD_C + 1) + c];
-  if (c < HEAD_C) gw[c] = (float)s; else gbias[0] = (float)s;
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int t = threadIdx.x; t < T; t += 256) s += partial[t * (HEAD_C + 1) + c];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    if (c < HEAD_C) gw[c] = tot; else gbias[0] = tot;
+  }
 }
 
 // serving: logits -> u8 mask at the model resolution (sigmoid(x) > thr  <=>  x > logit(thr))
@@ -212,7 +218,7 @@ int rdp_head_bwd(const void* a, int apitch, const float* w, const float* logits,
   const int nb = blocks_for(M);
   hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, logits, target, sums,
                      (u16*)da, dapitch, partial, M, dice_w, dice_eps, gscale);
-  hipLaunchKernelGGL(head_grad_finalize_kernel, dim3(1), dim3(128), 0, s, partial, nb, gw, gb);
+  hipLaunchKernelGGL(head_grad_finalize_kernel, dim3(HEAD_C + 1), dim3(256), 0, s, partial, nb, gw, gb);
   return nb;
 }
 

@@ -11,6 +11,39 @@
 #include "common.h"
 #include <algorithm>
 
+// Stage-1 column reduction: in[T][K] -> out[S][K], S row-chunks reduced by S x ceil(K/64) blocks
+// (many CUs, 4 independent accumulators per thread) so the finalize kernels read <= 64 rows.
+__global__ void colsum_kernel(const float* __restrict__ in, int T, int K, int rpc, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * rpc, r1 = min(T, r0 + rpc);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < K) {
+    int r = r0 + ty;
+    for (; r + 12 < r1; r += 16) {
+      a0 += in[(size_t)r * K + col];
+      a1 += in[(size_t)(r + 4) * K + col];
+      a2 += in[(size_t)(r + 8) * K + col];
+      a3 += in[(size_t)(r + 12) * K + col];
+    }
+    for (; r < r1; r += 4) a0 += in[(size_t)r * K + col];
+  }
+  red[ty][tx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (ty == 0 && col < K) out[(size_t)blockIdx.y * K + col] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+}
+
+// reduce [T][K] rows to <= 64 rows in `ws` if needed; returns (pointer, rows)
+static const float* shrink_rows(const float* in, int T, int K, float* ws, int& rows, hipStream_t s) {
+  if (T <= 64 || ws == nullptr) { rows = T; return in; }
+  const int S = 64;
+  const int rpc = (T + S - 1) / S;
+  hipLaunchKernelGGL(colsum_kernel, dim3((K + 63) / 64, S), dim3(256), 0, s, in, T, K, rpc, ws);
+  rows = S;
+  return ws;
+}
+
 // coef layout: [0:C) mean, [C:2C) invstd, [2C:3C) scale = gamma*invstd, [3C:4C) shift = beta - mean*scale
 __global__ void bn_finalize_kernel(const float* __restrict__ stats, int T, int C, double count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -78,6 +111,11 @@ RDP_DEV uint4 pack8(const float* f) {
   v.z = pack2bf(f[4], f[5]);
   v.w = pack2bf(f[6], f[7]);
   return v;
+}
+
+RDP_DEV void ld8(const float* p, float* f) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
 // a = relu(y*scale + shift), 8 channels per thread
@@ -199,14 +237,15 @@ __global__ void bn_relu_bwd_apply_kernel(const u16* __restrict__ da, int dapitch
   for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
     const int p = it / CG, g = it - (long)p * CG;
     const int c = g * 8;
-    float fd[8], fy[8], o[8];
+    float fd[8], fy[8], o[8], ss[8], hh[8], A[8], B[8], K[8];
     unpack8(*(const uint4*)(da + (size_t)p * dapitch + c), fd);
     unpack8(*(const uint4*)(y + (size_t)p * ypitch + c), fy);
+    ld8(coef + 2 * C + c, ss); ld8(coef + 3 * C + c, hh);
+    ld8(coef2 + c, A); ld8(coef2 + C + c, B); ld8(coef2 + 2 * C + c, K);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float ss = coef[2 * C + c + k], hh = coef[3 * C + c + k];
-      const float gg = (!relu || fmaf(fy[k], ss, hh) > 0.f) ? fd[k] : 0.f;
-      o[k] = fmaf(coef2[c + k], gg, fmaf(coef2[C + c + k], fy[k], coef2[2 * C + c + k]));
+      const float gg = (!relu || fmaf(fy[k], ss[k], hh[k]) > 0.f) ? fd[k] : 0.f;
+      o[k] = fmaf(A[k], gg, fmaf(B[k], fy[k], K[k]));
     }
     *(uint4*)(dy + (size_t)p * dypitch + c) = pack8(o);
   }
@@ -220,8 +259,9 @@ static int grid_for(long items, int block = 256, int cap = 2048) {
 extern "C" {
 
 int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* gamma, const float* beta,
-                    float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef,
+                    float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef, float* ws,
                     hipStream_t s) {
+  stats = shrink_rows(stats, T, 2 * C, ws, T, s);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, stats, T, C, (double)count, gamma,
                      beta, rmean, rvar, nbt, momentum, eps, coef);
   return 0;
@@ -255,7 +295,8 @@ int rdp_bn_relu_bwd_reduce(const void* da, int dapitch, const void* y, int ypitc
 }
 
 int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const float* gamma, const float* coef,
-                        float* dgamma, float* dbeta, float* coef2, hipStream_t s) {
+                        float* dgamma, float* dbeta, float* coef2, float* ws, hipStream_t s) {
+  partial = shrink_rows(partial, T, 2 * C, ws, T, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, partial, T, C, (double)count, gamma,
                      coef, dgamma, dbeta, coef2);
   return 0;

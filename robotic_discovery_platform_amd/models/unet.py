@@ -332,6 +332,7 @@ class UNetExecutor:
         max_rows = max(C.conv_stats_rows(L.x1.shape[0] * L.x1.shape[1] * L.x1.shape[2], L.spec.cout, 0) * 2 * L.spec.cout
                        for L in self.layers)
         self.stats = torch.zeros(max_rows, dtype=torch.float32, device=dev)
+        self.red_ws = torch.zeros(64 * 2 * max(L.spec.cout for L in self.layers), dtype=torch.float32, device=dev)
         if training:
             self._alloc_backward(C)
         else:
@@ -408,7 +409,7 @@ class UNetExecutor:
         if self.training:
             M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
-                          m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef)
+                          m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
         C.bn_relu_apply(L.y, L.a, L.coef, 1)
 
     def prepare_eval(self):
@@ -458,7 +459,8 @@ class UNetExecutor:
         M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
         T = C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
         C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
-                          st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2)
+                          st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
+                          self.red_ws)
         C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
 
     def _conv_bwd(self, C, L: _Layer, hooks=None):

@@ -158,7 +158,7 @@ def test_bn_relu_train_fwd_bwd(C):
     rm, rv = torch.zeros(Ch, device=dev), torch.ones(Ch, device=dev)
     nbt = torch.zeros(1, dtype=torch.int64, device=dev)
     coef = torch.zeros(4 * Ch, device=dev)
-    C.bn_finalize(stats, 1, M, gamma, beta, rm, rv, nbt, 0.1, 1e-5, coef)
+    C.bn_finalize(stats, 1, M, gamma, beta, rm, rv, nbt, 0.1, 1e-5, coef, None)
     a = torch.empty_like(y)
     C.bn_relu_apply(y, a, coef, 1)
     bn = torch.nn.BatchNorm2d(Ch).to(dev)
@@ -174,7 +174,7 @@ def test_bn_relu_train_fwd_bwd(C):
     part = torch.zeros(1024 * 2 * Ch, device=dev)
     T = C.bn_relu_bwd_reduce(da, y, coef, 1, part)
     dg, db, coef2 = torch.zeros(Ch, device=dev), torch.zeros(Ch, device=dev), torch.zeros(3 * Ch, device=dev)
-    C.bn_bwd_finalize(part, T, M, gamma, coef, dg, db, coef2)
+    C.bn_bwd_finalize(part, T, M, gamma, coef, dg, db, coef2, torch.zeros(64 * 2 * Ch, device=dev))
     dy = torch.empty_like(y)
     C.bn_relu_bwd_apply(da, y, coef, coef2, dy, 1)
     assert relerr(nchw(dy), yin.grad) < 2e-2
