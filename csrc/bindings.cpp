@@ -81,6 +81,7 @@ float* ws_ptr(const c10::optional<torch::Tensor>& ws, int K) {
 }
 
 int conv_stats_rows(long M, int Cout, int bm_pref) {
+  bm_pref %= 1000;
   if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return (M + 127) / 128;
   return (M + 255) / 256;
 }

@@ -16,8 +16,8 @@
 // (buffer_load ... lds, 16 B/lane) in MFMA-fragment-major order: one 1 KiB wave-instruction = one
 // 16x32 MFMA operand fragment, so every ds_read_b128 is lane-contiguous (bank-conflict free).
 // Halo/zero padding comes from out-of-range buffer offsets (hardware returns 0).
-// Double-buffered LDS: tile k+1 is in flight during the MFMAs of tile k (counted vmcnt, raw
-// s_barrier so hipcc does not drain the DMA at the barrier).
+// Double-buffered LDS with ONE raw s_barrier per K step: tile k+1's DMA is issued right after the
+// barrier that retires tile k and lands under tile k's MFMAs.
 #include "common.h"
 
 struct ConvArgs {
@@ -43,7 +43,11 @@ struct ConvArgs {
   int tilesN;
 };
 
-template <int BM, int BN>
+// ROWMAJ=0: fragment-major LDS image (each DMA piece = one MFMA fragment: 16 rows x 64 B).
+// ROWMAJ=1: row-major [rows][128 B] image, 16-B chunk XOR-swizzled by (row & 7) on the SOURCE
+//           address; each DMA piece = 8 full 128-B lines (half the TA line lookups per byte), and
+//           the fragment ds_read_b128s stay bank-conflict free (checked by simulation).
+template <int BM, int BN, int ROWMAJ>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int WAVES_M = BM / 64;
   constexpr int NPR = BM / 64;        // pixel rows per lane handled by this wave's DMA
@@ -64,12 +68,14 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
   const auto rx2 = make_rsrc(a.x2 ? a.x2 : a.x1, a.x2 ? a.xbytes2 : 0u);
   const auto rw = make_rsrc(a.w, a.wbytes);
 
-  // ---- per-lane pixel rows this wave stages (subtiles wave*NPR .. wave*NPR+NPR-1) ----
-  int pm[NPR], ph[NPR], pw[NPR];
-  bool pv[NPR];
+  // ---- per-lane pixel rows this wave stages ----
+  constexpr int NROW = ROWMAJ ? BM / 32 : NPR;  // distinct pixel rows per lane
+  int pm[NROW], ph[NROW], pw[NROW];
+  bool pv[NROW];
 #pragma unroll
-  for (int r = 0; r < NPR; ++r) {
-    const int m = m0 + (wave * NPR + r) * 16 + (lane & 15);
+  for (int r = 0; r < NROW; ++r) {
+    const int row = ROWMAJ ? (wave * NROW + r) * 8 + (lane >> 3) : (wave * NPR + r) * 16 + (lane & 15);
+    const int m = m0 + row;
     pv[r] = m < a.M;
     const int mm = pv[r] ? m : 0;
     const int hw = mm % (a.H * a.W);
@@ -77,21 +83,56 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     ph[r] = hw / a.W;
     pw[r] = hw - ph[r] * a.W;
   }
-  const int qlane = lane >> 4;  // 16-B chunk (of 4) within a 32-wide K half
+  const int qlane = lane >> 4;  // 16-B chunk (of 4) within a 32-wide K half (fragment-major)
+  const int gch = (lane & 7) ^ (lane >> 3);  // row-major: global 16-B chunk fetched by this lane
 
-  // weight rows for this wave's fragments
-  uint32_t woff[FW_PER_WAVE];
+  // weight rows for this wave's DMA pieces
+  constexpr int WPIECES = ROWMAJ ? BN / 32 : FW_PER_WAVE;
+  uint32_t woff[WPIECES];
 #pragma unroll
-  for (int f = 0; f < FW_PER_WAVE; ++f) {
-    const int fw = wave * FW_PER_WAVE + f;  // fragment id in [0, BN/16*2)
-    const int j = fw >> 1, hf = fw & 1;
-    const int n = n0 + j * 16 + (lane & 15);
-    woff[f] = (uint32_t)(n * a.ldw + (qlane + 4 * hf) * 8) * 2u;
+  for (int f = 0; f < WPIECES; ++f) {
+    if (ROWMAJ) {
+      const int n = n0 + (wave * WPIECES + f) * 8 + (lane >> 3);
+      woff[f] = (uint32_t)(n * a.ldw + gch * 8) * 2u;
+    } else {
+      const int fw = wave * FW_PER_WAVE + f;  // fragment id in [0, BN/16*2)
+      const int j = fw >> 1, hf = fw & 1;
+      const int n = n0 + j * 16 + (lane & 15);
+      woff[f] = (uint32_t)(n * a.ldw + (qlane + 4 * hf) * 8) * 2u;
+    }
   }
 
   auto issue = [&](int ks, char* buf) {
     // --- pixel (im2col) operand ---
-    if (a.packed) {
+    if constexpr (ROWMAJ) {
+      if (a.packed) {
+        const int tap = ks * 8 + gch;
+        const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+#pragma unroll
+        for (int r = 0; r < NROW; ++r) {
+          const int hh = ph[r] + dr, ww = pw[r] + ds;
+          const bool ok = pv[r] && tap < 9 && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
+          dma16(rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
+        }
+      } else {
+        const int tap = ks / a.cpt;
+        const int c0 = (ks - tap * a.cpt) * 64;
+        const bool s2 = c0 >= a.C1;
+        const int ch = (s2 ? c0 - a.C1 : c0) + gch * 8;
+        const int pitch = s2 ? a.pitch2 : a.pitch1;
+        const int dr = a.taps == 9 ? tap / 3 - 1 : 0;
+        const int ds = a.taps == 9 ? tap % 3 - 1 : 0;
+#pragma unroll
+        for (int r = 0; r < NROW; ++r) {
+          const int hh = ph[r] + dr, ww = pw[r] + ds;
+          const bool ok = pv[r] && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * pitch + ch) * 2u : RDP_OOB;
+          lds_void* dst = (lds_void*)(buf + (wave * NROW + r) * 1024);
+          if (s2) dma16(rx2, dst, off); else dma16(rx1, dst, off);
+        }
+      }
+    } else if (a.packed) {
 #pragma unroll
       for (int r = 0; r < NPR; ++r) {
 #pragma unroll
@@ -128,11 +169,18 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     // --- weight operand ---
     char* wbuf = buf + P_BYTES;
 #pragma unroll
-    for (int f = 0; f < FW_PER_WAVE; ++f) {
-      const int fw = wave * FW_PER_WAVE + f;
+    for (int f = 0; f < WPIECES; ++f) {
+      const int fw = wave * WPIECES + f;
       dma16(rw, (lds_void*)(wbuf + fw * 1024), woff[f] + (uint32_t)ks * 128u);
     }
   };
+
+  // LDS byte offsets of this lane's fragment reads (k-half hf) relative to subtile 0
+  int rdoff[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+    rdoff[hf] = ROWMAJ ? (lane & 15) * 128 + 16 * (((lane >> 4) + 4 * hf) ^ (lane & 7)) : hf * 1024 + lane * 16;
+  constexpr int SUBSTRIDE = 2048;  // bytes per 16-row subtile (both layouts)
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -140,37 +188,30 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // One barrier per K step: the barrier retires this stage's DMA (every wave waited vmcnt(0)) and
+  // every wave's LDS reads of the previous stage (lgkmcnt(0)), so the next stage can be issued into
+  // the other buffer right after it and lands under this stage's MFMAs.
   issue(0, smem);
   for (int ks = 0; ks < a.nks; ++ks) {
-    char* cur = smem + (ks & 1) * BUF;
-    if (ks + 1 < a.nks) {
-      issue(ks + 1, smem + ((ks + 1) & 1) * BUF);
-      // this wave's DMA for stage ks has landed; stage ks+1 (NPR*2 + FW_PER_WAVE ops) stays in flight
-      if constexpr (NPR * 2 + FW_PER_WAVE == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if constexpr (NPR * 2 + FW_PER_WAVE == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      else if constexpr (NPR * 2 + FW_PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else wait_vm0();
-    } else {
-      wait_vm0();
-    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    const char* pb = cur;
-    const char* wb = cur + P_BYTES;
+    if (ks + 1 < a.nks) issue(ks + 1, smem + ((ks + 1) & 1) * BUF);
+    const char* pb = smem + (ks & 1) * BUF;
+    const char* wb = pb + P_BYTES;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fa[j] = *(const bf16x8*)(wb + ((wn * 4 + j) * 2 + hf) * 1024 + lane * 16);
+      for (int j = 0; j < 4; ++j) fa[j] = *(const bf16x8*)(wb + (wn * 4 + j) * SUBSTRIDE + rdoff[hf]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fb[i] = *(const bf16x8*)(pb + ((wm * 4 + i) * 2 + hf) * 1024 + lane * 16);
+      for (int i = 0; i < 4; ++i) fb[i] = *(const bf16x8*)(pb + (wm * 4 + i) * SUBSTRIDE + rdoff[hf]);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
-    wait_lgkm0();
-    raw_barrier();
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   // ---- epilogue: acc[j][i][r] = out[m = m0 + wm*64 + 16i + (lane&15)][n = n0 + wn*64 + 16j + 4*(lane>>4) + r]
   const auto ry1 = make_rsrc(a.y1, a.ybytes1);
@@ -241,10 +282,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 }
 
 template <int BM, int BN>
-static int launch_cfg(ConvArgs a, hipStream_t s) {
+static int launch_cfg(ConvArgs a, int variant, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(tilesM * a.tilesN), dim3(256), 0, s, a);
+  if (variant == 1)
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0>), dim3(tilesM * a.tilesN), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1>), dim3(tilesM * a.tilesN), dim3(256), 0, s, a);
   return tilesM;
 }
 
@@ -273,6 +317,9 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   }
   if (Cout % 64 || Cy1 % 4) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || ybytes1 >= (1l << 31) || ybytes2 >= (1l << 31)) return -1;
-  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, s);
-  return launch_cfg<256, 64>(a, s);
+  // bm_pref: 0 = auto, 128 / 256 = force tile; +1000 * variant selects the LDS layout (A/B tests)
+  const int variant = bm_pref / 1000;
+  bm_pref %= 1000;
+  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, variant, s);
+  return launch_cfg<256, 64>(a, variant, s);
 }

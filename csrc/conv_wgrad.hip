@@ -130,16 +130,13 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
   // transposed-read lane geometry: lane = 16g + 4q + pp
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tpp = lane & 3;
 
+  // one barrier per K step (see conv_igemm.hip)
   if (nks > 0) issue(0, smem);
   for (int ks = 0; ks < nks; ++ks) {
-    char* cur = smem + (ks & 1) * BUF;
-    if (ks + 1 < nks) {
-      issue(ks + 1, smem + ((ks + 1) & 1) * BUF);
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    } else {
-      wait_vm0();
-    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     raw_barrier();
+    if (ks + 1 < nks) issue(ks + 1, smem + ((ks + 1) & 1) * BUF);
+    const char* cur = smem + (ks & 1) * BUF;
     const char* xb = cur + wave * SUB;
     const char* db = cur + 4 * SUB;
 #pragma unroll
@@ -165,8 +162,6 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    wait_lgkm0();
-    raw_barrier();
   }
 
   // acc[i][j][r]: col = tc*256 + wave*64 + 16i + 4*(lane>>4) + r ; cout = cout0 + 16j + (lane&15)

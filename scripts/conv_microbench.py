@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""A/B microbenchmark of conv kernel variants on the U-Net's layer shapes (one process, interleaved).
+
+usage: python scripts/conv_microbench.py [--batch 32] [--variants 0,1] [--reps 10] [--wgrad]
+Prints TF/s per (layer, variant): median over interleaved rounds (cdna_hip_programming.md §5.4 r24).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from robotic_discovery_platform_amd.ops import native  # noqa: E402
+
+SHAPES = [  # (H, Cin1, Cin2, Cout)   spatial = H x H
+    (256, 64, 0, 64), (128, 64, 0, 128), (128, 128, 0, 128), (64, 256, 0, 256), (32, 512, 0, 512),
+    (16, 512, 0, 512), (32, 512, 512, 256), (64, 256, 256, 128), (128, 128, 128, 64), (256, 64, 64, 64),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--wgrad", action="store_true")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    C = native()
+    dev = torch.device("cuda")
+    variants = [int(v) for v in a.variants.split(",")]
+    results = []
+    for (H, C1, C2, Co) in SHAPES:
+        N = a.batch
+        x1 = torch.randn(N, H, H, C1, device=dev).to(torch.bfloat16)
+        x2 = torch.randn(N, H, H, C2, device=dev).to(torch.bfloat16) if C2 else None
+        Cin = C1 + C2
+        w = (torch.randn(Co, 9 * Cin, device=dev) * 0.02).to(torch.bfloat16)
+        y = torch.empty(N, H, H, Co, dtype=torch.bfloat16, device=dev)
+        stats = torch.zeros(C.conv_stats_rows(N * H * H, Co, 0) * 2 * Co, device=dev)
+        flops = 2.0 * N * H * H * 9 * Cin * Co
+        times = {v: [] for v in variants}
+        if a.wgrad:
+            dy = torch.randn(N, H, H, Co, device=dev).to(torch.bfloat16)
+            tiles = ((9 * Cin + 255) // 256) * (Co // 64)
+            splits = max(1, min((1024 + tiles - 1) // tiles, N * H * H // 2048))
+            slab = torch.zeros(C.wgrad_slab_elems(N, H, H, Cin, Co, 9, 0, splits), device=dev)
+            out = torch.zeros(Co * 9 * Cin, device=dev)
+
+        def run(v):
+            if a.wgrad:
+                C.conv_wgrad(x1, x2, dy, 9, 0, 1000 * v, slab, out, 0, splits)
+            else:
+                C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, 1000 * v)
+
+        for v in variants:
+            run(v)
+        torch.cuda.synchronize()
+        for _ in range(a.rounds):
+            for v in variants:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    run(v)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / a.reps)
+        row = {"shape": f"{N}x{H}x{H} {C1}+{C2}->{Co}", "kind": "wgrad" if a.wgrad else "fwd"}
+        for v in variants:
+            med = statistics.median(times[v])
+            row[f"v{v}_us"] = round(med * 1e3, 1)
+            row[f"v{v}_tflops"] = round(flops / (med * 1e-3) / 1e12, 1)
+        results.append(row)
+        print(json.dumps(row), flush=True)
+    if a.out:
+        json.dump(results, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
