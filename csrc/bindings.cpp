@@ -12,7 +12,7 @@ extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, hipStream_t);
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
-                   float*, int, int, int, int, int, int, int, int, int, hipStream_t);
+                   float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
 int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
                     float*, float*, hipStream_t);
@@ -118,7 +118,7 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
 
 
 int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor dy, int taps, int packed, int cin_real,
-               torch::Tensor slab, torch::Tensor out, int accumulate, int splits) {
+               torch::Tensor slab, torch::Tensor out, int accumulate, int splits, int variant) {
   Act a1 = act(x1, "x1"), a2;
   if (x2) a2 = act(*x2, "x2");
   Act d = act(dy, "dy");
@@ -130,7 +130,7 @@ int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor 
   const int r = rdp_conv_wgrad(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
                                a1.pitch, x2 ? a2.pitch : 0, d.ptr, d.bytes, d.pitch, slab.data_ptr<float>(),
                                slab.numel(), out.data_ptr<float>(), accumulate, a1.N, a1.H, a1.W, d.C, taps, packed,
-                               cin_real, splits, cur_stream());
+                               cin_real, splits, variant, cur_stream());
   TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
   return r;
 }

@@ -91,6 +91,9 @@ RDP_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (__umulhi(n, f.m) + n) >> f.s;
 }
 
+// branch-free 0 <= v < n (no short-circuit control flow around LDS-DMA issue)
+RDP_DEV bool inb(int v, int n) { return (unsigned)v < (unsigned)n; }
+
 RDP_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

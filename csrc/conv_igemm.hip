@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < NROW; ++r) {
           const int hh = ph[r] + dr, ww = pw[r] + ds;
-          const bool ok = pv[r] && tap < 9 && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const bool ok = pv[r] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
           const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
           dma16(rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
         }
@@ -126,10 +126,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < NROW; ++r) {
           const int hh = ph[r] + dr, ww = pw[r] + ds;
-          const bool ok = pv[r] && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const bool ok = pv[r] & inb(hh, a.H) & inb(ww, a.W);
           const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * pitch + ch) * 2u : RDP_OOB;
-          lds_void* dst = (lds_void*)(buf + (wave * NROW + r) * 1024);
-          if (s2) dma16(rx2, dst, off); else dma16(rx1, dst, off);
+          dma16(s2 ? rx2 : rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
         }
       }
     } else if (a.packed) {
@@ -140,7 +139,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
           const int tap = ks * 8 + qlane + 4 * hf;
           const int dr = tap / 3 - 1, ds = tap % 3 - 1;
           const int hh = ph[r] + dr, ww = pw[r] + ds;
-          const bool ok = pv[r] && tap < 9 && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const bool ok = pv[r] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
           const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
           dma16(rx1, (lds_void*)(buf + ((wave * NPR + r) * 2 + hf) * 1024), off);
         }
@@ -156,13 +155,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < NPR; ++r) {
         const int hh = ph[r] + dr, ww = pw[r] + ds;
-        const bool ok = pv[r] && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+        const bool ok = pv[r] & inb(hh, a.H) & inb(ww, a.W);
         const uint32_t base = (uint32_t)((pm[r] + dr * a.W + ds) * pitch + ch + qlane * 8) * 2u;
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           const uint32_t off = ok ? base + hf * 64u : RDP_OOB;
-          lds_void* dst = (lds_void*)(buf + ((wave * NPR + r) * 2 + hf) * 1024);
-          if (s2) dma16(rx2, dst, off); else dma16(rx1, dst, off);
+          dma16(s2 ? rx2 : rx1, (lds_void*)(buf + ((wave * NPR + r) * 2 + hf) * 1024), off);
         }
       }
     }

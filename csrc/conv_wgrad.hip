@@ -37,6 +37,7 @@ RDP_DEV int swz(int p) { return (((p >> 1) & 1) << 1) | (((p >> 3) & 1) << 2); }
 
 RDP_DEV uint32_t fdiv2(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
+template <bool PACKED, bool TILE_FAST>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int SUB = 8192;             // one [64][64] bf16 tile
   constexpr int BUF = 5 * SUB;          // 4 x-subtiles + 1 dy tile
@@ -47,9 +48,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
 
   const uint32_t nwg = gridDim.x;
   const uint32_t lid = xcd_remap(blockIdx.x, nwg);
-  // split fastest so one XCD keeps the same weight tile's pixel ranges together
-  const int split = lid % a.splits;
-  const int tile = lid / a.splits;
+  // TILE_FAST: consecutive logical ids (same XCD after the remap) = different weight tiles of the
+  // SAME pixel range, so they share the dY / X lines in that XCD's L2.
+  const int ntiles = a.colTiles * a.coutTiles;
+  const int split = TILE_FAST ? lid / ntiles : lid % a.splits;
+  const int tile = TILE_FAST ? lid % ntiles : lid / a.splits;
   const int tc = tile % a.colTiles, tn = tile / a.colTiles;
   const int cout0 = tn * 64;
   const int pbeg = split * a.pix_per_split;
@@ -66,7 +69,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
   for (int sub = 0; sub < 4; ++sub) {
     const int kc = tc * 256 + sub * 64;
     s_ok[sub] = kc < a.ncols;
-    if (a.packed) {
+    if (PACKED) {
       s_dr[sub] = 0; s_ds[sub] = 0; s_ch[sub] = kc / 8; s_src[sub] = 0;  // s_ch = first tap
     } else {
       const int tap = kc / a.Cin;
@@ -100,22 +103,21 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub) {
         int dr = s_dr[sub], ds = s_ds[sub], ch;
-        if (a.packed) {
+        if constexpr (PACKED) {
           const int tap = s_ch[sub] + g;
           dr = tap / 3 - 1; ds = tap % 3 - 1;
           ch = 0;
           const int hh = h + dr, ww = w + ds;
-          const bool ok = mv && s_ok[sub] && tap < 9 && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const bool ok = mv & (bool)s_ok[sub] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
           const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
           dma16(rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
         } else {
           ch = s_ch[sub] + g * 8;
           const int hh = h + dr, ww = w + ds;
-          const bool ok = mv && s_ok[sub] && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          const bool ok = mv & (bool)s_ok[sub] & inb(hh, a.H) & inb(ww, a.W);
           const int pitch = s_src[sub] ? a.pitch2 : a.pitch1;
           const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * pitch + ch) * 2u : RDP_OOB;
-          lds_void* dst = (lds_void*)(buf + sub * SUB + s * 1024);
-          if (s_src[sub]) dma16(rx2, dst, off); else dma16(rx1, dst, off);
+          dma16(s_src[sub] ? rx2 : rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
         }
       }
     }
@@ -142,20 +144,20 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       bf16x8 fa[4], fb[4];
+      const int p0 = 32 * hf + 8 * tg + tq;
+      const int sw0 = swz(p0), sw1 = swz(p0 + 4);
+      const int ro0 = p0 * 128 + 8 * (tpp & 1), ro1 = ro0 + 4 * 128;
 #pragma unroll
-      for (int rd = 0; rd < 2; ++rd) {
-        const int p = 32 * hf + 8 * tg + tq + 4 * rd;
-        const int rowoff = p * 128 + 8 * (tpp & 1);
-        const int sw = swz(p);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = 2 * i + (tpp >> 1);
-          const int off = rowoff + 16 * (c ^ sw);
-          bf16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(xb + off));
-          bf16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(db + off));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { fa[i][rd * 4 + e] = va[e]; fb[i][rd * 4 + e] = vb[e]; }
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int c = 2 * i + (tpp >> 1);
+        const int o0 = ro0 + 16 * (c ^ sw0), o1 = ro1 + 16 * (c ^ sw1);
+        typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+        const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + o0));
+        const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + o1));
+        const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + o0));
+        const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + o1));
+        fa[i] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -202,7 +204,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
 extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
                               int pitch2, const void* dy, long dybytes, int dypitch, float* slab, long slab_elems,
                               float* out, int accumulate, int N, int H, int W, int Cout, int taps, int packed,
-                              int cin_real, int splits, hipStream_t s) {
+                              int cin_real, int splits, int variant, hipStream_t s) {
   WgradArgs a;
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
   a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
@@ -232,7 +234,13 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
   a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
   const int nblk = a.colTiles * a.coutTiles * a.splits;
-  hipLaunchKernelGGL(conv_wgrad_kernel, dim3(nblk), dim3(256), 0, s, a);
+  if (packed) {
+    hipLaunchKernelGGL((conv_wgrad_kernel<true, true>), dim3(nblk), dim3(256), 0, s, a);
+  } else if (variant == 1) {
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, false>), dim3(nblk), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true>), dim3(nblk), dim3(256), 0, s, a);
+  }
   const int creal = packed ? cin_real : a.Cin;
   const long total = (long)Cout * taps * creal;
   const int rb = (int)std::min<long>((total + 255) / 256, 4096);

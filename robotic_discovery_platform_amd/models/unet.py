@@ -468,7 +468,7 @@ class UNetExecutor:
         st = self.m.store
         self._bn_bwd(C, L)
         gw = st.flat_slice(sp.name + ".weight", st.grad)
-        C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw, 0, L.splits)
+        C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw, 0, L.splits, 0)
         if L.dx1 is not None:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0)
         if hooks is not None:

@@ -125,7 +125,7 @@ def test_conv_wgrad(C, N, H, W, C1, C2, Cout, splits):
     F.conv2d(xin, w, padding=1).backward(nchw(dy).float())
     slab = torch.zeros(C.wgrad_slab_elems(N, H, W, C1 + C2, Cout, 9, 0, splits), device=dev)
     out = torch.zeros(Cout * 9 * (C1 + C2), device=dev)
-    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits)
+    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, 0)
     ref = w.grad.permute(0, 2, 3, 1).reshape(-1)
     assert relerr(out, ref) < 2e-3
 
@@ -142,7 +142,7 @@ def test_conv_wgrad_packed(C):
     F.conv2d(nchw(x).float(), w, padding=1).backward(nchw(dy).float())
     slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 8, Cout, 9, 1, 5), device=dev)
     out = torch.zeros(Cout * 27, device=dev)
-    C.conv_wgrad(x8, None, dy, 9, 1, 3, slab, out, 0, 5)
+    C.conv_wgrad(x8, None, dy, 9, 1, 3, slab, out, 0, 5, 0)
     assert relerr(out, w.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
 
 
