@@ -80,10 +80,11 @@ float* ws_ptr(const c10::optional<torch::Tensor>& ws, int K) {
   return ws->data_ptr<float>();
 }
 
+// stats slab rows written by conv_fwd: one per (M tile, wave row)
 int conv_stats_rows(long M, int Cout, int bm_pref) {
   bm_pref %= 1000;
-  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return (M + 127) / 128;
-  return (M + 255) / 256;
+  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return (M + 127) / 128 * 2;
+  return (M + 255) / 256 * 4;
 }
 
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)

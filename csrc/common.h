@@ -94,6 +94,20 @@ RDP_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) {
 // branch-free 0 <= v < n (no short-circuit control flow around LDS-DMA issue)
 RDP_DEV bool inb(int v, int n) { return (unsigned)v < (unsigned)n; }
 
+// Sum over each 16-lane DPP row with 4 VALU DPP ops (no LDS): quad xor1, quad xor2,
+// row_half_mirror (8-lane), row_mirror (16-lane). Every lane of the row receives the row sum.
+template <int CTRL>
+RDP_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+RDP_DEV float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
 RDP_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

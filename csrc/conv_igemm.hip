@@ -9,15 +9,20 @@
 //     segmentation_model.py:75) so the concat is never materialised.
 //   * Output may be split at channel Cy1 into two destinations (dgrad of the concat input).
 //   * Epilogue optionally emits per-channel (sum, sumsq) partials of the bf16-rounded output for
-//     training-mode BatchNorm (one slab row per M tile, reduced by bn_finalize).
+//     training-mode BatchNorm: one slab row per (M tile, wave row), reduced by bn_finalize.
 //
 // Tiling: block = 4 waves (256 threads), block tile BM x BN with each wave owning 64x64; K step
 // = 64 channels of one tap. Both operand tiles are staged global->LDS by LDS-DMA
-// (buffer_load ... lds, 16 B/lane) in MFMA-fragment-major order: one 1 KiB wave-instruction = one
-// 16x32 MFMA operand fragment, so every ds_read_b128 is lane-contiguous (bank-conflict free).
+// (buffer_load ... lds, 16 B/lane) as a row-major [rows][128 B] image: one wave-instruction moves
+// 8 full 128-B lines, with the 16-B chunk XOR-swizzled by (row & 7) on the SOURCE address so the
+// MFMA-fragment ds_read_b128s are bank-conflict free. (A fragment-shaped image -- 16 rows x 64 B
+// per instruction -- doubles the TA line lookups and ran 1.4-1.6x slower on deep layers.)
 // Halo/zero padding comes from out-of-range buffer offsets (hardware returns 0).
-// Double-buffered LDS with ONE raw s_barrier per K step: tile k+1's DMA is issued right after the
-// barrier that retires tile k and lands under tile k's MFMAs.
+//
+// Persistent: each block walks several output tiles with ONE continuous double-buffered K
+// pipeline (one raw s_barrier per K step), so tile t+1's first DMA lands under tile t's last
+// MFMAs and epilogue. This removes the per-tile prologue that dominated the small-K (K = 576)
+// 64-channel layers. The epilogue uses no LDS and no block barrier.
 #include "common.h"
 
 struct ConvArgs {
@@ -34,151 +39,117 @@ struct ConvArgs {
   uint32_t ybytes1, ybytes2;
   int Cy1;  // channels going to y1 (rest to y2)
   int ypitch1, ypitch2;
-  float* stats;  // [tilesM][2][Cout] partial (sum, sumsq) or nullptr
+  float* stats;  // [tilesM * WAVES_M][2][Cout] partial (sum, sumsq) or nullptr
   int N, H, W, Cout, M;
   int taps;  // 9 (3x3) or 1 (1x1)
   int packed;  // 1: Cin == 8, K packs 8 taps per 64-wide K step
-  int nks;  // number of K steps
+  int nks;  // number of K steps per tile
   int cpt;  // 64-channel chunks per tap (generic mode)
-  int tilesN;
+  int tilesN, ntiles;
+  uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
 };
 
-// ROWMAJ=0: fragment-major LDS image (each DMA piece = one MFMA fragment: 16 rows x 64 B).
-// ROWMAJ=1: row-major [rows][128 B] image, 16-B chunk XOR-swizzled by (row & 7) on the SOURCE
-//           address; each DMA piece = 8 full 128-B lines (half the TA line lookups per byte), and
-//           the fragment ds_read_b128s stay bank-conflict free (checked by simulation).
-template <int BM, int BN, int ROWMAJ>
+// tap (0..8) -> (dr, ds) without division: dr + 1 = (tap * 11) >> 5
+RDP_DEV int tap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
+RDP_DEV int tap_ds(int tap) { return tap - 3 * ((tap * 11) >> 5) - 1; }
+
+template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int WAVES_M = BM / 64;
-  constexpr int NPR = BM / 64;        // pixel rows per lane handled by this wave's DMA
-  constexpr int FW_PER_WAVE = BN / 32;  // weight fragments DMA'd per wave per K step
   constexpr int P_BYTES = BM * 128, W_BYTES = BN * 128, BUF = P_BYTES + W_BYTES;
+  constexpr int NROW = BM / 32;     // pixel rows (DMA pieces) per lane per K step
+  constexpr int WPIECES = BN / 32;  // weight rows (DMA pieces) per lane per K step
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int gch = (lane & 7) ^ (lane >> 3);  // global 16-B chunk this lane fetches (row-major image)
 
-  const uint32_t nwg = gridDim.x;
-  const uint32_t lid = xcd_remap(blockIdx.x, nwg);
-  const int tm = lid / a.tilesN, tn = lid % a.tilesN;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const uint32_t G = gridDim.x;
+  const uint32_t lid = xcd_remap(blockIdx.x, G);
+  const int my_tiles = lid < (uint32_t)a.ntiles ? (a.ntiles - 1 - (int)lid) / (int)G + 1 : 0;
+  const int total = my_tiles * a.nks;
 
   const auto rx1 = make_rsrc(a.x1, a.xbytes1);
   const auto rx2 = make_rsrc(a.x2 ? a.x2 : a.x1, a.x2 ? a.xbytes2 : 0u);
   const auto rw = make_rsrc(a.w, a.wbytes);
 
-  // ---- per-lane pixel rows this wave stages ----
-  constexpr int NROW = ROWMAJ ? BM / 32 : NPR;  // distinct pixel rows per lane
-  int pm[NROW], ph[NROW], pw[NROW];
-  bool pv[NROW];
-#pragma unroll
-  for (int r = 0; r < NROW; ++r) {
-    const int row = ROWMAJ ? (wave * NROW + r) * 8 + (lane >> 3) : (wave * NPR + r) * 16 + (lane & 15);
-    const int m = m0 + row;
-    pv[r] = m < a.M;
-    const int mm = pv[r] ? m : 0;
-    const int hw = mm % (a.H * a.W);
-    pm[r] = mm;
-    ph[r] = hw / a.W;
-    pw[r] = hw - ph[r] * a.W;
-  }
-  const int qlane = lane >> 4;  // 16-B chunk (of 4) within a 32-wide K half (fragment-major)
-  const int gch = (lane & 7) ^ (lane >> 3);  // row-major: global 16-B chunk fetched by this lane
-
-  // weight rows for this wave's DMA pieces
-  constexpr int WPIECES = ROWMAJ ? BN / 32 : FW_PER_WAVE;
+  // ---- DMA-side state of the tile currently being staged ----
+  // per pixel row: linear pixel index and a 9-bit mask of the taps whose source pixel is in the
+  // image (bit t set <=> row valid and (h+dr, w+ds) in bounds), computed once per tile.
+  int pm[NROW];
+  uint32_t tmask[NROW];
   uint32_t woff[WPIECES];
+  auto set_tile = [&](int t) {
+    const int tile = (int)lid + t * (int)G;
+    const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
 #pragma unroll
-  for (int f = 0; f < WPIECES; ++f) {
-    if (ROWMAJ) {
-      const int n = n0 + (wave * WPIECES + f) * 8 + (lane >> 3);
-      woff[f] = (uint32_t)(n * a.ldw + gch * 8) * 2u;
-    } else {
-      const int fw = wave * FW_PER_WAVE + f;  // fragment id in [0, BN/16*2)
-      const int j = fw >> 1, hf = fw & 1;
-      const int n = n0 + j * 16 + (lane & 15);
-      woff[f] = (uint32_t)(n * a.ldw + (qlane + 4 * hf) * 8) * 2u;
+    for (int r = 0; r < NROW; ++r) {
+      const int m = tm * BM + (wave * NROW + r) * 8 + (lane >> 3);
+      const bool valid = m < a.M;
+      const uint32_t mm = valid ? (uint32_t)m : 0u;
+      const uint32_t hw = mm - ((__umulhi(mm, a.fhw_m) + mm) >> a.fhw_s) * (uint32_t)(a.H * a.W);
+      const uint32_t h = (__umulhi(hw, a.fw_m) + hw) >> a.fw_s;
+      const uint32_t w = hw - h * (uint32_t)a.W;
+      // rows allowed: dr=-1 needs h>0, dr=+1 needs h<H-1; same for columns
+      const uint32_t rok = (h > 0 ? 1u : 0u) | 2u | (h + 1 < (uint32_t)a.H ? 4u : 0u);
+      const uint32_t cok = (w > 0 ? 1u : 0u) | 2u | (w + 1 < (uint32_t)a.W ? 4u : 0u);
+      // tap = 3*(dr+1) + (ds+1): mask = rows (x) cols outer product
+      uint32_t msk = 0;
+      msk |= (rok & 1u) ? cok : 0u;
+      msk |= (rok & 2u) ? (cok << 3) : 0u;
+      msk |= (rok & 4u) ? (cok << 6) : 0u;
+      if (a.taps == 1) msk = 1u;
+      tmask[r] = valid ? msk : 0u;
+      pm[r] = (int)mm;
     }
-  }
-
-  auto issue = [&](int ks, char* buf) {
-    // --- pixel (im2col) operand ---
-    if constexpr (ROWMAJ) {
-      if (a.packed) {
-        const int tap = ks * 8 + gch;
-        const int dr = tap / 3 - 1, ds = tap % 3 - 1;
-#pragma unroll
-        for (int r = 0; r < NROW; ++r) {
-          const int hh = ph[r] + dr, ww = pw[r] + ds;
-          const bool ok = pv[r] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
-          const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
-          dma16(rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
-        }
-      } else {
-        const int tap = ks / a.cpt;
-        const int c0 = (ks - tap * a.cpt) * 64;
-        const bool s2 = c0 >= a.C1;
-        const int ch = (s2 ? c0 - a.C1 : c0) + gch * 8;
-        const int pitch = s2 ? a.pitch2 : a.pitch1;
-        const int dr = a.taps == 9 ? tap / 3 - 1 : 0;
-        const int ds = a.taps == 9 ? tap % 3 - 1 : 0;
-#pragma unroll
-        for (int r = 0; r < NROW; ++r) {
-          const int hh = ph[r] + dr, ww = pw[r] + ds;
-          const bool ok = pv[r] & inb(hh, a.H) & inb(ww, a.W);
-          const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * pitch + ch) * 2u : RDP_OOB;
-          dma16(s2 ? rx2 : rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
-        }
-      }
-    } else if (a.packed) {
-#pragma unroll
-      for (int r = 0; r < NPR; ++r) {
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const int tap = ks * 8 + qlane + 4 * hf;
-          const int dr = tap / 3 - 1, ds = tap % 3 - 1;
-          const int hh = ph[r] + dr, ww = pw[r] + ds;
-          const bool ok = pv[r] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
-          const uint32_t off = ok ? (uint32_t)((pm[r] + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
-          dma16(rx1, (lds_void*)(buf + ((wave * NPR + r) * 2 + hf) * 1024), off);
-        }
-      }
-    } else {
-      const int tap = ks / a.cpt;
-      const int c0 = (ks - tap * a.cpt) * 64;
-      const bool s2 = c0 >= a.C1;
-      const int ch = s2 ? c0 - a.C1 : c0;
-      const int pitch = s2 ? a.pitch2 : a.pitch1;
-      const int dr = a.taps == 9 ? tap / 3 - 1 : 0;
-      const int ds = a.taps == 9 ? tap % 3 - 1 : 0;
-#pragma unroll
-      for (int r = 0; r < NPR; ++r) {
-        const int hh = ph[r] + dr, ww = pw[r] + ds;
-        const bool ok = pv[r] & inb(hh, a.H) & inb(ww, a.W);
-        const uint32_t base = (uint32_t)((pm[r] + dr * a.W + ds) * pitch + ch + qlane * 8) * 2u;
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const uint32_t off = ok ? base + hf * 64u : RDP_OOB;
-          dma16(s2 ? rx2 : rx1, (lds_void*)(buf + ((wave * NPR + r) * 2 + hf) * 1024), off);
-        }
-      }
-    }
-    // --- weight operand ---
-    char* wbuf = buf + P_BYTES;
 #pragma unroll
     for (int f = 0; f < WPIECES; ++f) {
-      const int fw = wave * WPIECES + f;
-      dma16(rw, (lds_void*)(wbuf + fw * 1024), woff[f] + (uint32_t)ks * 128u);
+      const int n = tn * BN + (wave * WPIECES + f) * 8 + (lane >> 3);
+      woff[f] = (uint32_t)(n * a.ldw + gch * 8) * 2u;
     }
   };
 
-  // LDS byte offsets of this lane's fragment reads (k-half hf) relative to subtile 0
+  int itap = 0, icc = 0;  // (tap, 64-channel chunk) of the stage being issued (generic mode)
+  auto issue = [&](int ks, char* buf) {
+    if (a.packed) {
+      const int tap = ks * 8 + gch;  // per lane; taps >= 9 have no mask bit -> zeros
+      const int toff = (tap_dr(tap) * a.W + tap_ds(tap)) * a.pitch1;
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        const bool ok = (tmask[r] >> tap) & 1u;
+        const uint32_t off = ok ? (uint32_t)(pm[r] * a.pitch1 + toff) * 2u : RDP_OOB;
+        dma16(rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
+      }
+    } else {
+      const int c0 = icc * 64;
+      const bool s2 = c0 >= a.C1;
+      const int pitch = s2 ? a.pitch2 : a.pitch1;
+      const int tap_lin = a.taps == 9 ? tap_dr(itap) * a.W + tap_ds(itap) : 0;
+      const int soff = tap_lin * pitch + (s2 ? c0 - a.C1 : c0) + gch * 8;  // uniform except gch
+      const int bit = a.taps == 9 ? itap : 0;
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        const bool ok = (tmask[r] >> bit) & 1u;
+        const uint32_t off = ok ? (uint32_t)(pm[r] * pitch + soff) * 2u : RDP_OOB;
+        dma16(s2 ? rx2 : rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
+      }
+      if (++icc == a.cpt) { icc = 0; ++itap; if (itap == a.taps) itap = 0; }
+    }
+    char* wbuf = buf + P_BYTES;
+#pragma unroll
+    for (int f = 0; f < WPIECES; ++f)
+      dma16(rw, (lds_void*)(wbuf + (wave * WPIECES + f) * 1024), woff[f] + (uint32_t)ks * 128u);
+  };
+
+  // LDS byte offsets of this lane's fragment reads (k-half hf) relative to a 16-row subtile
   int rdoff[2];
 #pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-    rdoff[hf] = ROWMAJ ? (lane & 15) * 128 + 16 * (((lane >> 4) + 4 * hf) ^ (lane & 7)) : hf * 1024 + lane * 16;
-  constexpr int SUBSTRIDE = 2048;  // bytes per 16-row subtile (both layouts)
+  for (int hf = 0; hf < 2; ++hf) rdoff[hf] = (lane & 15) * 128 + 16 * (((lane >> 4) + 4 * hf) ^ (lane & 7));
+
+  const auto ry1 = make_rsrc(a.y1, a.ybytes1);
+  const auto ry2 = make_rsrc(a.y2 ? a.y2 : a.y1, a.y2 ? a.ybytes2 : 0u);
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -186,111 +157,102 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // One barrier per K step: the barrier retires this stage's DMA (every wave waited vmcnt(0)) and
-  // every wave's LDS reads of the previous stage (lgkmcnt(0)), so the next stage can be issued into
-  // the other buffer right after it and lands under this stage's MFMAs.
-  issue(0, smem);
-  for (int ks = 0; ks < a.nks; ++ks) {
+  if (total > 0) {
+    set_tile(0);
+    issue(0, smem);
+  }
+  int ks = 0, t = 0;    // compute position (K step within tile, tile index)
+  int iks = 0, it = 0;  // issue position of the stage in flight
+  for (int g = 0; g < total; ++g) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (ks + 1 < a.nks) issue(ks + 1, smem + ((ks + 1) & 1) * BUF);
-    const char* pb = smem + (ks & 1) * BUF;
+    if (g + 1 < total) {
+      if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
+      issue(iks, smem + ((g + 1) & 1) * BUF);
+    }
+    const char* pb = smem + (g & 1) * BUF;
     const char* wb = pb + P_BYTES;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fa[j] = *(const bf16x8*)(wb + (wn * 4 + j) * SUBSTRIDE + rdoff[hf]);
+      for (int j = 0; j < 4; ++j) fa[j] = *(const bf16x8*)(wb + (wn * 4 + j) * 2048 + rdoff[hf]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fb[i] = *(const bf16x8*)(pb + (wm * 4 + i) * SUBSTRIDE + rdoff[hf]);
+      for (int i = 0; i < 4; ++i) fb[i] = *(const bf16x8*)(pb + (wm * 4 + i) * 2048 + rdoff[hf]);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (++ks < a.nks) continue;
 
-  // ---- epilogue: acc[j][i][r] = out[m = m0 + wm*64 + 16i + (lane&15)][n = n0 + wn*64 + 16j + 4*(lane>>4) + r]
-  const auto ry1 = make_rsrc(a.y1, a.ybytes1);
-  const auto ry2 = make_rsrc(a.y2 ? a.y2 : a.y1, a.y2 ? a.ybytes2 : 0u);
-  float s1[4][4], s2[4][4];
+    // ---- epilogue of tile t: acc[j][i][r] = out[m = m0 + wm*64 + 16i + (lane&15)][n = n0 + wn*64 + 16j + 4*(lane>>4) + r]
+    ks = 0;
+    const int tile = (int)lid + t * (int)G;
+    ++t;
+    const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    float s1[4][4], s2[4][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-    const bool d2 = n >= a.Cy1;
-    const int nn = d2 ? n - a.Cy1 : n;
-    const int yp = d2 ? a.ypitch2 : a.ypitch1;
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      const bool d2 = n >= a.Cy1;
+      const int nn = d2 ? n - a.Cy1 : n;
+      const int yp = d2 ? a.ypitch2 : a.ypitch1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-      uint2 v;
-      v.x = pack2bf(acc[j][i][0], acc[j][i][1]);
-      v.y = pack2bf(acc[j][i][2], acc[j][i][3]);
-      if (m < a.M) {
-        const uint32_t off = (uint32_t)(m * yp + nn) * 2u;
-        if (d2) bstore8(ry2, off, v); else bstore8(ry1, off, v);
-      }
-      if (a.stats) {
-        const float q0 = bf2f((u16)(v.x & 0xffff)), q1 = bf2f((u16)(v.x >> 16));
-        const float q2 = bf2f((u16)(v.y & 0xffff)), q3 = bf2f((u16)(v.y >> 16));
-        s1[j][0] += q0; s2[j][0] += q0 * q0;
-        s1[j][1] += q1; s2[j][1] += q1 * q1;
-        s1[j][2] += q2; s2[j][2] += q2 * q2;
-        s1[j][3] += q3; s2[j][3] += q3 * q3;
-      }
-    }
-  }
-  if (a.stats) {
-    // reduce over the 16 pixel lanes (lane & 15) sharing a channel group
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-          s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+        uint2 v;
+        v.x = pack2bf(acc[j][i][0], acc[j][i][1]);
+        v.y = pack2bf(acc[j][i][2], acc[j][i][3]);
+        acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const uint32_t off = m < a.M ? (uint32_t)(m * yp + nn) * 2u : RDP_OOB;
+        bstore8(d2 ? ry2 : ry1, off, v);
+        if (a.stats) {
+          const float q0 = bf2f((u16)(v.x & 0xffff)), q1 = bf2f((u16)(v.x >> 16));
+          const float q2 = bf2f((u16)(v.y & 0xffff)), q3 = bf2f((u16)(v.y >> 16));
+          s1[j][0] += q0; s2[j][0] += q0 * q0;
+          s1[j][1] += q1; s2[j][1] += q1 * q1;
+          s1[j][2] += q2; s2[j][2] += q2 * q2;
+          s1[j][3] += q3; s2[j][3] += q3 * q3;
         }
       }
-    // combine the WAVES_M waves sharing these channels through LDS (reuse buffer 0)
-    __syncthreads();
-    float* red = (float*)smem;  // [WAVES_M][BN][2]
-    if ((lane & 15) == 0) {
+    }
+    if (a.stats) {
+      // reduce over the 16 pixel lanes (lane & 15) sharing a channel group; one slab row per (tile, wm)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int c = wn * 64 + j * 16 + 4 * (lane >> 4) + r;
-          red[(wm * BN + c) * 2 + 0] = s1[j][r];
-          red[(wm * BN + c) * 2 + 1] = s2[j][r];
+          s1[j][r] = row16_sum(s1[j][r]);
+          s2[j][r] = row16_sum(s2[j][r]);
         }
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < BN; c += 256) {
-      float t1 = 0.f, t2 = 0.f;
+      if ((lane & 15) == 0) {
+        float* row = a.stats + (size_t)(tm * WAVES_M + wm) * 2 * a.Cout;
 #pragma unroll
-      for (int q = 0; q < WAVES_M; ++q) { t1 += red[(q * BN + c) * 2]; t2 += red[(q * BN + c) * 2 + 1]; }
-      a.stats[(size_t)tm * 2 * a.Cout + n0 + c] = t1;
-      a.stats[(size_t)tm * 2 * a.Cout + a.Cout + n0 + c] = t2;
+        for (int j = 0; j < 4; ++j) {
+          const int c = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+          *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+          *(float4*)(row + a.Cout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+        }
+      }
     }
   }
 }
 
 template <int BM, int BN>
-static int launch_cfg(ConvArgs a, int variant, hipStream_t s) {
+static int launch_cfg(ConvArgs a, int max_blocks, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
-  if (variant == 1)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0>), dim3(tilesM * a.tilesN), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1>), dim3(tilesM * a.tilesN), dim3(256), 0, s, a);
-  return tilesM;
+  a.ntiles = tilesM * a.tilesN;
+  const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(grid), dim3(256), 0, s, a);
+  return tilesM * (BM / 64);
 }
 
-// Returns the number of M tiles (rows of the stats slab), or -1 on unsupported shape.
+// Returns the number of stats-slab rows written, or -1 on unsupported shape.
 extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2,
                               int pitch1, int pitch2, const void* w, long wbytes, int ldw, void* y1, void* y2,
                               long ybytes1, long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats,
@@ -315,9 +277,14 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   }
   if (Cout % 64 || Cy1 % 4) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || ybytes1 >= (1l << 31) || ybytes2 >= (1l << 31)) return -1;
-  // bm_pref: 0 = auto, 128 / 256 = force tile; +1000 * variant selects the LDS layout (A/B tests)
-  const int variant = bm_pref / 1000;
+  const FastDiv fhw = make_fastdiv((uint32_t)(H * W)), fw = make_fastdiv((uint32_t)W);
+  a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;
+  // bm_pref: 0 = auto, 128 / 256 = force the tile; +1000*k: k = blocks per CU of the persistent
+  // grid (k = 0 => 2 per CU, every block resident; large k ~ one tile per block)
+  int per_cu = bm_pref / 1000;
   bm_pref %= 1000;
-  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, variant, s);
-  return launch_cfg<256, 64>(a, variant, s);
+  if (per_cu == 0) per_cu = 2;
+  const int max_blocks = 256 * per_cu;
+  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, s);
+  return launch_cfg<256, 64>(a, max_blocks, s);
 }

@@ -195,8 +195,17 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
     const int tap = t2 % taps;
     const int co = t2 / taps;
     const long col = (long)tap * cin_pad + cin;
-    float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += slab[((long)sp * Cout + co) * ncols_pad + col];
+    // 8 independent accumulators: the split loop is latency-bound otherwise (hundreds of splits)
+    const float* p = slab + (long)co * ncols_pad + col;
+    const long stride = (long)Cout * ncols_pad;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f;
+    int sp = 0;
+    for (; sp + 8 <= splits; sp += 8) {
+      s0 += p[(sp + 0) * stride]; s1 += p[(sp + 1) * stride]; s2 += p[(sp + 2) * stride]; s3 += p[(sp + 3) * stride];
+      s4 += p[(sp + 4) * stride]; s5 += p[(sp + 5) * stride]; s6 += p[(sp + 6) * stride]; s7 += p[(sp + 7) * stride];
+    }
+    for (; sp < splits; ++sp) s0 += p[sp * stride];
+    const float s = ((s0 + s1) + (s2 + s3)) + ((s4 + s5) + (s6 + s7));
     out[idx] = accumulate ? out[idx] + s : s;
   }
 }

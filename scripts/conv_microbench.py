@@ -29,12 +29,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--shapes", default=None, help="comma list of shape indices")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda")
     variants = [int(v) for v in a.variants.split(",")]
     results = []
-    for (H, C1, C2, Co) in SHAPES:
+    shapes = SHAPES if a.shapes is None else [SHAPES[int(i)] for i in a.shapes.split(",")]
+    for (H, C1, C2, Co) in shapes:
         N = a.batch
         x1 = torch.randn(N, H, H, C1, device=dev).to(torch.bfloat16)
         x2 = torch.randn(N, H, H, C2, device=dev).to(torch.bfloat16) if C2 else None
