@@ -37,11 +37,14 @@ RDP_DEV int swz(int p) { return (((p >> 1) & 1) << 1) | (((p >> 3) & 1) << 2); }
 
 RDP_DEV uint32_t fdiv2(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
-template <bool PACKED, bool TILE_FAST>
+// BKP pixels per K step (64 or 32), STAGES LDS buffers (STAGES-1 steps in flight under the MFMAs).
+template <bool PACKED, bool TILE_FAST, int BKP, int STAGES>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
-  constexpr int SUB = 8192;             // one [64][64] bf16 tile
+  constexpr int SUB = BKP * 128;        // one [BKP pixels][64 ch] bf16 tile
   constexpr int BUF = 5 * SUB;          // 4 x-subtiles + 1 dy tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  constexpr int PIECES = BKP / 8;       // 8-row DMA pieces per subtile
+  constexpr int PPW = PIECES / 4;       // pieces (row groups) per wave
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
   const int cout0 = tn * 64;
   const int pbeg = split * a.pix_per_split;
   const int pend = min(a.M, pbeg + a.pix_per_split);
-  const int nks = (pend - pbeg + 63) / 64;
+  const int nks = (pend - pbeg + BKP - 1) / BKP;
 
   const auto rx1 = make_rsrc(a.x1, a.xbytes1);
   const auto rx2 = make_rsrc(a.x2 ? a.x2 : a.x1, a.x2 ? a.xbytes2 : 0u);
@@ -86,11 +89,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
 
   auto issue = [&](int ks, char* buf) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int s = wave * 2 + t;  // DMA piece index (8 pixel rows)
-      const int p = s * 8 + rowl;  // pixel row in the 64-pixel K step
+    for (int t = 0; t < PPW; ++t) {
+      const int s = wave * PPW + t;  // DMA piece index (8 pixel rows)
+      const int p = s * 8 + rowl;  // pixel row in the BKP-pixel K step
       const int g = cpos ^ swz(p);  // global 16-B chunk this lane fetches
-      const int m = pbeg + ks * 64 + p;
+      const int m = pbeg + ks * BKP + p;
       const bool mv = m < pend;
       const uint32_t q = fdiv2((uint32_t)m, a.fw_m, a.fw_s);
       const int w = m - (int)q * a.W;
@@ -132,17 +135,26 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
   // transposed-read lane geometry: lane = 16g + 4q + pp
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tpp = lane & 3;
 
-  // one barrier per K step (see conv_igemm.hip)
-  if (nks > 0) issue(0, smem);
+  // one barrier per K step: wait for stage ks (STAGES-2 younger stages stay in flight), the
+  // barrier retires every wave's reads of the buffer about to be refilled, then issue ks+STAGES-1.
+  constexpr int DMA_PER_STAGE = PPW * 5;
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < nks) issue(st, smem + st * BUF);
   for (int ks = 0; ks < nks; ++ks) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if constexpr (STAGES == 3) {
+      if (ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(DMA_PER_STAGE) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     raw_barrier();
-    if (ks + 1 < nks) issue(ks + 1, smem + ((ks + 1) & 1) * BUF);
-    const char* cur = smem + (ks & 1) * BUF;
+    if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
+    const char* cur = smem + (ks % STAGES) * BUF;
     const char* xb = cur + wave * SUB;
     const char* db = cur + 4 * SUB;
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
+    for (int hf = 0; hf < BKP / 32; ++hf) {
       bf16x8 fa[4], fb[4];
       const int p0 = 32 * hf + 8 * tg + tq;
       const int sw0 = swz(p0), sw1 = swz(p0 + 4);
@@ -244,11 +256,13 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
   const int nblk = a.colTiles * a.coutTiles * a.splits;
   if (packed) {
-    hipLaunchKernelGGL((conv_wgrad_kernel<true, true>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_wgrad_kernel<true, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
   } else if (variant == 1) {
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, false>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
+  } else if (variant == 2) {
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 3>), dim3(nblk), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 32, 3>), dim3(nblk), dim3(256), 0, s, a);
   }
   const int creal = packed ? cin_real : a.Cin;
   const long total = (long)Cout * taps * creal;
