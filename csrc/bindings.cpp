@@ -38,6 +38,9 @@ int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, fl
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, hipStream_t);
 int rdp_wseg_size();
+int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
+double rdp_splev1(const double*, int, const double*, int, double, int);
+int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
 }
 
 namespace {
@@ -289,6 +292,53 @@ void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg
   rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, cur_stream());
 }
 
+void check_cpu_f64(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.device().is_cpu() && t.scalar_type() == torch::kFloat64 && t.is_contiguous(), name,
+              ": must be a contiguous float64 CPU tensor");
+}
+
+// FITPACK parcur: returns (ier, t[n], c[idim][n-k-1], fp)
+py::tuple parcur(torch::Tensor u, torch::Tensor x, double s, int k) {
+  check_cpu_f64(u, "u"); check_cpu_f64(x, "x");
+  const int m = u.numel(), idim = x.size(1);
+  TORCH_CHECK(x.size(0) == m, "x rows != len(u)");
+  const int nest = m + 2 * k;
+  auto t = torch::zeros({nest}, torch::kFloat64), c = torch::zeros({idim, nest}, torch::kFloat64);
+  int n = 0;
+  double fp = 0;
+  int ier;
+  {
+    py::gil_scoped_release nogil;
+    ier = rdp_parcur(idim, m, u.data_ptr<double>(), x.data_ptr<double>(), s, k, nest, t.data_ptr<double>(),
+                     c.data_ptr<double>(), &n, &fp);
+  }
+  if (ier == 10) return py::make_tuple(ier, torch::Tensor(), torch::Tensor(), fp);
+  return py::make_tuple(ier, t.narrow(0, 0, n).clone(), c.narrow(1, 0, n - k - 1).clone(), fp);
+}
+
+torch::Tensor splev(torch::Tensor t, torch::Tensor c, int k, torch::Tensor x, int der) {
+  check_cpu_f64(t, "t"); check_cpu_f64(x, "x");
+  auto cc = c.contiguous().to(torch::kFloat64);
+  auto out = torch::empty_like(x);
+  for (long i = 0; i < x.numel(); ++i)
+    out.data_ptr<double>()[i] = rdp_splev1(t.data_ptr<double>(), t.numel(), cc.data_ptr<double>(), k,
+                                           x.data_ptr<double>()[i], der);
+  return out;
+}
+
+// sorted edge points [m,3] -> (ier, mean_k, max_k, spline points [nsamp,3], fp, n)
+py::tuple fit_curvature(torch::Tensor pts, double s, int k, int nsamp, double eps) {
+  check_cpu_f64(pts, "pts");
+  auto out_pts = torch::zeros({nsamp, 3}, torch::kFloat64);
+  double out[4] = {0, 0, 0, 0};
+  int ier;
+  {
+    py::gil_scoped_release nogil;
+    ier = rdp_fit_curvature(pts.data_ptr<double>(), pts.size(0), s, k, nsamp, eps, out_pts.data_ptr<double>(), out);
+  }
+  return py::make_tuple(ier, out[0], out[1], out_pts, out[2], (int)out[3]);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -315,4 +365,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("wprep", &wprep);
   m.def("wseg_size", &rdp_wseg_size);
+  m.def("parcur", &parcur);
+  m.def("splev", &splev);
+  m.def("fit_curvature", &fit_curvature);
 }
