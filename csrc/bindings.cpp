@@ -10,7 +10,14 @@
 
 extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
-                   long, int, int, int, float*, int, int, int, int, int, int, int, hipStream_t);
+                   long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
+                   hipStream_t);
+int rdp_geo_nblocks(int);
+int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
+                  double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, hipStream_t);
+int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*,
+                   int, int, void*, hipStream_t);
+int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
                    float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
@@ -92,7 +99,8 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
 
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)
 int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, int taps, int packed,
-             torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref) {
+             torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref,
+             c10::optional<torch::Tensor> affine, int relu) {
   Act a1 = act(x1, "x1"), a2;
   if (x2) {
     a2 = act(*x2, "x2");
@@ -112,10 +120,18 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     TORCH_CHECK(stats->numel() >= rows * 2 * Cout, "stats slab too small");
     sp = stats->data_ptr<float>();
   }
+  const float* esc = nullptr;
+  const float* esh = nullptr;
+  if (affine) {  // BN coefficient block [mean | invstd | scale | shift] (4*Cout floats)
+    check_f32(*affine, "affine");
+    TORCH_CHECK(affine->numel() >= 4l * Cout, "affine must hold 4*Cout floats");
+    esc = affine->data_ptr<float>() + 2 * Cout;
+    esh = affine->data_ptr<float>() + 3 * Cout;
+  }
   const int r = rdp_conv_igemm(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
                                a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1), o1.ptr,
                                y2 ? o2.ptr : nullptr, o1.bytes, y2 ? o2.bytes : 0, o1.C, o1.pitch, y2 ? o2.pitch : 0,
-                               sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, cur_stream());
+                               sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu, cur_stream());
   TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
   return r;
 }
@@ -339,6 +355,51 @@ py::tuple fit_curvature(torch::Tensor pts, double s, int k, int nsamp, double ep
   return py::make_tuple(ier, out[0], out[1], out_pts, out[2], (int)out[3]);
 }
 
+// geometry: mask u8 [H,W], depth u16-as-int16 [H,W] (GPU) -> packed edge points; returns E via hdr (device)
+void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, double cx, double cy, double scale,
+               torch::Tensor work_i, torch::Tensor work_d, torch::Tensor pts, torch::Tensor npts, torch::Tensor out,
+               torch::Tensor kout, int nbins, double top, int min_points, torch::Tensor edges, torch::Tensor hdr) {
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == torch::kUInt8 && mask.dim() == 2 && mask.is_contiguous(), "mask");
+  TORCH_CHECK(depth.is_cuda() && depth.element_size() == 2 && depth.sizes() == mask.sizes() && depth.is_contiguous(),
+              "depth u16");
+  const int H = mask.size(0), W = mask.size(1);
+  const int nblk = rdp_geo_nblocks(H);
+  TORCH_CHECK(work_i.numel() >= nblk && work_i.scalar_type() == torch::kInt32, "work_i");
+  TORCH_CHECK(work_d.numel() >= 2 * nblk && work_d.scalar_type() == torch::kFloat64, "work_d");
+  TORCH_CHECK(pts.scalar_type() == torch::kFloat64 && pts.numel() >= (long)H * W * 4, "pts cap");
+  TORCH_CHECK(out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(0) >= nbins && out.size(2) == 4, "out");
+  TORCH_CHECK(edges.scalar_type() == torch::kFloat64 && edges.dim() == 2 && edges.size(1) == 4, "edges");
+  const int r = rdp_geo_edges(mask.data_ptr(), depth.data_ptr(), H, W, fx, fy, cx, cy, scale, work_i.data_ptr<int>(),
+                              work_d.data_ptr<double>(), work_d.data_ptr<double>() + nblk, pts.data_ptr<double>(), H * W,
+                              npts.data_ptr<int>(), out.data_ptr<double>(), out.size(1), kout.data_ptr<int>(), nbins,
+                              top, min_points, edges.data_ptr<double>(), edges.size(0), hdr.data_ptr<int>(),
+                              cur_stream());
+  TORCH_CHECK(r >= 0, "geo_edges: nbins must be in [1, 128]");
+}
+
+int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
+
+void preprocess(torch::Tensor bgr, torch::Tensor ystart, torch::Tensor ysize, torch::Tensor yw, torch::Tensor xstart,
+                torch::Tensor xsize, torch::Tensor xw, torch::Tensor out) {
+  TORCH_CHECK(bgr.is_cuda() && bgr.scalar_type() == torch::kUInt8 && bgr.dim() == 3 && bgr.size(2) == 3 &&
+              bgr.is_contiguous(), "bgr u8 HxWx3");
+  Act o = act(out, "out");
+  TORCH_CHECK(o.N == 1 && o.C == 8 && o.pitch == 8, "out must be [1,OH,OW,8] contiguous");
+  TORCH_CHECK(ystart.numel() == o.H && xstart.numel() == o.W && yw.numel() == (long)o.H * 16 &&
+              xw.numel() == (long)o.W * 16, "aa tables");
+  rdp_preprocess(bgr.data_ptr(), bgr.size(0), bgr.size(1), ystart.data_ptr<int>(), ysize.data_ptr<int>(),
+                 yw.data_ptr<float>(), xstart.data_ptr<int>(), xsize.data_ptr<int>(), xw.data_ptr<float>(), o.H, o.W,
+                 o.ptr, cur_stream());
+}
+
+void mask_upsample(torch::Tensor m, torch::Tensor out, torch::Tensor count) {
+  TORCH_CHECK(m.is_cuda() && m.scalar_type() == torch::kUInt8 && m.dim() == 2 && m.is_contiguous(), "m");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kUInt8 && out.dim() == 2 && out.is_contiguous(), "out");
+  TORCH_CHECK(count.is_cuda() && count.scalar_type() == torch::kInt32, "count int32");
+  rdp_mask_upsample(m.data_ptr(), m.size(0), m.size(1), out.data_ptr(), out.size(0), out.size(1),
+                    (unsigned*)count.data_ptr(), cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -366,6 +427,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wprep", &wprep);
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
+  m.def("geo_edges", &geo_edges);
+  m.def("geo_nblocks", &geo_nblocks);
+  m.def("preprocess", &preprocess);
+  m.def("mask_upsample", &mask_upsample);
   m.def("splev", &splev);
   m.def("fit_curvature", &fit_curvature);
 }

@@ -40,6 +40,9 @@ struct ConvArgs {
   int Cy1;  // channels going to y1 (rest to y2)
   int ypitch1, ypitch2;
   float* stats;  // [tilesM * WAVES_M][2][Cout] partial (sum, sumsq) or nullptr
+  const float* escale;  // eval-mode BN fold: out = relu?(acc * escale[n] + eshift[n]) (or nullptr)
+  const float* eshift;
+  int erelu;
   int N, H, W, Cout, M;
   int taps;  // 9 (3x3) or 1 (1x1)
   int packed;  // 1: Cin == 8, K packs 8 taps per 64-wide K step
@@ -204,9 +207,18 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+        f32x4 o = acc[j][i];
+        if (a.escale) {
+          const float4 sc = *(const float4*)(a.escale + n), sh = *(const float4*)(a.eshift + n);
+          o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+          o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+          if (a.erelu) {
+            o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
+          }
+        }
         uint2 v;
-        v.x = pack2bf(acc[j][i][0], acc[j][i][1]);
-        v.y = pack2bf(acc[j][i][2], acc[j][i][3]);
+        v.x = pack2bf(o[0], o[1]);
+        v.y = pack2bf(o[2], o[3]);
         acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
         const uint32_t off = m < a.M ? (uint32_t)(m * yp + nn) * 2u : RDP_OOB;
         bstore8(d2 ? ry2 : ry1, off, v);
@@ -256,8 +268,10 @@ static int launch_cfg(ConvArgs a, int max_blocks, hipStream_t s) {
 extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2,
                               int pitch1, int pitch2, const void* w, long wbytes, int ldw, void* y1, void* y2,
                               long ybytes1, long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats,
-                              int N, int H, int W, int Cout, int taps, int packed, int bm_pref, hipStream_t s) {
+                              int N, int H, int W, int Cout, int taps, int packed, int bm_pref,
+                              const float* escale, const float* eshift, int erelu, hipStream_t s) {
   ConvArgs a;
+  a.escale = escale; a.eshift = eshift; a.erelu = erelu;
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
   a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
   a.C1 = C1; a.C2 = C2; a.pitch1 = pitch1; a.pitch2 = pitch2;

@@ -403,7 +403,10 @@ class UNetExecutor:
         sp = L.spec
         m = self.m
         w = m.fwd_weight(sp)
-        rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats if self.training else None, 0)
+        if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
+            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1)
+            return
+        rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0)
         g = m.store.view(sp.bn + ".weight")
         b = m.store.view(sp.bn + ".bias")
         if self.training:
@@ -470,7 +473,7 @@ class UNetExecutor:
         gw = st.flat_slice(sp.name + ".weight", st.grad)
         C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw, 0, L.splits, 0)
         if L.dx1 is not None:
-            C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0)
+            C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0)
         if hooks is not None:
             hooks(sp)
 

@@ -50,7 +50,7 @@ def test_conv_fwd_and_stats(C, N, H, W, C1, C2, Cout):
     y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
     rows = C.conv_stats_rows(N * H * W, Cout, 0)
     stats = torch.zeros(rows * 2 * Cout, device=dev)
-    r = C.conv_fwd(x1, x2, ohwi(w).contiguous(), 9, 0, y, None, stats, 0)
+    r = C.conv_fwd(x1, x2, ohwi(w).contiguous(), 9, 0, y, None, stats, 0, None, 0)
     assert r == rows
     xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
     ref = F.conv2d(xin, w.float(), padding=1)
@@ -73,7 +73,7 @@ def test_conv_fwd_asymmetric_identity(C):
         for ci in range(Cin):
             w[co, ci, 1, 1] = float((co * 7 + ci * 3) % 11) - 5  # asymmetric, small ints (exact in bf16)
     y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
-    C.conv_fwd(bf(x), None, ohwi(bf(w)).contiguous(), 9, 0, y, None, None, 0)
+    C.conv_fwd(bf(x), None, ohwi(bf(w)).contiguous(), 9, 0, y, None, None, 0, None, 0)
     ref = F.conv2d(nchw(x), w, padding=1)
     assert torch.equal(nchw(y).float(), ref)
 
@@ -89,7 +89,7 @@ def test_conv_packed_first_layer(C):
     wp = torch.zeros(Cout, 16, 8, dtype=torch.bfloat16, device=dev)
     wp[:, :9, :3] = w.permute(0, 2, 3, 1).reshape(Cout, 9, 3)
     y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
-    C.conv_fwd(x8, None, wp.view(Cout, 128), 9, 1, y, None, None, 0)
+    C.conv_fwd(x8, None, wp.view(Cout, 128), 9, 1, y, None, None, 0, None, 0)
     ref = F.conv2d(nchw(x8[..., :3]).float(), w.float(), padding=1)
     assert relerr(nchw(y), ref) < 1e-2
 
@@ -107,7 +107,7 @@ def test_conv_dgrad_split_output(C):
     wt = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cs + Cu, 9 * Cout).contiguous()  # [cin][tap'][cout]
     d1 = torch.empty(N, H, W, Cs, dtype=torch.bfloat16, device=dev)
     d2 = torch.empty(N, H, W, Cu, dtype=torch.bfloat16, device=dev)
-    C.conv_fwd(nhwc(dy), None, wt, 9, 0, d1, d2, None, 0)
+    C.conv_fwd(nhwc(dy), None, wt, 9, 0, d1, d2, None, 0, None, 0)
     got = torch.cat([nchw(d1), nchw(d2)], 1)
     assert relerr(got, x.grad) < 1e-2
 
