@@ -257,12 +257,12 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   const int nblk = a.colTiles * a.coutTiles * a.splits;
   if (packed) {
     hipLaunchKernelGGL((conv_wgrad_kernel<true, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
-  } else if (variant == 1) {
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
+  } else if (variant == 1) {  // alternatives kept for the microbenchmark (measured slower on gfx950)
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 32, 3>), dim3(nblk), dim3(256), 0, s, a);
   } else if (variant == 2) {
     hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 3>), dim3(nblk), dim3(256), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 32, 3>), dim3(nblk), dim3(256), 0, s, a);
+  } else {  // default: BK=64 pixels per stage, double-buffered
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
   }
   const int creal = packed ? cin_real : a.Cin;
   const long total = (long)Cout * taps * creal;

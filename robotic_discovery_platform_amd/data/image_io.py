@@ -26,15 +26,16 @@ def encode_jpeg(bgr: np.ndarray, quality: int = 95) -> bytes:
     return buf.getvalue()
 
 
-def encode_png(arr: np.ndarray) -> bytes:
+def encode_png(arr: np.ndarray, compress_level: int = 6) -> bytes:
     """PNG of uint8 gray, uint8 BGR (stored as RGB) or uint16 gray (lossless 16-bit)."""
     buf = io.BytesIO()
+    kw = dict(format="PNG", compress_level=compress_level)
     if arr.dtype == np.uint16:
-        Image.fromarray(np.ascontiguousarray(arr), "I;16").save(buf, format="PNG")
+        Image.fromarray(np.ascontiguousarray(arr)).save(buf, **kw)  # uint16 -> mode I;16
     elif arr.ndim == 3:
-        Image.fromarray(np.ascontiguousarray(arr[..., ::-1]), "RGB").save(buf, format="PNG")
+        Image.fromarray(np.ascontiguousarray(arr[..., ::-1]), "RGB").save(buf, **kw)
     else:
-        Image.fromarray(np.ascontiguousarray(arr.astype(np.uint8)), "L").save(buf, format="PNG")
+        Image.fromarray(np.ascontiguousarray(arr.astype(np.uint8)), "L").save(buf, **kw)
     return buf.getvalue()
 
 

@@ -94,7 +94,7 @@ class GeometryEngine:
     """Device buffers + launch for one camera resolution (one per serving engine / stream)."""
 
     def __init__(self, H: int, W: int, device: torch.device, cfg: Optional[GeometryConfig] = None,
-                 ecap: int = 16384):
+                 ecap: Optional[int] = None):
         from ..ops import native
         self.C = native()
         self.cfg = cfg or GeometryConfig()
@@ -107,6 +107,8 @@ class GeometryEngine:
         kcap = max(1, int(H * W * self.cfg.top_k_percent) + 1)
         self.out = torch.zeros(self.cfg.num_bins, kcap, 4, dtype=torch.float64, device=device)
         self.kout = torch.zeros(self.cfg.num_bins, dtype=torch.int32, device=device)
+        # upper bound of sum_b max(1, int(n_b * top)) over <= H*W points: never truncates
+        ecap = ecap or (self.cfg.num_bins + int(H * W * self.cfg.top_k_percent) + 1)
         self.edges = torch.zeros(ecap, 4, dtype=torch.float64, device=device)
         self.hdr = torch.zeros(1, dtype=torch.int32, device=device)
 
@@ -120,8 +122,6 @@ class GeometryEngine:
     def finish(self, edges_host: np.ndarray, E: int, n_points: int) -> CurvatureResult:
         if n_points < self.cfg.min_points:
             return CurvatureResult(status="too_few_points", n_points=n_points)
-        if E > self.edges.shape[0]:
-            edges_host = self.edges[:E].cpu().numpy()  # rare: larger than the staged window
         return fit_edges(sort_edges(edges_host[:E]), self.cfg, n_points)
 
 

@@ -288,7 +288,9 @@ class UNetExecutor:
         it = iter(specs)
 
         def mk(spec, x1, x2, h, w):
-            L = _Layer(spec, x1, x2, t(h, w, spec.cout), t(h, w, spec.cout),
+            a = t(h, w, spec.cout)
+            y = t(h, w, spec.cout) if training else a  # eval writes BN+ReLU output directly
+            L = _Layer(spec, x1, x2, y, a,
                        torch.zeros(4 * spec.cout, device=dev), torch.zeros(3 * spec.cout, device=dev))
             self.layers.append(L)
             return L
@@ -423,7 +425,8 @@ class UNetExecutor:
             C.bn_eval_coef(m.store.view(sp.bn + ".weight"), m.store.view(sp.bn + ".bias"),
                            m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"), 1e-5, L.coef)
 
-    def forward(self):
+    def forward(self, head: bool = True):
+        """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead)."""
         C = _native()
         D = self.m.depth
         if not self.training:
@@ -447,6 +450,8 @@ class UNetExecutor:
             self._conv_bn_relu(C, la)
             self._conv_bn_relu(C, lb)
             low = lb.a
+        if not head:
+            return
         head_w = self.m.store.view("outc.conv.weight").reshape(-1)
         head_b = self.m.store.view("outc.conv.bias")
         C.head_fwd(self.final, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums, self.loss,

@@ -1,0 +1,157 @@
+"""Serving benchmark: e2e frames/s + p50/p99 latency (second half of the BASELINE.json metric).
+
+Two measurements on 640x480 synthetic RGB-D frames (the reference camera format, pkg/camera.py:35):
+  * engine:  ``FramePipeline.process`` per frame (H2D, hipGraph replay of preprocess + U-Net +
+             mask + geometry kernels, D2H, host spline fit) -- the per-frame work of
+             server.py:117-133 without codecs/transport.
+  * e2e:     the full gRPC service over loopback (client-encoded JPEG colour + 16-bit PNG depth,
+             server decode, engine, PNG mask encode, metrics CSV, response) -- one stream, streamed
+             (throughput FPS) and lock-step (round-trip p50/p99).
+
+Weights: the reference U-Net architecture, briefly trained on synthetic scenes (so masks look like
+an actuator and the geometry stage sees realistic point counts), unless ``train_steps=0``.
+"""
+from __future__ import annotations
+
+import os
+import queue
+import tempfile
+import threading
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+
+def _pct(v, q):
+    return float(np.percentile(np.asarray(v), q)) if len(v) else float("nan")
+
+
+def prepare_model(dev, train_steps: int = 200, batch: int = 16, n_scenes: int = 48, seed: int = 0):
+    from ..data.image_io import bgr2rgb, resize_area, resize_nearest
+    from ..data.synthetic import make_scene
+    from ..models.unet import UNetNative
+    from ..train.engine import NativeTrainer
+    torch.manual_seed(seed)
+    scenes = [make_scene(seed + i) for i in range(n_scenes)]
+    model = UNetNative(3, 1, device=dev)
+    if train_steps > 0:
+        x = np.stack([resize_area(bgr2rgb(s.color), (256, 256)) for s in scenes]).astype(np.float32) / 255
+        y = np.stack([resize_nearest(s.mask, (256, 256)) for s in scenes]).astype(np.float32) / 255
+        X = torch.from_numpy(x).permute(0, 3, 1, 2).contiguous().to(dev)
+        Y = torch.from_numpy(y)[:, None].contiguous().to(dev)
+        tr = NativeTrainer(model, batch, 256, 256, lr=1e-3, graph=True)
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        for _ in range(train_steps):
+            idx = torch.randint(0, n_scenes, (batch,), generator=g).to(dev)
+            tr.set_batch(X[idx], Y[idx])
+            tr.step()
+        torch.cuda.synchronize(dev)
+    return model.eval(), scenes
+
+
+def measure_engine(model, scenes, frames: int = 200, warmup: int = 20):
+    from ..data.synthetic import DEFAULT_K
+    from .engine import FramePipeline
+    p = FramePipeline(model, DEFAULT_K, 0.001, graph=True)
+    lat, gpu, fit = [], [], []
+    ok = 0
+    for i in range(warmup + frames):
+        s = scenes[i % len(scenes)]
+        t0 = time.perf_counter()
+        r = p.process(s.color, s.depth)
+        dt = (time.perf_counter() - t0) * 1e3
+        if i >= warmup:
+            lat.append(dt)
+            gpu.append(r.timings["gpu_ms"])
+            fit.append(r.timings["fit_ms"])
+            ok += r.curvature.status == "ok"
+    return {"engine_fps": round(1e3 * len(lat) / sum(lat), 1), "engine_p50_ms": round(_pct(lat, 50), 3),
+            "engine_p99_ms": round(_pct(lat, 99), 3), "engine_gpu_p50_ms": round(_pct(gpu, 50), 3),
+            "engine_fit_p50_ms": round(_pct(fit, 50), 3), "engine_ok_frac": ok / max(1, len(lat))}
+
+
+def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2):
+    import grpc
+    from ..camera import write_calibration
+    from ..config import ServeConfig
+    from ..data.synthetic import DEFAULT_K
+    from ..proto import vision as pb
+    from .client import make_request
+    from .engine import EnginePool
+    from .server import MetricsLog, VisionAnalysisService
+    from concurrent import futures
+    tmp = tempfile.mkdtemp(prefix="rdp_serve_")
+    engine = EnginePool(model, DEFAULT_K, 0.001, n=pool, graph=True)
+    svc = VisionAnalysisService(engine, MetricsLog(os.path.join(tmp, "metrics.csv")))
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10))
+    pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
+    port = server.add_insecure_port("127.0.0.1:0")
+    server.start()
+    reqs = [make_request(s.color, s.depth) for s in scenes]
+    out = {}
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_receive_message_length", 64 << 20),
+                                                                   ("grpc.max_send_message_length", 64 << 20)]) as ch:
+            stub = pb.VisionAnalysisServiceStub(ch)
+            # streamed throughput
+            n = warmup + frames
+            t_first = [None]
+
+            def gen():
+                for i in range(n):
+                    yield reqs[i % len(reqs)]
+
+            t_start = None
+            proc = []
+            for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen())):
+                if i == warmup - 1:
+                    t_start = time.perf_counter()
+                if i >= warmup:
+                    proc.append(resp.proc_time_ms)
+            t_end = time.perf_counter()
+            out["e2e_fps"] = round(frames / (t_end - t_start), 1)
+            out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)
+            # lock-step round trip
+            q: "queue.Queue" = queue.Queue()
+            sent = []
+
+            def gen_ls():
+                for i in range(n):
+                    sent.append(time.perf_counter())
+                    yield reqs[i % len(reqs)]
+                    q.get()
+
+            rtt = []
+            for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen_ls())):
+                now = time.perf_counter()
+                if i >= warmup:
+                    rtt.append((now - sent[i]) * 1e3)
+                q.put(1)
+            out["e2e_p50_ms"] = round(_pct(rtt, 50), 3)
+            out["e2e_p99_ms"] = round(_pct(rtt, 99), 3)
+    finally:
+        server.stop(0)
+    return out
+
+
+def measure_serving(dev: Optional[torch.device] = None, frames: int = 200, warmup: int = 20,
+                    train_steps: int = 200) -> dict:
+    dev = dev or torch.device("cuda")
+    model, scenes = prepare_model(dev, train_steps)
+    res = {"serve_frame": "640x480 RGB-D -> 256x256 U-Net", "serve_weights": f"trained {train_steps} steps on synthetic"}
+    res.update({"serve_" + k: v for k, v in measure_engine(model, scenes, frames, warmup).items()})
+    res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup).items()})
+    return res
+
+
+if __name__ == "__main__":
+    import argparse
+    import json
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--train-steps", type=int, default=200)
+    a = ap.parse_args()
+    print(json.dumps(measure_serving(torch.device("cuda"), a.frames, a.warmup, a.train_steps)), flush=True)

@@ -1,0 +1,278 @@
+"""Per-frame analysis engine: colour + depth frame -> mask, coverage, curvature profile.
+
+Replaces the serial per-frame body of ``/root/reference/services/vision_analysis/server.py:116-152``
+(decode -> ToTensor/Resize(256, antialias) -> UNet -> sigmoid>0.5 -> .cpu() -> cv2 nearest
+resize -> numpy/scipy geometry -> coverage) with one device program per frame:
+
+    pinned H2D (colour u8, depth u16)          side HIP stream, async
+    preprocess      u8 BGR -> AA resize -> bf16 NHWC8          csrc/serve_kernels.hip
+    UNet forward    18 implicit-GEMM convs, BN folded in epilogues   csrc/conv_igemm.hip
+    head_mask       1x1 head + (logit > 0) -> u8 256x256        csrc/head_loss.hip
+    mask_upsample   nearest -> HxW u8 + nnz count               csrc/serve_kernels.hip
+    geo_edges       deproject + compaction + 50-bin top-5 %     csrc/geometry.hip
+    pinned D2H (mask, edge points, counters)
+    host            x-sort + FITPACK-equivalent spline + curvature    csrc/spline.cpp
+
+The device part between the copies is captured once into a hipGraph (torch.cuda.CUDAGraph) and
+replayed per frame, so a frame costs one graph launch plus three copies instead of ~90 kernel
+launches. ``EnginePool`` holds one ``FramePipeline`` (own executor buffers, stream and graph) per
+concurrently served stream; weights are shared and updated in place on hot reload, so graphs stay
+valid. ``CpuFramePipeline`` is the same contract on the CPU (plain torch + numpy geometry) for
+hosts without a GPU and for the loopback tests.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..config import GeometryConfig
+from ..geometry.curvature import CurvatureResult, GeometryEngine, compute_curvature_profile
+
+AA_MAXTAP = 16
+
+
+def aa_tables(n_in: int, n_out: int):
+    """torch ``_upsample_bilinear2d_aa`` (align_corners=False) 1-D tables: start[n_out], size[n_out],
+    weights[n_out*16] (triangle filter, support = scale when downscaling, normalised)."""
+    scale = n_in / n_out
+    support = scale if scale >= 1.0 else 1.0
+    invscale = 1.0 / scale if scale >= 1.0 else 1.0
+    start = np.zeros(n_out, np.int32)
+    size = np.zeros(n_out, np.int32)
+    w = np.zeros((n_out, AA_MAXTAP), np.float32)
+    for i in range(n_out):
+        center = scale * (i + 0.5)
+        xmin = max(int(center - support + 0.5), 0)
+        xsize = min(int(center + support + 0.5), n_in) - xmin
+        if xsize > AA_MAXTAP:
+            raise ValueError(f"antialias support {xsize} > {AA_MAXTAP} taps (input {n_in} -> {n_out} too large)")
+        j = np.arange(xsize)
+        ww = np.maximum(0.0, 1.0 - np.abs((j + xmin - center + 0.5) * invscale))
+        tot = ww.sum()
+        if tot > 0:
+            ww = ww / tot
+        start[i], size[i] = xmin, xsize
+        w[i, :xsize] = ww
+    return start, size, w.reshape(-1)
+
+
+@dataclass
+class FrameResult:
+    mask: np.ndarray                # HxW uint8 {0,1}
+    coverage: float                 # percent of pixels in the mask
+    curvature: CurvatureResult
+    timings: dict = field(default_factory=dict)
+
+
+def _logit(p: float) -> float:
+    p = min(max(p, 1e-7), 1 - 1e-7)
+    return math.log(p / (1 - p))
+
+
+class FramePipeline:
+    """One static-shape (H, W) per-frame program on its own HIP stream (GPU, native kernels)."""
+
+    def __init__(self, model, K: np.ndarray, depth_scale: float, H: int = 480, W: int = 640, size: int = 256,
+                 threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
+                 device: Optional[torch.device] = None):
+        from ..models.unet import UNetExecutor, UNetNative
+        from ..ops import native
+        if not isinstance(model, UNetNative):
+            raise TypeError("FramePipeline needs the native UNet (UNetNative); use CpuFramePipeline otherwise")
+        self.C = native()
+        self.model = model
+        self.dev = device or model.store.device
+        self.H, self.W, self.S = H, W, size
+        self.K = np.asarray(K, np.float64)
+        self.scale = float(depth_scale)
+        self.thr_logit = _logit(threshold)
+        self.cfg = geo_cfg or GeometryConfig()
+        dev = self.dev
+        self.stream = torch.cuda.Stream(dev)
+        self.ex = UNetExecutor(model, 1, size, size, False, "bce", 1.0)
+        # AA resize tables (device)
+        ys, yn, yw = aa_tables(H, size)
+        xs, xn, xw = aa_tables(W, size)
+        self.tab = [torch.from_numpy(a).to(dev) for a in (ys, yn, yw, xs, xn, xw)]
+        # device buffers
+        self.d_color = torch.empty(H, W, 3, dtype=torch.uint8, device=dev)
+        self.d_depth = torch.empty(H, W, dtype=torch.int16, device=dev)
+        self.m256 = torch.empty(size * size, dtype=torch.uint8, device=dev)
+        self.mask = torch.empty(H, W, dtype=torch.uint8, device=dev)
+        self.meta = torch.zeros(4, dtype=torch.int32, device=dev)
+        ecap = self.cfg.num_bins + int(H * W * self.cfg.top_k_percent) + 1
+        self.geo = GeometryEngine(H, W, dev, self.cfg, ecap=ecap)
+        # pinned host staging
+        self.h_color = torch.empty(H, W, 3, dtype=torch.uint8, pin_memory=True)
+        self.h_depth = torch.empty(H, W, dtype=torch.int16, pin_memory=True)
+        self.h_mask = torch.empty(H, W, dtype=torch.uint8, pin_memory=True)
+        self.h_edges = torch.empty(ecap, 4, dtype=torch.float64, pin_memory=True)
+        self.h_meta = torch.empty(4, dtype=torch.int32, pin_memory=True)
+        self.ev0 = torch.cuda.Event(enable_timing=True)
+        self.ev1 = torch.cuda.Event(enable_timing=True)
+        self.graph = None
+        self.lock = threading.Lock()
+        if graph:
+            self._capture()
+
+    # ---------------------------------------------------------------- device program
+    def _device_program(self):
+        C, ex, m = self.C, self.ex, self.model
+        C.preprocess(self.d_color, *self.tab, ex.x_in)
+        ex.forward(head=False)
+        C.head_mask(ex.final, m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
+                    self.thr_logit, self.m256)
+        C.mask_upsample(self.m256.view(self.S, self.S), self.mask, self.meta[0:1])
+        self.geo.launch(self.mask, self.d_depth, self.K, self.scale)
+        self.meta[1:2].copy_(self.geo.hdr)
+        self.meta[2:3].copy_(self.geo.npts)
+
+    def _capture(self):
+        with torch.cuda.stream(self.stream):
+            self._device_program()  # warm-up (lazy allocations, kernel loading)
+        self.stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream):
+            self._device_program()
+        self.graph = g
+
+    # ---------------------------------------------------------------- per frame
+    def submit(self, color_bgr: np.ndarray, depth: np.ndarray):
+        """Stage a frame and enqueue its device work; returns immediately (call ``collect``)."""
+        if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
+            raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
+        self.h_color.numpy()[...] = color_bgr
+        self.h_depth.numpy()[...] = depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16)
+        s = self.stream
+        with torch.cuda.stream(s):
+            self.ev0.record(s)
+            self.d_color.copy_(self.h_color, non_blocking=True)
+            self.d_depth.copy_(self.h_depth, non_blocking=True)
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._device_program()
+            self.h_mask.copy_(self.mask, non_blocking=True)
+            self.h_edges.copy_(self.geo.edges, non_blocking=True)
+            self.h_meta.copy_(self.meta, non_blocking=True)
+            self.ev1.record(s)
+
+    def collect(self) -> FrameResult:
+        t0 = time.perf_counter()
+        self.ev1.synchronize()
+        t1 = time.perf_counter()
+        count, E, npts = (int(v) for v in self.h_meta.numpy()[:3])
+        res = self.geo.finish(self.h_edges.numpy(), E, npts)
+        t2 = time.perf_counter()
+        cov = 100.0 * count / (self.H * self.W)
+        return FrameResult(self.h_mask.numpy().copy(), cov, res,
+                           {"gpu_ms": self.ev0.elapsed_time(self.ev1), "wait_ms": (t1 - t0) * 1e3,
+                            "fit_ms": (t2 - t1) * 1e3})
+
+    def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
+        with self.lock:
+            self.submit(color_bgr, depth)
+            return self.collect()
+
+
+class CpuFramePipeline:
+    """Same contract on the CPU: torch (any UNet module) + numpy geometry + native C++ spline."""
+
+    def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, threshold: float = 0.5,
+                 geo_cfg: Optional[GeometryConfig] = None, **_):
+        self.model, self.K, self.scale = model, np.asarray(K, np.float64), float(depth_scale)
+        self.H, self.W, self.S, self.thr = H, W, size, threshold
+        self.cfg = geo_cfg or GeometryConfig()
+        self.lock = threading.Lock()
+
+    def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
+        import torch.nn.functional as F
+        from ..data.image_io import resize_nearest
+        t0 = time.perf_counter()
+        rgb = torch.from_numpy(np.ascontiguousarray(color_bgr[..., ::-1])).permute(2, 0, 1).float().div(255)
+        x = F.interpolate(rgb[None], size=(self.S, self.S), mode="bilinear", align_corners=False, antialias=True)
+        with torch.no_grad():
+            out = self.model(x.to(next(self.model.parameters()).device))
+        m = (torch.sigmoid(out.float()) > self.thr)[0, 0].cpu().numpy().astype(np.uint8)
+        mask = resize_nearest(m, (color_bgr.shape[1], color_bgr.shape[0]))
+        t1 = time.perf_counter()
+        res = compute_curvature_profile(mask, depth, self.K, self.scale, self.cfg, device="cpu")
+        cov = 100.0 * np.count_nonzero(mask) / mask.size
+        return FrameResult(mask, cov, res, {"model_ms": (t1 - t0) * 1e3,
+                                             "fit_ms": (time.perf_counter() - t1) * 1e3})
+
+
+class EnginePool:
+    """N per-frame pipelines shared by the server's worker threads (one checked out per frame)."""
+
+    def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
+                 threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None):
+        self.model = model
+        self.args = dict(K=K, depth_scale=depth_scale, size=size, threshold=threshold, geo_cfg=geo_cfg)
+        self.graph = graph
+        self.n = n
+        self.gpu = _is_native(model)
+        self._pools = {}
+        self._mk_lock = threading.Lock()
+        self._get(H, W)
+
+    def _new(self, H, W):
+        if self.gpu:
+            return FramePipeline(self.model, H=H, W=W, graph=self.graph, **self.args)
+        return CpuFramePipeline(self.model, H=H, W=W, **self.args)
+
+    def _get(self, H, W) -> "queue.Queue":
+        with self._mk_lock:
+            q = self._pools.get((H, W))
+            if q is None:
+                q = queue.Queue()
+                for _ in range(self.n):
+                    q.put(self._new(H, W))
+                self._pools[(H, W)] = q
+            return q
+
+    @contextlib.contextmanager
+    def exclusive(self):
+        """Hold every pipeline (no frame in flight), e.g. while weights are swapped in place."""
+        with self._mk_lock:
+            qs = list(self._pools.values())
+            held = [(q, q.get()) for q in qs for _ in range(self.n)]
+            try:
+                yield
+            finally:
+                for q, p in held:
+                    q.put(p)
+
+    def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
+        q = self._get(*depth.shape[:2])
+        p = q.get()
+        try:
+            return p.process(color_bgr, depth)
+        finally:
+            q.put(p)
+
+
+def _is_native(model) -> bool:
+    try:
+        from ..models.unet import UNetNative
+        return isinstance(model, UNetNative)
+    except Exception:
+        return False
+
+
+def smoke_frame(model, device) -> FrameResult:
+    """One synthetic 480x640 frame through the native pipeline (used by __graft_entry__.smoke)."""
+    from ..data.synthetic import DEFAULT_K, make_scene
+    sc = make_scene(0)
+    p = FramePipeline(model, DEFAULT_K, 0.001, graph=True, device=device)
+    r = p.process(sc.color, sc.depth)
+    assert r.mask.shape == (480, 640) and 0.0 <= r.coverage <= 100.0
+    return r

@@ -1,0 +1,239 @@
+"""VisionAnalysisService gRPC server (``evofab.vision``, stream -> stream).
+
+Behaviour of ``/root/reference/services/vision_analysis/server.py:22-183``:
+  * resources: model from the registry URI (default ``models:/Actuator-Segmenter/latest``,
+    ``@alias`` also accepted), intrinsics ``mtx`` + optional ``depth_scale`` (default 0.001) from
+    ``ml/configs/calibration_data.npz``; startup aborts if any is missing          (:74-99,166-170)
+  * per request: decode JPEG colour + 16-bit PNG depth, mask/curvature, response with mean/max
+    curvature, 100 spline points and the PNG mask (u8 {0,255}) at frame size       (:116-152)
+  * per-frame CSV ``timestamp,mean_curvature,max_curvature,mask_coverage_percent`` (:68-72,146-150)
+  * any exception: ``StatusCode.INTERNAL`` + details + one empty response         (:154-158)
+  * ``ThreadPoolExecutor(max_workers=10)`` on ``[::]:50051``                       (:172-179)
+
+Differences: ``status``, ``mask_coverage`` and ``proc_time_ms`` are populated (a
+wire-compatible superset); the CSV writer is locked and keeps its handle open (the reference appends
+from 10 threads without a lock); frames of one stream are decoded one ahead on a helper thread so
+host codecs overlap the device program; the model can hot-reload when a registry alias moves.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import queue
+import threading
+import time
+from concurrent import futures
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..config import ServeConfig
+from ..data.image_io import decode_image, encode_png
+from ..proto import vision as pb
+from .engine import EnginePool
+
+log = logging.getLogger(__name__)
+
+CSV_HEADER = "timestamp,mean_curvature,max_curvature,mask_coverage_percent\n"
+
+
+class MetricsLog:
+    """Thread-safe per-frame metrics CSV (same header/row format as the reference)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        if not os.path.exists(path):
+            with open(path, "w") as f:
+                f.write(CSV_HEADER)
+        self._f = open(path, "a", buffering=1)
+        self._lock = threading.Lock()
+
+    def write(self, mean_k: float, max_k: float, coverage: float, ts: Optional[float] = None) -> None:
+        line = f"{time.time() if ts is None else ts},{mean_k},{max_k},{coverage}\n"
+        with self._lock:
+            self._f.write(line)
+
+    def close(self) -> None:
+        with self._lock:
+            self._f.close()
+
+
+def load_resources(cfg: ServeConfig, device: Optional[torch.device] = None):
+    """(model, intrinsics, depth_scale, version) or Nones, logging the reason like the reference."""
+    from ..camera import load_calibration
+    from ..mlstore import pytorch as mlpt
+    from ..mlstore.store import FileStore
+    model = K = ds = version = None
+    try:
+        model = mlpt.load_model(cfg.model_uri, map_location=device, backend=cfg.backend,
+                                tracking_uri=cfg.mlruns_dir)
+        version = registry_version(FileStore(cfg.mlruns_dir), cfg.model_uri)
+        log.info("segmentation model '%s' loaded (version %s)", cfg.model_uri, version)
+    except Exception as e:
+        log.error("FATAL: failed to load model %s: %s", cfg.model_uri, e)
+        return None, None, None, None
+    if not os.path.exists(cfg.calib_file):
+        log.error("FATAL: calibration data not found at '%s'", cfg.calib_file)
+        return model, None, None, version
+    try:
+        K, _, ds = load_calibration(cfg.calib_file, cfg.default_depth_scale)
+    except Exception as e:
+        log.error("FATAL: failed to load intrinsics: %s", e)
+        return model, None, None, version
+    return model, K, ds, version
+
+
+def registry_version(store, uri: str) -> Optional[str]:
+    """The concrete version a ``models:/`` URI currently points at (None for run URIs)."""
+    if not uri.startswith("models:/"):
+        return None
+    name, _, ref = uri[len("models:/"):].partition("/")
+    if "@" in name:
+        name, alias = name.split("@", 1)
+        return str(store.get_model_version_by_alias(name, alias).version)
+    if ref in ("", "latest"):
+        vs = store.search_model_versions(name)
+        return str(max(int(v.version) for v in vs)) if vs else None
+    if ref.isdigit():
+        return ref
+    vs = store.get_latest_versions(name, stages=[ref])
+    return str(vs[0].version) if vs else None
+
+
+class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
+    def __init__(self, engine: EnginePool, metrics: Optional[MetricsLog] = None, prefetch: int = 2):
+        self.engine = engine
+        self.metrics = metrics
+        self.prefetch = prefetch
+        self.frames = 0
+
+    def _decoded(self, request_iterator):
+        """Decode requests one ahead on a helper thread (host codecs overlap device work)."""
+        q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
+        END = object()
+
+        def reader():
+            try:
+                for req in request_iterator:
+                    t = time.perf_counter()
+                    color = decode_image(req.color_image.data, True)
+                    depth = decode_image(req.depth_image.data, False)
+                    q.put((t, color, depth, None))
+            except Exception as e:  # surface decode / transport errors in the handler thread
+                q.put((None, None, None, e))
+            q.put(END)
+
+        th = threading.Thread(target=reader, daemon=True)
+        th.start()
+        while True:
+            item = q.get()
+            if item is END:
+                return
+            if item[3] is not None:
+                raise item[3]
+            yield item[:3]
+
+    def analyze_frame(self, color: np.ndarray, depth: np.ndarray, t0: Optional[float] = None):
+        t0 = time.perf_counter() if t0 is None else t0
+        if depth.dtype != np.uint16:
+            depth = depth.astype(np.uint16)
+        r = self.engine.process(color, depth)
+        c = r.curvature
+        resp = pb.AnalysisResponse(mean_curvature=c.mean_curvature, max_curvature=c.max_curvature, status=c.status,
+                                   mask_coverage=r.coverage)
+        if c.spline_points:
+            resp.spline_points.extend([pb.Point3D(x=p.x, y=p.y, z=p.z) for p in c.spline_points])
+        resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1)
+        resp.proc_time_ms = (time.perf_counter() - t0) * 1e3
+        if self.metrics is not None:
+            self.metrics.write(resp.mean_curvature, resp.max_curvature, r.coverage)
+        self.frames += 1
+        return resp
+
+    def AnalyzeActuatorPerformance(self, request_iterator, context):
+        import grpc
+        log.info("new analysis stream")
+        try:
+            for t0, color, depth in self._decoded(request_iterator):
+                yield self.analyze_frame(color, depth, t0)
+        except Exception as e:
+            log.error("unhandled exception during analysis: %s", e)
+            context.set_code(grpc.StatusCode.INTERNAL)
+            context.set_details(f"Internal error during analysis: {e}")
+            yield pb.AnalysisResponse()
+
+
+class ModelWatcher(threading.Thread):
+    """Hot reload: poll the registry; when the URI resolves to a new version, copy the weights in place."""
+
+    def __init__(self, cfg: ServeConfig, model, engine: EnginePool, version: Optional[str], period_s: float = 5.0):
+        super().__init__(daemon=True)
+        self.cfg, self.model, self.engine, self.version, self.period = cfg, model, engine, version, period_s
+        self.stop_evt = threading.Event()
+        self.reloads = 0
+
+    def check_once(self) -> bool:
+        from ..mlstore import pytorch as mlpt
+        from ..mlstore.store import FileStore
+        uri = self.cfg.model_uri
+        if self.cfg.hot_reload_alias:
+            name = uri[len("models:/"):].split("/")[0].split("@")[0]
+            uri = f"models:/{name}@{self.cfg.hot_reload_alias}"
+        try:
+            v = registry_version(FileStore(self.cfg.mlruns_dir), uri)
+        except Exception:
+            return False
+        if v is None or v == self.version:
+            return False
+        _, sd = mlpt.load_state(uri, self.cfg.mlruns_dir)
+        with self.engine.exclusive():
+            self.model.load_state_dict(sd)
+            if hasattr(self.model, "refresh_weights"):
+                self.model.refresh_weights()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+        log.info("hot-reloaded %s: version %s -> %s", uri, self.version, v)
+        self.version = v
+        self.reloads += 1
+        return True
+
+    def run(self):
+        while not self.stop_evt.wait(self.period):
+            self.check_once()
+
+
+def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_size: int = 2, port: Optional[int] = None):
+    """Create (server, service, watcher, bound_port); None if resources are missing (reference abort)."""
+    import grpc
+    model, K, ds, version = load_resources(cfg, device)
+    if model is None or K is None or ds is None:
+        log.error("FATAL: could not load all required resources")
+        return None
+    metrics = MetricsLog(cfg.metrics_log)
+    engine = EnginePool(model, K, ds, n=pool_size, threshold=cfg.mask_threshold, graph=cfg.graph,
+                        size=cfg.model_img_size)
+    service = VisionAnalysisService(engine, metrics)
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.max_workers))
+    pb.add_VisionAnalysisServiceServicer_to_server(service, server)
+    bound = server.add_insecure_port(f"{cfg.host}:{cfg.port if port is None else port}")
+    watcher = None
+    if cfg.hot_reload_alias:
+        watcher = ModelWatcher(cfg, model, engine, version)
+    return server, service, watcher, bound
+
+
+def serve(cfg: Optional[ServeConfig] = None, block: bool = True):
+    cfg = cfg or ServeConfig()
+    out = build_server(cfg)
+    if out is None:
+        return None
+    server, service, watcher, port = out
+    server.start()
+    if watcher is not None:
+        watcher.start()
+    log.info("VisionAnalysisService listening on %s:%d", cfg.host, port)
+    if block:
+        server.wait_for_termination()
+    return server, service, watcher, port

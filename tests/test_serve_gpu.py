@@ -1,0 +1,177 @@
+"""Serving path on the GPU: BN-folded eval conv epilogue, eval U-Net vs the fp32 reference,
+preprocess / mask upsample / geometry kernels vs their PyTorch / NumPy references, and the
+graph-captured per-frame pipeline vs the reference semantics (server.py:116-152)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def C():
+    from robotic_discovery_platform_amd.ops import native
+    return native()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(2, 16, 16, 64, 0, 64), (1, 9, 13, 64, 64, 128), (1, 8, 8, 256, 256, 256)])
+def test_conv_eval_bn_fold_epilogue(C, N, H, W, C1, C2, Cout):
+    torch.manual_seed(0)
+    dev = "cuda"
+    bf = torch.bfloat16
+    x1 = torch.randn(N, H, W, C1, device=dev).to(bf)
+    x2 = torch.randn(N, H, W, C2, device=dev).to(bf) if C2 else None
+    w = (torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2))).to(bf)
+    g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    a = torch.empty(N, H, W, Cout, dtype=bf, device=dev)
+    C.conv_fwd(x1, x2, w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous(), 9, 0, a, None, None, 0, coef, 1)
+    xin = torch.cat([x1, x2], -1) if C2 else x1
+    y = F.conv2d(xin.permute(0, 3, 1, 2).float(), w.float(), padding=1)
+    ref = F.relu(F.batch_norm(y, rm, rv, g, b, False, 0.0, 1e-5)).permute(0, 2, 3, 1)
+    assert _rel(a, ref) < 1e-2
+
+
+def test_eval_forward_matches_reference():
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    ref = UNetRef(3, 1).to(dev)
+    with torch.no_grad():  # non-trivial running statistics
+        for n, b in ref.named_buffers():
+            if n.endswith("running_mean"):
+                b.normal_(0, 0.1)
+            elif n.endswith("running_var"):
+                b.uniform_(0.5, 2.0)
+    ref.eval()
+    nat = UNetNative(3, 1, device=dev, init_from=ref.cpu()).eval()
+    ref.to(dev)
+    x = torch.rand(2, 3, 128, 128, device=dev)
+    xq = x.to(torch.bfloat16).float()
+    with torch.no_grad():
+        out = nat(x)
+        r32 = ref(xq)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            r16 = ref(xq).float()
+    e, e16 = _rel(out, r32), _rel(r16, r32)
+    print("native", e, "torch-bf16", e16)
+    assert e < max(2 * e16, 0.02)
+
+
+@pytest.mark.parametrize("H,W", [(480, 640), (720, 1280), (256, 256)])
+def test_preprocess_matches_torch_antialias(C, H, W):
+    from robotic_discovery_platform_amd.serve.engine import aa_tables
+    dev = "cuda"
+    rng = np.random.default_rng(0)
+    bgr = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    ys, yn, yw = aa_tables(H, 256)
+    xs, xn, xw = aa_tables(W, 256)
+    tabs = [torch.from_numpy(a).to(dev) for a in (ys, yn, yw, xs, xn, xw)]
+    out = torch.empty(1, 256, 256, 8, dtype=torch.bfloat16, device=dev)
+    C.preprocess(torch.from_numpy(bgr).to(dev), *tabs, out)
+    rgb = torch.from_numpy(bgr[..., ::-1].copy()).to(dev).permute(2, 0, 1).float() / 255
+    ref = F.interpolate(rgb[None], size=(256, 256), mode="bilinear", align_corners=False, antialias=True)
+    got = out[0, :, :, :3].permute(2, 0, 1).float()
+    assert (got - ref[0]).abs().max().item() < 1 / 128
+    assert out[..., 3:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("H,W", [(480, 640), (720, 1280), (100, 333)])
+def test_mask_upsample_and_count(C, H, W):
+    from robotic_discovery_platform_amd.data.image_io import resize_nearest
+    rng = np.random.default_rng(1)
+    m = (rng.random((256, 256)) < 0.3).astype(np.uint8)
+    out = torch.empty(H, W, dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    C.mask_upsample(torch.from_numpy(m).cuda(), out, cnt)
+    exp = resize_nearest(m, (W, H))
+    assert np.array_equal(out.cpu().numpy(), exp)
+    assert int(cnt.item()) == int(exp.sum())
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_geometry_kernels_match_oracle(seed):
+    from robotic_discovery_platform_amd.config import GeometryConfig
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K, make_scene
+    from robotic_discovery_platform_amd.geometry import reference as ref
+    from robotic_discovery_platform_amd.geometry.curvature import (GeometryEngine, compute_curvature_profile,
+                                                                   sort_edges)
+    sc = make_scene(seed)
+    eng = GeometryEngine(480, 640, torch.device("cuda"), GeometryConfig())
+    m = torch.from_numpy(sc.mask).cuda()
+    d = torch.from_numpy(sc.depth.view(np.int16)).cuda()
+    eng.launch(m, d, DEFAULT_K, 0.001)
+    n, E = int(eng.npts.item()), int(eng.hdr.item())
+    pcd = ref.point_cloud(sc.mask, sc.depth, DEFAULT_K, 0.001)
+    assert n == pcd.shape[0]
+    pts = eng.pts[: n * 4].view(n, 4).cpu().numpy()
+    assert np.array_equal(pts[:, :3], pcd)  # fp64 deprojection, row-major order
+    eo = ref.edge_points(pcd)
+    eo = eo[np.argsort(eo[:, 0], kind="stable")]
+    got = sort_edges(eng.edges[:E].cpu().numpy())
+    assert E == eo.shape[0] and np.array_equal(got, eo)
+    r = compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001, device="cuda")
+    x = ref.compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001)
+    assert r.status == x.status and r.mean_curvature == pytest.approx(x.mean_curvature, rel=1e-7)
+
+
+def test_geometry_early_exits():
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
+    from robotic_discovery_platform_amd.geometry.curvature import compute_curvature_profile
+    depth = np.full((480, 640), 500, np.uint16)
+    r = compute_curvature_profile(np.zeros((480, 640), np.uint8), depth, DEFAULT_K, 0.001, device="cuda")
+    assert r.status == "too_few_points"
+    m = np.zeros((480, 640), np.uint8)
+    m[100:250, 320] = 1
+    r = compute_curvature_profile(m, depth, DEFAULT_K, 0.001, device="cuda")
+    assert r.status == "too_few_edge_points"
+
+
+def test_frame_pipeline_matches_reference_semantics():
+    from robotic_discovery_platform_amd.data.image_io import resize_nearest
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K, make_scene
+    from robotic_discovery_platform_amd.geometry import reference as gref
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.serve.engine import FramePipeline, aa_tables
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    nat = UNetNative(3, 1, device=dev).eval()
+    # bias the head so the random-init network produces a mask with plenty of pixels
+    with torch.no_grad():
+        nat.store.view("outc.conv.bias").fill_(0.0)
+    sc = make_scene(2)
+    pg = FramePipeline(nat, DEFAULT_K, 0.001, graph=True)
+    pe = FramePipeline(nat, DEFAULT_K, 0.001, graph=False)
+    rg = pg.process(sc.color, sc.depth)
+    re_ = pe.process(sc.color, sc.depth)
+    assert np.array_equal(rg.mask, re_.mask) and rg.coverage == re_.coverage
+    # mask == nearest-upsampled (native logits > 0) of the same preprocessed input
+    ex = pe.ex
+    logits = torch.empty(0)
+    head_w = nat.store.view("outc.conv.weight").reshape(-1).float()
+    head_b = nat.store.view("outc.conv.bias").float()
+    lg = (ex.final.float().reshape(-1, 64) @ head_w + head_b).view(256, 256)
+    m256 = (lg > 0).cpu().numpy().astype(np.uint8)
+    exp_full = resize_nearest(m256, (640, 480))
+    agree = (exp_full == rg.mask).mean()
+    assert agree > 0.999, agree  # fp32 vs in-kernel dot order can flip |logit| ~ 0 pixels
+    assert rg.coverage == pytest.approx(100.0 * rg.mask.sum() / rg.mask.size)
+    x = gref.compute_curvature_profile(rg.mask, sc.depth, DEFAULT_K, 0.001)
+    assert rg.curvature.status == x.status
+    assert rg.curvature.mean_curvature == pytest.approx(x.mean_curvature, rel=1e-7, abs=1e-12)
+    # second frame through the graph (buffers reused)
+    sc2 = make_scene(5)
+    r2 = pg.process(sc2.color, sc2.depth)
+    x2 = gref.compute_curvature_profile(r2.mask, sc2.depth, DEFAULT_K, 0.001)
+    assert r2.curvature.status == x2.status
+    assert r2.curvature.max_curvature == pytest.approx(x2.max_curvature, rel=1e-7, abs=1e-12)
