@@ -64,8 +64,9 @@ def setup_dist(args):
         dev = torch.device("cpu")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if dev.type == "cuda" else "gloo"
-        dist.init_process_group(backend=backend, device_id=dev if dev.type == "cuda" else None)
+        # nccl == RCCL on ROCm (xGMI); RDP_DIST_BACKEND=gloo lets several ranks share one GPU in tests
+        backend = os.environ.get("RDP_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
+        dist.init_process_group(backend=backend, device_id=dev if dev.type == "cuda" and backend == "nccl" else None)
     return rank, world, dev
 
 

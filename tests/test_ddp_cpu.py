@@ -1,0 +1,147 @@
+"""Data-parallel path on a fake 2-rank cluster (gloo, CPU processes).
+
+Checks the pieces the RCCL path uses unchanged: FlatBucketer's bucket layout and all-reduce,
+parameter broadcast, DDP gradient equivalence (2 ranks x bs b == 1 process averaging the two
+shard gradients, per-replica BatchNorm like the native path), and rank-0-only store writes in
+train_model.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(fn, world, *args):
+    port = _free_port()
+    mp.spawn(_entry, args=(world, port, fn, args), nprocs=world, join=True)
+
+
+def _entry(rank, world, port, fn, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world, *args)
+    finally:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- bucketer
+def _bucketer_worker(rank, world, out):
+    from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer
+    sizes = [5, 300, 17, 1024, 64, 3, 700]
+    ranges, off = [], 0
+    for i, n in enumerate(sizes):
+        ranges.append((f"p{i}", off, off + n))
+        off += n + (3 if i % 2 else 0)  # alignment gaps like the native ParamStore
+    g = torch.arange(off, dtype=torch.float32) * (rank + 1)
+    b = FlatBucketer(g, ranges, bucket_mb=1200 * 4 / 2 ** 20)
+    # buckets: contiguous, reverse order, cover [0, numel)
+    spans = sorted(b.buckets)
+    assert spans[0][0] == 0 and spans[-1][1] == off
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(len(spans) - 1))
+    assert b.buckets[0][1] == off  # first bucket launched holds the last parameters
+    for _ in range(2):  # reuse across steps
+        g.copy_(torch.arange(off, dtype=torch.float32) * (rank + 1))
+        b.reset()
+        for n, _, _ in reversed(ranges[2:]):
+            b.mark_ready([n])
+        b.finish()  # p0, p1 never marked -> flushed here
+        exp = torch.arange(off, dtype=torch.float32) * sum(r + 1 for r in range(world))
+        assert torch.equal(g, exp)
+    if rank == 0:
+        json.dump({"nbuckets": len(b.buckets)}, open(out, "w"))
+
+
+def test_flat_bucketer_allreduce(tmp_path):
+    out = str(tmp_path / "r.json")
+    _run(_bucketer_worker, 2, out)
+    assert json.load(open(out))["nbuckets"] > 1
+
+
+# ----------------------------------------------------------------------------- gradient equivalence
+def _make(seed):
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    torch.manual_seed(seed)
+    return UNetRef(3, 1, True, base_width=8, depth=2)
+
+
+def _data():
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(4, 3, 32, 32, generator=g)
+    y = (torch.rand(4, 1, 32, 32, generator=g) > 0.5).float()
+    return x, y
+
+
+def _ddp_worker(rank, world, out):
+    from robotic_discovery_platform_amd.train.engine import EagerTrainer
+    model = _make(seed=100 + rank)  # different init per rank: broadcast must fix it
+    tr = EagerTrainer(model, lr=1e-3, bucket_mb=0.01)
+    x, y = _data()
+    sl = slice(rank * 2, rank * 2 + 2)
+    tr.step(x[sl], y[sl])
+    grad = tr.flat_grad.clone()  # all-reduced mean gradient of the step
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    assert torch.equal(gathered[0], gathered[1])
+    if rank == 0:
+        torch.save({"p": flat, "g": grad}, out)
+
+
+def test_ddp_matches_single_process_shard_average(tmp_path):
+    out = str(tmp_path / "p.pt")
+    _run(_ddp_worker, 2, out)
+    got = torch.load(out, weights_only=True)
+    # single process: same init as rank 0, gradient = mean of the two shard gradients
+    model = _make(seed=100)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    x, y = _data()
+    opt.zero_grad()
+    for r in range(2):
+        sl = slice(r * 2, r * 2 + 2)
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(model(x[sl]), y[sl]) / 2
+        loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    opt.step()
+    exp = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    assert torch.allclose(got["g"], g, rtol=1e-4, atol=1e-7), (got["g"] - g).abs().max()
+    # Adam's first step is ~lr*sign(g): only elements with |g| ~ 0 may differ
+    assert (got["p"] - exp).abs().max() < 2.1e-3 and ((got["p"] - exp).abs() > 1e-6).float().mean() < 1e-3
+
+
+# ----------------------------------------------------------------------------- rank-0 writes
+def _train_worker(rank, world, root):
+    from robotic_discovery_platform_amd.config import TrainConfig
+    from robotic_discovery_platform_amd.train.trainer import train_model
+    c = TrainConfig(epochs=1, batch_size=2, image_size=32, synthetic_samples=8, model_depth=2,
+                    dataset_dir=os.path.join(root, "nodata"), mlruns_dir=os.path.join(root, "mlruns"),
+                    model_output_dir=os.path.join(root, "models"), backend="eager", learning_rate=1e-3)
+    res = train_model(c)
+    json.dump({"rank": rank, "version": res.get("registered_version")}, open(os.path.join(root, f"r{rank}.json"), "w"))
+
+
+@pytest.mark.slow
+def test_train_model_two_ranks_rank0_writes(tmp_path):
+    _run(_train_worker, 2, str(tmp_path))
+    r0 = json.load(open(tmp_path / "r0.json"))
+    assert r0["version"] == "1"
+    from robotic_discovery_platform_amd import mlstore
+    st = mlstore.FileStore(str(tmp_path / "mlruns"))
+    assert len(st.search_model_versions("Actuator-Segmenter")) == 1  # only rank 0 registered
+    exp = st.get_experiment_by_name("Actuator Segmentation")
+    runs = st.search_runs(exp["experiment_id"])
+    assert len(runs) == 1 and runs[0].data["params"]["world_size"] == "2"

@@ -1,0 +1,13 @@
+#!/usr/bin/env python3
+"""Entry point at the reference's path (/root/reference/workflows/retraining_pipeline.py): `rdp retrain` with the same defaults.
+
+All options: `python workflows/retraining_pipeline.py --help`. Equivalent: `python -m robotic_discovery_platform_amd retrain`.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
+from robotic_discovery_platform_amd.cli import main  # noqa: E402
+
+if __name__ == "__main__":
+    sys.exit(main(["retrain", *sys.argv[1:]]))
