@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 kernel stats/traces under gpurun_out/ into markdown tables in profiles/.
+
+Writes profiles/train_step_kernels.md (per-kernel totals for 5 native training steps at bs32, plus
+the per-layer conv table for the last step) and profiles/serve_frame_kernels.md (per-kernel totals
+of the serving benchmark), and copies the raw *_kernel_stats.csv next to them.
+"""
+import csv
+import glob
+import io
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def stats_table(path, top=25):
+    rows = list(csv.DictReader(open(path)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    out = ["| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
+    for r in rows[:top]:
+        name = r["Name"].split("(")[0][:80]
+        out.append(f"| `{name}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
+                   f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
+    out.append(f"| **all kernels** | | **{tot / 1e6:.3f}** | | 100 |")
+    return "\n".join(out)
+
+
+def find(pattern):
+    m = glob.glob(os.path.join(ROOT, "gpurun_out", pattern), recursive=True)
+    return sorted(m)[-1] if m else None
+
+
+def main():
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    tr = find("prof_train/**/train_kernel_stats.csv")
+    if tr:
+        shutil.copy(tr, os.path.join(ROOT, "profiles", "train_kernel_stats.csv"))
+        md = ["# Native training step: kernel time (rocprofv3 --kernel-trace --stats)", "",
+              "`bench.py --impl native --batch 32 --steps 3 --warmup 2 --graph 0` on one MI355X (5 steps total, "
+              "eager launches so every kernel is visible).", "", stats_table(tr)]
+        trace = find("prof_train/**/train_kernel_trace.csv")
+        if trace:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "analyze_trace.py"), trace, "32"],
+                               capture_output=True, text=True, cwd=ROOT)
+            md += ["", "## Per-layer conv kernels (last step)", "", "```", r.stdout.strip(), "```"]
+        open(os.path.join(ROOT, "profiles", "train_step_kernels.md"), "w").write("\n".join(md) + "\n")
+        print("wrote profiles/train_step_kernels.md")
+    sv = find("prof_serve/**/serve_kernel_stats.csv")
+    if sv:
+        shutil.copy(sv, os.path.join(ROOT, "profiles", "serve_kernel_stats.csv"))
+        md = ["# Serving benchmark: kernel time (rocprofv3 --kernel-trace --stats)", "",
+              "`python -m robotic_discovery_platform_amd.serve.bench_serve --frames 50 --warmup 10 --train-steps 20` "
+              "(includes the 20 short training steps that produce realistic masks, then per-frame graph replays).",
+              "", stats_table(sv, 40)]
+        open(os.path.join(ROOT, "profiles", "serve_frame_kernels.md"), "w").write("\n".join(md) + "\n")
+        print("wrote profiles/serve_frame_kernels.md")
+
+
+if __name__ == "__main__":
+    main()
