@@ -93,8 +93,11 @@ float* ws_ptr(const c10::optional<torch::Tensor>& ws, int K) {
 // stats slab rows written by conv_fwd: one per (M tile, wave row)
 int conv_stats_rows(long M, int Cout, int bm_pref) {
   bm_pref %= 1000;
-  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return (M + 127) / 128 * 2;
-  return (M + 255) / 256 * 4;
+  if (bm_pref == 128 && Cout % 128 == 0) return (M + 127) / 128 * 2;
+  if (bm_pref == 256) return (M + 255) / 256 * 4;
+  // auto / halo: upper bound over every tile choice (halo: up to 8 wave rows per 256-pixel tile)
+  const long a = (M + 127) / 128 * 2, b = (M + 255) / 256 * 8;
+  return (int)(a > b ? a : b);
 }
 
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)

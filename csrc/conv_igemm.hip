@@ -254,6 +254,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
   }
 }
 
+extern "C" int rdp_conv_halo_tiles(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed);
+extern "C" int rdp_conv_halo(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
+                             int pitch2, const void* w, long wbytes, int ldw, void* y1, void* y2, long ybytes1,
+                             long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats, int N, int H, int W,
+                             int Cout, const float* escale, const float* eshift, int erelu, hipStream_t s);
+
 template <int BM, int BN>
 static int launch_cfg(ConvArgs a, int max_blocks, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM;
@@ -270,6 +276,18 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
                               long ybytes1, long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats,
                               int N, int H, int W, int Cout, int taps, int packed, int bm_pref,
                               const float* escale, const float* eshift, int erelu, hipStream_t s) {
+  // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 128 / 256 = force this kernel's tile
+  {
+    const int pref = bm_pref % 1000;
+    const int ht = rdp_conv_halo_tiles(N, H, W, C1, C2, Cout, taps, packed);
+    // auto: the halo kernel wins only where a 64-channel output reads >= 256 input channels
+    // (measured, scripts/conv_microbench.py); elsewhere this kernel's 2 blocks/CU overlap better
+    const bool halo_auto = pref == 0 && ht >= 256 && Cout == 64 && C1 + C2 >= 256;
+    if (ht > 0 && (pref == 1 || halo_auto))
+      return rdp_conv_halo(x1, x2, xbytes1, xbytes2, C1, C2, pitch1, pitch2, w, wbytes, ldw, y1, y2, ybytes1,
+                           ybytes2, Cy1, ypitch1, ypitch2, stats, N, H, W, Cout, escale, eshift, erelu, s);
+    if (pref == 1) return -1;
+  }
   ConvArgs a;
   a.escale = escale; a.eshift = eshift; a.erelu = erelu;
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;

@@ -57,7 +57,7 @@ def main():
             if a.wgrad:
                 C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
             else:
-                C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, 1000 * v, None, 0)
+                C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, v, None, 0)  # v = bm_pref (1 halo, 128/256 igemm)
 
         for v in variants:
             run(v)
