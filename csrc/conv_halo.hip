@@ -298,6 +298,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(const HaloAr
       }
     }
   }
+  // no LDS-DMA (dummy weight / halo sink loads) may still be in flight when LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int TC, int TR, int WM, int WN>

@@ -13,6 +13,14 @@
 // Block = 4 waves; wave w owns col-subtile w (64 (tap,cin) columns) x 64 output channels.
 // Split-K over pixels; each split writes an fp32 slab [split][Cout][ncols_pad]; rdp_wgrad_reduce
 // sums the splits into the parameter-gradient layout (OHWI, i.e. channels_last OIHW).
+//
+// Measured dead ends (kept out of the code, numbers from scripts/conv_microbench.py at bs32):
+//   * STAGES=3 (one block/CU) and BKP=32 variants: slower than (64, 2) on every layer.
+//   * software L2 prefetch with 4-B-per-lane loads one line per lane: 1.7x SLOWER (64 distinct
+//     lines per wave-instruction saturate the address path, MI355X_MICROARCH.md "access shape").
+//   * DMA issue moved between the MFMA halves: slower (DMA latency matters more than VALU slots).
+// PMC (256^2 x 64ch): ~48 % of wave cycles in s_waitcnt/barrier, i.e. latency-bound on x/dY
+// streamed from HBM with only one K step of lookahead.
 #include "common.h"
 #include <algorithm>
 
