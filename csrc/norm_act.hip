@@ -119,27 +119,41 @@ RDP_DEV void ld8(const float* p, float* f) {
 }
 
 // a = relu(y*scale + shift), 8 channels per thread
-__global__ void bn_relu_apply_kernel(const u16* __restrict__ y, int ypitch, u16* __restrict__ out, int opitch,
-                                     const float* __restrict__ coef, int M, int C, int relu) {
-  const int CG = C >> 3;
-  const long total = (long)M * CG;
-  const float* sc = coef + 2 * C;
-  const float* sh = coef + 3 * C;
-  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
-    const int p = it / CG, g = it - (long)p * CG;
-    const int c = g * 8;
-    float f[8];
-    unpack8(*(const uint4*)(y + (size_t)p * ypitch + c), f);
-    const float4 s0 = *(const float4*)(sc + c), s1 = *(const float4*)(sc + c + 4);
-    const float4 h0 = *(const float4*)(sh + c), h1 = *(const float4*)(sh + c + 4);
-    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+// Elementwise kernels: each thread owns ONE 8-channel group for the whole launch (its BN
+// coefficients stay in registers) and walks pixels with a grid stride, APX pixels in flight
+// (16-B loads), so the loop carries no division and no coefficient reloads.
+#define APX 4
+__global__ __launch_bounds__(256) void bn_relu_apply_kernel(const u16* __restrict__ y, int ypitch,
+                                                            u16* __restrict__ out, int opitch,
+                                                            const float* __restrict__ coef, int M, int C, int relu) {
+  const int CG = C >> 3, RPB = 256 / CG;  // C is a power of two in [8, 2048]
+  const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
+  const int c = g * 8;
+  float ss[8], hh[8];
+  ld8(coef + 2 * C + c, ss);
+  ld8(coef + 3 * C + c, hh);
+  const int stride = gridDim.x * RPB;
+  for (int p0 = blockIdx.x * RPB + r; p0 < M; p0 += stride * APX) {
+    uint4 v[APX];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float z = fmaf(f[k], ss[k], hh[k]);
-      f[k] = relu ? fmaxf(z, 0.f) : z;
+    for (int u = 0; u < APX; ++u) {
+      const int p = p0 + u * stride;
+      if (p < M) v[u] = *(const uint4*)(y + (size_t)p * ypitch + c);
     }
-    *(uint4*)(out + (size_t)p * opitch + c) = pack8(f);
+#pragma unroll
+    for (int u = 0; u < APX; ++u) {
+      const int p = p0 + u * stride;
+      if (p < M) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = fmaf(f[k], ss[k], hh[k]);
+          f[k] = relu ? fmaxf(z, 0.f) : z;
+        }
+        *(uint4*)(out + (size_t)p * opitch + c) = pack8(f);
+      }
+    }
   }
 }
 
@@ -228,32 +242,53 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int T,
   }
 }
 
-__global__ void bn_relu_bwd_apply_kernel(const u16* __restrict__ da, int dapitch, const u16* __restrict__ y,
-                                         int ypitch, const float* __restrict__ coef,
-                                         const float* __restrict__ coef2, u16* __restrict__ dy, int dypitch,
-                                         int M, int C, int relu) {
-  const int CG = C >> 3;
-  const long total = (long)M * CG;
-  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
-    const int p = it / CG, g = it - (long)p * CG;
-    const int c = g * 8;
-    float fd[8], fy[8], o[8], ss[8], hh[8], A[8], B[8], K[8];
-    unpack8(*(const uint4*)(da + (size_t)p * dapitch + c), fd);
-    unpack8(*(const uint4*)(y + (size_t)p * ypitch + c), fy);
-    ld8(coef + 2 * C + c, ss); ld8(coef + 3 * C + c, hh);
-    ld8(coef2 + c, A); ld8(coef2 + C + c, B); ld8(coef2 + 2 * C + c, K);
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(const u16* __restrict__ da, int dapitch,
+                                                                const u16* __restrict__ y, int ypitch,
+                                                                const float* __restrict__ coef,
+                                                                const float* __restrict__ coef2,
+                                                                u16* __restrict__ dy, int dypitch, int M, int C,
+                                                                int relu) {
+  const int CG = C >> 3, RPB = 256 / CG;
+  const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
+  const int c = g * 8;
+  float ss[8], hh[8], A[8], B[8], K[8];
+  ld8(coef + 2 * C + c, ss); ld8(coef + 3 * C + c, hh);
+  ld8(coef2 + c, A); ld8(coef2 + C + c, B); ld8(coef2 + 2 * C + c, K);
+  const int stride = gridDim.x * RPB;
+  for (int p0 = blockIdx.x * RPB + r; p0 < M; p0 += stride * APX) {
+    uint4 vd[APX], vy[APX];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float gg = (!relu || fmaf(fy[k], ss[k], hh[k]) > 0.f) ? fd[k] : 0.f;
-      o[k] = fmaf(A[k], gg, fmaf(B[k], fy[k], K[k]));
+    for (int u = 0; u < APX; ++u) {
+      const int p = p0 + u * stride;
+      if (p < M) {
+        vd[u] = *(const uint4*)(da + (size_t)p * dapitch + c);
+        vy[u] = *(const uint4*)(y + (size_t)p * ypitch + c);
+      }
     }
-    *(uint4*)(dy + (size_t)p * dypitch + c) = pack8(o);
+#pragma unroll
+    for (int u = 0; u < APX; ++u) {
+      const int p = p0 + u * stride;
+      if (p < M) {
+        float fd[8], fy[8], o[8];
+        unpack8(vd[u], fd);
+        unpack8(vy[u], fy);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gg = (!relu || fmaf(fy[k], ss[k], hh[k]) > 0.f) ? fd[k] : 0.f;
+          o[k] = fmaf(A[k], gg, fmaf(B[k], fy[k], K[k]));
+        }
+        *(uint4*)(dy + (size_t)p * dypitch + c) = pack8(o);
+      }
+    }
   }
 }
 
-static int grid_for(long items, int block = 256, int cap = 2048) {
-  long g = (items + block - 1) / block;
-  return (int)std::max<long>(1, std::min<long>(g, cap));
+static bool pow2_channels(int C) { return C >= 8 && C <= 2048 && (C & (C - 1)) == 0; }
+
+static int grid_px(long M, int C) {  // blocks for the pixel-walking elementwise kernels
+  const long rpb = 256 / (C / 8);
+  const long g = (M + rpb * APX - 1) / (rpb * APX);
+  return (int)std::max<long>(1, std::min<long>(g, 2048));
 }
 
 extern "C" {
@@ -275,9 +310,9 @@ int rdp_bn_eval_coef(int C, const float* gamma, const float* beta, const float* 
 
 int rdp_bn_relu_apply(const void* y, int ypitch, void* out, int opitch, const float* coef, int M, int C, int relu,
                       hipStream_t s) {
-  if (C % 8 || ypitch % 8 || opitch % 8) return -1;
-  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 0, s, (const u16*)y, ypitch,
-                     (u16*)out, opitch, coef, M, C, relu);
+  if (!pow2_channels(C) || ypitch % 8 || opitch % 8) return -1;
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(grid_px(M, C)), dim3(256), 0, s, (const u16*)y, ypitch, (u16*)out,
+                     opitch, coef, M, C, relu);
   return 0;
 }
 
@@ -304,9 +339,9 @@ int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const fl
 
 int rdp_bn_relu_bwd_apply(const void* da, int dapitch, const void* y, int ypitch, const float* coef,
                           const float* coef2, void* dy, int dypitch, int M, int C, int relu, hipStream_t s) {
-  if (C % 8) return -1;
-  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3(grid_for((long)M * (C / 8))), dim3(256), 0, s, (const u16*)da,
-                     dapitch, (const u16*)y, ypitch, coef, coef2, (u16*)dy, dypitch, M, C, relu);
+  if (!pow2_channels(C) || dapitch % 8 || ypitch % 8 || dypitch % 8) return -1;
+  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3(grid_px(M, C)), dim3(256), 0, s, (const u16*)da, dapitch,
+                     (const u16*)y, ypitch, coef, coef2, (u16*)dy, dypitch, M, C, relu);
   return 0;
 }
 
