@@ -34,6 +34,9 @@ int rdp_maxpool2_fwd(const void*, int, void*, int, int, int, int, int, hipStream
 int rdp_maxpool2_bwd(const void*, int, const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_upT_shuffle(const void*, int, const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_upT_unshuffle(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_colsum_bf16(const void*, int, long, int, int, float*, float*, int, hipStream_t);
 int rdp_head_partial_blocks(long);
 int rdp_head_fwd(const void*, int, const float*, const float*, const float*, float*, float*, float*, float*, int, float,
                  float, hipStream_t);
@@ -250,6 +253,34 @@ void upsample2_bwd(torch::Tensor dout, torch::Tensor dx, int oy, int ox) {
               "upsample bwd");
 }
 
+// ConvTranspose2d(2, s2): yT [N,h,w,4C] (+bias) -> u [N,H2,W2,C] at offset (oy, ox), zero elsewhere
+void upT_shuffle(torch::Tensor yT, torch::Tensor bias, torch::Tensor u, int oy, int ox) {
+  Act y = act(yT, "yT"), o = act(u, "u");
+  check_f32(bias, "bias");
+  TORCH_CHECK(y.N == o.N && y.C == 4 * o.C && bias.numel() == o.C, "upT_shuffle shapes");
+  TORCH_CHECK(oy >= 0 && ox >= 0 && 2 * y.H + oy <= o.H && 2 * y.W + ox <= o.W, "upT_shuffle placement");
+  TORCH_CHECK(rdp_upT_shuffle(y.ptr, y.pitch, bias.data_ptr<float>(), o.ptr, o.pitch, y.N, y.H, y.W, o.H, o.W, oy, ox,
+                              o.C, cur_stream()) == 0, "upT_shuffle");
+}
+
+void upT_unshuffle(torch::Tensor du, torch::Tensor dyT, int oy, int ox) {
+  Act d = act(du, "du"), y = act(dyT, "dyT");
+  TORCH_CHECK(y.N == d.N && y.C == 4 * d.C, "upT_unshuffle shapes");
+  TORCH_CHECK(oy >= 0 && ox >= 0 && 2 * y.H + oy <= d.H && 2 * y.W + ox <= d.W, "upT_unshuffle placement");
+  TORCH_CHECK(rdp_upT_unshuffle(d.ptr, d.pitch, y.ptr, y.pitch, y.N, y.H, y.W, d.H, d.W, oy, ox, d.C, cur_stream()) == 0,
+              "upT_unshuffle");
+}
+
+// out[c] (+)= sum over pixels and the `groups` channel blocks of x [N,H,W,groups*C]
+void colsum_bf16(torch::Tensor x, int groups, torch::Tensor partial, torch::Tensor out, int accumulate) {
+  Act a = act(x, "x");
+  check_f32(partial, "partial"); check_f32(out, "out");
+  TORCH_CHECK(partial.numel() >= 1024L * a.C && out.numel() * groups == a.C, "colsum_bf16 sizes");
+  TORCH_CHECK(rdp_colsum_bf16(a.ptr, a.pitch, (long)a.N * a.H * a.W, a.C, groups, partial.data_ptr<float>(),
+                              out.data_ptr<float>(), accumulate, cur_stream()) == 0,
+              "colsum_bf16: channels must be a power of two in [8, 2048]");
+}
+
 int head_partial_blocks(long M) { return rdp_head_partial_blocks(M); }
 
 void head_fwd(torch::Tensor a, torch::Tensor w, torch::Tensor b, torch::Tensor target, torch::Tensor logits,
@@ -420,6 +451,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2_fwd", &maxpool2_fwd);
   m.def("maxpool2_bwd", &maxpool2_bwd);
   m.def("upsample2_fwd", &upsample2_fwd);
+  m.def("upT_shuffle", &upT_shuffle);
+  m.def("upT_unshuffle", &upT_unshuffle);
+  m.def("colsum_bf16", &colsum_bf16);
   m.def("upsample2_bwd", &upsample2_bwd);
   m.def("head_partial_blocks", &head_partial_blocks);
   m.def("head_fwd", &head_fwd);

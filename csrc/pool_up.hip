@@ -213,6 +213,100 @@ static int gridN(long items) {
 }
 static float ac_scale(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
 
+// ---- ConvTranspose2d(k=2, s=2) around a 1x1 GEMM (Up block of the transposed decoder) ----
+// Reference op: nn.ConvTranspose2d(cin, cin//2, 2, stride=2) + F.pad in Up.forward
+// (/root/reference/pkg/segmentation_model.py:64,68-74). The GEMM yT[px][(dh*2+dw)*C + c] =
+// sum_ci x[px][ci] W[ci][c][dh][dw] runs on the conv kernel (taps = 1); these kernels move the
+// 2x2 sub-pixels into place (+ bias, zero pad) and back.
+struct UpTGeom {
+  int N, h, w, H2, W2, oy, ox, C;
+};
+
+// u[n][y][x][c..c+7] = yT[n][(y-oy)/2][(x-ox)/2][((y-oy)&1)*2 + ((x-ox)&1)][c..] + bias, 0 outside
+__global__ void upT_shuffle_kernel(const u16* __restrict__ yT, int ypitch, const float* __restrict__ bias,
+                                   u16* __restrict__ u, int upitch, UpTGeom g) {
+  const int CG = g.C >> 3;
+  const long total = (long)g.N * g.H2 * g.W2 * CG;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(it % CG);
+    const long pix = it / CG;
+    const int x = (int)(pix % g.W2);
+    const long t = pix / g.W2;
+    const int y = (int)(t % g.H2), n = (int)(t / g.H2);
+    const int hy = y - g.oy, wx = x - g.ox;
+    const int c = cg * 8;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (hy >= 0 && hy < 2 * g.h && wx >= 0 && wx < 2 * g.w) {
+      const long src = ((long)n * g.h + (hy >> 1)) * g.w + (wx >> 1);
+      const int j = ((hy & 1) * 2 + (wx & 1)) * g.C + c;
+      float f[8];
+      unpack8f(*(const uint4*)(yT + src * ypitch + j), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] += bias[c + k];
+      v = pack8f(f);
+    }
+    *(uint4*)(u + pix * upitch + c) = v;
+  }
+}
+
+// dyT[n][h][w][(dh*2+dw)*C + c] = du[n][2h+dh+oy][2w+dw+ox][c]
+__global__ void upT_unshuffle_kernel(const u16* __restrict__ du, int dpitch, u16* __restrict__ dyT, int ypitch,
+                                     UpTGeom g) {
+  const int CG4 = (4 * g.C) >> 3;
+  const long total = (long)g.N * g.h * g.w * CG4;
+  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+    const int jg = (int)(it % CG4);
+    const long pix = it / CG4;
+    const int ww = (int)(pix % g.w);
+    const long t = pix / g.w;
+    const int hh = (int)(t % g.h), n = (int)(t / g.h);
+    const int j = jg * 8, sub = j / g.C, c = j - sub * g.C;
+    const int y = 2 * hh + (sub >> 1) + g.oy, x = 2 * ww + (sub & 1) + g.ox;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (y >= 0 && y < g.H2 && x >= 0 && x < g.W2) v = *(const uint4*)(du + (((long)n * g.H2 + y) * g.W2 + x) * dpitch + c);
+    *(uint4*)(dyT + pix * ypitch + j) = v;
+  }
+}
+
+// Bias gradient: out[c] (+)= sum_rows sum_{g < groups} x[row][g*C + c]  (x bf16 [M][groups*C]).
+// Stage 1: per-block partial column sums (thread = fixed 8-column group); stage 2: fold + write.
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const u16* __restrict__ x, int pitch, long M, int K,
+                                                          float* __restrict__ partial) {
+  extern __shared__ float sred2[];
+  const int CG = K >> 3, RPB = 256 / CG;  // K = groups*C, power of two <= 2048
+  const int g = threadIdx.x % CG, r = threadIdx.x / CG;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  if (r < RPB)
+    for (long p = blockIdx.x * (long)RPB + r; p < M; p += (long)gridDim.x * RPB) {
+      float f[8];
+      unpack8f(*(const uint4*)(x + p * pitch + g * 8), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += f[k];
+    }
+  if (r < RPB)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sred2[r * K + g * 8 + k] = acc[k];
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < K; cc += 256) {
+    float s = 0.f;
+    for (int q = 0; q < RPB; ++q) s += sred2[q * K + cc];
+    partial[(long)blockIdx.x * K + cc] = s;
+  }
+}
+__global__ void colsum_fold_kernel(const float* __restrict__ partial, int nblk, int K, int groups,
+                                   float* __restrict__ out, int accumulate) {
+  const int C = K / groups;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b)
+    for (int gq = 0; gq < groups; ++gq) s += partial[(long)b * K + gq * C + c];
+  out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+
 extern "C" {
 int rdp_maxpool2_fwd(const void* x, int xpitch, void* out, int opitch, int N, int H, int W, int C, hipStream_t s) {
   if (C % 8 || xpitch % 8 || opitch % 8) return -1;
@@ -242,6 +336,34 @@ int rdp_upsample2_bwd(const void* dout, int dpitch, void* dx, int xpitch, int N,
   UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
   hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(gridN((long)N * hin * win * (C / 8))), dim3(256), 0, s,
                      (const u16*)dout, dpitch, (u16*)dx, xpitch, g);
+  return 0;
+}
+int rdp_upT_shuffle(const void* yT, int ypitch, const float* bias, void* u, int upitch, int N, int h, int w, int H2,
+                    int W2, int oy, int ox, int C, hipStream_t s) {
+  if (C % 8 || ypitch % 8 || upitch % 8) return -1;
+  UpTGeom g{N, h, w, H2, W2, oy, ox, C};
+  hipLaunchKernelGGL(upT_shuffle_kernel, dim3(gridN((long)N * H2 * W2 * (C / 8))), dim3(256), 0, s, (const u16*)yT,
+                     ypitch, bias, (u16*)u, upitch, g);
+  return 0;
+}
+int rdp_upT_unshuffle(const void* du, int dpitch, void* dyT, int ypitch, int N, int h, int w, int H2, int W2, int oy,
+                      int ox, int C, hipStream_t s) {
+  if (C % 8 || ypitch % 8 || dpitch % 8) return -1;
+  UpTGeom g{N, h, w, H2, W2, oy, ox, C};
+  hipLaunchKernelGGL(upT_unshuffle_kernel, dim3(gridN((long)N * h * w * (4 * C / 8))), dim3(256), 0, s,
+                     (const u16*)du, dpitch, (u16*)dyT, ypitch, g);
+  return 0;
+}
+// partial must hold >= 1024 * K floats
+int rdp_colsum_bf16(const void* x, int pitch, long M, int K, int groups, float* partial, float* out, int accumulate,
+                    hipStream_t s) {
+  if (K < 8 || K > 2048 || (K & (K - 1)) || K % groups || pitch % 8) return -1;
+  const int rpb = 256 / (K / 8);
+  const int nblk = (int)std::max<long>(1, std::min<long>(1024, (M + rpb * 16 - 1) / (rpb * 16)));
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3(nblk), dim3(256), (size_t)rpb * K * sizeof(float), s, (const u16*)x,
+                     pitch, M, K, partial);
+  const int C = K / groups;
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((C + 63) / 64), dim3(64), 0, s, partial, nblk, K, groups, out, accumulate);
   return 0;
 }
 }

@@ -65,6 +65,7 @@ class TrainConfig:
     grad_bucket_mb: float = 16.0
     graph: bool = True  # capture the train step in a hipGraph when on GPU
     model_depth: int = 4  # U-Net levels (reference: 4; the plumbing config uses 2)
+    bilinear: bool = True  # decoder: bilinear upsample (reference default) or transposed conv (fixed)
 
 
 @dataclass

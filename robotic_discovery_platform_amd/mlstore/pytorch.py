@@ -83,7 +83,7 @@ def build_model(cfg: dict, backend: str = "auto", device: Optional[torch.device]
               bilinear=cfg.get("bilinear", True), base_width=cfg.get("base_width", 64), depth=cfg.get("depth", 4))
     device = torch.device(device) if device is not None else (torch.device("cuda") if torch.cuda.is_available()
                                                               else torch.device("cpu"))
-    use_native = backend == "native" or (backend == "auto" and device.type == "cuda" and kw["bilinear"])
+    use_native = backend == "native" or (backend == "auto" and device.type == "cuda")
     if use_native:
         from ..models.unet import UNetNative
         return UNetNative(device=device, **kw)

@@ -30,6 +30,18 @@ ALIGN = 64  # elements; keeps every parameter 256-B aligned in fp32, 128-B in bf
 
 
 @dataclass
+class UpTSpec:
+    """ConvTranspose2d(cin, cout, 2, stride=2) of a transposed-decoder Up block, run as a 1x1 GEMM
+    [pixels, cin] x [cin, 4*cout] (conv kernel, taps=1) + sub-pixel shuffle with bias."""
+    name: str  # reference module path, e.g. "up1.up"
+    cin: int
+    cout: int
+
+    def param_names(self) -> List[str]:
+        return [self.name + ".weight", self.name + ".bias"]
+
+
+@dataclass
 class ConvSpec:
     name: str  # reference module path of the conv, e.g. "down1.maxpool_conv.1.double_conv.0"
     bn: str  # reference module path of its BatchNorm
@@ -38,6 +50,9 @@ class ConvSpec:
     taps: int = 9
     packed: bool = False  # first layer: Cin padded to 8, 8 taps per K step
     cin_real: int = 0
+
+    def param_names(self) -> List[str]:
+        return [self.name + ".weight", self.bn + ".weight", self.bn + ".bias"]
 
 
 class ParamStore:
@@ -117,8 +132,6 @@ class UNetNative(nn.Module):
         super().__init__()
         if n_classes != 1:
             raise NotImplementedError("native head supports n_classes == 1 (reference: UNet(3, 1))")
-        if not bilinear:
-            raise NotImplementedError("native transposed-conv decoder not built yet; use UNetRef")
         if n_channels > 8:
             raise NotImplementedError("native first layer packs <= 8 input channels")
         if base_width != 64:
@@ -136,6 +149,12 @@ class UNetNative(nn.Module):
         for name, buf in ref.named_buffers():
             self._register_buffer_path(name, buf.detach().clone().to(device))
         self.specs = unet_conv_specs(depth, base_width, n_channels, bilinear)
+        # transposed decoder: the Up blocks' ConvTranspose2d(cin, cin // 2, 2, 2), up1 .. up_depth
+        self.up_specs: List[UpTSpec] = []
+        if not bilinear:
+            for i in range(1, depth + 1):
+                cin = base_width * (2 ** (depth - i + 1))
+                self.up_specs.append(UpTSpec(f"up{i}.up", cin, cin // 2))
         self._derived_built = False
         self._build_derived()
 
@@ -194,6 +213,13 @@ class UNetNative(nn.Module):
                 segs.append((st.offsets[wname], off, 0, sp.cout, sp.cin, sp.taps))
             self._dw[sp.name] = (off, n)
             off += (n + ALIGN - 1) // ALIGN * ALIGN
+        for us in self.up_specs:
+            # master (channels_last view of [cin, cout, 2, 2]) is physically [cin][(dh, dw, cout)];
+            # the forward GEMM needs its transpose [(dh, dw, cout)][cin] (a taps=1 "dgrad" re-layout)
+            n = us.cin * 4 * us.cout
+            segs.append((st.offsets[us.name + ".weight"], off, 0, us.cin, 4 * us.cout, 1))
+            self._dw[us.name] = (off, n)
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.derived = torch.zeros(max(off, 1), dtype=torch.bfloat16, device=st.device)
         seg_size = C.wseg_size()
         raw = bytearray()
@@ -220,6 +246,13 @@ class UNetNative(nn.Module):
     def dgrad_weight(self, sp: ConvSpec) -> torch.Tensor:
         o, n = self._dw[sp.name]
         return self.derived[o:o + n].view(sp.cin, sp.taps * sp.cout)
+
+    def upT_fwd_weight(self, us: UpTSpec) -> torch.Tensor:
+        o, n = self._dw[us.name]
+        return self.derived[o:o + n].view(4 * us.cout, us.cin)
+
+    def upT_dgrad_weight(self, us: UpTSpec) -> torch.Tensor:
+        return self.store.flat_slice(us.name + ".weight", self.store.shadow).view(us.cin, 4 * us.cout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """NCHW float input -> NCHW fp32 logits (inference helper; training uses UNetExecutor)."""
@@ -314,11 +347,15 @@ class UNetExecutor:
         self.ups: List[torch.Tensor] = []
         self.up_layers: List[Tuple[_Layer, _Layer]] = []
         low = self.skips[D]
+        self.yTs: List[torch.Tensor] = []  # transposed decoder: [N, h_low, w_low, 4 * cout] GEMM outputs
         for i in range(1, D + 1):
             lv = D - i
             h, w = sizes[lv]
-            u = t(h, w, low.shape[3])
+            uc = low.shape[3] if model.bilinear else model.up_specs[i - 1].cout
+            u = t(h, w, uc)
             self.ups.append(u)
+            if not model.bilinear:
+                self.yTs.append(t(low.shape[1], low.shape[2], 4 * uc))
             la = mk(next(it), self.skips[lv], u, h, w)
             lb = mk(next(it), la.a, None, h, w)
             self.up_layers.append((la, lb))
@@ -384,7 +421,20 @@ class UNetExecutor:
             tiles = ((ncols + 255) // 256) * (L.spec.cout // 64)
             L.splits = int(max(1, min((1024 + tiles - 1) // tiles, M // 2048)))
             slab = max(slab, C.wgrad_slab_elems(n, h, w, cin, L.spec.cout, L.spec.taps, int(L.spec.packed), L.splits))
+        self.dyTs: List[torch.Tensor] = [like(y) for y in self.yTs]
+        self.upT_splits: List[int] = []
+        for i, us in enumerate(self.m.up_specs):
+            n, h, w, _ = self.yTs[i].shape
+            M = n * h * w
+            tiles = ((4 * us.cout + 255) // 256) * (us.cin // 64)
+            sp_ = int(max(1, min((1024 + tiles - 1) // tiles, max(1, M // 2048))))
+            self.upT_splits.append(sp_)
+            # roles swapped in conv_wgrad: "x" = dyT (4*cout ch), "dy" = the ConvT input (cin ch)
+            slab = max(slab, C.wgrad_slab_elems(n, h, w, 4 * us.cout, us.cin, 1, 0, sp_))
         self.slab = torch.zeros(slab, dtype=torch.float32, device=dev)
+        if self.m.up_specs:
+            self.colsum_ws = torch.zeros(1024 * max(4 * us.cout for us in self.m.up_specs), dtype=torch.float32,
+                                         device=dev)
         maxc = max(L.spec.cout for L in self.layers)
         self.bn_partial = torch.zeros(1024 * 2 * maxc, dtype=torch.float32, device=dev)
 
@@ -445,7 +495,12 @@ class UNetExecutor:
             u = self.ups[i - 1]
             oy = (u.shape[1] - 2 * low.shape[1]) // 2
             ox = (u.shape[2] - 2 * low.shape[2]) // 2
-            C.upsample2_fwd(low, u, oy, ox)
+            if self.m.bilinear:
+                C.upsample2_fwd(low, u, oy, ox)
+            else:
+                us = self.m.up_specs[i - 1]
+                C.conv_fwd(low, None, self.m.upT_fwd_weight(us), 1, 0, self.yTs[i - 1], None, None, 0, None, 0)
+                C.upT_shuffle(self.yTs[i - 1], self.m.store.view(us.name + ".bias"), u, oy, ox)
             la, lb = self.up_layers[i - 1]
             self._conv_bn_relu(C, la)
             self._conv_bn_relu(C, lb)
@@ -495,12 +550,23 @@ class UNetExecutor:
             la, lb = self.up_layers[i - 1]
             self._conv_bwd(C, lb, grad_hook)
             self._conv_bwd(C, la, grad_hook)
-            # d(low) = upsample backward of du
+            # d(low) = upsample / transposed-conv backward of du
             low_layer = self.down_layers[D][1] if i == 1 else self.up_layers[i - 2][1]
             du = self.dups[i - 1]
             oy = (du.shape[1] - 2 * low_layer.a.shape[1]) // 2
             ox = (du.shape[2] - 2 * low_layer.a.shape[2]) // 2
-            C.upsample2_bwd(du, low_layer.da, oy, ox)
+            if self.m.bilinear:
+                C.upsample2_bwd(du, low_layer.da, oy, ox)
+            else:
+                us = self.m.up_specs[i - 1]
+                dyT = self.dyTs[i - 1]
+                C.upT_unshuffle(du, dyT, oy, ox)
+                C.colsum_bf16(dyT, 4, self.colsum_ws, st.flat_slice(us.name + ".bias", st.grad), 0)
+                C.conv_wgrad(dyT, None, low_layer.a, 1, 0, 4 * us.cout, self.slab,
+                             st.flat_slice(us.name + ".weight", st.grad), 0, self.upT_splits[i - 1], 0)
+                C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0)
+                if grad_hook is not None:
+                    grad_hook(us)
         for i in range(D, 0, -1):
             la, lb = self.down_layers[i]
             self._conv_bwd(C, lb, grad_hook)
@@ -511,13 +577,15 @@ class UNetExecutor:
         self._conv_bwd(C, l1, grad_hook)
         self._conv_bwd(C, l0, grad_hook)
 
-    def backward_order(self) -> List[ConvSpec]:
+    def backward_order(self) -> List:
         """Conv layers in the order their gradients become final during backward()."""
         D = self.m.depth
         out = []
         for i in range(D, 0, -1):
             la, lb = self.up_layers[i - 1]
             out += [lb.spec, la.spec]
+            if not self.m.bilinear:
+                out.append(self.m.up_specs[i - 1])
         for i in range(D, 0, -1):
             la, lb = self.down_layers[i]
             out += [lb.spec, la.spec]

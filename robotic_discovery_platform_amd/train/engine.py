@@ -40,8 +40,7 @@ class NativeTrainer:
             model.refresh_weights()
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
             self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb)
-            self._layer_params = {sp.name: [sp.name + ".weight", sp.bn + ".weight", sp.bn + ".bias"]
-                                  for sp in model.specs}
+            self._layer_params = {sp.name: sp.param_names() for sp in list(model.specs) + list(model.up_specs)}
         self.use_graph = graph and self.world == 1 and torch.cuda.is_available()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.steps = 0
@@ -161,11 +160,10 @@ class EagerTrainer:
 def build_bench_step(batch: int, size: int, decoder: str, device: torch.device, world: int, graph: bool,
                      bucket_mb: float, loss: str = "bce"):
     """bench.py hook: returns a zero-arg callable running one full native training step."""
-    if decoder != "bilinear":
-        raise NotImplementedError("native bench runs the reference (bilinear) decoder")
+    bilinear = decoder == "bilinear"
     torch.manual_seed(0)
-    ref = UNetRef(3, 1, bilinear=True)
-    model = UNetNative(3, 1, bilinear=True, device=device, init_from=ref)
+    ref = UNetRef(3, 1, bilinear=bilinear)
+    model = UNetNative(3, 1, bilinear=bilinear, device=device, init_from=ref)
     tr = NativeTrainer(model, batch, size, size, loss=loss, graph=graph, bucket_mb=bucket_mb)
     g = torch.Generator(device="cpu").manual_seed(1234 + tr.rank)
     x = torch.rand(batch, 3, size, size, generator=g).to(device)

@@ -160,7 +160,7 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
     sampler = DistributedShardSampler(len(train_set), rank, world, shuffle=True, seed=cfg.seed)
 
     # ---- model / engine ----
-    ref = UNetRef(3, 1, bilinear=True, depth=cfg.model_depth)
+    ref = UNetRef(3, 1, bilinear=cfg.bilinear, depth=cfg.model_depth)
     if backend == "native":
         from ..models.unet import UNetNative
         model = UNetNative(3, 1, depth=cfg.model_depth, device=dev, init_from=ref)

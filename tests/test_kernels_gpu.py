@@ -324,3 +324,43 @@ def test_adam_matches_torch(C):
     assert step.item() == 5
     assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5)
     assert torch.equal(sh, p.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout,H2,W2", [(2, 8, 8, 128, 64, 16, 16), (1, 4, 5, 256, 128, 9, 11)])
+def test_conv_transpose2x2(C, N, h, w, Cin, Cout, H2, W2):
+    """ConvTranspose2d(k=2, s=2) as taps=1 GEMM + shuffle(+bias, zero pad), and its backward
+    (unshuffle, bias colsum, role-swapped wgrad, dgrad) vs torch fp32."""
+    torch.manual_seed(5)
+    dev = "cuda"
+    x = bf(torch.randn(N, Cin, h, w, device=dev))
+    W = bf(torch.randn(Cin, Cout, 2, 2, device=dev) / math.sqrt(Cin))
+    b = torch.randn(Cout, device=dev)
+    oy, ox = (H2 - 2 * h) // 2, (W2 - 2 * w) // 2
+    xr = x.float().requires_grad_(True)
+    Wr = W.float().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    y = F.conv_transpose2d(xr, Wr, br, stride=2)
+    ref = F.pad(y, [ox, W2 - 2 * w - ox, oy, H2 - 2 * h - oy])
+    wphys = W.permute(0, 2, 3, 1).reshape(Cin, 4 * Cout).contiguous()  # [ci][(dh, dw, co)]
+    yT = torch.empty(N, h, w, 4 * Cout, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(nhwc(x), None, wphys.t().contiguous(), 1, 0, yT, None, None, 0, None, 0)
+    u = torch.full((N, H2, W2, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    C.upT_shuffle(yT, b, u, oy, ox)
+    assert relerr(nchw(u), ref) < 1e-2
+    # backward
+    du = bf(torch.randn(N, Cout, H2, W2, device=dev))
+    ref.backward(du.float())
+    dyT = torch.empty_like(yT)
+    C.upT_unshuffle(nhwc(du), dyT, oy, ox)
+    db = torch.zeros(Cout, device=dev)
+    C.colsum_bf16(dyT, 4, torch.zeros(1024 * 4 * Cout, device=dev), db, 0)
+    assert torch.allclose(db, br.grad, rtol=1e-3, atol=1e-2)
+    M = N * h * w
+    splits = max(1, M // 64)
+    slab = torch.zeros(C.wgrad_slab_elems(N, h, w, 4 * Cout, Cin, 1, 0, splits), device=dev)
+    gw = torch.zeros(Cin * 4 * Cout, device=dev)
+    C.conv_wgrad(dyT, None, nhwc(x), 1, 0, 4 * Cout, slab, gw, 0, splits, 0)
+    assert relerr(gw.view(Cin, 2, 2, Cout).permute(0, 3, 1, 2), Wr.grad) < 1e-2
+    dx = torch.empty(N, h, w, Cin, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(dyT, None, wphys, 1, 0, dx, None, None, 0, None, 0)
+    assert relerr(nchw(dx), xr.grad) < 1e-2
