@@ -49,7 +49,8 @@ def parse():
     p.add_argument("--graph", type=int, default=1, help="capture the native step in a hipGraph")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--loss", choices=["bce", "bce_dice"], default="bce")
-    p.add_argument("--serve", type=int, default=0, help="also measure e2e serving FPS / p50 latency")
+    p.add_argument("--serve", type=int, default=-1,
+                   help="also measure e2e serving FPS / p50 latency (default: on for single-GPU runs)")
     return p.parse_args()
 
 
@@ -131,9 +132,13 @@ def main():
     ms = dt / args.steps * 1e3
     imgs = args.batch * world * args.steps / dt
     extra = {}
-    if args.serve and rank == 0:
-        from robotic_discovery_platform_amd.serve.bench_serve import measure_serving
-        extra = measure_serving(dev)
+    serve = args.serve if args.serve >= 0 else int(world == 1 and args.impl == "native" and dev.type == "cuda")
+    if serve and rank == 0:
+        try:  # second half of the metric; never let it break the training result line
+            from robotic_discovery_platform_amd.serve.bench_serve import measure_serving
+            extra = measure_serving(dev)
+        except Exception as e:  # pragma: no cover - reported in the JSON
+            extra = {"serve_error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         out = {
             "metric": METRIC,

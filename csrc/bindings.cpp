@@ -11,7 +11,8 @@
 extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
-                   hipStream_t);
+                   float*, long, hipStream_t);
+long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
                   double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, hipStream_t);
@@ -106,7 +107,7 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)
 int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, int taps, int packed,
              torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref,
-             c10::optional<torch::Tensor> affine, int relu) {
+             c10::optional<torch::Tensor> affine, int relu, c10::optional<torch::Tensor> ws) {
   Act a1 = act(x1, "x1"), a2;
   if (x2) {
     a2 = act(*x2, "x2");
@@ -134,10 +135,12 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     esc = affine->data_ptr<float>() + 2 * Cout;
     esh = affine->data_ptr<float>() + 3 * Cout;
   }
+  if (ws) check_f32(*ws, "ws");
   const int r = rdp_conv_igemm(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
                                a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1), o1.ptr,
                                y2 ? o2.ptr : nullptr, o1.bytes, y2 ? o2.bytes : 0, o1.C, o1.pitch, y2 ? o2.pitch : 0,
-                               sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu, cur_stream());
+                               sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu,
+                               ws ? ws->data_ptr<float>() : nullptr, ws ? (long)ws->numel() : 0L, cur_stream());
   TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
   return r;
 }
@@ -438,7 +441,12 @@ void mask_upsample(torch::Tensor m, torch::Tensor out, torch::Tensor count) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "rdp MI355X (gfx950) HIP kernels";
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
+        py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
+        py::arg("ws") = py::none());
+  m.def("conv_ws_elems", [](int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
+    return rdp_conv_ws_elems(N, H, W, C1, C2, Cout, taps, packed, bm_pref);
+  });
   m.def("conv_stats_rows", &conv_stats_rows);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_slab_elems", &wgrad_slab_elems);

@@ -46,8 +46,10 @@ struct ConvArgs {
   int N, H, W, Cout, M;
   int taps;  // 9 (3x3) or 1 (1x1)
   int packed;  // 1: Cin == 8, K packs 8 taps per 64-wide K step
-  int nks;  // number of K steps per tile
+  int nks;  // number of K steps per work item (= per tile unless split-K)
   int cpt;  // 64-channel chunks per tap (generic mode)
+  int ksplit;    // > 1: split-K, work item = (tile, split), fp32 partial tiles go to kslab
+  float* kslab;  // [ksplit][M][Cout] fp32
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
 };
@@ -84,8 +86,14 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
   int pm[NROW];
   uint32_t tmask[NROW];
   uint32_t woff[WPIECES];
+  int itap = 0, icc = 0;  // (tap, 64-channel chunk) of the stage being issued (generic mode)
+  int ks0 = 0;  // first global K step of the work item being staged (split-K)
   auto set_tile = [&](int t) {
-    const int tile = (int)lid + t * (int)G;
+    const int item = (int)lid + t * (int)G;
+    const int tile = a.ksplit > 1 ? item % (a.ntiles / a.ksplit) : item;
+    ks0 = a.ksplit > 1 ? (item / (a.ntiles / a.ksplit)) * a.nks : 0;
+    itap = ks0 / a.cpt;
+    icc = ks0 - itap * a.cpt;
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
@@ -114,7 +122,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     }
   };
 
-  int itap = 0, icc = 0;  // (tap, 64-channel chunk) of the stage being issued (generic mode)
   auto issue = [&](int ks, char* buf) {
     if (a.packed) {
       const int tap = ks * 8 + gch;  // per lane; taps >= 9 have no mask bit -> zeros
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     char* wbuf = buf + P_BYTES;
 #pragma unroll
     for (int f = 0; f < WPIECES; ++f)
-      dma16(rw, (lds_void*)(wbuf + (wave * WPIECES + f) * 1024), woff[f] + (uint32_t)ks * 128u);
+      dma16(rw, (lds_void*)(wbuf + (wave * WPIECES + f) * 1024), woff[f] + (uint32_t)(ks0 + ks) * 128u);
   };
 
   // LDS byte offsets of this lane's fragment reads (k-half hf) relative to a 16-row subtile
@@ -191,8 +198,29 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
 
     // ---- epilogue of tile t: acc[j][i][r] = out[m = m0 + wm*64 + 16i + (lane&15)][n = n0 + wn*64 + 16j + 4*(lane>>4) + r]
     ks = 0;
-    const int tile = (int)lid + t * (int)G;
+    const int item = (int)lid + t * (int)G;
     ++t;
+    if (a.ksplit > 1) {  // fp32 partial tile -> slab[split][m][n]; epilogue runs in the reduce
+      const int tiles1 = a.ntiles / a.ksplit;
+      const int tile = item % tiles1, split = item / tiles1;
+      const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
+      const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = tm * BM + wm * 64 + i * 16 + (lane & 15);
+          const f32x4 o = acc[j][i];
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          const uint32_t off = m < a.M ? (uint32_t)(((long)split * a.M + m) * a.Cout + n) * 4u : RDP_OOB;
+          bstore16(rk, off, make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
+                                       __float_as_uint(o[3])));
+        }
+      }
+      continue;
+    }
+    const int tile = item;
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
     float s1[4][4], s2[4][4];
@@ -260,11 +288,101 @@ extern "C" int rdp_conv_halo(const void* x1, const void* x2, long xbytes1, long 
                              long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats, int N, int H, int W,
                              int Cout, const float* escale, const float* eshift, int erelu, hipStream_t s);
 
+// Split-K reduction + epilogue: y[m][n] = epi(sum_s slab[s][m][n]); optional BN-stats rows (one per
+// block). Thread = fixed 8-channel group (epilogue coefficients in registers), rows grid-strided.
+__global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs a, int nrow_blocks) {
+  extern __shared__ float sst[];  // [rows][2][8 per thread-group] stats staging
+  const int CG = a.Cout >> 3, RPB = 256 / CG;  // Cout power of two, <= 2048
+  const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
+  const int n = g * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = a.escale ? a.escale[n + k] : 1.f; sh[k] = a.eshift ? a.eshift[n + k] : 0.f; }
+  const bool d2 = n >= a.Cy1;
+  const int nn = d2 ? n - a.Cy1 : n;
+  u16* const y = d2 ? a.y2 : a.y1;
+  const int yp = d2 ? a.ypitch2 : a.ypitch1;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  for (int m = blockIdx.x * RPB + r; m < a.M; m += nrow_blocks * RPB) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+    for (int sp = 0; sp < a.ksplit; ++sp) {
+      const float* p = a.kslab + ((long)sp * a.M + m) * a.Cout + n;
+      const float4 p0 = *(const float4*)p, p1 = *(const float4*)(p + 4);
+      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = fmaf(v[k], sc[k], sh[k]);
+      if (a.erelu) v[k] = fmaxf(v[k], 0.f);
+    }
+    uint4 o;
+    o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]); o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+    *(uint4*)(y + (long)m * yp + nn) = o;
+    if (a.stats) {
+      const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float q0 = __uint_as_float(w[k] << 16), q1 = __uint_as_float(w[k] & 0xffff0000u);
+        s1[2 * k] += q0; s2[2 * k] += q0 * q0;
+        s1[2 * k + 1] += q1; s2[2 * k + 1] += q1 * q1;
+      }
+    }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sst[(r * 2 + 0) * a.Cout + n + k] = s1[k];
+    sst[(r * 2 + 1) * a.Cout + n + k] = s2[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * a.Cout; c += 256) {
+    const int half = c / a.Cout, ch = c - half * a.Cout;
+    float acc = 0.f;
+    for (int q = 0; q < RPB; ++q) acc += sst[(q * 2 + half) * a.Cout + ch];
+    a.stats[(long)blockIdx.x * 2 * a.Cout + c] = acc;
+  }
+}
+
+// Split-K when the tile grid leaves most CUs idle: the smallest divisor of the K steps that gives
+// >= 256 work items with >= 4 K steps each, as long as the fp32 slab fits `ws_elems`.
+static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long ws_elems) {
+  const bool pow2 = Cout >= 8 && Cout <= 2048 && (Cout & (Cout - 1)) == 0;
+  int ks = 1;
+  if (!pow2 || packed || ntiles >= 192) return 1;
+  for (int d = 2; d <= nks / 4; ++d) {
+    if (nks % d) continue;
+    if ((long)d * M * Cout > ws_elems) break;
+    ks = d;
+    if (ntiles * d >= 256) break;
+  }
+  return ks;
+}
+
 template <int BM, int BN>
-static int launch_cfg(ConvArgs a, int max_blocks, hipStream_t s) {
+static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
   a.ntiles = tilesM * a.tilesN;
+  a.ksplit = a.kslab ? choose_ksplit(a.ntiles, a.nks, a.M, a.Cout, a.packed, ws_elems) : 1;
+  if (a.ksplit > 1) {
+    a.nks /= a.ksplit;
+    a.ntiles *= a.ksplit;
+    const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(grid), dim3(256), 0, s, a);
+    const int rpb = 256 / (a.Cout / 8);
+    const int cap = tilesM * (BM / 64);  // <= conv_stats_rows() bound
+    int nblk = (a.M + rpb - 1) / rpb;
+    nblk = nblk < 512 ? nblk : 512;
+    nblk = nblk < cap ? nblk : cap;
+    const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
+    return nblk;
+  }
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
   hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(grid), dim3(256), 0, s, a);
   return tilesM * (BM / 64);
@@ -275,7 +393,8 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
                               int pitch1, int pitch2, const void* w, long wbytes, int ldw, void* y1, void* y2,
                               long ybytes1, long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats,
                               int N, int H, int W, int Cout, int taps, int packed, int bm_pref,
-                              const float* escale, const float* eshift, int erelu, hipStream_t s) {
+                              const float* escale, const float* eshift, int erelu, float* ws, long ws_elems,
+                              hipStream_t s) {
   // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 128 / 256 = force this kernel's tile
   {
     const int pref = bm_pref % 1000;
@@ -290,6 +409,9 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   }
   ConvArgs a;
   a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  a.kslab = ws;
+  a.ksplit = 1;
+  const long wse = ws_elems < (1L << 29) ? ws_elems : (1L << 29);  // slab bytes < 2 GiB (buffer offsets)
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
   a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
   a.C1 = C1; a.C2 = C2; a.pitch1 = pitch1; a.pitch2 = pitch2;
@@ -317,6 +439,20 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   bm_pref %= 1000;
   if (per_cu == 0) per_cu = 2;
   const int max_blocks = 256 * per_cu;
-  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, s);
-  return launch_cfg<256, 64>(a, max_blocks, s);
+  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s);
+  return launch_cfg<256, 64>(a, max_blocks, wse, s);
+}
+
+// fp32 workspace elements the auto dispatch would use for split-K on this shape (0 = no split)
+extern "C" long rdp_conv_ws_elems(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
+  const int pref = bm_pref % 1000;
+  const int ht = rdp_conv_halo_tiles(N, H, W, C1, C2, Cout, taps, packed);
+  if (ht > 0 && (pref == 1 || (pref == 0 && ht >= 256 && Cout == 64 && C1 + C2 >= 256))) return 0;
+  if (packed) return 0;
+  const int M = N * H * W;
+  const int nks = taps * ((C1 + C2) / 64);
+  const int BM = ((pref == 128 || pref == 0) && Cout % 128 == 0) ? 128 : 256, BN = BM == 128 ? 128 : 64;
+  const int ntiles = (M + BM - 1) / BM * (Cout / BN);
+  const int d = choose_ksplit(ntiles, nks, M, Cout, packed, 1L << 29);
+  return d > 1 ? (long)d * M * Cout : 0;
 }

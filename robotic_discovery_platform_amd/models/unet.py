@@ -372,6 +372,21 @@ class UNetExecutor:
                        for L in self.layers)
         self.stats = torch.zeros(max_rows, dtype=torch.float32, device=dev)
         self.red_ws = torch.zeros(64 * 2 * max(L.spec.cout for L in self.layers), dtype=torch.float32, device=dev)
+        # split-K workspace (fp32 partial tiles) for the convs whose tile grid alone underfills the
+        # chip (deep layers at small batch, e.g. serving at N=1); shared: convs run in sequence
+        ws = 0
+        for L in self.layers:
+            n, h, w, c1 = L.x1.shape
+            c2 = L.x2.shape[3] if L.x2 is not None else 0
+            ws = max(ws, C.conv_ws_elems(n, h, w, c1, c2, L.spec.cout, L.spec.taps, int(L.spec.packed), 0))
+            if training and not L.spec.packed:  # dgrad: dy (cout ch) -> d(input) (c1 + c2 ch)
+                ws = max(ws, C.conv_ws_elems(n, h, w, L.spec.cout, 0, c1 + c2, L.spec.taps, 0, 0))
+        for i, us in enumerate(model.up_specs):
+            n, h, w, _ = self.yTs[i].shape
+            ws = max(ws, C.conv_ws_elems(n, h, w, us.cin, 0, 4 * us.cout, 1, 0, 0))
+            if training:
+                ws = max(ws, C.conv_ws_elems(n, h, w, 4 * us.cout, 0, us.cin, 1, 0, 0))
+        self.kws = torch.zeros(ws, dtype=torch.float32, device=dev) if ws else None
         if training:
             self._alloc_backward(C)
         else:
@@ -456,9 +471,9 @@ class UNetExecutor:
         m = self.m
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
-            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1)
+            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws)
             return
-        rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0)
+        rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
         g = m.store.view(sp.bn + ".weight")
         b = m.store.view(sp.bn + ".bias")
         if self.training:
@@ -475,11 +490,15 @@ class UNetExecutor:
             C.bn_eval_coef(m.store.view(sp.bn + ".weight"), m.store.view(sp.bn + ".bias"),
                            m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"), 1e-5, L.coef)
 
-    def forward(self, head: bool = True):
-        """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead)."""
+    def forward(self, head: bool = True, refresh_eval: bool = True):
+        """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead).
+
+        Eval mode folds BN into the conv epilogues with coefficients from the running statistics;
+        ``refresh_eval=False`` reuses the coefficients from the last ``prepare_eval()`` (the serving
+        pipeline recomputes them only when the weights change, not per frame)."""
         C = _native()
         D = self.m.depth
-        if not self.training:
+        if not self.training and refresh_eval:
             self.prepare_eval()
         l0, l1 = self.down_layers[0]
         self._conv_bn_relu(C, l0)
@@ -499,7 +518,8 @@ class UNetExecutor:
                 C.upsample2_fwd(low, u, oy, ox)
             else:
                 us = self.m.up_specs[i - 1]
-                C.conv_fwd(low, None, self.m.upT_fwd_weight(us), 1, 0, self.yTs[i - 1], None, None, 0, None, 0)
+                C.conv_fwd(low, None, self.m.upT_fwd_weight(us), 1, 0, self.yTs[i - 1], None, None, 0, None, 0,
+                           self.kws)
                 C.upT_shuffle(self.yTs[i - 1], self.m.store.view(us.name + ".bias"), u, oy, ox)
             la, lb = self.up_layers[i - 1]
             self._conv_bn_relu(C, la)
@@ -533,7 +553,7 @@ class UNetExecutor:
         gw = st.flat_slice(sp.name + ".weight", st.grad)
         C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw, 0, L.splits, 0)
         if L.dx1 is not None:
-            C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0)
+            C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:
             hooks(sp)
 
@@ -564,7 +584,8 @@ class UNetExecutor:
                 C.colsum_bf16(dyT, 4, self.colsum_ws, st.flat_slice(us.name + ".bias", st.grad), 0)
                 C.conv_wgrad(dyT, None, low_layer.a, 1, 0, 4 * us.cout, self.slab,
                              st.flat_slice(us.name + ".weight", st.grad), 0, self.upT_splits[i - 1], 0)
-                C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0)
+                C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
+                           self.kws)
                 if grad_hook is not None:
                     grad_hook(us)
         for i in range(D, 0, -1):

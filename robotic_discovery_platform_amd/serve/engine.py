@@ -122,12 +122,14 @@ class FramePipeline:
         self.lock = threading.Lock()
         if graph:
             self._capture()
+        else:
+            self.refresh_weights()
 
     # ---------------------------------------------------------------- device program
     def _device_program(self):
         C, ex, m = self.C, self.ex, self.model
         C.preprocess(self.d_color, *self.tab, ex.x_in)
-        ex.forward(head=False)
+        ex.forward(head=False, refresh_eval=False)  # BN-fold coefficients: see refresh_weights()
         C.head_mask(ex.final, m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
                     self.thr_logit, self.m256)
         C.mask_upsample(self.m256.view(self.S, self.S), self.mask, self.meta[0:1])
@@ -135,7 +137,15 @@ class FramePipeline:
         self.meta[1:2].copy_(self.geo.hdr)
         self.meta[2:3].copy_(self.geo.npts)
 
+    def refresh_weights(self):
+        """Recompute the BN-fold coefficients from the current weights / running stats (after a
+        hot reload). The captured graph reads them from fixed buffers, so it stays valid."""
+        with torch.cuda.stream(self.stream):
+            self.ex.prepare_eval()
+        self.stream.synchronize()
+
     def _capture(self):
+        self.refresh_weights()
         with torch.cuda.stream(self.stream):
             self._device_program()  # warm-up (lazy allocations, kernel loading)
         self.stream.synchronize()
@@ -193,6 +203,9 @@ class CpuFramePipeline:
         self.cfg = geo_cfg or GeometryConfig()
         self.lock = threading.Lock()
 
+    def refresh_weights(self):
+        pass  # the torch module reads its parameters directly
+
     def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
         import torch.nn.functional as F
         from ..data.image_io import resize_nearest
@@ -241,15 +254,22 @@ class EnginePool:
 
     @contextlib.contextmanager
     def exclusive(self):
-        """Hold every pipeline (no frame in flight), e.g. while weights are swapped in place."""
+        """Hold every pipeline (no frame in flight), e.g. while weights are swapped in place;
+        yields the held pipelines."""
         with self._mk_lock:
             qs = list(self._pools.values())
             held = [(q, q.get()) for q in qs for _ in range(self.n)]
             try:
-                yield
+                yield [p for _, p in held]
             finally:
                 for q, p in held:
                     q.put(p)
+
+    @staticmethod
+    def refresh_weights(pipelines):
+        """After the shared weights changed (inside ``exclusive()``): refresh derived state."""
+        for p in pipelines:
+            p.refresh_weights()
 
     def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
         q = self._get(*depth.shape[:2])

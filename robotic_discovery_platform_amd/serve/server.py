@@ -12,8 +12,9 @@ Behaviour of ``/root/reference/services/vision_analysis/server.py:22-183``:
 
 Differences: ``status``, ``mask_coverage`` and ``proc_time_ms`` are populated (a
 wire-compatible superset); the CSV writer is locked and keeps its handle open (the reference appends
-from 10 threads without a lock); frames of one stream are decoded one ahead on a helper thread so
-host codecs overlap the device program; the model can hot-reload when a registry alias moves.
+from 10 threads without a lock); colour and depth are decoded concurrently on a codec thread pool,
+up to ``prefetch`` frames ahead, so host codecs overlap the device program; the model can hot-reload
+when a registry alias moves.
 """
 from __future__ import annotations
 
@@ -103,14 +104,18 @@ def registry_version(store, uri: str) -> Optional[str]:
 
 
 class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
-    def __init__(self, engine: EnginePool, metrics: Optional[MetricsLog] = None, prefetch: int = 2):
+    def __init__(self, engine: EnginePool, metrics: Optional[MetricsLog] = None, prefetch: int = 4,
+                 decode_workers: int = 8):
         self.engine = engine
         self.metrics = metrics
         self.prefetch = prefetch
         self.frames = 0
+        # shared host-codec pool: JPEG / 16-bit PNG decodes release the GIL, so colour and depth of a
+        # frame, and up to `prefetch` frames of a stream, decode concurrently
+        self._pool = futures.ThreadPoolExecutor(max_workers=decode_workers, thread_name_prefix="rdp-decode")
 
     def _decoded(self, request_iterator):
-        """Decode requests one ahead on a helper thread (host codecs overlap device work)."""
+        """Yield (t0, colour, depth) in request order; decoding runs ahead on the codec pool."""
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         END = object()
 
@@ -118,10 +123,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             try:
                 for req in request_iterator:
                     t = time.perf_counter()
-                    color = decode_image(req.color_image.data, True)
-                    depth = decode_image(req.depth_image.data, False)
-                    q.put((t, color, depth, None))
-            except Exception as e:  # surface decode / transport errors in the handler thread
+                    fc = self._pool.submit(decode_image, req.color_image.data, True)
+                    fd = self._pool.submit(decode_image, req.depth_image.data, False)
+                    q.put((t, fc, fd, None))
+            except Exception as e:  # surface transport errors in the handler thread
                 q.put((None, None, None, e))
             q.put(END)
 
@@ -133,7 +138,8 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                 return
             if item[3] is not None:
                 raise item[3]
-            yield item[:3]
+            t, fc, fd, _ = item
+            yield t, fc.result(), fd.result()
 
     def analyze_frame(self, color: np.ndarray, depth: np.ndarray, t0: Optional[float] = None):
         t0 = time.perf_counter() if t0 is None else t0
@@ -188,10 +194,11 @@ class ModelWatcher(threading.Thread):
         if v is None or v == self.version:
             return False
         _, sd = mlpt.load_state(uri, self.cfg.mlruns_dir)
-        with self.engine.exclusive():
+        with self.engine.exclusive() as pipelines:
             self.model.load_state_dict(sd)
             if hasattr(self.model, "refresh_weights"):
                 self.model.refresh_weights()
+            self.engine.refresh_weights(pipelines)
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
         log.info("hot-reloaded %s: version %s -> %s", uri, self.version, v)

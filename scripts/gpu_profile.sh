@@ -13,4 +13,7 @@ echo train_prof_ok
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_serve -o serve --output-format csv -- \
   python3 -m robotic_discovery_platform_amd.serve.bench_serve --frames 50 --warmup 10 --train-steps 20 > $R/gpurun_out/prof_serve.log 2>&1 || { echo serve_prof_failed; tail -20 $R/gpurun_out/prof_serve.log; exit 1; }
 echo serve_prof_ok
+cd $R
+timeout -k 10 300 python3 scripts/conv_microbench.py --variants 0,1,128 --rounds 3 > gpurun_out/micro_fwd.log 2>&1 || { echo micro_failed; exit 1; }
+timeout -k 10 300 python3 scripts/conv_microbench.py --wgrad --variants 0 --rounds 3 > gpurun_out/micro_wgrad.log 2>&1 || { echo micro_failed; exit 1; }
 cd $R && python3 scripts/profile_summary.py

@@ -59,5 +59,42 @@ def main():
         print("wrote profiles/serve_frame_kernels.md")
 
 
+def micro_table(paths):
+    rows = []
+    for p in paths:
+        for line in open(p):
+            line = line.strip()
+            if line.startswith("{") and '"shape"' in line:
+                import json
+                rows.append(json.loads(line))
+    if not rows:
+        return None
+    keys = sorted({k for r in rows for k in r if k.endswith("_tflops")})
+    out = ["| layer shape | kind | " + " | ".join(k.replace("_tflops", " TF/s") for k in keys) + " |",
+           "|---|---|" + "---:|" * len(keys)]
+    for r in rows:
+        out.append(f"| {r['shape']} | {r['kind']} | " + " | ".join(str(r.get(k, "")) for k in keys) + " |")
+    return "\n".join(out)
+
+
+def micro_main():
+    paths = sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "micro_*.log")))
+    t = micro_table(paths)
+    if t:
+        md = ["# Conv kernels per U-Net layer shape (scripts/conv_microbench.py, bs 32, median of rounds)", "",
+              "fwd variants: v0 = auto dispatch, v1 = halo-tile kernel, v128/v256 = implicit-GEMM tiles; "
+              "wgrad: v0 = default (BK=64, 2 stages). TF/s counts 2*N*H*W*9*Cin*Cout.", "", t]
+        open(os.path.join(ROOT, "profiles", "conv_microbench.md"), "w").write("\n".join(md) + "\n")
+        print("wrote profiles/conv_microbench.md")
+    pmc = os.path.join(ROOT, "gpurun_out", "pmc")
+    if glob.glob(os.path.join(pmc, "set*", "pmc_counter_collection.csv")):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), pmc], capture_output=True,
+                           text=True)
+        open(os.path.join(ROOT, "profiles", "conv_pmc.md"), "w").write(
+            "# PMC counters of the conv kernels (rocprofv3 --pmc, kernel-trace only)\n\n```\n" + r.stdout + "```\n")
+        print("wrote profiles/conv_pmc.md")
+
+
 if __name__ == "__main__":
+    micro_main()
     main()

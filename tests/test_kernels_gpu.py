@@ -364,3 +364,43 @@ def test_conv_transpose2x2(C, N, h, w, Cin, Cout, H2, W2):
     dx = torch.empty(N, h, w, Cin, dtype=torch.bfloat16, device=dev)
     C.conv_fwd(dyT, None, wphys, 1, 0, dx, None, None, 0, None, 0)
     assert relerr(nchw(dx), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(1, 16, 16, 512, 0, 512), (1, 8, 8, 256, 256, 256),
+                                              (2, 7, 9, 128, 0, 64), (1, 32, 32, 256, 0, 128)])
+def test_conv_splitk(C, N, H, W, C1, C2, Cout):
+    """Split-K path (small M, large K) with the stats epilogue, the BN-fold epilogue and split output."""
+    torch.manual_seed(6)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    n_ws = C.conv_ws_elems(N, H, W, C1, C2, Cout, 9, 0, 0)
+    assert n_ws > 0, "shape should take the split-K path"
+    ws = torch.zeros(n_ws, device=dev)
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.conv2d(xin, w.float(), padding=1)
+    rows = C.conv_stats_rows(N * H * W, Cout, 0)
+    stats = torch.zeros(rows * 2 * Cout, device=dev)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, stats, 0, None, 0, ws)
+    assert 0 < r <= rows
+    assert relerr(nchw(y), ref) < 1e-2
+    yq = nchw(y).float()
+    s = stats.view(rows, 2, Cout)[:r].sum(0)
+    assert torch.allclose(s[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    # BN fold + ReLU
+    g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    a = torch.empty_like(y)
+    C.conv_fwd(x1, x2, wk, 9, 0, a, None, None, 0, coef, 1, ws)
+    assert relerr(nchw(a), F.relu(F.batch_norm(ref, rm, rv, g, b, False, 0.0, 1e-5))) < 1e-2
+    # split destinations
+    y1 = torch.empty(N, H, W, Cout // 2, dtype=torch.bfloat16, device=dev)
+    y2 = torch.empty(N, H, W, Cout // 2, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, y1, y2, None, 0, None, 0, ws)
+    assert relerr(torch.cat([nchw(y1), nchw(y2)], 1), ref) < 1e-2
