@@ -14,6 +14,7 @@ int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, con
                    float*, long, hipStream_t);
 long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
+long rdp_geo_work_ints(int, int);
 int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
                   double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, hipStream_t);
 int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*,
@@ -100,8 +101,10 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
   if (bm_pref == 128 && Cout % 128 == 0) return (M + 127) / 128 * 2;
   if (bm_pref == 256) return (M + 255) / 256 * 4;
   // auto / halo: upper bound over every tile choice (halo: up to 8 wave rows per 256-pixel tile)
+  // split-K reduce: up to 512 rows
   const long a = (M + 127) / 128 * 2, b = (M + 255) / 256 * 8;
-  return (int)(a > b ? a : b);
+  const long ab = a > b ? a : b;
+  return (int)(ab > 512 ? ab : 512);
 }
 
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)
@@ -401,7 +404,8 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
               "depth u16");
   const int H = mask.size(0), W = mask.size(1);
   const int nblk = rdp_geo_nblocks(H);
-  TORCH_CHECK(work_i.numel() >= nblk && work_i.scalar_type() == torch::kInt32, "work_i");
+  TORCH_CHECK(work_i.numel() >= rdp_geo_work_ints(H, W) && work_i.scalar_type() == torch::kInt32 &&
+              work_i.is_contiguous(), "work_i: needs geo_work_ints(H, W) int32");
   TORCH_CHECK(work_d.numel() >= 2 * nblk && work_d.scalar_type() == torch::kFloat64, "work_d");
   TORCH_CHECK(pts.scalar_type() == torch::kFloat64 && pts.numel() >= (long)H * W * 4, "pts cap");
   TORCH_CHECK(out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(0) >= nbins && out.size(2) == 4, "out");
@@ -415,6 +419,7 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
 }
 
 int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
+long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 
 void preprocess(torch::Tensor bgr, torch::Tensor ystart, torch::Tensor ysize, torch::Tensor yw, torch::Tensor xstart,
                 torch::Tensor xsize, torch::Tensor xw, torch::Tensor out) {
@@ -474,6 +479,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("parcur", &parcur);
   m.def("geo_edges", &geo_edges);
   m.def("geo_nblocks", &geo_nblocks);
+  m.def("geo_work_ints", &geo_work_ints);
   m.def("preprocess", &preprocess);
   m.def("mask_upsample", &mask_upsample);
   m.def("splev", &splev);

@@ -375,10 +375,8 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(grid), dim3(256), 0, s, a);
     const int rpb = 256 / (a.Cout / 8);
-    const int cap = tilesM * (BM / 64);  // <= conv_stats_rows() bound
-    int nblk = (a.M + rpb - 1) / rpb;
+    int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
-    nblk = nblk < cap ? nblk : cap;
     const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
     return nblk;

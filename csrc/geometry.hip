@@ -127,53 +127,115 @@ RDP_DEV uint64_t dkey(double d) {
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
-// One workgroup per bin. out: [nbins][kcap][4]; kout[b] = k written (0 if empty bin).
-__global__ __launch_bounds__(GEO_THREADS) void geo_edges_kernel(const double* __restrict__ pts,
-                                                                const int* __restrict__ npts_p,
-                                                                const double* __restrict__ bxmin,
-                                                                const double* __restrict__ bxmax, int nblk, int nbins,
-                                                                double top, double* __restrict__ out, int kcap,
-                                                                int* __restrict__ kout, int min_points) {
-  __shared__ unsigned hist[256];
-  __shared__ double s_lo, s_hi;
-  __shared__ int s_tot[GEO_THREADS / 64];
-  __shared__ uint64_t s_prefix;
-  __shared__ int s_need;
-  __shared__ int s_gt_cnt, s_eq_cnt;
-  const int bin = blockIdx.x;
+// ---- binning: counting sort of point indices by x bin (bin computed once per point) ----
+// bin = clip(floor((x - lo) / w), 0, nbins-1) with the reference's division (not a reciprocal
+// multiply), so boundary points land in exactly the reference's bin.
+struct GeoBins {
+  int* bin_of;     // [cap]   bin of every point
+  int* bidx;       // [cap]   point indices grouped by bin (order within a bin is arbitrary)
+  int* cnt;        // [128]   points per bin
+  int* cursor;     // [128]   scatter cursors
+};
+
+RDP_DEV void geo_range(const double* bxmin, const double* bxmax, int nblk, double* s_lo, double* s_hi) {
+  // every block reduces the per-row-block partials itself (nblk ~ H/4 doubles)
+  __shared__ double rlo[GEO_THREADS], rhi[GEO_THREADS];
+  double a = 1e300, b = -1e300;
+  for (int i = threadIdx.x; i < nblk; i += GEO_THREADS) { a = fmin(a, bxmin[i]); b = fmax(b, bxmax[i]); }
+  rlo[threadIdx.x] = a;
+  rhi[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = GEO_THREADS / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      rlo[threadIdx.x] = fmin(rlo[threadIdx.x], rlo[threadIdx.x + o]);
+      rhi[threadIdx.x] = fmax(rhi[threadIdx.x], rhi[threadIdx.x + o]);
+    }
+    __syncthreads();
+  }
+  *s_lo = rlo[0];
+  *s_hi = rhi[0];
+}
+
+__global__ __launch_bounds__(GEO_THREADS) void geo_bin_count_kernel(const double* __restrict__ pts,
+                                                                    const int* __restrict__ npts_p,
+                                                                    const double* __restrict__ bxmin,
+                                                                    const double* __restrict__ bxmax, int nblk,
+                                                                    int nbins, GeoBins gb) {
+  __shared__ unsigned lc[128];
+  double lo, hi;
+  geo_range(bxmin, bxmax, nblk, &lo, &hi);
   const int n = npts_p[0];
+  const double width = (hi - lo) / (double)nbins;
+  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS) lc[i] = 0;
+  __syncthreads();
+  if (width > 0.0)
+    for (int i = blockIdx.x * GEO_THREADS + threadIdx.x; i < n; i += gridDim.x * GEO_THREADS) {
+      const double f = floor((pts[(size_t)i * 4] - lo) / width);
+      const int b = (int)fmin(fmax(f, 0.0), (double)(nbins - 1));
+      gb.bin_of[i] = b;
+      atomicAdd(&lc[b], 1u);
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS)
+    if (lc[i]) atomicAdd(&gb.cnt[i], (int)lc[i]);
+}
+
+__global__ __launch_bounds__(GEO_THREADS) void geo_bin_scatter_kernel(const int* __restrict__ npts_p, int nbins,
+                                                                      GeoBins gb) {
+  __shared__ int base[128];
+  __shared__ unsigned lc[128], lbase[128];
   if (threadIdx.x == 0) {
-    double a = 1e300, b = -1e300;
-    for (int i = 0; i < nblk; ++i) { a = fmin(a, bxmin[i]); b = fmax(b, bxmax[i]); }
-    s_lo = a;
-    s_hi = b;
+    int o = 0;
+    for (int b = 0; b < nbins; ++b) { base[b] = o; o += gb.cnt[b]; }
+  }
+  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS) lc[i] = 0;
+  __syncthreads();
+  const int n = npts_p[0];
+  // block-aggregated cursors: one global atomic per (block, bin)
+  const int i0 = blockIdx.x * GEO_THREADS * 4;
+  int bins[4], pos[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = i0 + u * GEO_THREADS + threadIdx.x;
+    bins[u] = i < n ? gb.bin_of[i] : -1;
+    pos[u] = bins[u] >= 0 ? (int)atomicAdd(&lc[bins[u]], 1u) : 0;
   }
   __syncthreads();
-  const double lo = s_lo, hi = s_hi;
-  const double width = (hi - lo) / (double)nbins;
-  if (n < min_points || !(width > 0.0)) {
+  for (int b = threadIdx.x; b < nbins; b += GEO_THREADS)
+    lbase[b] = lc[b] ? (unsigned)atomicAdd(&gb.cursor[b], (int)lc[b]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = i0 + u * GEO_THREADS + threadIdx.x;
+    if (bins[u] >= 0) gb.bidx[base[bins[u]] + (int)lbase[bins[u]] + pos[u]] = i;
+  }
+}
+
+// One workgroup per bin, over that bin's points only. out: [nbins][kcap][4]; kout[b] = k written.
+// k = max(1, int(n_b * top)) largest y; ties at the k-th value go to the smallest point indices
+// (= the reference's stable descending sort), found by a second radix select on the index.
+__global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* __restrict__ pts,
+                                                                 const int* __restrict__ npts_p, int nbins,
+                                                                 double top, GeoBins gb, double* __restrict__ out,
+                                                                 int kcap, int* __restrict__ kout, int min_points) {
+  __shared__ unsigned hist[256];
+  __shared__ uint64_t s_prefix;
+  __shared__ int s_need;
+  __shared__ int s_cnt;
+  const int bin = blockIdx.x;
+  const int n = npts_p[0];
+  const int nb = gb.cnt[bin];
+  if (n < min_points || nb == 0) {
     if (threadIdx.x == 0) kout[bin] = 0;
     return;
   }
-  auto bin_of = [&](double x) {
-    double f = floor((x - lo) / width);
-    int b = (int)fmin(fmax(f, 0.0), (double)(nbins - 1));
-    return b;
-  };
-  // 1) bin size
-  int c = 0;
-  for (int i = threadIdx.x; i < n; i += GEO_THREADS) c += bin_of(pts[(size_t)i * 4]) == bin;
-  int tot;
-  (void)block_scan_excl(c, s_tot, tot);
-  const int nb = tot;
-  if (nb == 0) {
-    if (threadIdx.x == 0) kout[bin] = 0;
-    return;
-  }
+  int start = 0;
+  for (int b = 0; b < bin; ++b) start += gb.cnt[b];
+  const int* ids = gb.bidx + start;
   int k = (int)((double)nb * top);
   if (k < 1) k = 1;
   if (k > kcap) k = kcap;
-  // 2) radix select (8 passes x 8 bits, MSB first) of the k-th largest y key within the bin
+  // 1) radix select (8 x 8 bits, MSB first) of the k-th largest y key in the bin
   if (threadIdx.x == 0) { s_prefix = 0; s_need = k; }
   __syncthreads();
   for (int pass = 0; pass < 8; ++pass) {
@@ -182,17 +244,14 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_edges_kernel(const double* __
     __syncthreads();
     const uint64_t prefix = s_prefix;
     const uint64_t pmask = pass == 0 ? 0ull : (~0ull << (64 - 8 * pass));
-    for (int i = threadIdx.x; i < n; i += GEO_THREADS) {
-      if (bin_of(pts[(size_t)i * 4]) != bin) continue;
-      const uint64_t key = dkey(pts[(size_t)i * 4 + 1]);
-      if ((key & pmask) != prefix) continue;
-      atomicAdd(&hist[(key >> shift) & 255], 1u);
+    for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
+      const uint64_t key = dkey(pts[(size_t)ids[i] * 4 + 1]);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      int need = s_need;
-      int d = 255;
-      for (; d > 0; --d) {  // walk from the largest digit down
+      int need = s_need, d = 255;
+      for (; d > 0; --d) {
         if ((int)hist[d] >= need) break;
         need -= hist[d];
       }
@@ -201,61 +260,83 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_edges_kernel(const double* __
     }
     __syncthreads();
   }
-  const uint64_t kth = s_prefix;  // exact key of the k-th largest y
-  // 3) write: every key > kth, plus the (need) smallest-index keys == kth
-  if (threadIdx.x == 0) { s_gt_cnt = 0; s_eq_cnt = 0; }
+  const uint64_t kth = s_prefix;
+  const int need_eq = s_need;  // ties at kth to take, by smallest point index
+  // 2) radix select (4 x 8 bits) of the need_eq-th smallest index among the ties
+  if (threadIdx.x == 0) { s_prefix = 0; s_need = need_eq; }
   __syncthreads();
-  const int need_eq = s_need;  // number of ties to take
-  double* ob = out + (size_t)bin * kcap * 4;
-  // keys > kth (order irrelevant: the host sorts the edge set)
-  for (int i = threadIdx.x; i < n; i += GEO_THREADS) {
-    if (bin_of(pts[(size_t)i * 4]) != bin) continue;
-    if (dkey(pts[(size_t)i * 4 + 1]) > kth) {
-      const int o = atomicAdd(&s_gt_cnt, 1);
-      for (int j = 0; j < 4; ++j) ob[(size_t)o * 4 + j] = pts[(size_t)i * 4 + j];
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = threadIdx.x; i < 256; i += GEO_THREADS) hist[i] = 0;
+    __syncthreads();
+    const uint32_t prefix = (uint32_t)s_prefix;
+    const uint32_t pmask = pass == 0 ? 0u : (~0u << (32 - 8 * pass));
+    for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
+      const int id = ids[i];
+      if (dkey(pts[(size_t)id * 4 + 1]) == kth && ((uint32_t)id & pmask) == prefix)
+        atomicAdd(&hist[((uint32_t)id >> shift) & 255], 1u);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int need = s_need, d = 0;
+      for (; d < 255; ++d) {  // smallest digits first
+        if ((int)hist[d] >= need) break;
+        need -= hist[d];
+      }
+      s_need = need;
+      s_prefix = prefix | ((uint32_t)d << shift);
+    }
+    __syncthreads();
   }
+  const uint32_t last_id = (uint32_t)s_prefix;  // largest index among the selected ties
+  // 3) write: y key > kth, or == kth with index <= last_id (exactly k points)
+  if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  // ties in ascending point index: ordered scan over the points
-  int written = 0;
-  const int gt = s_gt_cnt;
-  for (int i0 = 0; i0 < n && written < need_eq; i0 += GEO_THREADS) {
-    const int i = i0 + threadIdx.x;
-    const int e = (i < n) && bin_of(pts[(size_t)i * 4]) == bin && dkey(pts[(size_t)i * 4 + 1]) == kth;
-    int t;
-    const int off = block_scan_excl(e, s_tot, t);
-    if (e && written + off < need_eq) {
-      const int o = gt + written + off;
-      for (int j = 0; j < 4; ++j) ob[(size_t)o * 4 + j] = pts[(size_t)i * 4 + j];
+  double* ob = out + (size_t)bin * kcap * 4;
+  for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
+    const int id = ids[i];
+    const uint64_t key = dkey(pts[(size_t)id * 4 + 1]);
+    if (key > kth || (key == kth && (uint32_t)id <= last_id)) {
+      const int o = atomicAdd(&s_cnt, 1);
+      if (o < kcap)
+        for (int j = 0; j < 4; ++j) ob[(size_t)o * 4 + j] = pts[(size_t)id * 4 + j];
     }
-    written += t;
   }
   if (threadIdx.x == 0) kout[bin] = k;
 }
 
-// Pack the per-bin edge points contiguously: hdr[0] = E (total), edges[E][4].
+// Pack the per-bin edge points contiguously (one block per bin): hdr[0] = E, edges[E][4].
 __global__ void geo_pack_kernel(const double* __restrict__ out, int kcap, const int* __restrict__ kout, int nbins,
                                 double* __restrict__ edges, int ecap, int* __restrict__ hdr) {
-  __shared__ int offs[128];
+  __shared__ int s_off;
+  const int b = blockIdx.x;
   if (threadIdx.x == 0) {
     int o = 0;
-    for (int b = 0; b < nbins; ++b) { offs[b] = o; o += kout[b]; }
-    hdr[0] = o;
+    for (int i = 0; i < b; ++i) o += kout[i];
+    s_off = o;
+    if (b == nbins - 1) hdr[0] = o + kout[b];
   }
   __syncthreads();
-  for (int b = 0; b < nbins; ++b) {
-    const int k = kout[b], o = offs[b];
-    for (int i = threadIdx.x; i < k * 4; i += blockDim.x) {
-      const int e = o * 4 + i;
-      if (e < ecap * 4) edges[e] = out[(size_t)b * kcap * 4 + i];
-    }
+  const int k = kout[b], o = s_off;
+  for (int i = threadIdx.x; i < k * 4; i += blockDim.x) {
+    const int e = o * 4 + i;
+    if (e < ecap * 4) edges[e] = out[(size_t)b * kcap * 4 + i];
   }
+}
+
+__global__ void geo_zero_kernel(int* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0;
 }
 
 extern "C" {
 int rdp_geo_nblocks(int H) { return (H + GEO_ROWS_PER_BLOCK - 1) / GEO_ROWS_PER_BLOCK; }
 
-// work: counts[nblk] ints, xmin/xmax[nblk] doubles (caller-provided); pts [cap][4]; out [nbins][kcap][4]
+// int32 workspace needed beyond the per-row-block counts: bin_of + bidx [cap] each + 2 x 128
+long rdp_geo_work_ints(int H, int W) { return (long)rdp_geo_nblocks(H) + 2L * H * W + 256; }
+
+// work_i: [nblk] counts | [cap] bin_of | [cap] bidx | [128] cnt | [128] cursor ; work_d: xmin/xmax
+// pts [cap][4]; out [nbins][kcap][4]
 int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, double fy, double cx, double cy,
                   double scale, int* counts, double* xmin, double* xmax, double* pts, int cap, int* npts,
                   double* out, int kcap, int* kout, int nbins, double top, int min_points, double* edges,
@@ -263,13 +344,23 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
   if (nbins > 128 || nbins < 1) return -1;
   const int nblk = rdp_geo_nblocks(H);
   GeoCam cam{fx, fy, cx, cy, scale};
+  GeoBins gb;
+  gb.bin_of = counts + nblk;
+  gb.bidx = gb.bin_of + cap;
+  gb.cnt = gb.bidx + cap;
+  gb.cursor = gb.cnt + 128;
+  hipLaunchKernelGGL(geo_zero_kernel, dim3(1), dim3(256), 0, s, gb.cnt, 256);
   hipLaunchKernelGGL(geo_count_kernel, dim3(nblk), dim3(GEO_THREADS), 0, s, (const uint8_t*)mask,
                      (const uint16_t*)depth, H, W, cam, counts, xmin, xmax);
   hipLaunchKernelGGL(geo_write_kernel, dim3(nblk), dim3(GEO_THREADS), 0, s, (const uint8_t*)mask,
                      (const uint16_t*)depth, H, W, cam, counts, nblk, pts, cap, npts);
-  hipLaunchKernelGGL(geo_edges_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, xmin, xmax, nblk, nbins, top,
-                     out, kcap, kout, min_points);
-  hipLaunchKernelGGL(geo_pack_kernel, dim3(1), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
+  const int pblocks = (cap + GEO_THREADS * 4 - 1) / (GEO_THREADS * 4);
+  hipLaunchKernelGGL(geo_bin_count_kernel, dim3(pblocks < 256 ? pblocks : 256), dim3(GEO_THREADS), 0, s, pts, npts,
+                     xmin, xmax, nblk, nbins, gb);
+  hipLaunchKernelGGL(geo_bin_scatter_kernel, dim3(pblocks), dim3(GEO_THREADS), 0, s, npts, nbins, gb);
+  hipLaunchKernelGGL(geo_select_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, nbins, top, gb, out, kcap,
+                     kout, min_points);
+  hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
   return nblk;
 }
 }

@@ -100,7 +100,7 @@ class GeometryEngine:
         self.cfg = cfg or GeometryConfig()
         self.H, self.W, self.dev = H, W, device
         nblk = self.C.geo_nblocks(H)
-        self.work_i = torch.zeros(nblk, dtype=torch.int32, device=device)
+        self.work_i = torch.zeros(self.C.geo_work_ints(H, W), dtype=torch.int32, device=device)
         self.work_d = torch.zeros(2 * nblk, dtype=torch.float64, device=device)
         self.pts = torch.zeros(H * W * 4, dtype=torch.float64, device=device)
         self.npts = torch.zeros(1, dtype=torch.int32, device=device)

@@ -113,6 +113,7 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
             t_end = time.perf_counter()
             out["e2e_fps"] = round(frames / (t_end - t_start), 1)
             out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)
+            _progress(f"streamed: {out}")
             # lock-step round trip
             q: "queue.Queue" = queue.Queue()
             sent = []
@@ -136,13 +137,21 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
     return out
 
 
+def _progress(msg):
+    import sys
+    print(f"[bench_serve] {msg}", file=sys.stderr, flush=True)
+
+
 def measure_serving(dev: Optional[torch.device] = None, frames: int = 200, warmup: int = 20,
                     train_steps: int = 200) -> dict:
     dev = dev or torch.device("cuda")
     model, scenes = prepare_model(dev, train_steps)
+    _progress("model ready")
     res = {"serve_frame": "640x480 RGB-D -> 256x256 U-Net", "serve_weights": f"trained {train_steps} steps on synthetic"}
     res.update({"serve_" + k: v for k, v in measure_engine(model, scenes, frames, warmup).items()})
+    _progress(f"engine done: {res}")
     res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup).items()})
+    _progress("e2e done")
     return res
 
 
