@@ -35,6 +35,7 @@ import torch
 
 from ..config import GeometryConfig
 from ..geometry.curvature import CurvatureResult, GeometryEngine, compute_curvature_profile
+from ..utils import trace
 
 AA_MAXTAP = 16
 
@@ -162,7 +163,7 @@ class FramePipeline:
         self.h_color.numpy()[...] = color_bgr
         self.h_depth.numpy()[...] = depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16)
         s = self.stream
-        with torch.cuda.stream(s):
+        with trace.range("serve.frame.enqueue"), torch.cuda.stream(s):
             self.ev0.record(s)
             self.d_color.copy_(self.h_color, non_blocking=True)
             self.d_depth.copy_(self.h_depth, non_blocking=True)
@@ -177,10 +178,12 @@ class FramePipeline:
 
     def collect(self) -> FrameResult:
         t0 = time.perf_counter()
-        self.ev1.synchronize()
+        with trace.range("serve.frame.wait_gpu"):
+            self.ev1.synchronize()
         t1 = time.perf_counter()
         count, E, npts = (int(v) for v in self.h_meta.numpy()[:3])
-        res = self.geo.finish(self.h_edges.numpy(), E, npts)
+        with trace.range("serve.frame.spline_fit"):
+            res = self.geo.finish(self.h_edges.numpy(), E, npts)
         t2 = time.perf_counter()
         cov = 100.0 * count / (self.H * self.W)
         return FrameResult(self.h_mask.numpy().copy(), cov, res,

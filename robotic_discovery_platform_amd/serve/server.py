@@ -32,6 +32,7 @@ import torch
 from ..config import ServeConfig
 from ..data.image_io import decode_image, encode_png
 from ..proto import vision as pb
+from ..utils import trace
 from .engine import EnginePool
 
 log = logging.getLogger(__name__)
@@ -163,7 +164,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         log.info("new analysis stream")
         try:
             for t0, color, depth in self._decoded(request_iterator):
-                yield self.analyze_frame(color, depth, t0)
+                with trace.range("serve.rpc.frame"):
+                    resp = self.analyze_frame(color, depth, t0)
+                yield resp
         except Exception as e:
             log.error("unhandled exception during analysis: %s", e)
             context.set_code(grpc.StatusCode.INTERNAL)

@@ -24,6 +24,7 @@ import torch.nn as nn
 from ..models.unet import NativeAdam, UNetNative
 from ..models.unet_ref import UNetRef
 from ..parallel.ddp import FlatBucketer, broadcast_module_state, dist_info
+from ..utils import trace
 
 
 class NativeTrainer:
@@ -50,16 +51,21 @@ class NativeTrainer:
 
     def _step_body(self):
         ex = self.ex
-        ex.forward()
+        with trace.range("train.forward"):
+            ex.forward()
         if self.bucketer is not None:
             self.bucketer.reset()
-            ex.backward(grad_hook=self._hook)
-            self.bucketer.mark_ready(["outc.conv.weight", "outc.conv.bias"])
-            self.bucketer.finish()
-            self.opt.step(gscale=1.0 / self.world)
+            with trace.range("train.backward+allreduce"):
+                ex.backward(grad_hook=self._hook)
+                self.bucketer.mark_ready(["outc.conv.weight", "outc.conv.bias"])
+                self.bucketer.finish()
+            with trace.range("train.adam"):
+                self.opt.step(gscale=1.0 / self.world)
         else:
-            ex.backward()
-            self.opt.step()
+            with trace.range("train.backward"):
+                ex.backward()
+            with trace.range("train.adam"):
+                self.opt.step()
 
     def set_batch(self, x: torch.Tensor, target: torch.Tensor):
         self.ex.set_input(x, target)
