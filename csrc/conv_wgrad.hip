@@ -19,6 +19,8 @@
 //   * software L2 prefetch with 4-B-per-lane loads one line per lane: 1.7x SLOWER (64 distinct
 //     lines per wave-instruction saturate the address path, MI355X_MICROARCH.md "access shape").
 //   * DMA issue moved between the MFMA halves: slower (DMA latency matters more than VALU slots).
+//   * 3-wave blocks (192 columns: no padding for Cin = 64 / 128): +3 % at Cin = 64, -5 % at 128 --
+//     the padded MFMAs are not on the critical path of this latency-bound loop.
 // PMC (256^2 x 64ch): ~48 % of wave cycles in s_waitcnt/barrier, i.e. latency-bound on x/dY
 // streamed from HBM with only one K step of lookahead.
 #include "common.h"
