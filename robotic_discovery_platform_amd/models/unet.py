@@ -18,6 +18,7 @@ execution model is MI355X-first:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -395,6 +396,11 @@ class UNetExecutor:
     # ------------------------------------------------------------------ backward buffers
     def _alloc_backward(self, C):
         dev, bf = self.dev, torch.bfloat16
+        self.overlap_wgrad = dev.type == "cuda"
+        self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
+        # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS)
+        # (measured at bs32 with the side-stream overlap: 1024 -> 2025, 2048 -> 2086, 4096 -> 2068 img/s)
+        self.wgrad_blocks = int(os.environ.get("RDP_WGRAD_BLOCKS", "2048"))
         N = self.N
         D = self.m.depth
 
@@ -434,7 +440,7 @@ class UNetExecutor:
             cin = L.spec.cin if not L.spec.packed else 8
             ncols = 72 if L.spec.packed else L.spec.taps * cin
             tiles = ((ncols + 255) // 256) * (L.spec.cout // 64)
-            L.splits = int(max(1, min((1024 + tiles - 1) // tiles, M // 2048)))
+            L.splits = int(max(1, min((self.wgrad_blocks + tiles - 1) // tiles, M // 2048)))
             slab = max(slab, C.wgrad_slab_elems(n, h, w, cin, L.spec.cout, L.spec.taps, int(L.spec.packed), L.splits))
         self.dyTs: List[torch.Tensor] = [like(y) for y in self.yTs]
         self.upT_splits: List[int] = []
@@ -442,7 +448,7 @@ class UNetExecutor:
             n, h, w, _ = self.yTs[i].shape
             M = n * h * w
             tiles = ((4 * us.cout + 255) // 256) * (us.cin // 64)
-            sp_ = int(max(1, min((1024 + tiles - 1) // tiles, max(1, M // 2048))))
+            sp_ = int(max(1, min((self.wgrad_blocks + tiles - 1) // tiles, max(1, M // 2048))))
             self.upT_splits.append(sp_)
             # roles swapped in conv_wgrad: "x" = dyT (4*cout ch), "dy" = the ConvT input (cin ch)
             slab = max(slab, C.wgrad_slab_elems(n, h, w, 4 * us.cout, us.cin, 1, 0, sp_))
@@ -546,22 +552,45 @@ class UNetExecutor:
                           self.red_ws)
         C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
 
+    def _on_side(self, fn):
+        """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream
+        (fork); without a side stream it runs inline."""
+        if self.side is None:
+            return fn()
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            return fn()
+
     def _conv_bwd(self, C, L: _Layer, hooks=None):
         sp = L.spec
         st = self.m.store
         self._bn_bwd(C, L)
         gw = st.flat_slice(sp.name + ".weight", st.grad)
-        C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw, 0, L.splits, 0)
+        # wgrad (latency-bound on x / dY streams) overlaps the main stream's dgrad + next BN backward;
+        # all wgrads share the slab, so they stay serialized on the one side stream
+        self._on_side(lambda: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw,
+                                           0, L.splits, 0))
         if L.dx1 is not None:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:
-            hooks(sp)
+            self._on_side(lambda: hooks(sp))  # the bucket's all-reduce waits for the wgrad too
 
     def backward(self, grad_hook=None, gscale: float = 1.0):
-        """Full backward; ``grad_hook(spec)`` fires after each conv layer's grads are final."""
+        """Full backward; ``grad_hook(spec)`` fires after each conv layer's grads are final.
+
+        Weight gradients run on a side stream (``overlap_wgrad``) and join the caller's stream at
+        the end, so the optimizer (or a graph capture) sees every gradient complete."""
         C = _native()
         D = self.m.depth
         st = self.m.store
+        main = torch.cuda.current_stream() if self.overlap_wgrad else None
+        try:
+            self._backward(C, D, st, grad_hook, gscale)
+        finally:
+            if main is not None:
+                main.wait_stream(self.side)  # join
+
+    def _backward(self, C, D, st, grad_hook, gscale):
         head_w = st.view("outc.conv.weight").reshape(-1)
         C.head_bwd(self.final, head_w, self.logits, self.target, self.loss_sums, self.up_layers[-1][1].da,
                    self.head_partial, st.flat_slice("outc.conv.weight", st.grad), st.flat_slice("outc.conv.bias", st.grad),
@@ -582,12 +611,13 @@ class UNetExecutor:
                 dyT = self.dyTs[i - 1]
                 C.upT_unshuffle(du, dyT, oy, ox)
                 C.colsum_bf16(dyT, 4, self.colsum_ws, st.flat_slice(us.name + ".bias", st.grad), 0)
-                C.conv_wgrad(dyT, None, low_layer.a, 1, 0, 4 * us.cout, self.slab,
-                             st.flat_slice(us.name + ".weight", st.grad), 0, self.upT_splits[i - 1], 0)
+                self._on_side(lambda: C.conv_wgrad(dyT, None, low_layer.a, 1, 0, 4 * us.cout, self.slab,
+                                                   st.flat_slice(us.name + ".weight", st.grad), 0,
+                                                   self.upT_splits[i - 1], 0))
                 C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
                            self.kws)
                 if grad_hook is not None:
-                    grad_hook(us)
+                    self._on_side(lambda: grad_hook(us))
         for i in range(D, 0, -1):
             la, lb = self.down_layers[i]
             self._conv_bwd(C, lb, grad_hook)
