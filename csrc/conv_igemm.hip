@@ -24,6 +24,7 @@
 // MFMAs and epilogue. This removes the per-tile prologue that dominated the small-K (K = 576)
 // 64-channel layers. The epilogue uses no LDS and no block barrier.
 #include "common.h"
+#include <stdlib.h>
 
 struct ConvArgs {
   const u16* x1;
@@ -435,7 +436,13 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // grid (k = 0 => 2 per CU, every block resident; large k ~ one tile per block)
   int per_cu = bm_pref / 1000;
   bm_pref %= 1000;
-  if (per_cu == 0) per_cu = 2;
+  if (per_cu == 0) {  // tuning knob for sweeps (RDP_CONV_PERCU), default 2 = every block resident
+    static const int env_per_cu = [] {
+      const char* e = getenv("RDP_CONV_PERCU");
+      return e ? atoi(e) : 0;
+    }();
+    per_cu = env_per_cu > 0 ? env_per_cu : 2;
+  }
   const int max_blocks = 256 * per_cu;
   if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s);
   return launch_cfg<256, 64>(a, max_blocks, wse, s);
