@@ -59,6 +59,9 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
+        # test mode: several gloo ranks may share one GPU (RCCL refuses that; the real runs use nccl)
+        if os.environ.get("RDP_DIST_BACKEND") == "gloo" and local >= torch.cuda.device_count():
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
