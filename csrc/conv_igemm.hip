@@ -59,12 +59,15 @@ struct ConvArgs {
 RDP_DEV int tap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
 RDP_DEV int tap_ds(int tap) { return tap - 3 * ((tap * 11) >> 5) - 1; }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
+template <int BM, int BN, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int WAVES_M = BM / 64;
+  constexpr int WAVES_N = NWV / WAVES_M;
+  constexpr int WNT = BN / WAVES_N;  // couts per wave (64, or 32 with 8-wave blocks)
+  constexpr int NJ = WNT / 16;
   constexpr int P_BYTES = BM * 128, W_BYTES = BN * 128, BUF = P_BYTES + W_BYTES;
-  constexpr int NROW = BM / 32;     // pixel rows (DMA pieces) per lane per K step
-  constexpr int WPIECES = BN / 32;  // weight rows (DMA pieces) per lane per K step
+  constexpr int NROW = BM / 8 / NWV;     // pixel-row DMA pieces per wave per K step
+  constexpr int WPIECES = BN / 8 / NWV;  // weight-row DMA pieces per wave per K step
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int lane = threadIdx.x & 63;
@@ -162,9 +165,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
   const auto ry1 = make_rsrc(a.y1, a.ybytes1);
   const auto ry2 = make_rsrc(a.y2 ? a.y2 : a.y1, a.y2 ? a.ybytes2 : 0u);
 
-  f32x4 acc[4][4];
+  f32x4 acc[NJ][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -185,13 +188,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     const char* wb = pb + P_BYTES;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      bf16x8 fa[4], fb[4];
+      bf16x8 fa[NJ], fb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fa[j] = *(const bf16x8*)(wb + (wn * 4 + j) * 2048 + rdoff[hf]);
+      for (int j = 0; j < NJ; ++j) fa[j] = *(const bf16x8*)(wb + (wn * NJ + j) * 2048 + rdoff[hf]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) fb[i] = *(const bf16x8*)(pb + (wm * 4 + i) * 2048 + rdoff[hf]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
@@ -207,8 +210,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
       const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
       const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
+      for (int j = 0; j < NJ; ++j) {
+        const int n = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = tm * BM + wm * 64 + i * 16 + (lane & 15);
@@ -224,10 +227,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     const int tile = item;
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
-    float s1[4][4], s2[4][4];
+    float s1[NJ][4], s2[NJ][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * WNT + j * 16 + 4 * (lane >> 4);
       const bool d2 = n >= a.Cy1;
       const int nn = d2 ? n - a.Cy1 : n;
       const int yp = d2 ? a.ypitch2 : a.ypitch1;
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
     if (a.stats) {
       // reduce over the 16 pixel lanes (lane & 15) sharing a channel group; one slab row per (tile, wm)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           s1[j][r] = row16_sum(s1[j][r]);
@@ -273,8 +276,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const ConvArgs a) {
       if ((lane & 15) == 0) {
         float* row = a.stats + (size_t)(tm * WAVES_M + wm) * 2 * a.Cout;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        for (int j = 0; j < NJ; ++j) {
+          const int c = n0 + wn * WNT + j * 16 + 4 * (lane >> 4);
           *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
           *(float4*)(row + a.Cout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
         }
@@ -364,7 +367,7 @@ static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long 
   return ks;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NWV = 4>
 static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
@@ -374,7 +377,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
     a.nks /= a.ksplit;
     a.ntiles *= a.ksplit;
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
     const int rpb = 256 / (a.Cout / 8);
     int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
@@ -383,7 +386,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
     return nblk;
   }
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN>), dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
   return tilesM * (BM / 64);
 }
 
@@ -444,8 +447,14 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
     per_cu = env_per_cu > 0 ? env_per_cu : 2;
   }
   const int max_blocks = 256 * per_cu;
-  if ((bm_pref == 128 || bm_pref == 0) && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s);
-  return launch_cfg<256, 64>(a, max_blocks, wse, s);
+  // bm_pref 2 / 3: 8-wave blocks (64 x 32 per wave; twice the waves per SIMD to hide the per-step
+  // barrier + DMA latency, 1.5x the LDS fragment reads per MFMA) for the 128x128 / 256x64 tiles
+  if (bm_pref == 2 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s);
+  if (bm_pref == 3) return launch_cfg<256, 64, 8>(a, max_blocks, wse, s);
+  if (bm_pref == 128 && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s);
+  if (bm_pref == 0 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s);
+  if (bm_pref == 256) return launch_cfg<256, 64>(a, max_blocks, wse, s);
+  return launch_cfg<256, 64, 8>(a, max_blocks, wse, s);
 }
 
 // fp32 workspace elements the auto dispatch would use for split-K on this shape (0 = no split)

@@ -404,3 +404,22 @@ def test_conv_splitk(C, N, H, W, C1, C2, Cout):
     y2 = torch.empty(N, H, W, Cout // 2, dtype=torch.bfloat16, device=dev)
     C.conv_fwd(x1, x2, wk, 9, 0, y1, y2, None, 0, None, 0, ws)
     assert relerr(torch.cat([nchw(y1), nchw(y2)], 1), ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(2, 16, 16, 128, 0, 128), (1, 9, 13, 64, 64, 256)])
+def test_conv_fwd_8wave_variant(C, N, H, W, C1, C2, Cout):
+    """bm_pref=2: 128x128 tiles with 8 waves (64x32 per wave) == the 4-wave kernel's result."""
+    torch.manual_seed(7)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    rows = C.conv_stats_rows(N * H * W, Cout, 0)
+    outs = []
+    for pref in (128, 2):
+        y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+        st = torch.zeros(rows * 2 * Cout, device=dev)
+        r = C.conv_fwd(x1, x2, ohwi(w).contiguous(), 9, 0, y, None, st, pref, None, 0)
+        outs.append((y, st[: r * 2 * Cout].view(r, 2, Cout).sum(0)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-4)
