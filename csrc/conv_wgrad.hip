@@ -48,12 +48,16 @@ RDP_DEV int swz(int p) { return (((p >> 1) & 1) << 1) | (((p >> 3) & 1) << 2); }
 RDP_DEV uint32_t fdiv2(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
 // BKP pixels per K step (64 or 32), STAGES LDS buffers (STAGES-1 steps in flight under the MFMAs).
-template <bool PACKED, bool TILE_FAST, int BKP, int STAGES>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
+// NWV = 4: wave w owns x-subtile w (64 columns) x 64 couts; NWV = 8: waves 2s, 2s+1 split
+// x-subtile s into two 32-column halves (twice the waves per SIMD, same LDS footprint).
+template <bool PACKED, bool TILE_FAST, int BKP, int STAGES, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 2) void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int SUB = BKP * 128;        // one [BKP pixels][64 ch] bf16 tile
   constexpr int BUF = 5 * SUB;          // 4 x-subtiles + 1 dy tile
   constexpr int PIECES = BKP / 8;       // 8-row DMA pieces per subtile
-  constexpr int PPW = PIECES / 4;       // pieces (row groups) per wave
+  constexpr int PPW = PIECES / NWV;     // pieces (row groups) per wave
+  constexpr int NI = 4 * 4 / NWV;       // 16-column x fragments per wave (4 or 2)
+  static_assert(PPW >= 1, "BKP too small for the wave count");
   __shared__ __attribute__((aligned(16))) char smem[STAGES * BUF];
 
   const int lane = threadIdx.x & 63;
@@ -136,9 +140,9 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[NI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -161,42 +165,49 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const WgradArgs a) {
     raw_barrier();
     if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
     const char* cur = smem + (ks % STAGES) * BUF;
-    const char* xb = cur + wave * SUB;
+    const int xsub = NWV == 4 ? wave : (wave >> 1);
+    const int i0 = NWV == 4 ? 0 : (wave & 1) * NI;  // first 16-column group of this wave
+    const char* xb = cur + xsub * SUB;
     const char* db = cur + 4 * SUB;
 #pragma unroll
     for (int hf = 0; hf < BKP / 32; ++hf) {
-      bf16x8 fa[4], fb[4];
+      bf16x8 fa[NI], fb[4];
       const int p0 = 32 * hf + 8 * tg + tq;
       const int sw0 = swz(p0), sw1 = swz(p0 + 4);
       const int ro0 = p0 * 128 + 8 * (tpp & 1), ro1 = ro0 + 4 * 128;
+      typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = 2 * i + (tpp >> 1);
         const int o0 = ro0 + 16 * (c ^ sw0), o1 = ro1 + 16 * (c ^ sw1);
-        typedef __attribute__((address_space(3))) bf16x4 lds_v4;
-        const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + o0));
-        const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + o1));
         const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + o0));
         const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + o1));
-        fa[i] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
         fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i) {
+        const int c = 2 * (i0 + i) + (tpp >> 1);
+        const int o0 = ro0 + 16 * (c ^ sw0), o1 = ro1 + 16 * (c ^ sw1);
+        const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + o0));
+        const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + o1));
+        fa[i] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
   }
 
-  // acc[i][j][r]: col = tc*256 + wave*64 + 16i + 4*(lane>>4) + r ; cout = cout0 + 16j + (lane&15)
-  const int colbase = tc * 256 + wave * 64;
+  // acc[i][j][r]: col = colbase + 16i + 4*(lane>>4) + r ; cout = cout0 + 16j + (lane&15)
+  const int colbase = NWV == 4 ? tc * 256 + wave * 64 : tc * 256 + (wave >> 1) * 64 + (wave & 1) * 32;
   if (colbase >= a.ncols_pad) return;
   const auto rs = make_rsrc(a.slab, (uint32_t)min((long)a.splits * a.Cout * a.ncols_pad * 4l, (long)0x7fffffff));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int co = cout0 + 16 * j + (lane & 15);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int col = colbase + 16 * i + 4 * (lane >> 4);
       const uint32_t off = (uint32_t)(((long)split * a.Cout + co) * a.ncols_pad + col) * 4u;
       uint4 v;
@@ -266,13 +277,15 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
   const int nblk = a.colTiles * a.coutTiles * a.splits;
   if (packed) {
-    hipLaunchKernelGGL((conv_wgrad_kernel<true, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_wgrad_kernel<true, true, 64, 2, 8>), dim3(nblk), dim3(512), 0, s, a);
   } else if (variant == 1) {  // alternatives kept for the microbenchmark (measured slower on gfx950)
     hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 32, 3>), dim3(nblk), dim3(256), 0, s, a);
   } else if (variant == 2) {
     hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 3>), dim3(nblk), dim3(256), 0, s, a);
-  } else {  // default: BK=64 pixels per stage, double-buffered
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2>), dim3(nblk), dim3(256), 0, s, a);
+  } else if (variant == 3) {  // 4-wave blocks (previous default)
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2, 4>), dim3(nblk), dim3(256), 0, s, a);
+  } else {  // default: BK=64 pixels per stage, double-buffered, 8 waves (64 couts x 32 columns each)
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2, 8>), dim3(nblk), dim3(512), 0, s, a);
   }
   const int creal = packed ? cin_real : a.Cin;
   const long total = (long)Cout * taps * creal;
