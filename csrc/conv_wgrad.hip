@@ -25,6 +25,7 @@
 // streamed from HBM with only one K step of lookahead.
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 struct WgradArgs {
   const u16* x1;
@@ -218,6 +219,170 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_wgrad_kernel(const WgradArgs
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Halo-reuse weight gradient for 3x3 convs whose image rows are whole 64-pixel segments (W % 64 == 0:
+// the 256^2 / 128^2 / 64^2 layers that carry ~80 % of the wgrad FLOPs).
+//
+// The generic kernel above stages one [64 px][64 ch] x tile per (tap, cin-chunk) column subtile,
+// i.e. the same input pixels 9 times (once per tap) and 40 KB of DMA per 2 MFLOP. Here one K step
+// is one 64-pixel row segment (h, w0..w0+63) of one image, and the block owns ALL 9 taps of one
+// 64-channel input chunk: it stages the three input rows h-1, h, h+1 over pixels w0-1 .. w0+64
+// (66 used of 72 staged rows per region, zero halo from out-of-range offsets) plus the dY segment,
+// and every tap (dr, ds) is a row-shifted window (rows ds+1 .. ds+64 of region dr+1) of that one
+// image. Per K step: 27 KB of x + 8 KB per 64 couts of dY for 9 x 64 x BN x 64 MACs (2.7x the
+// FLOP per staged byte at BN = 64, 3.4x at BN = 128).
+//
+// Block = BN/16 waves; wave w owns input channels 16*(w&3) .. +15 of the chunk for all 9 taps and
+// output channels 64*(w>>2) .. +63: 9 x 4 MFMA 16x16x32 accumulators (144 VGPRs), A fragments by
+// ds_read_b64_tr_b16 from the shifted windows, B fragments from the dY tile (same LDS image and
+// swizzle as the generic kernel). Split-K over row segments into the same fp32 slab format, reduced
+// by wgrad_reduce_kernel.
+struct WgradHaloArgs {
+  const u16* x1;
+  const u16* x2;
+  uint32_t xbytes1, xbytes2;
+  int C1, C2, pitch1, pitch2;
+  const u16* dy;
+  uint32_t dybytes;
+  int dypitch;
+  float* slab;
+  uint32_t slab_bytes;
+  int H, W, Cout, ncols;  // ncols = 9 * Cin = slab row length
+  int cinTiles, coutTiles, splits, segs_per_split, nseg;
+  uint32_t fw_m, fw_s, fh_m, fh_s;
+};
+
+template <int BN, int STAGES>
+__global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradHaloArgs a) {
+  constexpr int NWV = BN / 16;
+  constexpr int XREG = 72 * 128;                  // one staged input row region (72 pixel rows x 64 ch)
+  constexpr int DSUB = 64 * 128;                  // one [64 px][64 cout] dY subtile
+  constexpr int BUF = 3 * XREG + (BN / 64) * DSUB;
+  constexpr int XPIECES = 27, NPIECES = XPIECES + 8 * (BN / 64);
+  constexpr int PPW = (NPIECES + NWV - 1) / NWV;  // DMA pieces (8 rows x 128 B) per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
+  // consecutive logical ids (one XCD) = different weight tiles of the same segment range: they
+  // share the dY / x lines in that XCD's L2
+  const int ntiles = a.cinTiles * a.coutTiles;
+  const int split = lid / ntiles, tile = lid - split * ntiles;
+  const int tc = tile % a.cinTiles, tn = tile / a.cinTiles;
+  const int cin0 = tc * 64, cout0 = tn * BN;
+  const int s0 = split * a.segs_per_split;
+  const int s1 = min(a.nseg, s0 + a.segs_per_split);
+  const int nks = s1 - s0;
+
+  const bool src2 = cin0 >= a.C1;
+  const auto rx = src2 ? make_rsrc(a.x2, a.xbytes2) : make_rsrc(a.x1, a.xbytes1);
+  const int pitch = src2 ? a.pitch2 : a.pitch1;
+  const int ch0 = src2 ? cin0 - a.C1 : cin0;
+  const auto rdy = make_rsrc(a.dy, a.dybytes);
+
+  const int rowl = lane >> 3, cpos = lane & 7;
+
+  auto issue = [&](int ks, char* buf) {
+    const int m0 = (s0 + ks) * 64;  // first pixel of the segment
+    const uint32_t q = fdiv2((uint32_t)m0, a.fw_m, a.fw_s);
+    const int w0 = m0 - (int)q * a.W;
+    const int h = (int)q - (int)fdiv2(q, a.fh_m, a.fh_s) * a.H;
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) {
+      const int piece = wave + t * NWV;  // wave-uniform
+      if (piece < XPIECES) {
+        const int r = piece / 9, pj = piece - r * 9;  // region (dr + 1), 8-row piece in the region
+        const int j = pj * 8 + rowl;                  // staged row: pixel w0 - 1 + j of image row h + dr
+        const int g = cpos ^ swz(j);
+        const bool ok = (j < 66) & inb(w0 - 1 + j, a.W) & inb(h + r - 1, a.H);
+        const uint32_t off = ok ? (uint32_t)((m0 + (r - 1) * a.W + j - 1) * pitch + ch0 + g * 8) * 2u : RDP_OOB;
+        dma16(rx, (lds_void*)(buf + r * XREG + pj * 1024), off);
+      } else if (piece < NPIECES) {
+        const int d = piece - XPIECES, sub = d >> 3, pj = d & 7;
+        const int p = pj * 8 + rowl;
+        const int g = cpos ^ swz(p);
+        const uint32_t off = (uint32_t)((m0 + p) * a.dypitch + cout0 + sub * 64 + g * 8) * 2u;
+        dma16(rdy, (lds_void*)(buf + 3 * XREG + sub * DSUB + pj * 1024), off);
+      }
+    }
+  };
+
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry (see conv_wgrad_kernel): lane = 16 tg + 4 tq + tpp
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tpp = lane & 3;
+  const int cf = wave & 3, cg = wave >> 2;
+  const int ca = 2 * cf + (tpp >> 1);  // 16-B chunk of this lane's A fragment row (input channels)
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < nks) issue(st, smem + st * BUF);
+  for (int ks = 0; ks < nks; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
+    const char* cur = smem + (ks % STAGES) * BUF;
+    const char* db = cur + 3 * XREG + cg * DSUB;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int p0 = 32 * hf + 8 * tg + tq;
+      bf16x8 fb[4];
+      {
+        const int sw0 = swz(p0), sw1 = swz(p0 + 4);
+        const int ro0 = p0 * 128 + 8 * (tpp & 1), ro1 = ro0 + 4 * 128;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 2 * i + (tpp >> 1);
+          const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro0 + 16 * (c ^ sw0)));
+          const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro1 + 16 * (c ^ sw1)));
+          fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+#pragma unroll
+      for (int sh = 0; sh < 3; ++sh) {  // ds + 1: window row shift
+        const int pa = p0 + sh, pb = p0 + sh + 4;
+        const int oa = pa * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pa));
+        const int ob = pb * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pb));
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {  // dr + 1: input row region
+          const char* xb = cur + r * XREG;
+          const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + oa));
+          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + ob));
+          const bf16x8 fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+          const int tap = r * 3 + sh;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[i], acc[tap][i], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // acc[tap][i][r]: cin = cin0 + 16 cf + 4 (lane >> 4) + r, cout = cout0 + 64 cg + 16 i + (lane & 15)
+  const auto rs = make_rsrc(a.slab, a.slab_bytes);
+  const int cin = cin0 + 16 * cf + 4 * (lane >> 4);
+  const int Cin = a.ncols / 9;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = cout0 + 64 * cg + 16 * i + (lane & 15);
+    const long rowbase = ((long)split * a.Cout + co) * a.ncols + cin;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint32_t off = (uint32_t)(rowbase + t * Cin) * 4u;
+      uint4 v;
+      v.x = __float_as_uint(acc[t][i][0]); v.y = __float_as_uint(acc[t][i][1]);
+      v.z = __float_as_uint(acc[t][i][2]); v.w = __float_as_uint(acc[t][i][3]);
+      bstore16(rs, off, v);
+    }
+  }
+}
+
 // out[cout][tap][cin_real] (+)= sum_split slab[split][cout][tap*cin_pad + cin]
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int splits, int Cout,
                                     int ncols_pad, int taps, int cin_pad, int cin_real, int accumulate) {
@@ -263,6 +428,44 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   }
   if (Cout % 64) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || dybytes >= (1l << 31)) return -1;
+  // halo-reuse kernel: 3x3, whole 64-pixel row segments (variant 0 = auto, 5 = force)
+  if ((variant == 0 || variant == 5) && !packed && taps == 9 && W % 64 == 0) {
+    static const int env_blocks = [] {
+      const char* e = getenv("RDP_WGRAD_HALO_BLOCKS");
+      return e ? atoi(e) : 0;
+    }();
+    WgradHaloArgs h;
+    h.x1 = a.x1; h.x2 = a.x2; h.xbytes1 = a.xbytes1; h.xbytes2 = a.xbytes2;
+    h.C1 = C1; h.C2 = C2; h.pitch1 = pitch1; h.pitch2 = pitch2;
+    h.dy = a.dy; h.dybytes = a.dybytes; h.dypitch = dypitch;
+    h.slab = slab; h.H = H; h.W = W; h.Cout = Cout; h.ncols = 9 * a.Cin;
+    const int BN = Cout % 128 == 0 ? 128 : 64;
+    h.cinTiles = a.Cin / 64; h.coutTiles = Cout / BN;
+    const int tiles = h.cinTiles * h.coutTiles;
+    h.nseg = a.M / 64;
+    // one resident wave of blocks (2/CU at BN = 64, 1/CU at BN = 128), within the slab
+    const int target = env_blocks > 0 ? env_blocks : (BN == 64 ? 512 : 256);
+    int sp = std::max(1, (target + tiles - 1) / tiles);
+    sp = std::min(sp, h.nseg);
+    const long per_split = (long)Cout * h.ncols;
+    sp = (int)std::min<long>(sp, slab_elems / per_split);
+    if (sp < 1) return -2;
+    h.segs_per_split = (h.nseg + sp - 1) / sp;
+    h.splits = (h.nseg + h.segs_per_split - 1) / h.segs_per_split;
+    if ((long)h.splits * per_split * 4l >= (1l << 31)) return -3;
+    h.slab_bytes = (uint32_t)(h.splits * per_split * 4l);
+    FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
+    h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
+    const int nblk = tiles * h.splits;
+    if (BN == 128) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2>), dim3(nblk), dim3(512), 0, s, h);
+    else hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2>), dim3(nblk), dim3(256), 0, s, h);
+    const long total = (long)Cout * 9 * a.Cin;
+    const int rb = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rb), dim3(256), 0, s, slab, out, h.splits, Cout, h.ncols, 9, a.Cin,
+                       a.Cin, accumulate);
+    return h.splits;
+  }
+  if (variant == 5) return -1;
   a.colTiles = (a.ncols + 255) / 256;
   a.ncols_pad = a.colTiles * 256;
   a.coutTiles = Cout / 64;

@@ -49,7 +49,7 @@ def main():
         if a.wgrad:
             dy = torch.randn(N, H, H, Co, device=dev).to(torch.bfloat16)
             tiles = ((9 * Cin + 255) // 256) * (Co // 64)
-            splits = max(1, min((1024 + tiles - 1) // tiles, N * H * H // 2048))
+            splits = max(1, min((2048 + tiles - 1) // tiles, N * H * H // 2048))
             slab = torch.zeros(C.wgrad_slab_elems(N, H, H, Cin, Co, 9, 0, splits), device=dev)
             out = torch.zeros(Co * 9 * Cin, device=dev)
 
