@@ -63,6 +63,26 @@ RDP_DEV void dma16(__amdgpu_buffer_rsrc_t r, lds_void* lds_base, uint32_t voff) 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_base, 16, voff, 0, 0, 0);
 }
 
+// The same LDS-DMA issued from inline asm. hipcc neither counts it nor orders later LDS reads
+// behind it: after the builtin form, hipcc puts `s_waitcnt vmcnt(0)` in front of every
+// ds_read_b64_tr_b16 (the transposed-read intrinsic may alias any DMA destination), which drains
+// the NEXT stage's DMA before the current stage computes and serialises a double-buffered loop.
+// Callers own the bookkeeping: `s_waitcnt vmcnt(N)` + barrier before reading a staged buffer.
+// M0 is saved/restored inside the statement (cdna_hip_programming.md §5.7 LDS-DMA recipe).
+RDP_DEV void dma16_async(__amdgpu_buffer_rsrc_t r, lds_void* lds_base, uint32_t voff) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_base);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(dst), "s"(r)
+      : "memory");
+}
+
 RDP_DEV void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 RDP_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 RDP_DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); }

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_wgrad_kernel(const WgradArgs
       // dY piece
       {
         const uint32_t off = mv ? (uint32_t)(m * a.dypitch + cout0 + g * 8) * 2u : RDP_OOB;
-        dma16(rdy, (lds_void*)(buf + 4 * SUB + s * 1024), off);
+        dma16_async(rdy, (lds_void*)(buf + 4 * SUB + s * 1024), off);
       }
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub) {
@@ -128,14 +128,14 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_wgrad_kernel(const WgradArgs
           const int hh = h + dr, ww = w + ds;
           const bool ok = mv & (bool)s_ok[sub] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
           const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
-          dma16(rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
+          dma16_async(rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
         } else {
           ch = s_ch[sub] + g * 8;
           const int hh = h + dr, ww = w + ds;
           const bool ok = mv & (bool)s_ok[sub] & inb(hh, a.H) & inb(ww, a.W);
           const int pitch = s_src[sub] ? a.pitch2 : a.pitch1;
           const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * pitch + ch) * 2u : RDP_OOB;
-          dma16(s_src[sub] ? rx2 : rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
+          dma16_async(s_src[sub] ? rx2 : rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
         }
       }
     }
@@ -220,12 +220,12 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_wgrad_kernel(const WgradArgs
 }
 
 // ---------------------------------------------------------------------------------------------
-// Halo-reuse weight gradient for 3x3 convs whose image rows are whole 64-pixel segments (W % 64 == 0:
-// the 256^2 / 128^2 / 64^2 layers that carry ~80 % of the wgrad FLOPs).
+// Halo-reuse weight gradient for 3x3 convs whose pixels split into 64-pixel segments of whole rows
+// or of one row (W % 64 == 0, or W | 64 with H * W % 64 == 0: every U-Net layer at 256^2..16^2).
 //
 // The generic kernel above stages one [64 px][64 ch] x tile per (tap, cin-chunk) column subtile,
 // i.e. the same input pixels 9 times (once per tap) and 40 KB of DMA per 2 MFLOP. Here one K step
-// is one 64-pixel row segment (h, w0..w0+63) of one image, and the block owns ALL 9 taps of one
+// is one 64-pixel segment (h, w0..w0+63) of one image (or 64 / W whole rows), and the block owns ALL 9 taps of one
 // 64-channel input chunk: it stages the three input rows h-1, h, h+1 over pixels w0-1 .. w0+64
 // (66 used of 72 staged rows per region, zero halo from out-of-range offsets) plus the dY segment,
 // and every tap (dr, ds) is a row-shifted window (rows ds+1 .. ds+64 of region dr+1) of that one
@@ -252,7 +252,8 @@ struct WgradHaloArgs {
   uint32_t fw_m, fw_s, fh_m, fh_s;
 };
 
-template <int BN, int STAGES>
+// ABL (microbenchmark ablations only): 1 = no DMA after the prologue, 2 = no MFMA, 4 = no LDS reads
+template <int BN, int STAGES, bool MULTIROW, int ABL = 0>
 __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradHaloArgs a) {
   constexpr int NWV = BN / 16;
   constexpr int XREG = 72 * 128;                  // one staged input row region (72 pixel rows x 64 ch)
@@ -296,15 +297,20 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
         const int r = piece / 9, pj = piece - r * 9;  // region (dr + 1), 8-row piece in the region
         const int j = pj * 8 + rowl;                  // staged row: pixel w0 - 1 + j of image row h + dr
         const int g = cpos ^ swz(j);
-        const bool ok = (j < 66) & inb(w0 - 1 + j, a.W) & inb(h + r - 1, a.H);
+        // image row of the staged pixel: row h + dr + floor((w0 - 1 + j) / W). Wide rows (W >= 64)
+        // keep only pixels of row h + dr (the rest is the zero halo); multi-row segments (W | 64)
+        // keep every in-image row and mask the row-crossing taps on the dY side instead.
+        const int wj = w0 - 1 + j;
+        const int wq = wj < 0 ? -1 : (int)fdiv2((uint32_t)wj, a.fw_m, a.fw_s);
+        const bool ok = (j < 66) & (MULTIROW || wq == 0) & inb(h + r - 1 + wq, a.H);
         const uint32_t off = ok ? (uint32_t)((m0 + (r - 1) * a.W + j - 1) * pitch + ch0 + g * 8) * 2u : RDP_OOB;
-        dma16(rx, (lds_void*)(buf + r * XREG + pj * 1024), off);
+        dma16_async(rx, (lds_void*)(buf + r * XREG + pj * 1024), off);
       } else if (piece < NPIECES) {
         const int d = piece - XPIECES, sub = d >> 3, pj = d & 7;
         const int p = pj * 8 + rowl;
         const int g = cpos ^ swz(p);
         const uint32_t off = (uint32_t)((m0 + p) * a.dypitch + cout0 + sub * 64 + g * 8) * 2u;
-        dma16(rdy, (lds_void*)(buf + 3 * XREG + sub * DSUB + pj * 1024), off);
+        dma16_async(rdy, (lds_void*)(buf + 3 * XREG + sub * DSUB + pj * 1024), off);
       }
     }
   };
@@ -325,11 +331,213 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
   for (int st = 0; st < STAGES - 1; ++st)
     if (st < nks) issue(st, smem + st * BUF);
   for (int ks = 0; ks < nks; ++ks) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (STAGES == 3 && ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPIECES / NWV) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
+    if (!(ABL & 1) && ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
     const char* cur = smem + (ks % STAGES) * BUF;
     const char* db = cur + 3 * XREG + cg * DSUB;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int p0 = 32 * hf + 8 * tg + tq;
+      bf16x8 fb[4];
+      {
+        const int sw0 = swz(p0), sw1 = swz(p0 + 4);
+        const int ro0 = p0 * 128 + 8 * (tpp & 1), ro1 = ro0 + 4 * 128;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 2 * i + (tpp >> 1);
+          if constexpr ((ABL & 4) != 0) {
+            fb[i] = bf16x8{(short)(lane + i), (short)ks, 1, 2, 3, 4, 5, (short)hf};
+          } else {
+            const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro0 + 16 * (c ^ sw0)));
+            const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro1 + 16 * (c ^ sw1)));
+            fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        }
+      }
+      // multi-row segments (W < 64): window pixel p + ds of tap ds = -1 / +1 crosses into the
+      // neighbouring image row where w = 0 / W - 1; zero those dY pixels for that tap. This lane
+      // holds B rows (pixels) 32 hf + 8 (lane >> 4) + e, e = 0..7 (MFMA 16x16x32 B layout).
+      const int pl = 32 * hf + 8 * (lane >> 4);
+      const bool mL = MULTIROW && (pl & (a.W - 1)) == 0;      // e = 0 has w = 0
+      const bool mR = MULTIROW && ((pl + 8) & (a.W - 1)) == 0;  // e = 7 has w = W - 1
+#pragma unroll
+      for (int sh = 0; sh < 3; ++sh) {  // ds + 1: window row shift
+        bf16x8 fbs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          fbs[i] = fb[i];
+          if (MULTIROW && sh == 0) fbs[i][0] = mL ? (short)0 : fb[i][0];
+          if (MULTIROW && sh == 2) fbs[i][7] = mR ? (short)0 : fb[i][7];
+        }
+        const int pa = p0 + sh, pb = p0 + sh + 4;
+        const int oa = pa * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pa));
+        const int ob = pb * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pb));
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {  // dr + 1: input row region
+          const char* xb = cur + r * XREG;
+          bf16x8 fa;
+          if constexpr ((ABL & 4) != 0) {
+            fa = bf16x8{(short)(oa + r), (short)ob, (short)sh, 2, 3, 4, 5, (short)ks};
+          } else {
+            const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + oa));
+            const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + ob));
+            fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+          const int tap = r * 3 + sh;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(fa), "v"(fbs[i]));
+            else acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbs[i], acc[tap][i], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // acc[tap][i][r]: cin = cin0 + 16 cf + 4 (lane >> 4) + r, cout = cout0 + 64 cg + 16 i + (lane & 15)
+  const auto rs = make_rsrc(a.slab, a.slab_bytes);
+  const int cin = cin0 + 16 * cf + 4 * (lane >> 4);
+  const int Cin = a.ncols / 9;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = cout0 + 64 * cg + 16 * i + (lane & 15);
+    const long rowbase = ((long)split * a.Cout + co) * a.ncols + cin;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint32_t off = (uint32_t)(rowbase + t * Cin) * 4u;
+      uint4 v;
+      v.x = __float_as_uint(acc[t][i][0]); v.y = __float_as_uint(acc[t][i][1]);
+      v.z = __float_as_uint(acc[t][i][2]); v.w = __float_as_uint(acc[t][i][3]);
+      bstore16(rs, off, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row-ring variant of the halo wgrad for wide rows (W % 64 == 0). K steps walk each 64-pixel
+// column (image n, segment wseg) top to bottom: position P = column * H + h. Step P needs input
+// rows P - 1, P, P + 1, and rows P - 1 and P were staged by the two previous steps, so a step
+// stages ONE new input row region (9 KB) plus its dY tile instead of three regions: half the DMA
+// bytes of conv_wgrad_halo_kernel at BN = 64. Input rows live in a 5-slot ring (slot = P % 5), dY
+// in a 3-slot ring; two steps stay in flight across the per-step barrier (counted vmcnt). At a
+// column's first / last row the dr = -1 / +1 taps are skipped (the neighbouring ring slot holds
+// another column's row: that is the zero padding row of this one).
+struct WgradRingArgs {
+  const u16* x1;
+  const u16* x2;
+  uint32_t xbytes1, xbytes2;
+  int C1, C2, pitch1, pitch2;
+  const u16* dy;
+  uint32_t dybytes;
+  int dypitch;
+  float* slab;
+  uint32_t slab_bytes;
+  int H, W, Cout, ncols;
+  int cinTiles, coutTiles, splits, pos_per_split, npos;
+  int WS;                           // 64-pixel segments per image row
+  uint32_t fh_m, fh_s, fs_m, fs_s;  // fast div by H and by WS
+};
+
+template <int BN, int ABL = 0>
+__global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradRingArgs a) {
+  constexpr int NWV = BN / 16;
+  constexpr int XREG = 72 * 128;   // one staged input row region: pixels w0-1 .. w0+70 (66 used)
+  constexpr int DSUB = 64 * 128;   // [64 px][64 cout] dY subtile
+  constexpr int NX = 5, ND = 3;    // ring slots
+  constexpr int DT = (BN / 64) * DSUB;
+  constexpr int XPIECES = 9, NPIECES = XPIECES + 8 * (BN / 64);
+  constexpr int PPW = (NPIECES + NWV - 1) / NWV;
+  constexpr int MINPW = NPIECES / NWV;  // DMAs issued per step by the wave that issues fewest
+  __shared__ __attribute__((aligned(16))) char smem[NX * XREG + ND * DT];
+  char* const xring = smem;
+  char* const dring = smem + NX * XREG;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = a.cinTiles * a.coutTiles;
+  const int split = lid / ntiles, tile = lid - split * ntiles;
+  const int tc = tile % a.cinTiles, tn = tile / a.cinTiles;
+  const int cin0 = tc * 64, cout0 = tn * BN;
+  const int p0s = split * a.pos_per_split;
+  const int nks = min(a.npos, p0s + a.pos_per_split) - p0s;
+
+  const bool src2 = cin0 >= a.C1;
+  const auto rx = src2 ? make_rsrc(a.x2, a.xbytes2) : make_rsrc(a.x1, a.xbytes1);
+  const int pitch = src2 ? a.pitch2 : a.pitch1;
+  const int ch0 = src2 ? cin0 - a.C1 : cin0;
+  const auto rdy = make_rsrc(a.dy, a.dybytes);
+  const int rowl = lane >> 3, cpos = lane & 7;
+
+  // position -> (first pixel of the segment, row h); P may be -1 or npos (loads read zeros)
+  auto locate = [&](int P, int& m0, int& h, int& w0) {
+    const uint32_t up = (uint32_t)max(P, 0);
+    const uint32_t col = fdiv2(up, a.fh_m, a.fh_s);
+    h = (int)(up - col * (uint32_t)a.H);
+    const uint32_t n = fdiv2(col, a.fs_m, a.fs_s);
+    const int wseg = (int)(col - n * (uint32_t)a.WS);
+    m0 = (((int)n * a.H + h) * a.WS + wseg) * 64;
+    w0 = wseg * 64;
+    if (P < 0 || P >= a.npos) h = -2;  // no such row: every pixel out of the image
+  };
+  // piece t of this wave: x-row pieces (when wx) then dY pieces (when wd)
+  auto issue = [&](int P, bool wx, bool wd) {
+    int m0, h, w0;
+    locate(P, m0, h, w0);
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) {
+      const int piece = wave + t * NWV;
+      if (piece < XPIECES) {
+        if (!wx) continue;
+        const int j = piece * 8 + rowl;
+        const int g = cpos ^ swz(j);
+        const bool ok = (j < 66) & inb(w0 - 1 + j, a.W) & inb(h, a.H);
+        const uint32_t off = ok ? (uint32_t)((m0 + j - 1) * pitch + ch0 + g * 8) * 2u : RDP_OOB;
+        dma16_async(rx, (lds_void*)(xring + ((P + NX) % NX) * XREG + piece * 1024), off);
+      } else if (piece < NPIECES) {
+        if (!wd) continue;
+        const int d = piece - XPIECES, sub = d >> 3, pj = d & 7;
+        const int p = pj * 8 + rowl;
+        const int g = cpos ^ swz(p);
+        const bool ok = inb(h, a.H);
+        const uint32_t off = ok ? (uint32_t)((m0 + p) * a.dypitch + cout0 + sub * 64 + g * 8) * 2u : RDP_OOB;
+        dma16_async(rdy, (lds_void*)(dring + (((P - p0s) % ND) * DT) + sub * DSUB + pj * 1024), off);
+      }
+    }
+  };
+
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tpp = lane & 3;
+  const int cf = wave & 3, cg = wave >> 2;
+  const int ca = 2 * cf + (tpp >> 1);
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+
+  // prologue: rows P0 - 1, P0 (x only), then steps 0 and 1 (row P + 1 and dY P)
+  if (nks > 0) {
+    issue(p0s - 1, true, false);
+    issue(p0s, true, false);
+    issue(p0s + 1, true, false);
+    issue(p0s, false, true);
+    if (nks > 1) { issue(p0s + 2, true, false); issue(p0s + 1, false, true); }
+  }
+  for (int ks = 0; ks < nks; ++ks) {
+    const int P = p0s + ks;
+    // step ks's data: everything but the (up to MINPW-per-wave) DMAs of step ks + 1
+    if (ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (!(ABL & 1) && ks + 2 < nks) { issue(P + 3, true, false); issue(P + 2, false, true); }
+    int m0, h, w0;
+    locate(P, m0, h, w0);
+    const bool top = h == 0, bottom = h == a.H - 1;
+    const char* db = dring + ((ks % ND) * DT) + cg * DSUB;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       const int p0 = 32 * hf + 8 * tg + tq;
@@ -346,25 +554,28 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
         }
       }
 #pragma unroll
-      for (int sh = 0; sh < 3; ++sh) {  // ds + 1: window row shift
+      for (int sh = 0; sh < 3; ++sh) {
         const int pa = p0 + sh, pb = p0 + sh + 4;
         const int oa = pa * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pa));
         const int ob = pb * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pb));
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {  // dr + 1: input row region
-          const char* xb = cur + r * XREG;
+        for (int r = 0; r < 3; ++r) {
+          if ((r == 0 && top) || (r == 2 && bottom)) continue;  // wave-uniform
+          const char* xb = xring + ((P + r - 1 + NX) % NX) * XREG;
           const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + oa));
           const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + ob));
           const bf16x8 fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
           const int tap = r * 3 + sh;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[i], acc[tap][i], 0, 0, 0);
+          for (int i = 0; i < 4; ++i) {
+            if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(fa), "v"(fb[i]));
+            else acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[i], acc[tap][i], 0, 0, 0);
+          }
         }
       }
     }
   }
 
-  // acc[tap][i][r]: cin = cin0 + 16 cf + 4 (lane >> 4) + r, cout = cout0 + 64 cg + 16 i + (lane & 15)
   const auto rs = make_rsrc(a.slab, a.slab_bytes);
   const int cin = cin0 + 16 * cf + 4 * (lane >> 4);
   const int Cin = a.ncols / 9;
@@ -429,7 +640,8 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   if (Cout % 64) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || dybytes >= (1l << 31)) return -1;
   // halo-reuse kernel: 3x3, whole 64-pixel row segments (variant 0 = auto, 5 = force)
-  if ((variant == 0 || variant == 5) && !packed && taps == 9 && W % 64 == 0) {
+  const bool halo_ok = !packed && taps == 9 && (W % 64 == 0 || (W >= (variant == 5 ? 8 : 32) && 64 % W == 0 && (H * W) % 64 == 0));
+  if ((variant == 0 || variant == 5 || (variant >= 30 && variant < 40)) && halo_ok) {
     static const int env_blocks = [] {
       const char* e = getenv("RDP_WGRAD_HALO_BLOCKS");
       return e ? atoi(e) : 0;
@@ -457,8 +669,46 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
     h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
     const int nblk = tiles * h.splits;
-    if (BN == 128) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2>), dim3(nblk), dim3(512), 0, s, h);
-    else hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2>), dim3(nblk), dim3(256), 0, s, h);
+    if (variant == 0 && W % 64 == 0 && BN == 64) {  // row-ring variant: same split of the positions
+      WgradRingArgs g;
+      g.x1 = h.x1; g.x2 = h.x2; g.xbytes1 = h.xbytes1; g.xbytes2 = h.xbytes2;
+      g.C1 = C1; g.C2 = C2; g.pitch1 = pitch1; g.pitch2 = pitch2;
+      g.dy = h.dy; g.dybytes = h.dybytes; g.dypitch = dypitch;
+      g.slab = slab; g.slab_bytes = h.slab_bytes; g.H = H; g.W = W; g.Cout = Cout; g.ncols = h.ncols;
+      g.cinTiles = h.cinTiles; g.coutTiles = h.coutTiles; g.splits = h.splits;
+      g.pos_per_split = h.segs_per_split; g.npos = h.nseg; g.WS = W / 64;
+      FastDiv fs = make_fastdiv(W / 64);
+      g.fh_m = fh.m; g.fh_s = fh.s; g.fs_m = fs.m; g.fs_s = fs.s;
+      if (BN == 128) hipLaunchKernelGGL((conv_wgrad_ring_kernel<128>), dim3(nblk), dim3(512), 0, s, g);
+      else hipLaunchKernelGGL((conv_wgrad_ring_kernel<64>), dim3(nblk), dim3(256), 0, s, g);
+    } else if (variant >= 30 && variant < 40 && W % 64 == 0) {  // ring ablations (microbenchmark)
+      WgradRingArgs g;
+      g.x1 = h.x1; g.x2 = h.x2; g.xbytes1 = h.xbytes1; g.xbytes2 = h.xbytes2;
+      g.C1 = C1; g.C2 = C2; g.pitch1 = pitch1; g.pitch2 = pitch2;
+      g.dy = h.dy; g.dybytes = h.dybytes; g.dypitch = dypitch;
+      g.slab = slab; g.slab_bytes = h.slab_bytes; g.H = H; g.W = W; g.Cout = Cout; g.ncols = h.ncols;
+      g.cinTiles = h.cinTiles; g.coutTiles = h.coutTiles; g.splits = h.splits;
+      g.pos_per_split = h.segs_per_split; g.npos = h.nseg; g.WS = W / 64;
+      FastDiv fs = make_fastdiv(W / 64);
+      g.fh_m = fh.m; g.fh_s = fh.s; g.fs_m = fs.m; g.fs_s = fs.s;
+      const int abl = variant % 10;
+      if (BN == 128 && abl == 1) hipLaunchKernelGGL((conv_wgrad_ring_kernel<128, 1>), dim3(nblk), dim3(512), 0, s, g);
+      if (BN == 128 && abl == 2) hipLaunchKernelGGL((conv_wgrad_ring_kernel<128, 2>), dim3(nblk), dim3(512), 0, s, g);
+      if (BN == 64 && abl == 1) hipLaunchKernelGGL((conv_wgrad_ring_kernel<64, 1>), dim3(nblk), dim3(256), 0, s, g);
+      if (BN == 64 && abl == 2) hipLaunchKernelGGL((conv_wgrad_ring_kernel<64, 2>), dim3(nblk), dim3(256), 0, s, g);
+    } else {
+    const bool mr = W < 64;
+    static const int env_stages = [] {
+      const char* e = getenv("RDP_WGRAD_HALO_STAGES");  // 3 measured 3-8 % slower than 2
+      return e ? atoi(e) : 2;
+    }();
+    if (BN == 128 && mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, true>), dim3(nblk), dim3(512), 0, s, h);
+    else if (BN == 128 && env_stages == 3)
+      hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 3, false>), dim3(nblk), dim3(512), 0, s, h);
+    else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, false>), dim3(nblk), dim3(512), 0, s, h);
+    else if (mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2, true>), dim3(nblk), dim3(256), 0, s, h);
+    else hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2, false>), dim3(nblk), dim3(256), 0, s, h);
+    }
     const long total = (long)Cout * 9 * a.Cin;
     const int rb = (int)std::min<long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rb), dim3(256), 0, s, slab, out, h.splits, Cout, h.ncols, 9, a.Cin,
@@ -466,6 +716,33 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     return h.splits;
   }
   if (variant == 5) return -1;
+  if (variant >= 10 && variant < 30 && halo_ok && W % 64 == 0) {  // ablation builds (microbenchmark)
+    WgradHaloArgs h;
+    h.x1 = a.x1; h.x2 = a.x2; h.xbytes1 = a.xbytes1; h.xbytes2 = a.xbytes2;
+    h.C1 = C1; h.C2 = C2; h.pitch1 = pitch1; h.pitch2 = pitch2;
+    h.dy = a.dy; h.dybytes = a.dybytes; h.dypitch = dypitch;
+    h.slab = slab; h.H = H; h.W = W; h.Cout = Cout; h.ncols = 9 * a.Cin;
+    const int BN = variant >= 20 ? 128 : 64;
+    if (Cout % BN) return -1;
+    h.cinTiles = a.Cin / 64; h.coutTiles = Cout / BN;
+    const int tiles = h.cinTiles * h.coutTiles;
+    h.nseg = a.M / 64;
+    int sp = std::min(std::max(1, ((BN == 64 ? 512 : 256) + tiles - 1) / tiles), h.nseg);
+    sp = (int)std::min<long>(sp, slab_elems / ((long)Cout * h.ncols));
+    h.segs_per_split = (h.nseg + sp - 1) / sp;
+    h.splits = (h.nseg + h.segs_per_split - 1) / h.segs_per_split;
+    h.slab_bytes = (uint32_t)(h.splits * (long)Cout * h.ncols * 4l);
+    FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
+    h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
+    const int nblk = tiles * h.splits;
+    const int abl = variant % 10;
+#define RDP_ABL(B, A) \
+    if (BN == B && abl == A) hipLaunchKernelGGL((conv_wgrad_halo_kernel<B, 2, false, A>), dim3(nblk), dim3(B * 4), 0, s, h);
+    RDP_ABL(64, 0) RDP_ABL(64, 1) RDP_ABL(64, 2) RDP_ABL(64, 4) RDP_ABL(64, 6)
+    RDP_ABL(128, 0) RDP_ABL(128, 1) RDP_ABL(128, 2) RDP_ABL(128, 4) RDP_ABL(128, 6)
+#undef RDP_ABL
+    return h.splits;
+  }
   a.colTiles = (a.ncols + 255) / 256;
   a.ncols_pad = a.colTiles * 256;
   a.coutTiles = Cout / 64;

@@ -11,5 +11,5 @@ while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $line -d $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i -o pmc --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/conv_microbench.py ${MB_ARGS} > $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i.log 2>&1 || { echo "set $i failed"; tail -5 $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i.log; }
-done < $GRAFT_REPO_ROOT/scripts/pmc_sets.txt
+done < $GRAFT_REPO_ROOT/scripts/${PMC_FILE:-pmc_sets.txt}
 echo done

@@ -168,7 +168,9 @@ def test_conv_dgrad_split_output(C):
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,splits", [
     (2, 16, 16, 64, 0, 64, 3), (1, 32, 32, 128, 0, 128, 4), (2, 9, 13, 64, 64, 128, 2), (1, 8, 8, 256, 0, 512, 1),
     # W % 64 == 0: the halo-reuse kernel (row-segment K steps, 9 taps from one staged row triple)
-    (2, 5, 64, 64, 0, 64, 3), (1, 6, 128, 64, 64, 128, 4), (3, 3, 64, 128, 0, 64, 64), (1, 4, 192, 64, 128, 256, 2)])
+    (2, 5, 64, 64, 0, 64, 3), (1, 6, 128, 64, 64, 128, 4), (3, 3, 64, 128, 0, 64, 64), (1, 4, 192, 64, 128, 256, 2),
+    # W | 64: multi-row segments, row-crossing taps masked on the dY side
+    (2, 6, 32, 64, 0, 64, 3), (1, 8, 16, 128, 128, 128, 2), (3, 8, 8, 64, 0, 128, 5)])
 def test_conv_wgrad(C, N, H, W, C1, C2, Cout, splits):
     torch.manual_seed(3)
     dev = "cuda"
