@@ -229,39 +229,55 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
     const int m0 = tm * BM, n0 = tn * BN;
     float s1[NJ][4], s2[NJ][4];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * WNT + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+    // Widened stores: a lane holds 4 couts (16 j + 4 g + r, g = lane >> 4) of one pixel per
+    // fragment. v_permlane16_swap of fragment pair (j, j+1) gives every lane 8 consecutive couts
+    // (lanes g: 0 -> 0..7, 1 -> 16..23, 2 -> 8..15, 3 -> 24..31 of the pair) = one 16-B store, and a
+    // pixel's 32 couts become 64 contiguous bytes per instruction (cdna_hip_programming.md T21).
+    const int gq = lane >> 4;
+    const int coff = 16 * (gq & 1) + 8 * (gq >> 1);
+#pragma unroll
+    for (int jp = 0; jp < NJ; jp += 2) {
+      const int nb = n0 + wn * WNT + jp * 16;  // first cout of the pair
+      const int n = nb + coff;                  // this lane's 8 couts after the swap
       const bool d2 = n >= a.Cy1;
       const int nn = d2 ? n - a.Cy1 : n;
       const int yp = d2 ? a.ypitch2 : a.ypitch1;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
-#pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-        f32x4 o = acc[j][i];
-        if (a.escale) {
-          const float4 sc = *(const float4*)(a.escale + n), sh = *(const float4*)(a.eshift + n);
-          o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
-          o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
-          if (a.erelu) {
-            o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
+        uint2 v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = jp + h;
+          f32x4 o = acc[j][i];
+          if (a.escale) {
+            const int nc = nb + h * 16 + 4 * gq;
+            const float4 sc = *(const float4*)(a.escale + nc), sh = *(const float4*)(a.eshift + nc);
+            o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+            o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+            if (a.erelu) {
+              o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
+            }
+          }
+          v[h].x = pack2bf(o[0], o[1]);
+          v[h].y = pack2bf(o[2], o[3]);
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (a.stats) {
+            const float q0 = __uint_as_float(v[h].x << 16), q1 = __uint_as_float(v[h].x & 0xffff0000u);
+            const float q2 = __uint_as_float(v[h].y << 16), q3 = __uint_as_float(v[h].y & 0xffff0000u);
+            s1[j][0] += q0; s2[j][0] += q0 * q0;
+            s1[j][1] += q1; s2[j][1] += q1 * q1;
+            s1[j][2] += q2; s2[j][2] += q2 * q2;
+            s1[j][3] += q3; s2[j][3] += q3 * q3;
           }
         }
-        uint2 v;
-        v.x = pack2bf(o[0], o[1]);
-        v.y = pack2bf(o[2], o[3]);
-        acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
+        const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
         const uint32_t off = m < a.M ? (uint32_t)(m * yp + nn) * 2u : RDP_OOB;
-        bstore8(d2 ? ry2 : ry1, off, v);
-        if (a.stats) {
-          const float q0 = bf2f((u16)(v.x & 0xffff)), q1 = bf2f((u16)(v.x >> 16));
-          const float q2 = bf2f((u16)(v.y & 0xffff)), q3 = bf2f((u16)(v.y >> 16));
-          s1[j][0] += q0; s2[j][0] += q0 * q0;
-          s1[j][1] += q1; s2[j][1] += q1 * q1;
-          s1[j][2] += q2; s2[j][2] += q2 * q2;
-          s1[j][3] += q3; s2[j][3] += q3 * q3;
-        }
+        bstore16(d2 ? ry2 : ry1, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
       }
     }
     if (a.stats) {
@@ -431,7 +447,7 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
     a.nks = taps * a.cpt;
     if (ldw < taps * (C1 + C2)) return -1;
   }
-  if (Cout % 64 || Cy1 % 4) return -1;
+  if (Cout % 64 || Cy1 % 8) return -1;  // widened 16-B epilogue stores never straddle the split
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || ybytes1 >= (1l << 31) || ybytes2 >= (1l << 31)) return -1;
   const FastDiv fhw = make_fastdiv((uint32_t)(H * W)), fw = make_fastdiv((uint32_t)W);
   a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;

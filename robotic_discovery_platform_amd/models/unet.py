@@ -396,7 +396,8 @@ class UNetExecutor:
     # ------------------------------------------------------------------ backward buffers
     def _alloc_backward(self, C):
         dev, bf = self.dev, torch.bfloat16
-        self.overlap_wgrad = dev.type == "cuda"
+        # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
+        self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
         self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
         # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS)
         # (measured at bs32 with the side-stream overlap: 1024 -> 2025, 2048 -> 2086, 4096 -> 2068 img/s)
