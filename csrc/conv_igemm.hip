@@ -465,6 +465,8 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   const int max_blocks = 256 * per_cu;
   // bm_pref 2 / 3: 8-wave blocks (64 x 32 per wave; twice the waves per SIMD to hide the per-step
   // barrier + DMA latency, 1.5x the LDS fragment reads per MFMA) for the 128x128 / 256x64 tiles
+  // (measured dead end: 256 x 256 / 256 x 128 tiles in this 2-phase structure, one 8-wave block
+  // per CU -- 49 spilled VGPRs at 256 x 256; +6 % on 32^2 x 512 -> 512 only, -5..-40 % elsewhere)
   if (bm_pref == 2 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s);
   if (bm_pref == 3) return launch_cfg<256, 64, 8>(a, max_blocks, wse, s);
   if (bm_pref == 128 && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s);
