@@ -133,7 +133,12 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
             out["e2e_p50_ms"] = round(_pct(rtt, 50), 3)
             out["e2e_p99_ms"] = round(_pct(rtt, 99), 3)
     finally:
-        server.stop(0)
+        # wait for the gRPC core to finish shutting down before its objects are collected: a
+        # server torn down at interpreter exit aborts the process ("terminate called without an
+        # active exception") after the results were printed
+        server.stop(0).wait()
+        svc.close()
+        del server
     return out
 
 

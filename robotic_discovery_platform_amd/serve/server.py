@@ -142,6 +142,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             t, fc, fd, _ = item
             yield t, fc.result(), fd.result()
 
+    def close(self) -> None:
+        """Stop the codec pool (its threads must not outlive the gRPC server at interpreter exit)."""
+        self._pool.shutdown(wait=True)
+
     def analyze_frame(self, color: np.ndarray, depth: np.ndarray, t0: Optional[float] = None):
         t0 = time.perf_counter() if t0 is None else t0
         if depth.dtype != np.uint16:

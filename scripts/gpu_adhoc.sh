@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export RDP_NO_BUILD=1
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_race_screens_gpu.py > gpurun_out/t_k.log 2>&1 || { tail -30 gpurun_out/t_k.log; exit 1; }
-tail -2 gpurun_out/t_k.log
-timeout -k 10 300 python scripts/conv_microbench.py --variants 0,1 --rounds 3 > gpurun_out/micro_f.log 2>&1 || { tail -20 gpurun_out/micro_f.log; exit 1; }
-cat gpurun_out/micro_f.log
+timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
+cat gpurun_out/bench_default.json
+timeout -k 10 300 python bench.py --impl eager --batch 64 --steps 10 --warmup 3 > gpurun_out/eager_b64.json 2> gpurun_out/eager_b64.err || { tail -20 gpurun_out/eager_b64.err; exit 1; }
+cat gpurun_out/eager_b64.json
