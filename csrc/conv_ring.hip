@@ -1,0 +1,263 @@
+// Row-ring 3x3 convolution (stride 1, pad 1) for the 64 -> 64 channel layers at full resolution:
+// the forward of inc.double_conv.3 / up4.conv.double_conv.3 and the dgrad of the same layers
+// (/root/reference/pkg/segmentation_model.py:34 DoubleConv conv2 at 256^2; autograd's
+// conv backward for it, scripts/train_segmenter.py:162).
+//
+// Why a separate kernel: at 64 output channels the implicit-GEMM kernel (conv_igemm.hip) re-stages
+// its 256-pixel A tile for every one of the 9 taps -- ~3 MFMAs per 1-KiB LDS-DMA piece -- and runs
+// at the L2 -> LDS gather rate (~540-580 TF/s), not the MFMA rate. Here:
+//   * the whole weight tensor (64 x 576 bf16 = 72 KiB) lives in VGPRs: every wave keeps the A
+//     fragments of its 32 output channels for all 18 K-steps (144 VGPRs), loaded once per block;
+//   * a block walks one 64-pixel column (image n, 64-pixel segment of the row) top to bottom, two
+//     output rows per step; an output row needs input rows h-1, h, h+1, so a step stages only the
+//     TWO new input rows (66 pixels x 128 B each, zero halo by out-of-range offsets) into an
+//     8-slot LDS ring -- ~32 MFMAs per DMA piece, 10x fewer than the implicit GEMM;
+//   * the 9 taps read the staged rows at shifted offsets (B fragments, ds_read_b128 of 16 rows),
+//     two steps of DMA stay in flight across the per-step barrier (counted vmcnt, asm LDS-DMA).
+// At a column's first / last row the dr = -1 / +1 taps are skipped (that ring slot holds another
+// column's row: the zero padding row of this one). Epilogue: bf16 store (permlane16-widened, 16 B
+// per lane), optional training BN statistics (per-block partial rows) or eval BN fold + ReLU.
+#include "common.h"
+#include <algorithm>
+
+struct RingArgs {
+  const u16* x;
+  uint32_t xbytes;
+  int pitch;
+  const u16* w;  // [64][ldw], k = tap * 64 + cin
+  uint32_t wbytes;
+  int ldw;
+  u16* y;
+  uint32_t ybytes;
+  int ypitch;
+  float* stats;  // [gridDim.x * 4][2][64] partial (sum, sumsq) or nullptr
+  const float* escale;
+  const float* eshift;
+  int erelu;
+  int H, W, WS;  // WS = W / 64 segments per image row
+  int nrows;     // N * WS * H: input rows in column order (R = column * H + h)
+  int npairs;    // nrows / 2: steps (two output rows each)
+  int pairs_per_block;
+  uint32_t fh_m, fh_s, fs_m, fs_s;  // fast division by H and by WS
+};
+
+RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
+
+__global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
+  constexpr int XREG = 72 * 128;  // one ring slot: pixels w0-1 .. w0+70 of one input row (66 used)
+  constexpr int NX = 8;           // ring slots: 4 rows in use + 2 steps x 2 rows in flight
+  constexpr int PIECES = 18;      // 1-KiB DMA pieces per step (2 rows x 9)
+  constexpr int MINPW = PIECES / 8;
+  __shared__ __attribute__((aligned(16))) char ring[NX * XREG];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave >> 2;  // output channels 32 cg .. 32 cg + 31
+  const int pg = wave & 3;   // pixel group: output row (pg >> 1) of the pair, pixels 32 (pg & 1) ..
+  const int orow = pg >> 1, px0 = 32 * (pg & 1);
+
+  const int P0 = blockIdx.x * a.pairs_per_block;
+  const int nks = min(a.npairs, P0 + a.pairs_per_block) - P0;
+  if (nks <= 0) return;
+
+  const auto rx = make_rsrc(a.x, a.xbytes);
+  const auto rw = make_rsrc(a.w, a.wbytes);
+  const auto ry = make_rsrc(a.y, a.ybytes);
+
+  // ---- weights -> registers: wa[ks][j] = W[32 cg + 16 j + (lane & 15)][32 ks + 8 (lane >> 4) .. +7]
+  bf16x8 wa[18][2];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 32 * cg + 16 * j + (lane & 15);
+      const uint32_t off = (uint32_t)(n * a.ldw + 32 * ks + 8 * (lane >> 4)) * 2u;
+      const uint4 v = bload16(rw, off);
+      wa[ks][j] = __builtin_bit_cast(bf16x8, v);
+    }
+  // the ring DMAs below are invisible to hipcc's vmcnt bookkeeping: land the weights first
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- ring DMA: input row R (column order) into slot R % NX ----
+  const int gch = (lane & 7) ^ (lane >> 3);  // global 16-B chunk (LDS row & 7 == lane >> 3)
+  auto row_base = [&](int R, int& m0, int& w0) {  // first pixel of the row segment; -1: no such row
+    if (R < 0 || R >= a.nrows) { m0 = -1; w0 = 0; return; }
+    const uint32_t col = rdiv((uint32_t)R, a.fh_m, a.fh_s);
+    const int h = R - (int)col * a.H;
+    const uint32_t n = rdiv(col, a.fs_m, a.fs_s);
+    const int ws = (int)col - (int)n * a.WS;
+    w0 = ws * 64;
+    m0 = ((int)n * a.H + h) * a.W + w0;
+  };
+  // pieces p = 0..17 of stage P (rows 2P + 1 and 2P + 2), wave w issues p = w, w + 8, w + 16
+  auto issue = [&](int P) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int p = wave + 8 * t;
+      if (p >= PIECES) continue;  // wave-uniform
+      const int rr = p >= 9 ? 1 : 0, pj = p - 9 * rr;
+      const int R = 2 * P + 1 + rr;
+      int m0, w0;
+      row_base(R, m0, w0);
+      const int j = pj * 8 + (lane >> 3);
+      const bool ok = (m0 >= 0) & (j < 66) & inb(w0 - 1 + j, a.W);
+      const uint32_t off = ok ? (uint32_t)((m0 + j - 1) * a.pitch + gch * 8) * 2u : RDP_OOB;
+      dma16_async(rx, (lds_void*)(ring + ((R + NX) % NX) * XREG + pj * 1024), off);
+    }
+  };
+  auto issue_row = [&](int R) {  // prologue rows: 9 pieces of one row (wave 0 also takes piece 8)
+    int m0, w0;
+    row_base(R, m0, w0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int pj = wave + 8 * t;
+      if (pj >= 9) continue;  // wave-uniform
+      const int j = pj * 8 + (lane >> 3);
+      const bool ok = (m0 >= 0) & (j < 66) & inb(w0 - 1 + j, a.W);
+      const uint32_t off = ok ? (uint32_t)((m0 + j - 1) * a.pitch + gch * 8) * 2u : RDP_OOB;
+      dma16_async(rx, (lds_void*)(ring + ((R + NX) % NX) * XREG + pj * 1024), off);
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float s1[2][4], s2[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+  // eval BN fold coefficients of this lane's 4 + 4 output channels
+  float esc[2][4], esh[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 32 * cg + 16 * j + 4 * (lane >> 4) + r;
+      esc[j][r] = a.escale ? a.escale[c] : 1.f;
+      esh[j][r] = a.escale ? a.eshift[c] : 0.f;
+    }
+
+  // prologue: rows 2 P0 - 1 (wave 0..8, one row) and 2 P0, then stages P0 and P0 + 1
+  issue_row(2 * P0 - 1);
+  issue_row(2 * P0);
+  issue(P0);
+  if (nks > 1) issue(P0 + 1);
+
+  // fragment read geometry: B rows = pixels px0 + 16 i + (lane & 15) (+ ds + 1), chunk (lane >> 4)
+  // (+ 4 for the second K-half of a tap), XOR-swizzled by the LDS row
+  const int gq = lane >> 4;
+  const int coff = 16 * (gq & 1) + 8 * (gq >> 1);  // this lane's 8 channels after the pair swap
+
+  for (int ks = 0; ks < nks; ++ks) {
+    const int P = P0 + ks;
+    if (ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (ks + 2 < nks) issue(P + 2);
+
+    const int R0 = 2 * P + orow;  // this wave's output row (column order)
+    const int h = R0 - (int)rdiv((uint32_t)R0, a.fh_m, a.fh_s) * a.H;
+    const bool top = h == 0, bottom = h == a.H - 1;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+      if ((dr < 0 && top) || (dr > 0 && bottom)) continue;  // wave-uniform
+      const char* xb = ring + ((R0 + dr + NX) % NX) * XREG;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        bf16x8 fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = px0 + 16 * i + (lane & 15) + ds + 1;
+          fb[i] = *(const bf16x8*)(xb + row * 128 + 16 * ((gq + 4 * kh) ^ (row & 7)));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fb[i], acc[j][i], 0, 0, 0);
+      }
+    }
+
+    // ---- epilogue of the step: acc[j][i][r] = out[pixel px0 + 16 i + (lane & 15)][cout 32 cg + 16 j + 4 gq + r]
+    int m0, w0;
+    row_base(R0, m0, w0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint2 v[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 o = acc[j][i];
+        acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (a.escale) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            o[r] = fmaf(o[r], esc[j][r], esh[j][r]);
+            if (a.erelu) o[r] = fmaxf(o[r], 0.f);
+          }
+        }
+        v[j].x = pack2bf(o[0], o[1]);
+        v[j].y = pack2bf(o[2], o[3]);
+        if (a.stats) {
+          const float q0 = __uint_as_float(v[j].x << 16), q1 = __uint_as_float(v[j].x & 0xffff0000u);
+          const float q2 = __uint_as_float(v[j].y << 16), q3 = __uint_as_float(v[j].y & 0xffff0000u);
+          s1[j][0] += q0; s2[j][0] += q0 * q0;
+          s1[j][1] += q1; s2[j][1] += q1 * q1;
+          s1[j][2] += q2; s2[j][2] += q2 * q2;
+          s1[j][3] += q3; s2[j][3] += q3 * q3;
+        }
+      }
+      const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
+      const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
+      const int m = m0 + px0 + 16 * i + (lane & 15);
+      const uint32_t off = (uint32_t)(m * a.ypitch + 32 * cg + coff) * 2u;
+      bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
+    }
+  }
+
+  if (a.stats) {  // one partial row per (block, pixel group); waves cg = 0 / 1 fill its two halves
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] = row16_sum(s1[j][r]);
+        s2[j][r] = row16_sum(s2[j][r]);
+      }
+    if ((lane & 15) == 0) {
+      float* row = a.stats + (size_t)(blockIdx.x * 4 + pg) * 2 * 64;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = 32 * cg + 16 * j + 4 * gq;
+        *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+        *(float4*)(row + 64 + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+      }
+    }
+  }
+}
+
+// Applicability of the ring kernel (3x3, one 64-channel source, 64 outputs, no output split,
+// W % 64 == 0, even H); returns the stats rows it writes, or -1 when not applicable.
+extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                             void* y, long ybytes, int Cout, int ypitch, float* stats, int N, int H, int W,
+                             const float* escale, const float* eshift, int erelu, int max_blocks, hipStream_t s) {
+  if (C != 64 || Cout != 64 || W % 64 || H % 2 || ldw < 576) return -1;
+  if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+  RingArgs a;
+  a.x = (const u16*)x; a.xbytes = (uint32_t)xbytes; a.pitch = pitch;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+  a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  a.H = H; a.W = W; a.WS = W / 64;
+  a.nrows = N * a.WS * H;
+  a.npairs = a.nrows / 2;
+  const int blocks = std::max(1, std::min(max_blocks > 0 ? max_blocks : 256, a.npairs));
+  a.pairs_per_block = (a.npairs + blocks - 1) / blocks;
+  const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
+  const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
+  a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
+  hipLaunchKernelGGL(conv_ring64_kernel, dim3(grid), dim3(512), 0, s, a);
+  return grid * 4;
+}

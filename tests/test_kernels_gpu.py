@@ -427,3 +427,44 @@ def test_conv_fwd_8wave_variant(C, N, H, W, C1, C2, Cout):
         outs.append((y, st[: r * 2 * Cout].view(r, 2, Cout).sum(0)))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 6, 64), (1, 4, 128), (3, 2, 192), (1, 10, 64)])
+def test_conv_ring_fwd_stats_eval_dgrad(C, N, H, W):
+    """Row-ring kernel (64 -> 64, W % 64 == 0): forward + BN stats, eval BN fold + ReLU, and the
+    dgrad use (conv of dy with the flipped transposed weight) against torch fp32; forced (pref 6)
+    and via the auto dispatch, which must pick it and agree bitwise."""
+    torch.manual_seed(11)
+    dev = "cuda"
+    x = bf(torch.randn(N, H, W, 64, device=dev))
+    w = bf(torch.randn(64, 64, 3, 3, device=dev) / 24)
+    ref = F.conv2d(nchw(x).float(), w.float(), padding=1)
+    rows = C.conv_stats_rows(N * H * W, 64, 0)
+    outs = []
+    for pref in (6, 0):
+        y = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+        stats = torch.zeros(rows * 2 * 64, device=dev)
+        r = C.conv_fwd(x, None, ohwi(w).contiguous(), 9, 0, y, None, stats, pref, None, 0)
+        assert 0 < r <= rows
+        assert relerr(nchw(y), ref) < 1e-2
+        yq = nchw(y).float()
+        s = stats.view(rows, 2, 64)[:r].sum(0)
+        assert torch.allclose(s[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        assert torch.allclose(s[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])
+    # eval: BN fold + ReLU in the epilogue (affine block [mean | invstd | scale | shift])
+    sc, sh = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
+    aff = torch.cat([torch.zeros(64, device=dev), torch.ones(64, device=dev), sc, sh])
+    ye = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x, None, ohwi(w).contiguous(), 9, 0, ye, None, None, 6, aff, 1)
+    refe = torch.relu(ref * sc[None, :, None, None] + sh[None, :, None, None])
+    assert relerr(nchw(ye), refe) < 1e-2
+    # dgrad: dX = conv(dY, flip(W)^T)
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    xr = nchw(x).float().requires_grad_(True)
+    F.conv2d(xr, w.float(), padding=1).backward(nchw(dy).float())
+    wt = w.flip(2, 3).permute(1, 2, 3, 0).reshape(64, 9 * 64).contiguous()
+    dx = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(dy, None, wt, 9, 0, dx, None, None, 6, None, 0)
+    assert relerr(nchw(dx), xr.grad) < 1e-2
