@@ -14,11 +14,12 @@
 //     8-slot LDS ring -- ~32 MFMAs per DMA piece, 10x fewer than the implicit GEMM;
 //   * the 9 taps read the staged rows at shifted offsets (B fragments, ds_read_b128 of 16 rows),
 //     two steps of DMA stay in flight across the per-step barrier (counted vmcnt, asm LDS-DMA).
-// At a column's first / last row the dr = -1 / +1 taps are skipped (that ring slot holds another
-// column's row: the zero padding row of this one). Epilogue: bf16 store (permlane16-widened, 16 B
+// At a column's first / last row the dr = -1 / +1 taps read an all-zero slot instead (the ring slot
+// holds another column's row there: the zero padding row of this one). Epilogue: bf16 store (permlane16-widened, 16 B
 // per lane), optional training BN statistics (per-block partial rows) or eval BN fold + ReLU.
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 struct RingArgs {
   const u16* x;
@@ -43,12 +44,15 @@ struct RingArgs {
 
 RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
+// ABL (ablation builds for the microbenchmark, RDP_RING_ABL): 1 = no ring DMA after the prologue,
+// 2 = no MFMA, 4 = no epilogue stores
+template <int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
   constexpr int XREG = 72 * 128;  // one ring slot: pixels w0-1 .. w0+70 of one input row (66 used)
   constexpr int NX = 8;           // ring slots: 4 rows in use + 2 steps x 2 rows in flight
   constexpr int PIECES = 18;      // 1-KiB DMA pieces per step (2 rows x 9)
   constexpr int MINPW = PIECES / 8;
-  __shared__ __attribute__((aligned(16))) char ring[NX * XREG];
+  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG];  // + one all-zero slot
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -75,8 +79,14 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
       const uint4 v = bload16(rw, off);
       wa[ks][j] = __builtin_bit_cast(bf16x8, v);
     }
-  // the ring DMAs below are invisible to hipcc's vmcnt bookkeeping: land the weights first
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // Consume every weight register here, so hipcc waits for these loads before the ring DMAs are
+  // issued. Otherwise its waits for them stay inside the step loop (the loop-header state merges
+  // "loads pending" from the preheader) and their trailing vmcnt(0..2) drain the ring DMAs that
+  // must stay in flight across the step barrier.
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(wa[ks][j]));
 
   // ---- ring DMA: input row R (column order) into slot R % NX ----
   const int gch = (lane & 7) ^ (lane >> 3);  // global 16-B chunk (LDS row & 7 == lane >> 3)
@@ -138,7 +148,12 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
       const int c = 32 * cg + 16 * j + 4 * (lane >> 4) + r;
       esc[j][r] = a.escale ? a.escale[c] : 1.f;
       esh[j][r] = a.escale ? a.eshift[c] : 0.f;
+      asm volatile("" ::"v"(esc[j][r]), "v"(esh[j][r]));  // loaded before the DMAs (see above)
     }
+
+  // slot NX stays zero: the padding row read by a column's first / last output row, so the tap loop
+  // has no branches and the compiler can overlap one tap's fragment reads with the previous MFMAs
+  for (int o = threadIdx.x * 16; o < XREG; o += 512 * 16) *(uint4*)(ring + NX * XREG + o) = make_uint4(0, 0, 0, 0);
 
   // prologue: rows 2 P0 - 1 (wave 0..8, one row) and 2 P0, then stages P0 and P0 + 1
   issue_row(2 * P0 - 1);
@@ -153,32 +168,61 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
 
   for (int ks = 0; ks < nks; ++ks) {
     const int P = P0 + ks;
-    if (ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // Stage P must have landed. vmcnt also counts the 2 output stores every wave issues at the end
+    // of a step, in issue order: younger than stage P are the stores of steps ks-2 and ks-1 and
+    // (unless this is the last step) stage P+1 -- leave exactly those in flight.
+    if (ks + 1 < nks) {
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 4) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
+    } else {
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     raw_barrier();
-    if (ks + 2 < nks) issue(P + 2);
+    if (!(ABL & 1) && ks + 2 < nks) issue(P + 2);
 
     const int R0 = 2 * P + orow;  // this wave's output row (column order)
     const int h = R0 - (int)rdiv((uint32_t)R0, a.fh_m, a.fh_s) * a.H;
     const bool top = h == 0, bottom = h == a.H - 1;
+    // software-pipelined over the 9 taps: the 4 B fragments of tap t + 1 are read while tap t's 8
+    // MFMAs run (with only 2 waves per SIMD, a read -> wait -> MFMA chain per tap leaves the
+    // matrix pipe idle for the LDS latency)
+    auto tap_base = [&](int tap) {
+      const int dr = tap / 3 - 1;
+      const bool pad = (dr < 0 && top) || (dr > 0 && bottom);  // wave-uniform
+      return ring + (pad ? NX : (R0 + dr + NX) % NX) * XREG;
+    };
+    auto read_tap = [&](int tap, bf16x8 (&fb)[2][2]) {
+      const char* xb = tap_base(tap);
+      const int ds = tap % 3 - 1;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int dr = tap / 3 - 1, ds = tap % 3 - 1;
-      if ((dr < 0 && top) || (dr > 0 && bottom)) continue;  // wave-uniform
-      const char* xb = ring + ((R0 + dr + NX) % NX) * XREG;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        bf16x8 fb[2];
+      for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int row = px0 + 16 * i + (lane & 15) + ds + 1;
-          fb[i] = *(const bf16x8*)(xb + row * 128 + 16 * ((gq + 4 * kh) ^ (row & 7)));
+          fb[kh][i] = *(const bf16x8*)(xb + row * 128 + 16 * ((gq + 4 * kh) ^ (row & 7)));
         }
+    };
+    bf16x8 fcur[2][2], fnxt[2][2];
+    read_tap(0, fcur);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) read_tap(tap + 1, fnxt);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int i = 0; i < 2; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fb[i], acc[j][i], 0, 0, 0);
+            if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(wa[2 * tap + kh][j]), "v"(fcur[kh][i]));
+            else acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fcur[kh][i], acc[j][i], 0, 0, 0);
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) fcur[kh][i] = fnxt[kh][i];
       }
     }
 
@@ -214,7 +258,8 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
       const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
       const int m = m0 + px0 + 16 * i + (lane & 15);
       const uint32_t off = (uint32_t)(m * a.ypitch + 32 * cg + coff) * 2u;
-      bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
+      if constexpr ((ABL & 4) != 0) asm volatile("" ::"v"(rxs[0]), "v"(rys[0]), "v"(rxs[1]), "v"(rys[1]), "v"(off));
+      else bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
     }
   }
 
@@ -258,6 +303,16 @@ extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const
   const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
   const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
   a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
-  hipLaunchKernelGGL(conv_ring64_kernel, dim3(grid), dim3(512), 0, s, a);
+  static const int abl = [] {
+    const char* e = getenv("RDP_RING_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  switch (abl) {
+    case 1: hipLaunchKernelGGL(conv_ring64_kernel<1>, dim3(grid), dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(conv_ring64_kernel<2>, dim3(grid), dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(conv_ring64_kernel<4>, dim3(grid), dim3(512), 0, s, a); break;
+    case 6: hipLaunchKernelGGL(conv_ring64_kernel<6>, dim3(grid), dim3(512), 0, s, a); break;
+    default: hipLaunchKernelGGL(conv_ring64_kernel<0>, dim3(grid), dim3(512), 0, s, a);
+  }
   return grid * 4;
 }
