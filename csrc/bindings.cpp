@@ -23,6 +23,7 @@ int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStre
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
                    float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
+void rdp_conv_set_debug_flags(int);
 int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
                     float*, float*, hipStream_t);
 int rdp_bn_eval_coef(int, const float*, const float*, const float*, const float*, float, float*, hipStream_t);
@@ -453,6 +454,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return rdp_conv_ws_elems(N, H, W, C1, C2, Cout, taps, packed, bm_pref);
   });
   m.def("conv_stats_rows", &conv_stats_rows);
+  m.def("conv_set_debug_flags", [](int f) { rdp_conv_set_debug_flags(f); }, "A/B flags for microbenchmarks");
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
   m.def("bn_finalize", &bn_finalize);

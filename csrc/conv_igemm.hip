@@ -53,7 +53,12 @@ struct ConvArgs {
   float* kslab;  // [ksplit][M][Cout] fp32
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
+  int store_aware;  // 1: the per-step vmcnt leaves the previous epilogue's stores in flight
 };
+
+// debug / A-B flags for the microbenchmark (rdp_conv_set_debug_flags): bit 0 = plain vmcnt(0)
+static int g_conv_debug_flags = 0;
+extern "C" void rdp_conv_set_debug_flags(int f) { g_conv_debug_flags = f; }
 
 // tap (0..8) -> (dr, ds) without division: dr + 1 = (tap * 11) >> 5
 RDP_DEV int tap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
@@ -177,8 +182,15 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
   }
   int ks = 0, t = 0;    // compute position (K step within tile, tile index)
   int iks = 0, it = 0;  // issue position of the stage in flight
+  // vector-memory stores the previous step's epilogue issued after stage g's DMA: vmcnt counts
+  // them in issue order, so stage g has landed once at most that many ops are outstanding (a plain
+  // vmcnt(0) would also wait for the output stores of every tile before its next K step)
+  int pend = 0;
   for (int g = 0; g < total; ++g) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (pend == 0 || !a.store_aware) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if (pend == 2 * NJ) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NJ) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * NJ) : "memory");
+    pend = 0;
     raw_barrier();
     if (g + 1 < total) {
       if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
@@ -222,6 +234,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
                                        __float_as_uint(o[3])));
         }
       }
+      pend = 4 * NJ;  // NJ x 4 slab stores
       continue;
     }
     const int tile = item;
@@ -299,6 +312,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
         }
       }
     }
+    pend = a.stats ? 4 * NJ : 2 * NJ;  // 2 NJ output stores (+ 2 NJ stats-row stores)
   }
 }
 
@@ -456,6 +470,7 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   a.Cy1 = Cy1; a.ypitch1 = ypitch1; a.ypitch2 = ypitch2; a.stats = stats;
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.M = N * H * W;
   a.taps = taps; a.packed = packed;
+  a.store_aware = (g_conv_debug_flags & 1) ? 0 : 1;
   if (packed) {
     if (C1 != 8 || C2 != 0 || taps != 9 || ldw != 128) return -1;
     a.nks = 2; a.cpt = 1;

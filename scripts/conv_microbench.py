@@ -54,6 +54,9 @@ def main():
             out = torch.zeros(Co * 9 * Cin, device=dev)
 
         def run(v):
+            # variant v >= 10000: same kernel with debug flags (v // 10000) (A/B in one process)
+            C.conv_set_debug_flags(v // 10000)
+            v = v % 10000
             if a.wgrad:
                 C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
             else:
