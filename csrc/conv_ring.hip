@@ -1,5 +1,7 @@
-// Row-ring 3x3 convolution (stride 1, pad 1) for the 64 -> 64 channel layers at full resolution:
-// the forward of inc.double_conv.3 / up4.conv.double_conv.3 and the dgrad of the same layers
+// Row-ring 3x3 convolution (stride 1, pad 1) for the 64-input-channel layers at W % 64 == 0: the
+// forward of inc.double_conv.3 / up4.conv.double_conv.3 (64 -> 64) and down1...double_conv.0
+// (64 -> 128), and the dgrad of inc.3 / up4.3 (64 -> 64) and of up4.conv.double_conv.0 (64 -> 64 + 64
+// into the skip / upsample halves of the concat)
 // (/root/reference/pkg/segmentation_model.py:34 DoubleConv conv2 at 256^2; autograd's
 // conv backward for it, scripts/train_segmenter.py:162).
 //
@@ -31,7 +33,10 @@ struct RingArgs {
   u16* y;
   uint32_t ybytes;
   int ypitch;
-  float* stats;  // [gridDim.x * 4][2][64] partial (sum, sumsq) or nullptr
+  u16* y2;  // output channels >= Cy1 go here (dgrad of a concatenated input), or nullptr
+  uint32_t ybytes2;
+  int ypitch2, Cy1;
+  float* stats;  // [gridDim.x * NPG][2][COUT] partial (sum, sumsq) or nullptr
   const float* escale;
   const float* eshift;
   int erelu;
@@ -46,19 +51,23 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 
 // ABL (ablation builds for the microbenchmark, RDP_RING_ABL): 1 = no ring DMA after the prologue,
 // 2 = no MFMA, 4 = no epilogue stores
-template <int ABL = 0>
-__global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
+// COUT = 64: 8 waves = 2 channel groups x 4 pixel groups (32 px); COUT = 128: 4 x 2 (64 px).
+template <int COUT, int ABL = 0>
+__global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
+  constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
+  constexpr int PXW = 128 / NPG, NI = PXW / 16;  // pixels per wave (one output row half or whole)
   constexpr int XREG = 72 * 128;  // one ring slot: pixels w0-1 .. w0+70 of one input row (66 used)
   constexpr int NX = 8;           // ring slots: 4 rows in use + 2 steps x 2 rows in flight
   constexpr int PIECES = 18;      // 1-KiB DMA pieces per step (2 rows x 9)
   constexpr int MINPW = PIECES / 8;
-  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG];  // + one all-zero slot
+  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 2 * COUT * 4];  // + zero slot, BN fold
+  float* const efold = (float*)(ring + (NX + 1) * XREG);  // eval BN fold [scale | shift] (LDS, not VGPRs)
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int cg = wave >> 2;  // output channels 32 cg .. 32 cg + 31
-  const int pg = wave & 3;   // pixel group: output row (pg >> 1) of the pair, pixels 32 (pg & 1) ..
-  const int orow = pg >> 1, px0 = 32 * (pg & 1);
+  const int cg = wave / NPG;  // output channels 32 cg .. 32 cg + 31
+  const int pg = wave % NPG;  // pixel group: output row of the pair and first pixel
+  const int orow = pg / (NPG / 2), px0 = PXW * (pg % (NPG / 2));
 
   const int P0 = blockIdx.x * a.pairs_per_block;
   const int nks = min(a.npairs, P0 + a.pairs_per_block) - P0;
@@ -66,7 +75,11 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
 
   const auto rx = make_rsrc(a.x, a.xbytes);
   const auto rw = make_rsrc(a.w, a.wbytes);
-  const auto ry = make_rsrc(a.y, a.ybytes);
+  // this wave's 32 output channels all go to one destination (Cy1 % 32 == 0)
+  const bool d2 = 32 * cg >= a.Cy1;
+  const auto ry = d2 ? make_rsrc(a.y2, a.ybytes2) : make_rsrc(a.y, a.ybytes);
+  const int ypitch = d2 ? a.ypitch2 : a.ypitch;
+  const int cbase = d2 ? 32 * cg - a.Cy1 : 32 * cg;
 
   // ---- weights -> registers: wa[ks][j] = W[32 cg + 16 j + (lane & 15)][32 ks + 8 (lane >> 4) .. +7]
   bf16x8 wa[18][2];
@@ -129,27 +142,19 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
     }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[2][NI];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float s1[2][4], s2[2][4];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
-  // eval BN fold coefficients of this lane's 4 + 4 output channels
-  float esc[2][4], esh[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = 32 * cg + 16 * j + 4 * (lane >> 4) + r;
-      esc[j][r] = a.escale ? a.escale[c] : 1.f;
-      esh[j][r] = a.escale ? a.eshift[c] : 0.f;
-      asm volatile("" ::"v"(esc[j][r]), "v"(esh[j][r]));  // loaded before the DMAs (see above)
-    }
+  if (a.escale) {
+    for (int c = threadIdx.x; c < COUT; c += 512) { efold[c] = a.escale[c]; efold[COUT + c] = a.eshift[c]; }
+  }
 
   // slot NX stays zero: the padding row read by a column's first / last output row, so the tap loop
   // has no branches and the compiler can overlap one tap's fragment reads with the previous MFMAs
@@ -168,16 +173,16 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
 
   for (int ks = 0; ks < nks; ++ks) {
     const int P = P0 + ks;
-    // Stage P must have landed. vmcnt also counts the 2 output stores every wave issues at the end
+    // Stage P must have landed. vmcnt also counts the NI output stores every wave issues at the end
     // of a step, in issue order: younger than stage P are the stores of steps ks-2 and ks-1 and
     // (unless this is the last step) stage P+1 -- leave exactly those in flight.
     if (ks + 1 < nks) {
-      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 4) : "memory");
-      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2) : "memory");
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2 * NI) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + NI) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
     } else {
-      if (ks >= 2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-      else if (ks == 1) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NI) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     raw_barrier();
@@ -194,35 +199,58 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
       const bool pad = (dr < 0 && top) || (dr > 0 && bottom);  // wave-uniform
       return ring + (pad ? NX : (R0 + dr + NX) % NX) * XREG;
     };
-    auto read_tap = [&](int tap, bf16x8 (&fb)[2][2]) {
+    auto read_tap = [&](int tap, bf16x8 (&fb)[2][NI]) {
       const char* xb = tap_base(tap);
       const int ds = tap % 3 - 1;
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NI; ++i) {
           const int row = px0 + 16 * i + (lane & 15) + ds + 1;
           fb[kh][i] = *(const bf16x8*)(xb + row * 128 + 16 * ((gq + 4 * kh) ^ (row & 7)));
         }
     };
-    bf16x8 fcur[2][2], fnxt[2][2];
-    read_tap(0, fcur);
+    // (NI = 4 has twice the MFMAs per fragment read and no registers for a second set: no pipelining)
+    constexpr bool PIPE = NI <= 2;
+    if constexpr (!PIPE) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      if (tap + 1 < 9) read_tap(tap + 1, fnxt);
+      for (int tap = 0; tap < 9; ++tap) {
+        const char* xb = tap_base(tap);
+        const int ds = tap % 3 - 1;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          bf16x8 fb[NI];
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            const int row = px0 + 16 * i + (lane & 15) + ds + 1;
+            fb[i] = *(const bf16x8*)(xb + row * 128 + 16 * ((gq + 4 * kh) ^ (row & 7)));
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fb[i], acc[j][i], 0, 0, 0);
+        }
+      }
+    }
+    bf16x8 fcur[2][NI], fnxt[2][NI];
+    if (PIPE) read_tap(0, fcur);
+#pragma unroll
+    for (int tap = 0; tap < 9 && PIPE; ++tap) {
+      if (PIPE && tap + 1 < 9) read_tap(tap + 1, fnxt);
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < NI; ++i)
             if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(wa[2 * tap + kh][j]), "v"(fcur[kh][i]));
             else acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fcur[kh][i], acc[j][i], 0, 0, 0);
-      if (tap + 1 < 9) {
+      if (PIPE && tap + 1 < 9) {
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-          for (int i = 0; i < 2; ++i) fcur[kh][i] = fnxt[kh][i];
+          for (int i = 0; i < NI; ++i) fcur[kh][i] = fnxt[kh][i];
       }
     }
 
@@ -230,17 +258,20 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
     int m0, w0;
     row_base(R0, m0, w0);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       uint2 v[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x4 o = acc[j][i];
         acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (a.escale) {
+          const int c = 32 * cg + 16 * j + 4 * gq;
+          const float4 sc = *(const float4*)(efold + c), sh = *(const float4*)(efold + COUT + c);
+          o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+          o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+          if (a.erelu) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            o[r] = fmaf(o[r], esc[j][r], esh[j][r]);
-            if (a.erelu) o[r] = fmaxf(o[r], 0.f);
+            for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
           }
         }
         v[j].x = pack2bf(o[0], o[1]);
@@ -257,7 +288,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
       const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
       const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
       const int m = m0 + px0 + 16 * i + (lane & 15);
-      const uint32_t off = (uint32_t)(m * a.ypitch + 32 * cg + coff) * 2u;
+      const uint32_t off = (uint32_t)(m * ypitch + cbase + coff) * 2u;
       if constexpr ((ABL & 4) != 0) asm volatile("" ::"v"(rxs[0]), "v"(rys[0]), "v"(rxs[1]), "v"(rys[1]), "v"(off));
       else bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
     }
@@ -272,28 +303,33 @@ __global__ __launch_bounds__(512, 2) void conv_ring64_kernel(const RingArgs a) {
         s2[j][r] = row16_sum(s2[j][r]);
       }
     if ((lane & 15) == 0) {
-      float* row = a.stats + (size_t)(blockIdx.x * 4 + pg) * 2 * 64;
+      float* row = a.stats + (size_t)(blockIdx.x * NPG + pg) * 2 * COUT;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = 32 * cg + 16 * j + 4 * gq;
         *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
-        *(float4*)(row + 64 + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+        *(float4*)(row + COUT + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
       }
     }
   }
 }
 
-// Applicability of the ring kernel (3x3, one 64-channel source, 64 outputs, no output split,
-// W % 64 == 0, even H); returns the stats rows it writes, or -1 when not applicable.
+// Applicability of the ring kernel (3x3, one 64-channel source, 64 or 128 outputs -- split at a
+// multiple of 32 into two destinations --, W % 64 == 0, even H); returns the stats rows it writes,
+// or -1 when not applicable.
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
-                             void* y, long ybytes, int Cout, int ypitch, float* stats, int N, int H, int W,
-                             const float* escale, const float* eshift, int erelu, int max_blocks, hipStream_t s) {
-  if (C != 64 || Cout != 64 || W % 64 || H % 2 || ldw < 576) return -1;
-  if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+                             void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
+                             int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
+                             int erelu, int max_blocks, hipStream_t s) {
+  if (C != 64 || (Cout != 64 && Cout != 128) || W % 64 || H % 2 || ldw < 576 || Cy1 % 32) return -1;
+  if (y2 == nullptr && Cy1 != Cout) return -1;
+  if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || ybytes2 >= (1l << 31) || wbytes >= (1l << 31)) return -1;
   RingArgs a;
   a.x = (const u16*)x; a.xbytes = (uint32_t)xbytes; a.pitch = pitch;
   a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
   a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+  a.y2 = (u16*)(y2 ? y2 : y); a.ybytes2 = y2 ? (uint32_t)ybytes2 : 0u; a.ypitch2 = y2 ? ypitch2 : ypitch;
+  a.Cy1 = Cy1;
   a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
@@ -307,12 +343,15 @@ extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const
     const char* e = getenv("RDP_RING_ABL");
     return e ? atoi(e) : 0;
   }();
+  if (Cout == 128) {
+    hipLaunchKernelGGL((conv_ring_kernel<128>), dim3(grid), dim3(512), 0, s, a);
+    return grid * 2;
+  }
   switch (abl) {
-    case 1: hipLaunchKernelGGL(conv_ring64_kernel<1>, dim3(grid), dim3(512), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(conv_ring64_kernel<2>, dim3(grid), dim3(512), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(conv_ring64_kernel<4>, dim3(grid), dim3(512), 0, s, a); break;
-    case 6: hipLaunchKernelGGL(conv_ring64_kernel<6>, dim3(grid), dim3(512), 0, s, a); break;
-    default: hipLaunchKernelGGL(conv_ring64_kernel<0>, dim3(grid), dim3(512), 0, s, a);
+    case 1: hipLaunchKernelGGL((conv_ring_kernel<64, 1>), dim3(grid), dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((conv_ring_kernel<64, 2>), dim3(grid), dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((conv_ring_kernel<64, 4>), dim3(grid), dim3(512), 0, s, a); break;
+    default: hipLaunchKernelGGL((conv_ring_kernel<64>), dim3(grid), dim3(512), 0, s, a);
   }
   return grid * 4;
 }

@@ -468,3 +468,34 @@ def test_conv_ring_fwd_stats_eval_dgrad(C, N, H, W):
     dx = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
     C.conv_fwd(dy, None, wt, 9, 0, dx, None, None, 6, None, 0)
     assert relerr(nchw(dx), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,split", [(2, 4, 64, False), (1, 6, 128, True), (2, 2, 64, True)])
+def test_conv_ring_cout128(C, N, H, W, split):
+    """Row-ring kernel with 128 outputs (down1 conv0 forward; up4 conv0 dgrad into the two halves of
+    the concat input) + BN stats, against torch fp32; auto dispatch picks it and agrees bitwise."""
+    torch.manual_seed(12)
+    dev = "cuda"
+    x = bf(torch.randn(N, H, W, 64, device=dev))
+    w = bf(torch.randn(128, 64, 3, 3, device=dev) / 24)
+    ref = F.conv2d(nchw(x).float(), w.float(), padding=1)
+    rows = C.conv_stats_rows(N * H * W, 128, 0)
+    outs = []
+    for pref in (6, 0):
+        stats = torch.zeros(rows * 2 * 128, device=dev)
+        if split:
+            y1 = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+            y2 = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+            r = C.conv_fwd(x, None, ohwi(w).contiguous(), 9, 0, y1, y2, stats, pref, None, 0)
+            y = torch.cat([y1, y2], -1)
+        else:
+            y = torch.empty(N, H, W, 128, dtype=torch.bfloat16, device=dev)
+            r = C.conv_fwd(x, None, ohwi(w).contiguous(), 9, 0, y, None, stats, pref, None, 0)
+        assert 0 < r <= rows
+        assert relerr(nchw(y), ref) < 1e-2
+        yq = nchw(y).float()
+        s = stats.view(rows, 2, 128)[:r].sum(0)
+        assert torch.allclose(s[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        assert torch.allclose(s[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])
