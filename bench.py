@@ -176,12 +176,14 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return bool(serve) and rank == 0
 
 
 if __name__ == "__main__":
-    main()
-    # The result line is out; skip interpreter teardown so no third-party destructor (gRPC core
-    # threads of the serving measurement, RCCL/HIP runtime) can turn a finished run into an abort.
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(0)
+    if main():
+        # The result line is out and the serving measurement ran: skip interpreter teardown so the
+        # gRPC core's threads cannot turn a finished run into an abort at exit. (Not taken with
+        # --serve 0 -- profilers such as rocprofv3 write their output in exit handlers.)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
