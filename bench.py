@@ -116,12 +116,31 @@ def make_native_step(args, dev, world):
                             world=world, graph=bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss)
 
 
+class _Progress:
+    """Prints the current phase to stderr every 30 s until the timed region is done (rank 0)."""
+
+    def __init__(self, rank: int, period: float = 30.0):
+        import threading
+        self.phase, self.t0 = "setup", time.perf_counter()
+        if rank == 0:
+            self._stop = threading.Event()
+            th = threading.Thread(target=self._run, args=(period,), daemon=True)
+            th.start()
+
+    def _run(self, period):
+        while not self._stop.wait(period):
+            print(f"[bench] {self.phase} ({time.perf_counter() - self.t0:.0f} s)", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     rank, world, dev = setup_dist(args)
     step = make_eager_step(args, dev, world) if args.impl == "eager" else make_native_step(args, dev, world)
-    for _ in range(args.warmup):
+    progress = _Progress(rank)  # stderr heartbeat: first eager steps can spend minutes in MIOpen kernel builds
+    for i in range(args.warmup):
+        progress.phase = f"warmup step {i + 1}/{args.warmup}"
         step()
+    progress.phase = "timed steps"
     barrier(world, dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):

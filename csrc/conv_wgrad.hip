@@ -594,29 +594,75 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradR
   }
 }
 
-// out[cout][tap][cin_real] (+)= sum_split slab[split][cout][tap*cin_pad + cin]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int splits, int Cout,
+// Split-K slab reduction, two levels. A layer's slab is [splits][Cout][ncols_pad] fp32 with up to
+// ~500-2000 splits but often only a few 10^4 elements per split (64 x 576 for a 64 -> 64 layer):
+// one thread per output walking all splits left ~150 blocks, each latency-bound on a long chain of
+// loads (412 us for 75 MB on inc.double_conv.3 at bs64, at the very end of backward). Level 1 sums
+// G contiguous groups of splits into the group's first row in place (~1000 blocks, 16-B loads, 4
+// independent accumulators); level 2 sums the G group rows into the weight-gradient layout.
+
+// slab rows s0(g) = g * splits / G (g < G) become sum_{s in [s0(g), s0(g+1))} slab[s]
+__global__ __launch_bounds__(256) void wgrad_group_sum_kernel(float* __restrict__ slab, long E, int splits, int G) {
+  const long e4 = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index within one split row
+  if (e4 * 4 >= E) return;
+  const int g = blockIdx.y;
+  const int s0 = (int)((long)g * splits / G), s1 = (int)((long)(g + 1) * splits / G);
+  const float4* p = (const float4*)slab + e4;
+  const long st = E >> 2;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  int sp = s0;
+  for (; sp + 4 <= s1; sp += 4) {
+    const float4 v0 = p[(long)sp * st], v1 = p[(long)(sp + 1) * st], v2 = p[(long)(sp + 2) * st],
+                 v3 = p[(long)(sp + 3) * st];
+    a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+    a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+    a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
+    a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+  }
+  for (; sp < s1; ++sp) {
+    const float4 v = p[(long)sp * st];
+    a0.x += v.x; a0.y += v.y; a0.z += v.z; a0.w += v.w;
+  }
+  ((float4*)slab)[(long)s0 * st + e4] = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                                                    (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+}
+
+// out[cout][tap][cin_real] (+)= sum_g slab[s0(g)][cout][tap*cin_pad + cin]   (s0(g) = g * splits / G)
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int splits, int G, int Cout,
                                     int ncols_pad, int taps, int cin_pad, int cin_real, int accumulate) {
   const long total = (long)Cout * taps * cin_real;
+  const long stride = (long)Cout * ncols_pad;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int cin = idx % cin_real;
     const long t2 = idx / cin_real;
     const int tap = t2 % taps;
     const int co = t2 / taps;
     const long col = (long)tap * cin_pad + cin;
-    // 8 independent accumulators: the split loop is latency-bound otherwise (hundreds of splits)
     const float* p = slab + (long)co * ncols_pad + col;
-    const long stride = (long)Cout * ncols_pad;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f;
-    int sp = 0;
-    for (; sp + 8 <= splits; sp += 8) {
-      s0 += p[(sp + 0) * stride]; s1 += p[(sp + 1) * stride]; s2 += p[(sp + 2) * stride]; s3 += p[(sp + 3) * stride];
-      s4 += p[(sp + 4) * stride]; s5 += p[(sp + 5) * stride]; s6 += p[(sp + 6) * stride]; s7 += p[(sp + 7) * stride];
-    }
-    for (; sp < splits; ++sp) s0 += p[sp * stride];
-    const float s = ((s0 + s1) + (s2 + s3)) + ((s4 + s5) + (s6 + s7));
-    out[idx] = accumulate ? out[idx] + s : s;
+    // 8 independent accumulators: the row loop is latency-bound otherwise
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int g = 0;
+    for (; g + 8 <= G; g += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += p[((long)(g + u) * splits / G) * stride];
+    for (; g < G; ++g) s[0] += p[((long)g * splits / G) * stride];
+    const float r = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    out[idx] = accumulate ? out[idx] + r : r;
   }
+}
+
+static void launch_wgrad_reduce(float* slab, float* out, int splits, int Cout, int ncols_pad, int taps, int cin_pad,
+                                int cin_real, int accumulate, hipStream_t s) {
+  const long E = (long)Cout * ncols_pad;  // multiple of 4 (Cout % 64 == 0)
+  const long chunks = (E / 4 + 255) / 256;
+  // ~1000 level-1 blocks, at most 32 group rows for level 2; few splits (deep layers) need no level 1
+  int G = (int)std::min<long>(std::min<long>(splits, 32), std::max<long>(1, (1024 + chunks - 1) / chunks));
+  if (splits <= 8) G = splits;
+  if (G < splits) hipLaunchKernelGGL(wgrad_group_sum_kernel, dim3((unsigned)chunks, G), dim3(256), 0, s, slab, E, splits, G);
+  const long total = (long)Cout * taps * cin_real;
+  const int rb = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rb), dim3(256), 0, s, slab, out, splits, G, Cout, ncols_pad, taps, cin_pad,
+                     cin_real, accumulate);
 }
 
 extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
@@ -709,10 +755,7 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     else if (mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2, true>), dim3(nblk), dim3(256), 0, s, h);
     else hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2, false>), dim3(nblk), dim3(256), 0, s, h);
     }
-    const long total = (long)Cout * 9 * a.Cin;
-    const int rb = (int)std::min<long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rb), dim3(256), 0, s, slab, out, h.splits, Cout, h.ncols, 9, a.Cin,
-                       a.Cin, accumulate);
+    launch_wgrad_reduce(slab, out, h.splits, Cout, h.ncols, 9, a.Cin, a.Cin, accumulate, s);
     return h.splits;
   }
   if (variant == 5) return -1;
@@ -767,11 +810,8 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   } else {  // default: BK=64 pixels per stage, double-buffered, 8 waves (64 couts x 32 columns each)
     hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2, 8>), dim3(nblk), dim3(512), 0, s, a);
   }
-  const int creal = packed ? cin_real : a.Cin;
-  const long total = (long)Cout * taps * creal;
-  const int rb = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rb), dim3(256), 0, s, slab, out, a.splits, Cout, a.ncols_pad, taps,
-                     packed ? 8 : a.Cin, creal, accumulate);
+  launch_wgrad_reduce(slab, out, a.splits, Cout, a.ncols_pad, taps, packed ? 8 : a.Cin, packed ? cin_real : a.Cin,
+                      accumulate, s);
   return a.splits;
 }
 

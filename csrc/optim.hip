@@ -58,21 +58,41 @@ struct WSeg {
   int kind, cout, cin, taps;
 };
 
-__global__ void wprep_kernel(const float* __restrict__ master, u16* __restrict__ out, const WSeg* __restrict__ segs) {
+// kind 0 is a per-tap 2-D transpose ([cout][cin] -> [cin][cout]); it goes through a 64x64 LDS tile
+// so both the fp32 reads (along cin) and the bf16 writes (along cout) are coalesced. (The direct
+// element-wise gather read the masters with a stride of taps*cin floats: ~130 us per step.)
+__global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ master, u16* __restrict__ out,
+                                                    const WSeg* __restrict__ segs) {
   const WSeg sg = segs[blockIdx.y];
+  const int tid = threadIdx.x;
   if (sg.kind == 0) {
-    const long n = (long)sg.cout * sg.taps * sg.cin;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-      // destination-major so the bf16 writes are coalesced: i -> (ci, tp, co)
-      const int co = i % sg.cout;
-      const long r = i / sg.cout;
-      const int tp = r % sg.taps, ci = r / sg.taps;
-      const int tap = sg.taps - 1 - tp;
-      out[sg.dst + i] = f2bf(master[sg.src + ((long)co * sg.taps + tap) * sg.cin + ci]);
+    __shared__ u16 tile[64][66];
+    const int tco = (sg.cout + 63) >> 6, tci = (sg.cin + 63) >> 6;
+    const int ntiles = sg.taps * tco * tci;
+    const int lc = tid & 63, lr = tid >> 6;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      const int tap = t % sg.taps, r = t / sg.taps;
+      const int co0 = (r % tco) << 6, ci0 = (r / tco) << 6;
+      const int ci = ci0 + lc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int co = co0 + lr + 4 * j;
+        float v = 0.f;
+        if (co < sg.cout && ci < sg.cin) v = master[sg.src + ((long)co * sg.taps + tap) * sg.cin + ci];
+        tile[lr + 4 * j][lc] = f2bf(v);
+      }
+      __syncthreads();
+      const int tp = sg.taps - 1 - tap, co = co0 + lc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int ci2 = ci0 + lr + 4 * j;
+        if (co < sg.cout && ci2 < sg.cin) out[sg.dst + ((long)ci2 * sg.taps + tp) * sg.cout + co] = tile[lc][lr + 4 * j];
+      }
+      __syncthreads();
     }
   } else {
     const long n = (long)sg.cout * 128;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    for (long i = blockIdx.x * (long)blockDim.x + tid; i < n; i += (long)gridDim.x * blockDim.x) {
       const int c = i % 8, tap = (i / 8) % 16, co = i / 128;
       float val = 0.f;
       if (tap < sg.taps && c < sg.cin) val = master[sg.src + ((long)co * sg.taps + tap) * sg.cin + c];
@@ -102,7 +122,7 @@ int rdp_cast_bf16(const float* p, void* out, long n, hipStream_t s) {
 // segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps} (32 bytes each)
 int rdp_wprep(const float* master, void* out, const void* segs, int nseg, hipStream_t s) {
   if (nseg <= 0) return 0;
-  hipLaunchKernelGGL(wprep_kernel, dim3(64, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs);
+  hipLaunchKernelGGL(wprep_kernel, dim3(128, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs);
   return 0;
 }
 int rdp_wseg_size() { return (int)sizeof(WSeg); }

@@ -178,7 +178,7 @@ int rdp_parcur(int idim, int m, const double* u_in, const double* x_in, double s
                double* c_out, int* n_out, double* fp_out) {
   if (k < 1 || k > 5 || m <= k || s < 0.0 || idim < 1 || idim > 10 || nest < 2 * (k + 1)) return 10;
   for (int i = 1; i < m; ++i)
-    if (u_in[i] < u_in[i - 1]) return 10;
+    if (u_in[i] <= u_in[i - 1]) return 10;  // FITPACK: u strictly increasing (scipy: "Invalid inputs")
   const double tol = 0.001, con1 = 0.1, con9 = 0.9, con4 = 0.04, half = 0.5;
   const int maxit = 20, k1 = k + 1, k2 = k + 2, nmin = 2 * k1, nmax = m + k1;
   // 1-based working arrays

@@ -170,7 +170,9 @@ def test_conv_dgrad_split_output(C):
     # W % 64 == 0: the halo-reuse kernel (row-segment K steps, 9 taps from one staged row triple)
     (2, 5, 64, 64, 0, 64, 3), (1, 6, 128, 64, 64, 128, 4), (3, 3, 64, 128, 0, 64, 64), (1, 4, 192, 64, 128, 256, 2),
     # W | 64: multi-row segments, row-crossing taps masked on the dY side
-    (2, 6, 32, 64, 0, 64, 3), (1, 8, 16, 128, 128, 128, 2), (3, 8, 8, 64, 0, 128, 5)])
+    (2, 6, 32, 64, 0, 64, 3), (1, 8, 16, 128, 128, 128, 2), (3, 8, 8, 64, 0, 128, 5),
+    # >8 splits with few elements per split: two-level slab reduction (group rows, then layout)
+    (2, 64, 64, 64, 0, 64, 512), (1, 64, 128, 64, 64, 128, 512), (4, 20, 20, 64, 0, 64, 150)])
 def test_conv_wgrad(C, N, H, W, C1, C2, Cout, splits):
     torch.manual_seed(3)
     dev = "cuda"
@@ -187,19 +189,20 @@ def test_conv_wgrad(C, N, H, W, C1, C2, Cout, splits):
     assert relerr(out, ref) < 2e-3
 
 
-def test_conv_wgrad_packed(C):
+@pytest.mark.parametrize("N,H,W,splits", [(2, 18, 14, 5), (2, 64, 64, 300)])
+def test_conv_wgrad_packed(C, N, H, W, splits):
     torch.manual_seed(4)
     dev = "cuda"
-    N, H, W, Cout = 2, 18, 14, 64
+    Cout = 64
     x = bf(torch.rand(N, H, W, 3, device=dev))
     x8 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device=dev)
     x8[..., :3] = x
     dy = bf(torch.randn(N, H, W, Cout, device=dev))
     w = torch.zeros(Cout, 3, 3, 3, device=dev, requires_grad=True)
     F.conv2d(nchw(x).float(), w, padding=1).backward(nchw(dy).float())
-    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 8, Cout, 9, 1, 5), device=dev)
+    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 8, Cout, 9, 1, splits), device=dev)
     out = torch.zeros(Cout * 27, device=dev)
-    C.conv_wgrad(x8, None, dy, 9, 1, 3, slab, out, 0, 5, 0)
+    C.conv_wgrad(x8, None, dy, 9, 1, 3, slab, out, 0, splits, 0)
     assert relerr(out, w.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
 
 
@@ -499,3 +502,29 @@ def test_conv_ring_cout128(C, N, H, W, split):
         assert torch.allclose(s[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
         outs.append(y)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("decoder", ["bilinear", "transposed"])
+def test_wprep_derived_layouts(C, decoder):
+    """wprep (LDS-tiled transpose) rebuilds every derived bf16 weight layout from the fp32 masters."""
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    m = UNetNative(3, 1, bilinear=(decoder == "bilinear"), device=dev)
+    st = m.store
+    st.flat.copy_(torch.randn_like(st.flat))
+    m.refresh_weights()
+    torch.cuda.synchronize()
+    for sp in m.specs:
+        w = st.flat_slice(sp.name + ".weight", st.flat).view(sp.cout, sp.taps, -1)  # OHWI master
+        if sp.packed:
+            ref = torch.zeros(sp.cout, 16, 8, device=dev)
+            ref[:, :sp.taps, :w.shape[2]] = w
+            got = m.fwd_weight(sp).view(sp.cout, 16, 8).float()
+        else:
+            ref = w.flip(1).permute(2, 1, 0).reshape(sp.cin, -1)  # [cin][flipped tap][cout]
+            got = m.dgrad_weight(sp).float()
+        assert torch.equal(got, bf(ref).float()), sp.name
+    for us in m.up_specs:
+        w = st.flat_slice(us.name + ".weight", st.flat).view(us.cin, 4 * us.cout)
+        assert torch.equal(m.upT_fwd_weight(us).float(), bf(w.t()).float()), us.name

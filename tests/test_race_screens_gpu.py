@@ -43,7 +43,8 @@ def test_conv_fwd_stats_deterministic(C, N, H, W, C1, C2, Cout, pref):
 
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,splits", [(4, 32, 32, 64, 0, 64, 7), (2, 17, 23, 128, 128, 128, 3),
-                                                     (8, 16, 16, 512, 0, 512, 16), (2, 7, 128, 64, 64, 128, 9)])
+                                                     (8, 16, 16, 512, 0, 512, 16), (2, 7, 128, 64, 64, 128, 9),
+                                                     (2, 64, 64, 64, 0, 64, 512)])
 def test_conv_wgrad_deterministic(C, N, H, W, C1, C2, Cout, splits):
     torch.manual_seed(1)
     x1, x2 = _bf((N, H, W, C1)), (_bf((N, H, W, C2)) if C2 else None)
