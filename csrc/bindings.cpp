@@ -35,6 +35,9 @@ int rdp_bn_relu_bwd_apply(const void*, int, const void*, int, const float*, cons
                           hipStream_t);
 int rdp_maxpool2_fwd(const void*, int, void*, int, int, int, int, int, hipStream_t);
 int rdp_maxpool2_bwd(const void*, int, const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
+int rdp_bn_relu_apply_pool(const void*, int, void*, int, void*, int, const float*, int, int, int, int, hipStream_t);
+int rdp_maxpool2_bwd_bn_reduce(const void*, int, const void*, int, const void*, int, void*, int, const void*, int,
+                               const float*, int, int, int, int, float*, int, hipStream_t);
 int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_upT_shuffle(const void*, int, const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -244,6 +247,38 @@ void maxpool2_bwd(torch::Tensor dp, torch::Tensor x, c10::optional<torch::Tensor
   TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && o.C == a.C, "maxpool bwd dx shape");
   TORCH_CHECK(rdp_maxpool2_bwd(p.ptr, p.pitch, a.ptr, a.pitch, dskip ? s.ptr : nullptr, dskip ? s.pitch : 0, o.ptr,
                                o.pitch, a.N, a.H, a.W, a.C, cur_stream()) == 0, "maxpool bwd");
+}
+
+// training forward at a Down boundary: a = relu(bn(y)) (skip activation) and its 2x2 max pool, one pass
+void bn_relu_apply_pool(torch::Tensor y, torch::Tensor out, torch::Tensor pool, torch::Tensor coef) {
+  Act a = act(y, "y"), o = act(out, "out"), p = act(pool, "pool");
+  TORCH_CHECK(a.N == o.N && a.H == o.H && a.W == o.W && a.C == o.C, "bn_relu_apply_pool shape");
+  TORCH_CHECK(p.N == a.N && p.H == a.H / 2 && p.W == a.W / 2 && p.C == a.C, "bn_relu_apply_pool pool shape");
+  check_f32(coef, "coef");
+  TORCH_CHECK(coef.numel() >= 4 * a.C, "coef");
+  TORCH_CHECK(rdp_bn_relu_apply_pool(a.ptr, a.pitch, o.ptr, o.pitch, p.ptr, p.pitch, coef.data_ptr<float>(), a.N, a.H,
+                                     a.W, a.C, cur_stream()) == 0, "bn_relu_apply_pool: channels must be 2^k in [8, 2048]");
+}
+
+// maxpool backward (+ skip gradient) fused with the BN backward reduction of the pooled layer;
+// returns the partial rows written (input T of bn_bwd_finalize)
+int maxpool2_bwd_bn_reduce(torch::Tensor dp, torch::Tensor x, c10::optional<torch::Tensor> dskip, torch::Tensor dx,
+                           torch::Tensor y, torch::Tensor coef, torch::Tensor partial) {
+  Act p = act(dp, "dp"), a = act(x, "x"), o = act(dx, "dx"), yy = act(y, "y"), s;
+  if (dskip) { s = act(*dskip, "dskip"); TORCH_CHECK(s.N == a.N && s.H == a.H && s.W == a.W && s.C == a.C, "dskip shape"); }
+  TORCH_CHECK(p.N == a.N && p.H == a.H / 2 && p.W == a.W / 2 && p.C == a.C, "maxpool bwd shape");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && o.C == a.C, "maxpool bwd dx shape");
+  TORCH_CHECK(yy.N == a.N && yy.H == a.H && yy.W == a.W && yy.C == a.C, "maxpool bwd y shape");
+  check_f32(coef, "coef");
+  check_f32(partial, "partial");
+  TORCH_CHECK(coef.numel() >= 4 * a.C, "coef");
+  const int maxb = partial.numel() / (2 * a.C);
+  TORCH_CHECK(maxb >= 1, "partial too small");
+  const int T = rdp_maxpool2_bwd_bn_reduce(p.ptr, p.pitch, a.ptr, a.pitch, dskip ? s.ptr : nullptr, dskip ? s.pitch : 0,
+                                           o.ptr, o.pitch, yy.ptr, yy.pitch, coef.data_ptr<float>(), a.N, a.H, a.W, a.C,
+                                           partial.data_ptr<float>(), maxb, cur_stream());
+  TORCH_CHECK(T > 0, "maxpool2_bwd_bn_reduce: channels must be 2^k in [8, 2048]");
+  return T;
 }
 
 void upsample2_fwd(torch::Tensor x, torch::Tensor out, int oy, int ox) {
@@ -465,6 +500,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_bwd_apply", &bn_relu_bwd_apply);
   m.def("maxpool2_fwd", &maxpool2_fwd);
   m.def("maxpool2_bwd", &maxpool2_bwd);
+  m.def("bn_relu_apply_pool", &bn_relu_apply_pool);
+  m.def("maxpool2_bwd_bn_reduce", &maxpool2_bwd_bn_reduce);
   m.def("upsample2_fwd", &upsample2_fwd);
   m.def("upT_shuffle", &upT_shuffle);
   m.def("upT_unshuffle", &upT_unshuffle);

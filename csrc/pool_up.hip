@@ -113,6 +113,161 @@ __global__ void maxpool2_bwd_kernel(const u16* __restrict__ dp, int dppitch, con
   }
 }
 
+// ---- BN/ReLU <-> maxpool fusions at the encoder's Down boundaries (training) ----
+// Forward: the last conv of each encoder DoubleConv feeds both the skip connection and MaxPool2d
+// (segmentation_model.py:47,110-114). One pass reads its pre-BN output y once and writes the skip
+// activation a = relu(y*scale + shift) AND the pooled tensor (the standalone pool re-read a).
+// Backward: the pool's backward (+ skip gradient) is that layer's activation gradient, so the BN
+// backward reduction (sum g, sum g*xhat over the ReLU mask) runs in the same pass on the values it
+// just produced instead of re-reading them. Each thread owns one 8-channel group for the launch
+// (coefficients in registers) and walks 2x2 windows with a grid stride; C is a power of two.
+RDP_DEV void ld8f(const float* p, float* f) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+__global__ __launch_bounds__(256) void bn_relu_apply_pool_kernel(const u16* __restrict__ y, int ypitch,
+                                                                 u16* __restrict__ a, int apitch,
+                                                                 u16* __restrict__ pool, int ppitch,
+                                                                 const float* __restrict__ coef, int N, int H, int W,
+                                                                 int C) {
+  const int CG = C >> 3, RPB = 256 / CG;
+  const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
+  const int c = g * 8;
+  float ss[8], hh[8];
+  ld8f(coef + 2 * C + c, ss);
+  ld8f(coef + 3 * C + c, hh);
+  const int Ho = H / 2, Wo = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int nwin = N * Hc * Wc;
+  for (int wi = blockIdx.x * RPB + r; wi < nwin; wi += gridDim.x * RPB) {
+    const int wc = wi % Wc, t = wi / Wc;
+    const int hc = t % Hc, n = t / Hc;
+    uint4 v[4];
+    bool ok[4];
+    long px[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * hc + (q >> 1), w = 2 * wc + (q & 1);
+      ok[q] = h < H && w < W;
+      px[q] = ((long)n * H + h) * W + w;
+      if (ok[q]) v[q] = *(const uint4*)(y + px[q] * ypitch + c);
+    }
+    float av[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!ok[q]) continue;
+      float f[8];
+      unpack8f(v[q], f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], ss[k], hh[k]), 0.f);
+      const uint4 o = pack8f(f);
+      *(uint4*)(a + px[q] * apitch + c) = o;
+      unpack8f(o, av[q]);  // the pool sees exactly the stored (bf16) activation
+    }
+    if (hc < Ho && wc < Wo) {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float m = av[0][k];
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (av[q][k] > m || isnan(av[q][k])) m = av[q][k];
+        o[k] = m;
+      }
+      *(uint4*)(pool + (((long)n * Ho + hc) * Wo + wc) * ppitch + c) = pack8f(o);
+    }
+  }
+}
+
+// dx = maxpool_bwd(dp) (+ dskip), then partial[blk] = [sum_g | sum_g*xhat] per channel with
+// g = dx * (y*scale + shift > 0), xhat = (y - mean) * invstd (bn_relu_bwd_reduce's partial format).
+__global__ __launch_bounds__(256) void maxpool2_bwd_bn_reduce_kernel(
+    const u16* __restrict__ dp, int dppitch, const u16* __restrict__ x, int xpitch, const u16* __restrict__ dskip,
+    int dspitch, u16* __restrict__ dx, int dxpitch, const u16* __restrict__ y, int ypitch,
+    const float* __restrict__ coef, int N, int H, int W, int C, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [rows][C][2]
+  const int CG = C >> 3, RPB = 256 / CG;
+  const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
+  const int c = g * 8;
+  float mean[8], inv[8], ss[8], hh[8];
+  ld8f(coef + c, mean);
+  ld8f(coef + C + c, inv);
+  ld8f(coef + 2 * C + c, ss);
+  ld8f(coef + 3 * C + c, hh);
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sg[k] = 0.f; sgx[k] = 0.f; }
+  const int Ho = H / 2, Wo = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int nwin = N * Hc * Wc;
+  for (int wi = blockIdx.x * RPB + r; wi < nwin; wi += gridDim.x * RPB) {
+    const int wc = wi % Wc, t = wi / Wc;
+    const int hc = t % Hc, n = t / Hc;
+    const bool pooled = hc < Ho && wc < Wo;
+    bool ok[4];
+    long px[4];
+    uint4 vs[4], vy[4], vx[4], vd;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * hc + (q >> 1), w = 2 * wc + (q & 1);
+      ok[q] = h < H && w < W;
+      px[q] = ((long)n * H + h) * W + w;
+      if (ok[q]) {
+        vy[q] = *(const uint4*)(y + px[q] * ypitch + c);
+        vs[q] = dskip ? *(const uint4*)(dskip + px[q] * dspitch + c) : make_uint4(0, 0, 0, 0);
+        if (pooled) vx[q] = *(const uint4*)(x + px[q] * xpitch + c);
+      }
+    }
+    if (pooled) vd = *(const uint4*)(dp + (((long)n * Ho + hc) * Wo + wc) * dppitch + c);
+    int idx[8];
+    float d[8];
+    if (pooled) {
+      float v[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) unpack8f(vx[q], v[q]);
+      unpack8f(vd, d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float m = v[0][k];
+        int id = 0;
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (v[q][k] > m || isnan(v[q][k])) { m = v[q][k]; id = q; }
+        idx[k] = id;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!ok[q]) continue;
+      float sk[8], o[8], fy[8];
+      unpack8f(vs[q], sk);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = sk[k] + ((pooled && idx[k] == q) ? d[k] : 0.f);
+      const uint4 ov = pack8f(o);
+      *(uint4*)(dx + px[q] * dxpitch + c) = ov;
+      unpack8f(ov, o);  // reduce the stored (bf16) gradient, as the standalone reduce would
+      unpack8f(vy[q], fy);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = fmaf(fy[k], ss[k], hh[k]) > 0.f ? o[k] : 0.f;
+        sg[k] += gg;
+        sgx[k] += gg * (fy[k] - mean[k]) * inv[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sred[(r * C + c + k) * 2] = sg[k];
+    sred[(r * C + c + k) * 2 + 1] = sgx[k];
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int q = 0; q < RPB; ++q) { a0 += sred[(q * C + cc) * 2]; a1 += sred[(q * C + cc) * 2 + 1]; }
+    partial[(size_t)blockIdx.x * 2 * C + cc] = a0;
+    partial[(size_t)blockIdx.x * 2 * C + C + cc] = a1;
+  }
+}
+
 struct UpGeom {
   int N, hin, win, Hout, Wout, oy, ox, C;
   float rh, rw;
@@ -321,6 +476,30 @@ int rdp_maxpool2_bwd(const void* dp, int dppitch, const void* x, int xpitch, con
                      0, s, (const u16*)dp, dppitch, (const u16*)x, xpitch, (const u16*)dskip, dspitch, (u16*)dx,
                      dxpitch, N, H, W, C);
   return 0;
+}
+static bool pow2c(int C) { return C >= 8 && C <= 2048 && (C & (C - 1)) == 0; }
+int rdp_bn_relu_apply_pool(const void* y, int ypitch, void* a, int apitch, void* pool, int ppitch, const float* coef,
+                           int N, int H, int W, int C, hipStream_t s) {
+  if (!pow2c(C) || ypitch % 8 || apitch % 8 || ppitch % 8) return -1;
+  const long rpb = 256 / (C / 8), nwin = (long)N * ((H + 1) / 2) * ((W + 1) / 2);
+  const int grid = (int)std::max<long>(1, std::min<long>((nwin + rpb - 1) / rpb, 4096));
+  hipLaunchKernelGGL(bn_relu_apply_pool_kernel, dim3(grid), dim3(256), 0, s, (const u16*)y, ypitch, (u16*)a, apitch,
+                     (u16*)pool, ppitch, coef, N, H, W, C);
+  return 0;
+}
+// returns the number of partial rows written (T for bn_bwd_finalize), -1 if not applicable
+int rdp_maxpool2_bwd_bn_reduce(const void* dp, int dppitch, const void* x, int xpitch, const void* dskip, int dspitch,
+                               void* dx, int dxpitch, const void* y, int ypitch, const float* coef, int N, int H, int W,
+                               int C, float* partial, int max_blocks, hipStream_t s) {
+  if (!pow2c(C) || dppitch % 8 || xpitch % 8 || dspitch % 8 || dxpitch % 8 || ypitch % 8) return -1;
+  const long rpb = 256 / (C / 8), nwin = (long)N * ((H + 1) / 2) * ((W + 1) / 2);
+  // ~4 windows per thread row: enough bytes in flight, few partial rows for the finalize
+  const int grid = (int)std::max<long>(1, std::min<long>((nwin + 4 * rpb - 1) / (4 * rpb), max_blocks));
+  const size_t lds = (size_t)rpb * C * 2 * sizeof(float);
+  hipLaunchKernelGGL(maxpool2_bwd_bn_reduce_kernel, dim3(grid), dim3(256), lds, s, (const u16*)dp, dppitch,
+                     (const u16*)x, xpitch, (const u16*)dskip, dspitch, (u16*)dx, dxpitch, (const u16*)y, ypitch, coef,
+                     N, H, W, C, partial);
+  return grid;
 }
 int rdp_upsample2_fwd(const void* x, int xpitch, void* out, int opitch, int N, int hin, int win, int Hout, int Wout,
                       int oy, int ox, int C, hipStream_t s) {

@@ -290,6 +290,7 @@ class _Layer:
     dx1: Optional[torch.Tensor] = None  # dgrad destinations (None => no dgrad)
     dx2: Optional[torch.Tensor] = None
     splits: int = 1
+    bwd_rows: int = 0  # BN-backward partial rows already produced by a fused producer of da
 
 
 class UNetExecutor:
@@ -302,6 +303,9 @@ class UNetExecutor:
         self.dice_eps = 1.0
         dev = model.store.device
         self.dev = dev
+        # BN apply + maxpool (forward) and maxpool backward + BN reduce (backward) in one pass each at
+        # the Down boundaries (RDP_FUSE_POOL=0: separate kernels, for A/B measurements)
+        self.fuse_pool = os.environ.get("RDP_FUSE_POOL", "1") != "0"
         C = _native()
         D = model.depth
         bf = torch.bfloat16
@@ -473,13 +477,15 @@ class UNetExecutor:
                 self.target.copy_(target.reshape(-1))
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn_relu(self, C, L: _Layer):
+    def _conv_bn_relu(self, C, L: _Layer, pool: Optional[torch.Tensor] = None):
+        """conv -> BN(train: batch stats) -> ReLU into ``L.a``; with ``pool`` also MaxPool2d(2) of
+        ``L.a`` into ``pool`` (fused with the BN apply in training). Returns True if it pooled."""
         sp = L.spec
         m = self.m
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
             C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws)
-            return
+            return False
         rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
         g = m.store.view(sp.bn + ".weight")
         b = m.store.view(sp.bn + ".bias")
@@ -487,7 +493,11 @@ class UNetExecutor:
             M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
                           m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
+        if pool is not None and self.fuse_pool:
+            C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
+            return True
         C.bn_relu_apply(L.y, L.a, L.coef, 1)
+        return False
 
     def prepare_eval(self):
         C = _native()
@@ -509,12 +519,13 @@ class UNetExecutor:
             self.prepare_eval()
         l0, l1 = self.down_layers[0]
         self._conv_bn_relu(C, l0)
-        self._conv_bn_relu(C, l1)
+        pooled = self._conv_bn_relu(C, l1, self.pools[0] if D > 0 else None)
         for i in range(1, D + 1):
-            C.maxpool2_fwd(self.skips[i - 1], self.pools[i - 1])
+            if not pooled:
+                C.maxpool2_fwd(self.skips[i - 1], self.pools[i - 1])
             la, lb = self.down_layers[i]
             self._conv_bn_relu(C, la)
-            self._conv_bn_relu(C, lb)
+            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None)
         low = self.skips[D]
         for i in range(1, D + 1):
             lv = D - i
@@ -547,7 +558,9 @@ class UNetExecutor:
         sp = L.spec
         st = self.m.store
         M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
-        T = C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
+        # the reduction already ran inside the pool backward that produced L.da (fused), or runs now
+        T = L.bwd_rows if L.bwd_rows else C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
+        L.bwd_rows = 0
         C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
                           st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
                           self.red_ws)
@@ -624,7 +637,11 @@ class UNetExecutor:
             self._conv_bwd(C, lb, grad_hook)
             self._conv_bwd(C, la, grad_hook)
             prev = self.down_layers[i - 1][1]
-            C.maxpool2_bwd(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1], prev.da)
+            if self.fuse_pool:
+                prev.bwd_rows = C.maxpool2_bwd_bn_reduce(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1],
+                                                         prev.da, prev.y, prev.coef, self.bn_partial)
+            else:
+                C.maxpool2_bwd(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1], prev.da)
         l0, l1 = self.down_layers[0]
         self._conv_bwd(C, l1, grad_hook)
         self._conv_bwd(C, l0, grad_hook)

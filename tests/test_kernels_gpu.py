@@ -528,3 +528,41 @@ def test_wprep_derived_layouts(C, decoder):
     for us in m.up_specs:
         w = st.flat_slice(us.name + ".weight", st.flat).view(us.cin, 4 * us.cout)
         assert torch.equal(m.upT_fwd_weight(us).float(), bf(w.t()).float()), us.name
+
+
+@pytest.mark.parametrize("N,H,W,Ch", [(2, 16, 16, 64), (1, 9, 13, 128), (3, 8, 6, 512)])
+def test_bn_relu_pool_fusions(C, N, H, W, Ch):
+    """Fused BN-apply+maxpool and maxpool-bwd+BN-reduce match the separate kernels (odd sizes too)."""
+    torch.manual_seed(11)
+    dev = "cuda"
+    y = bf(torch.randn(N, H, W, Ch, device=dev) * 2 + 0.3)
+    mean, inv = torch.randn(Ch, device=dev) * 0.1, torch.rand(Ch, device=dev) + 0.5
+    gamma, beta = torch.randn(Ch, device=dev), torch.randn(Ch, device=dev) * 0.2
+    ss = gamma * inv
+    coef = torch.cat([mean, inv, ss, beta - mean * ss]).contiguous()
+    # forward: apply + pool in one pass == apply, then pool
+    a_ref = torch.empty_like(y)
+    p_ref = torch.empty(N, H // 2, W // 2, Ch, dtype=torch.bfloat16, device=dev)
+    C.bn_relu_apply(y, a_ref, coef, 1)
+    C.maxpool2_fwd(a_ref, p_ref)
+    a, p = torch.empty_like(y), torch.empty_like(p_ref)
+    C.bn_relu_apply_pool(y, a, p, coef)
+    assert torch.equal(a, a_ref) and torch.equal(p, p_ref)
+    # backward: pool bwd (+ skip grad) fused with the BN reduce == pool bwd, then reduce
+    dp = bf(torch.randn(N, H // 2, W // 2, Ch, device=dev))
+    dskip = bf(torch.randn(N, H, W, Ch, device=dev))
+    dx_ref = torch.empty_like(y)
+    C.maxpool2_bwd(dp, a_ref, dskip, dx_ref)
+    part_ref = torch.zeros(1024 * 2 * Ch, device=dev)
+    T_ref = C.bn_relu_bwd_reduce(dx_ref, y, coef, 1, part_ref)
+    dx = torch.empty_like(y)
+    part = torch.zeros(1024 * 2 * Ch, device=dev)
+    T = C.maxpool2_bwd_bn_reduce(dp, a_ref, dskip, dx, y, coef, part)
+    assert torch.equal(dx, dx_ref)
+    got = part[:T * 2 * Ch].view(T, 2, Ch).double().sum(0)
+    ref = part_ref[:T_ref * 2 * Ch].view(T_ref, 2, Ch).double().sum(0)
+    # exact fp32 reference of the same sums
+    g = dx_ref.float() * ((y.float() * ss + (beta - mean * ss)) > 0)
+    exact = torch.stack([g.sum((0, 1, 2)), (g * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
+    assert torch.allclose(got, exact, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(got, ref, rtol=1e-4, atol=1e-3)
