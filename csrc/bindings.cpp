@@ -45,9 +45,11 @@ int rdp_upT_unshuffle(const void*, int, void*, int, int, int, int, int, int, int
 int rdp_colsum_bf16(const void*, int, long, int, int, float*, float*, int, hipStream_t);
 int rdp_head_partial_blocks(long);
 int rdp_head_fwd(const void*, int, const float*, const float*, const float*, float*, float*, float*, float*, int, float,
-                 float, hipStream_t);
+                 float, const float*, hipStream_t);
 int rdp_head_bwd(const void*, int, const float*, const float*, const float*, const float*, void*, int, float*, float*,
-                 float*, int, float, float, float, hipStream_t);
+                 float*, int, float, float, float, const float*, float*, hipStream_t);
+int rdp_head_bn_bwd_apply(const void*, int, const float*, const float*, const float*, const float*, const float*,
+                          const float*, void*, int, int, float, float, float, hipStream_t);
 int rdp_head_mask(const void*, int, const float*, const float*, float, void*, int, hipStream_t);
 int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, int*,
              hipStream_t);
@@ -325,28 +327,69 @@ void colsum_bf16(torch::Tensor x, int groups, torch::Tensor partial, torch::Tens
 
 int head_partial_blocks(long M) { return rdp_head_partial_blocks(M); }
 
+// coef (training, optional): `a` is the last conv's pre-BN output y and coef its BN coefficients
 void head_fwd(torch::Tensor a, torch::Tensor w, torch::Tensor b, torch::Tensor target, torch::Tensor logits,
-              torch::Tensor partial, torch::Tensor sums, torch::Tensor loss, double dice_w, double dice_eps) {
+              torch::Tensor partial, torch::Tensor sums, torch::Tensor loss, double dice_w, double dice_eps,
+              c10::optional<torch::Tensor> coef) {
   Act x = act(a, "a");
   TORCH_CHECK(x.C == 64, "head expects 64 channels");
   const long M = (long)x.N * x.H * x.W;
   TORCH_CHECK(target.numel() == M && logits.numel() == M, "head target/logits numel");
   TORCH_CHECK(partial.numel() >= (long)rdp_head_partial_blocks(M) * 65, "head partial too small");
+  const float* cf = nullptr;
+  if (coef) {
+    TORCH_CHECK(coef->numel() >= 4 * 64 && coef->scalar_type() == torch::kFloat, "head coef");
+    cf = coef->data_ptr<float>();
+  }
   rdp_head_fwd(x.ptr, x.pitch, w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<float>(),
                logits.data_ptr<float>(), partial.data_ptr<float>(), sums.data_ptr<float>(), loss.data_ptr<float>(), M,
-               (float)dice_w, (float)dice_eps, cur_stream());
+               (float)dice_w, (float)dice_eps, cf, cur_stream());
 }
 
-void head_bwd(torch::Tensor a, torch::Tensor w, torch::Tensor logits, torch::Tensor target, torch::Tensor sums,
-              torch::Tensor da, torch::Tensor partial, torch::Tensor gw, torch::Tensor gb, double dice_w,
-              double dice_eps, double gscale) {
-  Act x = act(a, "a"), d = act(da, "da");
+// coef + bnpart given: BN-fused backward (da not written, returns the BN partial row count);
+// otherwise da = d loss / d a is written. Returns the number of partial rows.
+int head_bwd(torch::Tensor a, torch::Tensor w, torch::Tensor logits, torch::Tensor target, torch::Tensor sums,
+             c10::optional<torch::Tensor> da, torch::Tensor partial, torch::Tensor gw, torch::Tensor gb, double dice_w,
+             double dice_eps, double gscale, c10::optional<torch::Tensor> coef, c10::optional<torch::Tensor> bnpart) {
+  Act x = act(a, "a");
   const long M = (long)x.N * x.H * x.W;
-  TORCH_CHECK(d.C == 64 && x.C == 64, "head bwd channels");
+  TORCH_CHECK(x.C == 64, "head bwd channels");
   TORCH_CHECK(partial.numel() >= (long)rdp_head_partial_blocks(M) * 65, "head partial too small");
-  rdp_head_bwd(x.ptr, x.pitch, w.data_ptr<float>(), logits.data_ptr<float>(), target.data_ptr<float>(),
-               sums.data_ptr<float>(), d.ptr, d.pitch, partial.data_ptr<float>(), gw.data_ptr<float>(),
-               gb.data_ptr<float>(), M, (float)dice_w, (float)dice_eps, (float)gscale, cur_stream());
+  void* dptr = nullptr;
+  int dpitch = 0;
+  const float* cf = nullptr;
+  float* bp = nullptr;
+  if (coef) {
+    TORCH_CHECK(bnpart && bnpart->numel() >= (long)rdp_head_partial_blocks(M) * 128, "head bnpart too small");
+    TORCH_CHECK(coef->numel() >= 4 * 64 && coef->scalar_type() == torch::kFloat, "head coef");
+    cf = coef->data_ptr<float>();
+    bp = bnpart->data_ptr<float>();
+  } else {
+    TORCH_CHECK(da.has_value(), "head_bwd: da required without coef");
+    Act d = act(*da, "da");
+    TORCH_CHECK(d.C == 64 && (long)d.N * d.H * d.W == M, "head bwd da shape");
+    dptr = d.ptr;
+    dpitch = d.pitch;
+  }
+  return rdp_head_bwd(x.ptr, x.pitch, w.data_ptr<float>(), logits.data_ptr<float>(), target.data_ptr<float>(),
+                      sums.data_ptr<float>(), dptr, dpitch, partial.data_ptr<float>(), gw.data_ptr<float>(),
+                      gb.data_ptr<float>(), M, (float)dice_w, (float)dice_eps, (float)gscale, cf, bp, cur_stream());
+}
+
+// dy of the last conv from the logits (BN-fused head backward, second pass)
+void head_bn_bwd_apply(torch::Tensor y, torch::Tensor w, torch::Tensor logits, torch::Tensor target,
+                       torch::Tensor sums, torch::Tensor coef, torch::Tensor coef2, torch::Tensor dy, double dice_w,
+                       double dice_eps, double gscale) {
+  Act x = act(y, "y"), d = act(dy, "dy");
+  const long M = (long)x.N * x.H * x.W;
+  TORCH_CHECK(x.C == 64 && d.C == 64 && (long)d.N * d.H * d.W == M, "head_bn_bwd_apply shapes");
+  TORCH_CHECK(logits.numel() == M && target.numel() == M, "head_bn_bwd_apply logits/target numel");
+  TORCH_CHECK(coef.numel() >= 4 * 64 && coef2.numel() >= 3 * 64, "head_bn_bwd_apply coef sizes");
+  TORCH_CHECK(rdp_head_bn_bwd_apply(x.ptr, x.pitch, w.data_ptr<float>(), logits.data_ptr<float>(),
+                                    target.data_ptr<float>(), sums.data_ptr<float>(), coef.data_ptr<float>(),
+                                    coef2.data_ptr<float>(), d.ptr, d.pitch, M, (float)dice_w, (float)dice_eps,
+                                    (float)gscale, cur_stream()) == 0,
+              "head_bn_bwd_apply: pitches must be multiples of 8");
 }
 
 void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_thr, torch::Tensor mask) {
@@ -508,8 +551,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum_bf16", &colsum_bf16);
   m.def("upsample2_bwd", &upsample2_bwd);
   m.def("head_partial_blocks", &head_partial_blocks);
-  m.def("head_fwd", &head_fwd);
-  m.def("head_bwd", &head_bwd);
+  m.def("head_fwd", &head_fwd, py::arg("a"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("logits"),
+        py::arg("partial"), py::arg("sums"), py::arg("loss"), py::arg("dice_w"), py::arg("dice_eps"),
+        py::arg("coef") = py::none());
+  m.def("head_bwd", &head_bwd, py::arg("a"), py::arg("w"), py::arg("logits"), py::arg("target"), py::arg("sums"),
+        py::arg("da"), py::arg("partial"), py::arg("gw"), py::arg("gb"), py::arg("dice_w"), py::arg("dice_eps"),
+        py::arg("gscale"), py::arg("coef") = py::none(), py::arg("bnpart") = py::none());
+  m.def("head_bn_bwd_apply", &head_bn_bwd_apply);
   m.def("head_mask", &head_mask);
   m.def("adam", &adam);
   m.def("cast_bf16", &cast_bf16);

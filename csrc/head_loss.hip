@@ -40,21 +40,41 @@ RDP_DEV float sum8lanes(float v) {  // reduce across the 8 lanes of a pixel grou
   return v;
 }
 
+// BN = true (training): `a` holds the last conv's PRE-BN output y and coef its BN coefficients
+// [mean | invstd | scale | shift] (64 each); the head applies a = bf16(relu(y*scale + shift)) itself,
+// so that activation is never written or re-read (up4.conv.double_conv.3 -> outc).
+RDP_DEV uint4 bn_relu8(const uint4& v, const float* ss, const float* hh) {
+  float f[8];
+  unpack8h(v, f);
+  uint4 o;
+  o.x = pack2bf(fmaxf(fmaf(f[0], ss[0], hh[0]), 0.f), fmaxf(fmaf(f[1], ss[1], hh[1]), 0.f));
+  o.y = pack2bf(fmaxf(fmaf(f[2], ss[2], hh[2]), 0.f), fmaxf(fmaf(f[3], ss[3], hh[3]), 0.f));
+  o.z = pack2bf(fmaxf(fmaf(f[4], ss[4], hh[4]), 0.f), fmaxf(fmaf(f[5], ss[5], hh[5]), 0.f));
+  o.w = pack2bf(fmaxf(fmaf(f[6], ss[6], hh[6]), 0.f), fmaxf(fmaf(f[7], ss[7], hh[7]), 0.f));
+  return o;
+}
+
+template <bool BN>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const u16* __restrict__ a, int apitch,
                                                        const float* __restrict__ w, const float* __restrict__ b,
                                                        const float* __restrict__ target, float* __restrict__ logits,
-                                                       float* __restrict__ partial, int M) {
+                                                       float* __restrict__ partial, int M,
+                                                       const float* __restrict__ coef) {
   __shared__ float red[4][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane & 7;
-  float wl[8];
+  float wl[8], ss[8], hh[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) wl[k] = w[sub * 8 + k];
+  for (int k = 0; k < 8; ++k) {
+    wl[k] = w[sub * 8 + k];
+    if (BN) { ss[k] = coef[2 * HEAD_C + sub * 8 + k]; hh[k] = coef[3 * HEAD_C + sub * 8 + k]; }
+  }
   const float bias = b[0];
   float sb = 0.f, si = 0.f, sp = 0.f, st = 0.f;
   const long groups_per_iter = (long)gridDim.x * 32;  // 32 pixels per block-iteration
   for (long p = blockIdx.x * 32l + (threadIdx.x >> 3); p < M; p += groups_per_iter) {
-    const uint4 v = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+    uint4 v = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+    if (BN) v = bn_relu8(v, ss, hh);
     const float x = sum8lanes(dot8(v, wl)) + bias;
     if (sub == 0) {
       logits[p] = x;
@@ -104,48 +124,85 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partial, int T, i
   }
 }
 
+// d loss / d logit for one pixel (BCE mean + optional soft Dice), times the loss scale
+RDP_DEV float head_dlogit(float x, float t, float invM, float dice_w, float I, float den, float dice_eps,
+                          float gscale) {
+  const float e = __expf(-fabsf(x));
+  const float sg = x >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+  float dx = (sg - t) * invM;
+  if (dice_w != 0.f) {
+    const float ddp = -(2.f * t * den - (2.f * I + dice_eps)) / (den * den);
+    dx += dice_w * ddp * sg * (1.f - sg);
+  }
+  return dx * gscale;
+}
+
+RDP_DEV float bfround(float f) { return __uint_as_float(((uint32_t)f2bf(f)) << 16); }
+
+// BN = false: da[p][c] = bf16(dlogit*w[c]) is written for the consumer's BN backward.
+// BN = true : `a` is the pre-BN y of the last conv and da is never materialised. The block instead
+//   accumulates that BN's backward partials (sum g, sum g*xhat; g = bf16(dlogit*w)*relu'(.)) in the
+//   bn_relu_bwd_reduce layout [blk][2][64]; head_bn_bwd_apply recomputes g from the logits.
+template <bool BN>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a, int apitch,
                                                        const float* __restrict__ w, const float* __restrict__ logits,
                                                        const float* __restrict__ target, const float* __restrict__ sums,
                                                        u16* __restrict__ da, int dapitch, float* __restrict__ partial,
-                                                       int M, float dice_w, float dice_eps, float gscale) {
+                                                       int M, float dice_w, float dice_eps, float gscale,
+                                                       const float* __restrict__ coef, float* __restrict__ bnpart) {
   __shared__ float red[4][HEAD_C + 1];
+  __shared__ float bred[BN ? 4 : 1][BN ? 2 * HEAD_C : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane & 7;
-  float wl[8];
+  float wl[8], mu[8], iv[8], ss[8], hh[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) wl[k] = w[sub * 8 + k];
+  for (int k = 0; k < 8; ++k) {
+    wl[k] = w[sub * 8 + k];
+    if (BN) {
+      mu[k] = coef[sub * 8 + k];
+      iv[k] = coef[HEAD_C + sub * 8 + k];
+      ss[k] = coef[2 * HEAD_C + sub * 8 + k];
+      hh[k] = coef[3 * HEAD_C + sub * 8 + k];
+    }
+  }
   const float invM = 1.f / (float)M;
   float I = 0.f, U = 0.f;
   if (dice_w != 0.f) { I = sums[1]; U = sums[2] + sums[3]; }
   const float den = U + dice_eps;
-  float gw[8], gb = 0.f;
+  float gw[8], sg[8], sgx[8], gb = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) gw[k] = 0.f;
+  for (int k = 0; k < 8; ++k) { gw[k] = 0.f; sg[k] = 0.f; sgx[k] = 0.f; }
   for (long p = blockIdx.x * 32l + (threadIdx.x >> 3); p < M; p += (long)gridDim.x * 32) {
-    const float x = logits[p], t = target[p];
-    const float e = __expf(-fabsf(x));
-    const float sg = x >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
-    float dx = (sg - t) * invM;
-    if (dice_w != 0.f) {
-      const float ddp = -(2.f * t * den - (2.f * I + dice_eps)) / (den * den);
-      dx += dice_w * ddp * sg * (1.f - sg);
-    }
-    dx *= gscale;
-    const uint4 v = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+    const float dx = head_dlogit(logits[p], target[p], invM, dice_w, I, den, dice_eps, gscale);
+    const uint4 vy = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
     float f[8];
-    unpack8h(v, f);
+    if (BN) {
+      float fy[8];
+      unpack8h(vy, fy);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float z = fmaf(fy[k], ss[k], hh[k]);
+        f[k] = bfround(fmaxf(z, 0.f));  // the activation the forward head consumed
+        const float g = z > 0.f ? bfround(dx * wl[k]) : 0.f;
+        sg[k] += g;
+        sgx[k] += g * (fy[k] - mu[k]) * iv[k];
+      }
+    } else {
+      unpack8h(vy, f);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) gw[k] = fmaf(dx, f[k], gw[k]);
     if (sub == 0) gb += dx;
-    uint4 o;
-    o.x = pack2bf(dx * wl[0], dx * wl[1]);
-    o.y = pack2bf(dx * wl[2], dx * wl[3]);
-    o.z = pack2bf(dx * wl[4], dx * wl[5]);
-    o.w = pack2bf(dx * wl[6], dx * wl[7]);
-    *(uint4*)(da + (size_t)p * dapitch + sub * 8) = o;
+    if (!BN) {
+      uint4 o;
+      o.x = pack2bf(dx * wl[0], dx * wl[1]);
+      o.y = pack2bf(dx * wl[2], dx * wl[3]);
+      o.z = pack2bf(dx * wl[4], dx * wl[5]);
+      o.w = pack2bf(dx * wl[6], dx * wl[7]);
+      *(uint4*)(da + (size_t)p * dapitch + sub * 8) = o;
+    }
   }
-  // reduce gw over the 8 pixel-groups of the wave that share `sub`
+  // reduce over the 8 pixel-groups of the wave that share `sub`
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     float v = gw[k];
@@ -153,17 +210,102 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
     gw[k] = v;
+    if (BN) {
+      float u = sg[k], q = sgx[k];
+      u += __shfl_xor(u, 8, 64);
+      u += __shfl_xor(u, 16, 64);
+      u += __shfl_xor(u, 32, 64);
+      q += __shfl_xor(q, 8, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      sg[k] = u;
+      sgx[k] = q;
+    }
   }
   gb = wave_sum(gb);
   if (lane < 8) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[wave][lane * 8 + k] = gw[k];
+    for (int k = 0; k < 8; ++k) {
+      red[wave][lane * 8 + k] = gw[k];
+      if (BN) {
+        bred[wave][lane * 8 + k] = sg[k];
+        bred[wave][HEAD_C + lane * 8 + k] = sgx[k];
+      }
+    }
   }
   if (lane == 0) red[wave][HEAD_C] = gb;
   __syncthreads();
   if (threadIdx.x <= HEAD_C) {
     const int c = threadIdx.x;
     partial[blockIdx.x * (HEAD_C + 1) + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
+  if (BN && threadIdx.x < 2 * HEAD_C) {
+    const int c = threadIdx.x;
+    bnpart[(size_t)blockIdx.x * 2 * HEAD_C + c] = bred[0][c] + bred[1][c] + bred[2][c] + bred[3][c];
+  }
+}
+
+// dy = A*g + B*y + K with g = bf16(dlogit*w)*relu'(y*scale+shift) recomputed per pixel from the
+// logits: the last conv's bn_relu_bwd_apply without a materialised da. 4 pixels in flight per
+// 8-lane group.
+__global__ __launch_bounds__(256) void head_bn_bwd_apply_kernel(const u16* __restrict__ y, int ypitch,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ logits,
+                                                                const float* __restrict__ target,
+                                                                const float* __restrict__ sums,
+                                                                const float* __restrict__ coef,
+                                                                const float* __restrict__ coef2,
+                                                                u16* __restrict__ dy, int dypitch, int M, float dice_w,
+                                                                float dice_eps, float gscale) {
+  const int c = (threadIdx.x & 7) * 8;
+  float wl[8], ss[8], hh[8], A[8], B[8], K[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wl[k] = w[c + k];
+    ss[k] = coef[2 * HEAD_C + c + k];
+    hh[k] = coef[3 * HEAD_C + c + k];
+    A[k] = coef2[c + k];
+    B[k] = coef2[HEAD_C + c + k];
+    K[k] = coef2[2 * HEAD_C + c + k];
+  }
+  const float invM = 1.f / (float)M;
+  float I = 0.f, U = 0.f;
+  if (dice_w != 0.f) { I = sums[1]; U = sums[2] + sums[3]; }
+  const float den = U + dice_eps;
+  constexpr int PX = 4;
+  const long stride = (long)gridDim.x * 32;
+  for (long p0 = blockIdx.x * 32l + (threadIdx.x >> 3); p0 < M; p0 += stride * PX) {
+    uint4 vy[PX];
+    float x[PX], t[PX];
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const long p = p0 + u * stride;
+      if (p < M) {
+        vy[u] = *(const uint4*)(y + (size_t)p * ypitch + c);
+        x[u] = logits[p];
+        t[u] = target[p];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const long p = p0 + u * stride;
+      if (p < M) {
+        const float dx = head_dlogit(x[u], t[u], invM, dice_w, I, den, dice_eps, gscale);
+        float fy[8], o[8];
+        unpack8h(vy[u], fy);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = fmaf(fy[k], ss[k], hh[k]) > 0.f ? bfround(dx * wl[k]) : 0.f;
+          o[k] = fmaf(A[k], g, fmaf(B[k], fy[k], K[k]));
+        }
+        uint4 v;
+        v.x = pack2bf(o[0], o[1]);
+        v.y = pack2bf(o[2], o[3]);
+        v.z = pack2bf(o[4], o[5]);
+        v.w = pack2bf(o[6], o[7]);
+        *(uint4*)(dy + (size_t)p * dypitch + c) = v;
+      }
+    }
   }
 }
 
@@ -203,23 +345,46 @@ static int blocks_for(long M) { return (int)std::max<long>(1, std::min<long>((M 
 extern "C" {
 int rdp_head_partial_blocks(long M) { return blocks_for(M); }
 
+// coef != nullptr: `a` is the last conv's pre-BN output; BN+ReLU are applied on the fly
 int rdp_head_fwd(const void* a, int apitch, const float* w, const float* b, const float* target, float* logits,
-                 float* partial, float* sums, float* loss, int M, float dice_w, float dice_eps, hipStream_t s) {
+                 float* partial, float* sums, float* loss, int M, float dice_w, float dice_eps, const float* coef,
+                 hipStream_t s) {
   if (apitch % 8) return -1;
   const int nb = blocks_for(M);
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target, logits, partial, M);
+  if (coef)
+    hipLaunchKernelGGL(head_fwd_kernel<true>, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target, logits,
+                       partial, M, coef);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<false>, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target, logits,
+                       partial, M, coef);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partial, nb, M, dice_w, dice_eps, sums, loss);
   return nb;
 }
 
+// coef != nullptr: BN-fused variant (da unused; bnpart receives the BN backward partial rows).
+// Returns the number of partial rows.
 int rdp_head_bwd(const void* a, int apitch, const float* w, const float* logits, const float* target,
                  const float* sums, void* da, int dapitch, float* partial, float* gw, float* gb, int M, float dice_w,
-                 float dice_eps, float gscale, hipStream_t s) {
+                 float dice_eps, float gscale, const float* coef, float* bnpart, hipStream_t s) {
   const int nb = blocks_for(M);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, logits, target, sums,
-                     (u16*)da, dapitch, partial, M, dice_w, dice_eps, gscale);
+  if (coef)
+    hipLaunchKernelGGL(head_bwd_kernel<true>, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, logits, target,
+                       sums, (u16*)da, dapitch, partial, M, dice_w, dice_eps, gscale, coef, bnpart);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<false>, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, logits, target,
+                       sums, (u16*)da, dapitch, partial, M, dice_w, dice_eps, gscale, coef, bnpart);
   hipLaunchKernelGGL(head_grad_finalize_kernel, dim3(HEAD_C + 1), dim3(256), 0, s, partial, nb, gw, gb);
   return nb;
+}
+
+int rdp_head_bn_bwd_apply(const void* y, int ypitch, const float* w, const float* logits, const float* target,
+                          const float* sums, const float* coef, const float* coef2, void* dy, int dypitch, int M,
+                          float dice_w, float dice_eps, float gscale, hipStream_t s) {
+  if (ypitch % 8 || dypitch % 8) return -1;
+  const int nb = (int)std::max<long>(1, std::min<long>(((long)M + 127) / 128, 2048));
+  hipLaunchKernelGGL(head_bn_bwd_apply_kernel, dim3(nb), dim3(256), 0, s, (const u16*)y, ypitch, w, logits, target,
+                     sums, coef, coef2, (u16*)dy, dypitch, M, dice_w, dice_eps, gscale);
+  return 0;
 }
 
 int rdp_head_mask(const void* a, int apitch, const float* w, const float* b, float logit_thr, void* mask, int M,

@@ -306,6 +306,10 @@ class UNetExecutor:
         # BN apply + maxpool (forward) and maxpool backward + BN reduce (backward) in one pass each at
         # the Down boundaries (RDP_FUSE_POOL=0: separate kernels, for A/B measurements)
         self.fuse_pool = os.environ.get("RDP_FUSE_POOL", "1") != "0"
+        # training: the 1x1 head applies the last conv's BN+ReLU itself (forward) and produces that BN's
+        # backward partials and dy from the logits (backward), so the 64-ch activation and its gradient
+        # are never materialised (RDP_FUSE_HEAD=0: separate kernels, for A/B measurements)
+        self.fuse_head = training and os.environ.get("RDP_FUSE_HEAD", "1") != "0"
         C = _native()
         D = model.depth
         bf = torch.bfloat16
@@ -477,9 +481,10 @@ class UNetExecutor:
                 self.target.copy_(target.reshape(-1))
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn_relu(self, C, L: _Layer, pool: Optional[torch.Tensor] = None):
+    def _conv_bn_relu(self, C, L: _Layer, pool: Optional[torch.Tensor] = None, apply: bool = True):
         """conv -> BN(train: batch stats) -> ReLU into ``L.a``; with ``pool`` also MaxPool2d(2) of
-        ``L.a`` into ``pool`` (fused with the BN apply in training). Returns True if it pooled."""
+        ``L.a`` into ``pool`` (fused with the BN apply in training). Returns True if it pooled.
+        ``apply=False`` (training) stops after the BN statistics: the consumer applies BN+ReLU."""
         sp = L.spec
         m = self.m
         w = m.fwd_weight(sp)
@@ -496,7 +501,8 @@ class UNetExecutor:
         if pool is not None and self.fuse_pool:
             C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
             return True
-        C.bn_relu_apply(L.y, L.a, L.coef, 1)
+        if apply:
+            C.bn_relu_apply(L.y, L.a, L.coef, 1)
         return False
 
     def prepare_eval(self):
@@ -541,30 +547,40 @@ class UNetExecutor:
                 C.upT_shuffle(self.yTs[i - 1], self.m.store.view(us.name + ".bias"), u, oy, ox)
             la, lb = self.up_layers[i - 1]
             self._conv_bn_relu(C, la)
-            self._conv_bn_relu(C, lb)
+            last = i == D
+            self._conv_bn_relu(C, lb, apply=not (last and self.fuse_head and head))
             low = lb.a
         if not head:
             return
         head_w = self.m.store.view("outc.conv.weight").reshape(-1)
         head_b = self.m.store.view("outc.conv.bias")
-        C.head_fwd(self.final, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums, self.loss,
-                   self.dice_w, self.dice_eps)
+        if self.fuse_head:
+            lb = self.up_layers[-1][1] if D else self.down_layers[0][1]
+            C.head_fwd(lb.y, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums, self.loss,
+                       self.dice_w, self.dice_eps, lb.coef)
+        else:
+            C.head_fwd(self.final, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums,
+                       self.loss, self.dice_w, self.dice_eps)
 
     def logits_nchw(self) -> torch.Tensor:
         return self.logits.view(self.N, 1, self.H, self.W)
 
     # ------------------------------------------------------------------ backward
-    def _bn_bwd(self, C, L: _Layer):
+    def _bn_bwd(self, C, L: _Layer, head_gscale: Optional[float] = None):
         sp = L.spec
         st = self.m.store
         M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
-        # the reduction already ran inside the pool backward that produced L.da (fused), or runs now
+        # the reduction already ran inside the pool/head backward that produced L.da (fused), or runs now
         T = L.bwd_rows if L.bwd_rows else C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
         L.bwd_rows = 0
         C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
                           st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
                           self.red_ws)
-        C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
+        if head_gscale is not None:  # fused head: g recomputed from the logits, no da
+            C.head_bn_bwd_apply(L.y, st.view("outc.conv.weight").reshape(-1), self.logits, self.target,
+                                self.loss_sums, L.coef, L.coef2, L.dy, self.dice_w, self.dice_eps, head_gscale)
+        else:
+            C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
 
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream
@@ -575,10 +591,10 @@ class UNetExecutor:
         with torch.cuda.stream(self.side):
             return fn()
 
-    def _conv_bwd(self, C, L: _Layer, hooks=None):
+    def _conv_bwd(self, C, L: _Layer, hooks=None, head_gscale: Optional[float] = None):
         sp = L.spec
         st = self.m.store
-        self._bn_bwd(C, L)
+        self._bn_bwd(C, L, head_gscale)
         gw = st.flat_slice(sp.name + ".weight", st.grad)
         # wgrad (latency-bound on x / dY streams) overlaps the main stream's dgrad + next BN backward;
         # all wgrads share the slab, so they stay serialized on the one side stream
@@ -606,12 +622,20 @@ class UNetExecutor:
 
     def _backward(self, C, D, st, grad_hook, gscale):
         head_w = st.view("outc.conv.weight").reshape(-1)
-        C.head_bwd(self.final, head_w, self.logits, self.target, self.loss_sums, self.up_layers[-1][1].da,
-                   self.head_partial, st.flat_slice("outc.conv.weight", st.grad), st.flat_slice("outc.conv.bias", st.grad),
-                   self.dice_w, self.dice_eps, gscale)
+        last = self.up_layers[-1][1] if D else self.down_layers[0][1]
+        hgw, hgb = st.flat_slice("outc.conv.weight", st.grad), st.flat_slice("outc.conv.bias", st.grad)
+        head_gscale = None
+        if self.fuse_head:
+            last.bwd_rows = C.head_bwd(last.y, head_w, self.logits, self.target, self.loss_sums, None,
+                                       self.head_partial, hgw, hgb, self.dice_w, self.dice_eps, gscale, last.coef,
+                                       self.bn_partial)
+            head_gscale = gscale
+        else:
+            C.head_bwd(self.final, head_w, self.logits, self.target, self.loss_sums, last.da, self.head_partial, hgw,
+                       hgb, self.dice_w, self.dice_eps, gscale)
         for i in range(D, 0, -1):
             la, lb = self.up_layers[i - 1]
-            self._conv_bwd(C, lb, grad_hook)
+            self._conv_bwd(C, lb, grad_hook, head_gscale if i == D else None)
             self._conv_bwd(C, la, grad_hook)
             # d(low) = upsample / transposed-conv backward of du
             low_layer = self.down_layers[D][1] if i == 1 else self.up_layers[i - 2][1]

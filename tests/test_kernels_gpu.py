@@ -566,3 +566,66 @@ def test_bn_relu_pool_fusions(C, N, H, W, Ch):
     exact = torch.stack([g.sum((0, 1, 2)), (g * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
     assert torch.allclose(got, exact, rtol=1e-3, atol=1e-3)
     assert torch.allclose(got, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dice_w", [0.0, 1.0])
+def test_head_bn_fused(C, dice_w):
+    """BN-fused head (training): forward on the pre-BN y == BN apply then head; backward partials
+    and the logit-recomputed dy == head bwd -> BN reduce -> BN apply of the separate kernels."""
+    torch.manual_seed(12)
+    dev = "cuda"
+    N, H, W, Ch = 2, 36, 28, 64
+    M = N * H * W
+    y = bf(torch.randn(N, H, W, Ch, device=dev) * 2 + 0.3)
+    mean, inv = torch.randn(Ch, device=dev) * 0.1, torch.rand(Ch, device=dev) + 0.5
+    gamma, beta = torch.randn(Ch, device=dev), torch.randn(Ch, device=dev) * 0.2
+    ss = gamma * inv
+    coef = torch.cat([mean, inv, ss, beta - mean * ss]).contiguous()
+    wt = torch.randn(64, device=dev) * 0.1
+    b = torch.randn(1, device=dev) * 0.1
+    t = (torch.rand(M, device=dev) > 0.5).float()
+    nb = C.head_partial_blocks(M)
+
+    def run_fwd(src, cf):
+        lg, part = torch.zeros(M, device=dev), torch.zeros(nb * 65, device=dev)
+        sums, loss = torch.zeros(4, device=dev), torch.zeros(2, device=dev)
+        C.head_fwd(src, wt, b, t, lg, part, sums, loss, dice_w, 1.0, cf)
+        return lg, part, sums, loss
+
+    a = torch.empty_like(y)
+    C.bn_relu_apply(y, a, coef, 1)
+    lg_r, part_r, sums_r, loss_r = run_fwd(a, None)
+    lg, part, sums, loss = run_fwd(y, coef)
+    assert torch.equal(lg, lg_r) and torch.equal(loss, loss_r)
+    # backward, separate kernels
+    gs = 0.5
+    da = torch.empty_like(y)
+    gw_r, gb_r = torch.zeros(64, device=dev), torch.zeros(1, device=dev)
+    C.head_bwd(a, wt, lg_r, t, sums_r, da, part_r, gw_r, gb_r, dice_w, 1.0, gs)
+    bp_r = torch.zeros(1024 * 2 * Ch, device=dev)
+    T_r = C.bn_relu_bwd_reduce(da, y, coef, 1, bp_r)
+    ws = torch.zeros(64 * 2 * Ch, device=dev)
+    dg_r, db_r, c2_r = torch.zeros(Ch, device=dev), torch.zeros(Ch, device=dev), torch.zeros(3 * Ch, device=dev)
+    C.bn_bwd_finalize(bp_r, T_r, M, gamma, coef, dg_r, db_r, c2_r, ws)
+    dy_r = torch.empty_like(y)
+    C.bn_relu_bwd_apply(da, y, coef, c2_r, dy_r, 1)
+    # fused
+    gw, gb = torch.zeros(64, device=dev), torch.zeros(1, device=dev)
+    bp = torch.zeros(nb * 128, device=dev)
+    T = C.head_bwd(y, wt, lg, t, sums, None, part, gw, gb, dice_w, 1.0, gs, coef, bp)
+    assert T == nb
+    dg, db, c2 = torch.zeros(Ch, device=dev), torch.zeros(Ch, device=dev), torch.zeros(3 * Ch, device=dev)
+    C.bn_bwd_finalize(bp, T, M, gamma, coef, dg, db, c2, ws)
+    dy = torch.empty_like(y)
+    C.head_bn_bwd_apply(y, wt, lg, t, sums, coef, c2, dy, dice_w, 1.0, gs)
+    assert relerr(gw, gw_r) < 1e-5 and relerr(gb, gb_r) < 1e-5
+    assert relerr(dg, dg_r) < 1e-4 and relerr(db, db_r) < 1e-4
+    assert relerr(c2, c2_r) < 1e-4
+    assert relerr(dy, dy_r) < 1e-2
+    # and against an fp32 torch reference of the composite (BN train backward through ReLU)
+    g = da.float() * ((y.float() * ss + (beta - mean * ss)) > 0)
+    xh = (y.float() - mean) * inv
+    exact_db, exact_dg = g.sum((0, 1, 2)), (g * xh).sum((0, 1, 2))
+    assert relerr(db, exact_db) < 1e-3 and relerr(dg, exact_dg) < 1e-3
+    dy_exact = gamma * inv * (g - exact_db / M - xh * exact_dg / M)
+    assert relerr(dy, dy_exact) < 1e-2
