@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--impl", choices=["native", "eager"], default="native")
     p.add_argument("--decoder", choices=["bilinear", "transposed"], default="bilinear")
-    p.add_argument("--graph", type=int, default=1, help="capture the native step in a hipGraph")
+    p.add_argument("--graph", type=int, default=-1,
+                   help="capture the native step in a hipGraph (1), eager launches (0), -1: auto by batch size")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--loss", choices=["bce", "bce_dice"], default="bce")
     p.add_argument("--serve", type=int, default=-1,
@@ -113,7 +114,7 @@ def make_eager_step(args, dev, world):
 def make_native_step(args, dev, world):
     from robotic_discovery_platform_amd.train.engine import build_bench_step
     return build_bench_step(batch=args.batch, size=args.size, decoder=args.decoder, device=dev,
-                            world=world, graph=bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss)
+                            world=world, graph="auto" if args.graph < 0 else bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss)
 
 
 class _Progress:
@@ -136,6 +137,8 @@ def main():
     args = parse()
     rank, world, dev = setup_dist(args)
     step = make_eager_step(args, dev, world) if args.impl == "eager" else make_native_step(args, dev, world)
+    tr = getattr(step, "trainer", None)
+    used_graph = bool(tr.use_graph) if tr is not None else False
     progress = _Progress(rank)  # stderr heartbeat: first eager steps can spend minutes in MIOpen kernel builds
     for i in range(args.warmup):
         progress.phase = f"warmup step {i + 1}/{args.warmup}"
@@ -186,7 +189,7 @@ def main():
                 "impl": args.impl,
                 "optimizer": "Adam(lr=1e-4)",
                 "loss": args.loss,
-                "hipgraph": bool(args.graph) if args.impl == "native" else False,
+                "hipgraph": used_graph,
             },
             "baseline_note": "vs_baseline = value / 2.14 img/s (BASELINE.md: reference bs4 fp32 on CPU; "
                              "no published GPU number exists)",

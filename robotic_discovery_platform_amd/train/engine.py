@@ -4,11 +4,19 @@ Both implement the reference step (``/root/reference/scripts/train_segmenter.py:
 zero_grad -> forward -> BCEWithLogits (optionally + Dice) -> backward -> Adam(lr 1e-4), and
 optionally DDP over RCCL with flat-buffer gradient buckets (``parallel/ddp.py``).
 
-``NativeTrainer`` runs everything on the hand-written gfx950 kernels. On a single GPU the whole
-step (forward + backward + Adam + weight re-layout) is captured once into a hipGraph
-(``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replayed: ~250 launches become one graph
-launch, so the step is never host-bound. With world > 1 the step runs as eager launches so the
-bucketed all-reduces can overlap backward on RCCL's stream (RCCL calls are not captured).
+``NativeTrainer`` runs everything on the hand-written gfx950 kernels, as eager launches of ~220
+kernels per step on two streams (main: forward, dgrad, BN backward; side: weight gradients). The
+whole step (forward + backward + Adam + weight re-layout) can instead be captured once into a
+hipGraph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm; ``graph=True``) and replayed, but measured
+on MI355X the replay is slower at every batch size (img/s eager vs graph: bs4 1369 vs 1189, bs16
+2308 vs 2225, bs32 2607 vs 2525, bs64 2710 vs 2664): the replayed graph spreads the wgrad side
+branch over two extra hardware queues, and the extra contention slows the critical-path main
+stream, while ~10 us of host time per launch stays ahead of the GPU even at bs 4. ``graph="auto"``
+therefore means eager launches for training; serving (N=1, latency-bound) keeps its graphs.
+With world > 1 the bucketed all-reduces overlap backward on RCCL's stream.
+
+``RDP_MAIN_PRIO=1`` runs the step on a high-priority stream (side stream at normal priority);
+measured neutral at bs 64 (2710 vs 2715 img/s), so off by default.
 
 ``EagerTrainer`` is the reference execution model (torch autograd + MIOpen) used for the CPU path,
 CPU/gloo DDP tests and as the measured comparison baseline.
@@ -16,6 +24,7 @@ CPU/gloo DDP tests and as the measured comparison baseline.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Optional
 
 import torch
@@ -28,8 +37,12 @@ from ..utils import trace
 
 
 class NativeTrainer:
+    # per-GPU pixels per step at or below which the step is graph-captured in "auto" mode
+    # (0: never -- eager launches measured faster at every batch, see the module docstring)
+    GRAPH_AUTO_MAX_PIXELS = 0
+
     def __init__(self, model: UNetNative, batch: int, h: int, w: int, lr: float = 1e-4, loss: str = "bce",
-                 dice_weight: float = 1.0, graph: bool = True, bucket_mb: float = 16.0):
+                 dice_weight: float = 1.0, graph="auto", bucket_mb: float = 16.0):
         self.model = model
         self.ex = model.executor(batch, h, w, training=True, loss=loss, dice_weight=dice_weight)
         self.opt = NativeAdam(model, lr=lr)
@@ -42,8 +55,16 @@ class NativeTrainer:
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
             self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb)
             self._layer_params = {sp.name: sp.param_names() for sp in list(model.specs) + list(model.up_specs)}
-        self.use_graph = graph and self.world == 1 and torch.cuda.is_available()
+        if graph == "auto":
+            graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
+        self.use_graph = bool(graph) and self.world == 1 and torch.cuda.is_available()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.stream = None
+        if torch.cuda.is_available() and model.store.device.type == "cuda" and \
+                os.environ.get("RDP_MAIN_PRIO", "0") != "0":
+            lo, hi = torch.cuda.Stream.priority_range()
+            if hi != lo:
+                self.stream = torch.cuda.Stream(device=model.store.device, priority=hi)
         self.steps = 0
 
     def _hook(self, spec):
@@ -87,6 +108,12 @@ class NativeTrainer:
                 torch.cuda.current_stream().wait_stream(s)
                 self.graph = g
             self.graph.replay()
+        elif self.stream is not None:
+            cur = torch.cuda.current_stream()
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                self._step_body()
+            cur.wait_stream(self.stream)
         else:
             self._step_body()
         self.steps += 1
