@@ -39,7 +39,8 @@ int rdp_bn_relu_apply_pool(const void*, int, void*, int, void*, int, const float
 int rdp_maxpool2_bwd_bn_reduce(const void*, int, const void*, int, const void*, int, void*, int, const void*, int,
                                const float*, int, int, int, int, float*, int, hipStream_t);
 int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
-int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, const void*, int,
+                      const float*, float*, int, hipStream_t);
 int rdp_upT_shuffle(const void*, int, const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_upT_unshuffle(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_colsum_bf16(const void*, int, long, int, int, float*, float*, int, hipStream_t);
@@ -286,15 +287,37 @@ int maxpool2_bwd_bn_reduce(torch::Tensor dp, torch::Tensor x, c10::optional<torc
 void upsample2_fwd(torch::Tensor x, torch::Tensor out, int oy, int ox) {
   Act a = act(x, "x"), o = act(out, "out");
   TORCH_CHECK(o.N == a.N && o.C == a.C, "upsample shape");
+  TORCH_CHECK(2 * a.H + oy <= o.H && 2 * a.W + ox <= o.W && oy >= 0 && ox >= 0, "upsample fwd placement");
   TORCH_CHECK(rdp_upsample2_fwd(a.ptr, a.pitch, o.ptr, o.pitch, a.N, a.H, a.W, o.H, o.W, oy, ox, a.C, cur_stream()) == 0,
-              "upsample fwd");
+              "upsample fwd: channels must be 2^k in [8, 2048], pitches multiples of 8");
 }
 
-void upsample2_bwd(torch::Tensor dout, torch::Tensor dx, int oy, int ox) {
-  Act d = act(dout, "dout"), o = act(dx, "dx");
+// y/coef/partial (optional): also accumulate the training-BN backward reduction of dx's BN (dx = da of
+// the layer whose pre-BN output is y); returns the partial row count (0 without the fusion)
+int upsample2_bwd(torch::Tensor dout, torch::Tensor dx, int oy, int ox, c10::optional<torch::Tensor> y,
+                  c10::optional<torch::Tensor> coef, c10::optional<torch::Tensor> partial) {
+  Act d = act(dout, "dout"), o = act(dx, "dx"), yy;
   TORCH_CHECK(o.N == d.N && o.C == d.C, "upsample bwd shape");
-  TORCH_CHECK(rdp_upsample2_bwd(d.ptr, d.pitch, o.ptr, o.pitch, o.N, o.H, o.W, d.H, d.W, oy, ox, o.C, cur_stream()) == 0,
-              "upsample bwd");
+  TORCH_CHECK(2 * o.H + oy <= d.H && 2 * o.W + ox <= d.W && oy >= 0 && ox >= 0, "upsample bwd placement");
+  const float* cf = nullptr;
+  float* pp = nullptr;
+  int maxb = 0;
+  if (y) {
+    TORCH_CHECK(coef && partial, "upsample2_bwd: y needs coef and partial");
+    yy = act(*y, "y");
+    TORCH_CHECK(yy.N == o.N && yy.H == o.H && yy.W == o.W && yy.C == o.C, "upsample bwd y shape");
+    check_f32(*coef, "coef");
+    check_f32(*partial, "partial");
+    TORCH_CHECK(coef->numel() >= 4 * o.C, "coef");
+    maxb = std::min<long>(partial->numel() / (2 * o.C), 4096);
+    TORCH_CHECK(maxb >= 1, "partial too small");
+    cf = coef->data_ptr<float>();
+    pp = partial->data_ptr<float>();
+  }
+  const int T = rdp_upsample2_bwd(d.ptr, d.pitch, o.ptr, o.pitch, o.N, o.H, o.W, d.H, d.W, oy, ox, o.C,
+                                  y ? yy.ptr : nullptr, y ? yy.pitch : 0, cf, pp, maxb, cur_stream());
+  TORCH_CHECK(T >= 0, "upsample2_bwd: channels must be 2^k in [8, 2048], pitches multiples of 8");
+  return T;
 }
 
 // ConvTranspose2d(2, s2): yT [N,h,w,4C] (+bias) -> u [N,H2,W2,C] at offset (oy, ox), zero elsewhere
@@ -549,7 +572,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("upT_shuffle", &upT_shuffle);
   m.def("upT_unshuffle", &upT_unshuffle);
   m.def("colsum_bf16", &colsum_bf16);
-  m.def("upsample2_bwd", &upsample2_bwd);
+  m.def("upsample2_bwd", &upsample2_bwd, py::arg("dout"), py::arg("dx"), py::arg("oy"), py::arg("ox"),
+        py::arg("y") = py::none(), py::arg("coef") = py::none(), py::arg("partial") = py::none());
   m.def("head_partial_blocks", &head_partial_blocks);
   m.def("head_fwd", &head_fwd, py::arg("a"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("logits"),
         py::arg("partial"), py::arg("sums"), py::arg("loss"), py::arg("dice_w"), py::arg("dice_eps"),

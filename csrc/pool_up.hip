@@ -280,17 +280,21 @@ RDP_DEV void up_src(int u, int in, float r, int& i0, int& i1, float& l1) {
   l1 = s - (float)i0;
 }
 
-__global__ void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch, u16* __restrict__ out, int opitch,
-                                     UpGeom g) {
-  const int CG = g.C >> 3;
-  const long total = (long)g.N * g.Hout * g.Wout * CG;
-  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
-    const int cg = it % CG;
-    const long po = it / CG;
-    const int X = po % g.Wout;
-    const long t = po / g.Wout;
-    const int Y = t % g.Hout, n = t / g.Hout;
-    const int c = cg * 8;
+// Row-blocked bilinear x2 (align_corners=True). One work item = one output (fwd) / input-gradient
+// (bwd) image row segment of 256 (pixel, 8-channel group) pairs: the row's source rows and weights
+// are block-uniform (scalar), channel groups are a power of two, so the per-thread indexing is shifts
+// and masks (no 64-bit division), and every access is a 16-B, line-coalesced vector.
+__global__ __launch_bounds__(256) void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch,
+                                                            u16* __restrict__ out, int opitch, UpGeom g, int lcg,
+                                                            int nchunk) {
+  const int CG = 1 << lcg;
+  const int items = g.N * g.Hout * nchunk;
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int row = it / nchunk, q = it - row * nchunk;
+    const int n = row / g.Hout, Y = row - n * g.Hout;
+    const int t = q * 256 + threadIdx.x;
+    const int X = t >> lcg, c = (t & (CG - 1)) * 8;
+    if (X >= g.Wout) continue;
     const int uy = Y - g.oy, ux = X - g.ox;
     float o[8];
     if (uy < 0 || ux < 0 || uy >= 2 * g.hin || ux >= 2 * g.win) {
@@ -311,7 +315,7 @@ __global__ void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch, u16*
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = hy * (hx * a[k] + lx * b[k]) + ly * (hx * cc[k] + lx * d[k]);
     }
-    *(uint4*)(out + po * opitch + c) = pack8f(o);
+    *(uint4*)(out + ((long)row * g.Wout + X) * opitch + c) = pack8f(o);
   }
 }
 
@@ -322,43 +326,103 @@ RDP_DEV float up_weight(int u, int in, float r, int i) {
   return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
 }
 
-__global__ void upsample2_bwd_kernel(const u16* __restrict__ dout, int dpitch, u16* __restrict__ dx, int xpitch,
-                                     UpGeom g) {
-  const int CG = g.C >> 3;
-  const long total = (long)g.N * g.hin * g.win * CG;
+// dx[n][i][j] = sum_{uy,ux} w(uy,i) w(ux,j) dout[n][uy+oy][ux+ox]. With r = (in-1)/(2in-1) < 1/2,
+// a nonzero w(u,i) needs floor(u*r) in {i-1, i}, which holds only for u in [2i-1, 2i+2]: a fixed
+// 4x4 window. All 16 taps are loaded unconditionally (clamped address, weight 0 when the tap is
+// outside the image or the window) so the loads issue back to back; the row weights are
+// block-uniform. Taps are summed in ascending (uy, ux) order like a plain gather.
+// BNR: the consumer's training-BN backward reduction of g = bf16(dx) * relu'(y*scale+shift) is
+// accumulated on the fly (bn_relu_bwd_reduce layout, one partial row per block), so dx is never
+// re-read for it.
+template <bool BNR>
+__global__ __launch_bounds__(256) void upsample2_bwd_kernel(const u16* __restrict__ dout, int dpitch,
+                                                            u16* __restrict__ dx, int xpitch, UpGeom g, int lcg,
+                                                            int nchunk, const u16* __restrict__ y, int ypitch,
+                                                            const float* __restrict__ coef,
+                                                            float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // BNR: [256 / CG][C][2]
+  const int CG = 1 << lcg;
   const int uh = 2 * g.hin, uw = 2 * g.win;
-  for (long it = blockIdx.x * (long)blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
-    const int cg = it % CG;
-    const long pi = it / CG;
-    const int j = pi % g.win;
-    const long t = pi / g.win;
-    const int i = t % g.hin, n = t / g.hin;
-    const int c = cg * 8;
-    // candidate u ranges: floor(u*r) in {i-1, i}
-    int ylo = 0, yhi = uh - 1, xlo = 0, xhi = uw - 1;
-    if (g.rh > 0.f) { ylo = max(0, (int)floorf((i - 1) / g.rh) - 1); yhi = min(uh - 1, (int)ceilf((i + 1) / g.rh) + 1); }
-    if (g.rw > 0.f) { xlo = max(0, (int)floorf((j - 1) / g.rw) - 1); xhi = min(uw - 1, (int)ceilf((j + 1) / g.rw) + 1); }
+  const int c = (threadIdx.x & (CG - 1)) * 8;
+  float mean[8], inv[8], ss[8], hh[8], sg[8], sgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sg[k] = 0.f;
+    sgx[k] = 0.f;
+    if (BNR) {
+      mean[k] = coef[c + k];
+      inv[k] = coef[g.C + c + k];
+      ss[k] = coef[2 * g.C + c + k];
+      hh[k] = coef[3 * g.C + c + k];
+    }
+  }
+  const int items = g.N * g.hin * nchunk;
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int row = it / nchunk, q = it - row * nchunk;
+    const int n = row / g.hin, i = row - n * g.hin;
+    const int j = (q * 256 + threadIdx.x) >> lcg;
+    if (j >= g.win) continue;
+    float wy[4], wx[4];
+    long ro[4];
+    int xo[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int uy = 2 * i - 1 + t, ux = 2 * j - 1 + t;
+      const int Y = uy + g.oy, X = ux + g.ox;
+      const bool oky = uy >= 0 && uy < uh && Y >= 0 && Y < g.Hout;
+      const bool okx = ux >= 0 && ux < uw && X >= 0 && X < g.Wout;
+      wy[t] = oky ? up_weight(uy, g.hin, g.rh, i) : 0.f;
+      wx[t] = okx ? up_weight(ux, g.win, g.rw, j) : 0.f;
+      ro[t] = ((long)n * g.Hout + (oky ? Y : 0)) * g.Wout;
+      xo[t] = okx ? X : 0;
+    }
+    uint4 v[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) v[a][b] = *(const uint4*)(dout + (ro[a] + xo[b]) * dpitch + c);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    for (int uy = ylo; uy <= yhi; ++uy) {
-      const int Y = uy + g.oy;
-      if (Y < 0 || Y >= g.Hout) continue;
-      const float wy = up_weight(uy, g.hin, g.rh, i);
-      if (wy == 0.f) continue;
-      for (int ux = xlo; ux <= xhi; ++ux) {
-        const int X = ux + g.ox;
-        if (X < 0 || X >= g.Wout) continue;
-        const float wx = up_weight(ux, g.win, g.rw, j);
-        if (wx == 0.f) continue;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float w = wy[a] * wx[b];
         float d[8];
-        unpack8f(*(const uint4*)(dout + (((long)n * g.Hout + Y) * g.Wout + X) * dpitch + c), d);
-        const float w = wy * wx;
+        unpack8f(v[a][b], d);
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, d[k], acc[k]);
       }
+    const long p = (long)row * g.win + j;
+    const uint4 o = pack8f(acc);
+    *(uint4*)(dx + p * xpitch + c) = o;
+    if (BNR) {
+      float fg[8], fy[8];
+      unpack8f(o, fg);
+      unpack8f(*(const uint4*)(y + p * ypitch + c), fy);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = fmaf(fy[k], ss[k], hh[k]) > 0.f ? fg[k] : 0.f;
+        sg[k] += gg;
+        sgx[k] += gg * (fy[k] - mean[k]) * inv[k];
+      }
     }
-    *(uint4*)(dx + pi * xpitch + c) = pack8f(acc);
+  }
+  if (BNR) {
+    const int RPB = 256 >> lcg, r = threadIdx.x >> lcg;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sred[(r * g.C + c + k) * 2] = sg[k];
+      sred[(r * g.C + c + k) * 2 + 1] = sgx[k];
+    }
+    __syncthreads();
+    for (int cc = threadIdx.x; cc < g.C; cc += 256) {
+      float a0 = 0.f, a1 = 0.f;
+      for (int qq = 0; qq < RPB; ++qq) { a0 += sred[(qq * g.C + cc) * 2]; a1 += sred[(qq * g.C + cc) * 2 + 1]; }
+      partial[(size_t)blockIdx.x * 2 * g.C + cc] = a0;
+      partial[(size_t)blockIdx.x * 2 * g.C + g.C + cc] = a1;
+    }
   }
 }
 
@@ -501,20 +565,40 @@ int rdp_maxpool2_bwd_bn_reduce(const void* dp, int dppitch, const void* x, int x
                      N, H, W, C, partial);
   return grid;
 }
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
 int rdp_upsample2_fwd(const void* x, int xpitch, void* out, int opitch, int N, int hin, int win, int Hout, int Wout,
                       int oy, int ox, int C, hipStream_t s) {
-  if (C % 8) return -1;
+  if (!pow2c(C) || xpitch % 8 || opitch % 8) return -1;
   UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
-  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(gridN((long)N * Hout * Wout * (C / 8))), dim3(256), 0, s,
-                     (const u16*)x, xpitch, (u16*)out, opitch, g);
+  const int lcg = ilog2(C / 8), nchunk = (int)(((long)Wout * (C / 8) + 255) / 256);
+  const long items = (long)N * Hout * nchunk;
+  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3((int)std::min<long>(items, 8192)), dim3(256), 0, s, (const u16*)x,
+                     xpitch, (u16*)out, opitch, g, lcg, nchunk);
   return 0;
 }
+// y/coef/partial given: fused BN-backward reduction of dx's consumer BN; returns the partial rows
+// written (<= max_blocks). Otherwise returns 0.
 int rdp_upsample2_bwd(const void* dout, int dpitch, void* dx, int xpitch, int N, int hin, int win, int Hout, int Wout,
-                      int oy, int ox, int C, hipStream_t s) {
-  if (C % 8) return -1;
+                      int oy, int ox, int C, const void* y, int ypitch, const float* coef, float* partial,
+                      int max_blocks, hipStream_t s) {
+  if (!pow2c(C) || dpitch % 8 || xpitch % 8 || (y && ypitch % 8)) return -1;
   UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
-  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(gridN((long)N * hin * win * (C / 8))), dim3(256), 0, s,
-                     (const u16*)dout, dpitch, (u16*)dx, xpitch, g);
+  const int lcg = ilog2(C / 8), nchunk = (int)(((long)win * (C / 8) + 255) / 256);
+  const long items = (long)N * hin * nchunk;
+  if (y) {
+    const int grid = (int)std::max<long>(1, std::min<long>(items, max_blocks));
+    const size_t lds = (size_t)(256 / (C / 8)) * C * 2 * sizeof(float);
+    hipLaunchKernelGGL(upsample2_bwd_kernel<true>, dim3(grid), dim3(256), lds, s, (const u16*)dout, dpitch, (u16*)dx,
+                       xpitch, g, lcg, nchunk, (const u16*)y, ypitch, coef, partial);
+    return grid;
+  }
+  hipLaunchKernelGGL(upsample2_bwd_kernel<false>, dim3((int)std::min<long>(items, 8192)), dim3(256), 0, s,
+                     (const u16*)dout, dpitch, (u16*)dx, xpitch, g, lcg, nchunk, (const u16*)nullptr, 0,
+                     (const float*)nullptr, (float*)nullptr);
   return 0;
 }
 int rdp_upT_shuffle(const void* yT, int ypitch, const float* bias, void* u, int upitch, int N, int h, int w, int H2,

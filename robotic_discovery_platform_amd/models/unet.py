@@ -304,7 +304,8 @@ class UNetExecutor:
         dev = model.store.device
         self.dev = dev
         # BN apply + maxpool (forward) and maxpool backward + BN reduce (backward) in one pass each at
-        # the Down boundaries (RDP_FUSE_POOL=0: separate kernels, for A/B measurements)
+        # the Down boundaries, upsample backward + BN reduce at the Up boundaries (RDP_FUSE_POOL=0:
+        # separate kernels, for A/B measurements)
         self.fuse_pool = os.environ.get("RDP_FUSE_POOL", "1") != "0"
         # training: the 1x1 head applies the last conv's BN+ReLU itself (forward) and produces that BN's
         # backward partials and dy from the logits (backward), so the 64-ch activation and its gradient
@@ -643,7 +644,11 @@ class UNetExecutor:
             oy = (du.shape[1] - 2 * low_layer.a.shape[1]) // 2
             ox = (du.shape[2] - 2 * low_layer.a.shape[2]) // 2
             if self.m.bilinear:
-                C.upsample2_bwd(du, low_layer.da, oy, ox)
+                if self.fuse_pool:  # + the BN-backward reduction of low_layer (like the pool boundary)
+                    low_layer.bwd_rows = C.upsample2_bwd(du, low_layer.da, oy, ox, low_layer.y, low_layer.coef,
+                                                         self.bn_partial)
+                else:
+                    C.upsample2_bwd(du, low_layer.da, oy, ox)
             else:
                 us = self.m.up_specs[i - 1]
                 dyT = self.dyTs[i - 1]

@@ -278,6 +278,20 @@ def test_upsample_fwd_bwd(C, hin, win, H2, W2):
     dx = torch.empty_like(x)
     C.upsample2_bwd(nhwc(g), dx, dY // 2, dX // 2)
     assert relerr(nchw(dx), xr.grad) < 1e-2
+    # fused with the BN-backward reduction of dx's BN (dx = da of the layer with pre-BN output y)
+    y = bf(torch.randn(N, hin, win, Ch, device=dev) * 2 + 0.3)
+    mean, inv = torch.randn(Ch, device=dev) * 0.1, torch.rand(Ch, device=dev) + 0.5
+    gamma, beta = torch.randn(Ch, device=dev), torch.randn(Ch, device=dev) * 0.2
+    ss = gamma * inv
+    coef = torch.cat([mean, inv, ss, beta - mean * ss]).contiguous()
+    part = torch.zeros(64 * 2 * Ch, device=dev)
+    dx2 = torch.empty_like(x)
+    T = C.upsample2_bwd(nhwc(g), dx2, dY // 2, dX // 2, y, coef, part)
+    assert 1 <= T <= 64 and torch.equal(dx2, dx)
+    got = part[:T * 2 * Ch].view(T, 2, Ch).double().sum(0)
+    gg = dx.float() * ((y.float() * ss + (beta - mean * ss)) > 0)
+    exact = torch.stack([gg.sum((0, 1, 2)), (gg * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
+    assert torch.allclose(got, exact, rtol=1e-3, atol=1e-3)
 
 
 @pytest.mark.parametrize("dice_w", [0.0, 1.0])
