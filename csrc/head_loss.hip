@@ -14,6 +14,7 @@
 #include <algorithm>
 
 #define HEAD_C 64
+#define HPX 4  // pixels in flight per 8-lane group in the streaming head kernels
 
 RDP_DEV void unpack8h(const uint4& v, float* f) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -71,12 +72,27 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const u16* __restrict__ a
   }
   const float bias = b[0];
   float sb = 0.f, si = 0.f, sp = 0.f, st = 0.f;
-  const long groups_per_iter = (long)gridDim.x * 32;  // 32 pixels per block-iteration
-  for (long p = blockIdx.x * 32l + (threadIdx.x >> 3); p < M; p += groups_per_iter) {
-    uint4 v = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
-    if (BN) v = bn_relu8(v, ss, hh);
-    const float x = sum8lanes(dot8(v, wl)) + bias;
-    if (sub == 0) {
+  // HPX pixels in flight per 8-lane group (16-B loads issued back to back)
+  const long stride = (long)gridDim.x * 32;  // 32 pixel groups per block
+  for (long p0 = blockIdx.x * 32l + (threadIdx.x >> 3); p0 < M; p0 += stride * HPX) {
+    uint4 v[HPX];
+#pragma unroll
+    for (int u = 0; u < HPX; ++u) {
+      const long p = p0 + u * stride;
+      if (p < M) v[u] = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+    }
+    float xs[HPX];
+#pragma unroll
+    for (int u = 0; u < HPX; ++u) xs[u] = dot8(BN ? bn_relu8(v[u], ss, hh) : v[u], wl);  // (garbage if p >= M)
+#pragma unroll
+    for (int u = 0; u < HPX; ++u) xs[u] = sum8lanes(xs[u]);
+    // every lane of the group now holds the HPX logits: lane `sub` finishes pixel `sub`
+    float x = xs[0];
+#pragma unroll
+    for (int u = 1; u < HPX; ++u) x = sub == u ? xs[u] : x;
+    x += bias;
+    const long p = p0 + sub * stride;
+    if (sub < HPX && p < M) {
       logits[p] = x;
       const float t = target[p];
       const float e = __expf(-fabsf(x));
@@ -172,34 +188,51 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
   float gw[8], sg[8], sgx[8], gb = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) { gw[k] = 0.f; sg[k] = 0.f; sgx[k] = 0.f; }
-  for (long p = blockIdx.x * 32l + (threadIdx.x >> 3); p < M; p += (long)gridDim.x * 32) {
-    const float dx = head_dlogit(logits[p], target[p], invM, dice_w, I, den, dice_eps, gscale);
-    const uint4 vy = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
-    float f[8];
-    if (BN) {
-      float fy[8];
-      unpack8h(vy, fy);
+  const long stride = (long)gridDim.x * 32;
+  for (long p0 = blockIdx.x * 32l + (threadIdx.x >> 3); p0 < M; p0 += stride * HPX) {
+    uint4 vq[HPX];
+    float xq[HPX], tq[HPX];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float z = fmaf(fy[k], ss[k], hh[k]);
-        f[k] = bfround(fmaxf(z, 0.f));  // the activation the forward head consumed
-        const float g = z > 0.f ? bfround(dx * wl[k]) : 0.f;
-        sg[k] += g;
-        sgx[k] += g * (fy[k] - mu[k]) * iv[k];
+    for (int u = 0; u < HPX; ++u) {
+      const long p = p0 + u * stride;
+      if (p < M) {
+        vq[u] = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+        xq[u] = logits[p];
+        tq[u] = target[p];
       }
-    } else {
-      unpack8h(vy, f);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) gw[k] = fmaf(dx, f[k], gw[k]);
-    if (sub == 0) gb += dx;
-    if (!BN) {
-      uint4 o;
-      o.x = pack2bf(dx * wl[0], dx * wl[1]);
-      o.y = pack2bf(dx * wl[2], dx * wl[3]);
-      o.z = pack2bf(dx * wl[4], dx * wl[5]);
-      o.w = pack2bf(dx * wl[6], dx * wl[7]);
-      *(uint4*)(da + (size_t)p * dapitch + sub * 8) = o;
+    for (int u = 0; u < HPX; ++u) {
+      const long p = p0 + u * stride;
+      if (p >= M) break;
+      const float dx = head_dlogit(xq[u], tq[u], invM, dice_w, I, den, dice_eps, gscale);
+      const uint4 vy = vq[u];
+      float f[8];
+      if (BN) {
+        float fy[8];
+        unpack8h(vy, fy);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = fmaf(fy[k], ss[k], hh[k]);
+          f[k] = bfround(fmaxf(z, 0.f));  // the activation the forward head consumed
+          const float g = z > 0.f ? bfround(dx * wl[k]) : 0.f;
+          sg[k] += g;
+          sgx[k] += g * (fy[k] - mu[k]) * iv[k];
+        }
+      } else {
+        unpack8h(vy, f);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gw[k] = fmaf(dx, f[k], gw[k]);
+      if (sub == 0) gb += dx;
+      if (!BN) {
+        uint4 o;
+        o.x = pack2bf(dx * wl[0], dx * wl[1]);
+        o.y = pack2bf(dx * wl[2], dx * wl[3]);
+        o.z = pack2bf(dx * wl[4], dx * wl[5]);
+        o.w = pack2bf(dx * wl[6], dx * wl[7]);
+        *(uint4*)(da + (size_t)p * dapitch + sub * 8) = o;
+      }
     }
   }
   // reduce over the 8 pixel-groups of the wave that share `sub`

@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export RDP_NO_BUILD=1
 R=$GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "upsample" > gpurun_out/t_f.log 2>&1 || { tail -30 gpurun_out/t_f.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "upsample or head" > gpurun_out/t_f.log 2>&1 || { tail -30 gpurun_out/t_f.log; exit 1; }
 tail -1 gpurun_out/t_f.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_unet_native_gpu.py > gpurun_out/t_u.log 2>&1 || { tail -30 gpurun_out/t_u.log; exit 1; }
 tail -1 gpurun_out/t_u.log
