@@ -211,17 +211,56 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_bin_scatter_kernel(const int*
   }
 }
 
+// Digit selection over a 256-bucket histogram by wave 0 (4 buckets per lane + a wave scan), instead
+// of a serial walk by one thread. LARGEST = true: the largest digit d with #(digit >= d) >= need;
+// false: the smallest d with #(digit <= d) >= need. Lane owning d stores d, the remaining need and
+// the bucket count hist[d] (the number of candidates equal to the new prefix).
+template <bool LARGEST>
+RDP_DEV void geo_pick_digit(const unsigned* hist, int need, int* s_digit, int* s_need, int* s_eq) {
+  const int l = threadIdx.x;  // wave 0 only
+  int h[4], tot = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { h[j] = (int)hist[4 * l + j]; tot += h[j]; }
+  int sc = tot;  // LARGEST: inclusive suffix sum over lanes >= l; else inclusive prefix over lanes <= l
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = LARGEST ? __shfl_down(sc, off, 64) : __shfl_up(sc, off, 64);
+    if (LARGEST ? l + off < 64 : l >= off) sc += o;
+  }
+  const int before = sc - tot;  // candidates strictly beyond this lane's buckets (in scan order)
+  if (before < need && need <= sc) {
+    int acc = before;
+    if (LARGEST) {
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        if (acc + h[j] >= need) { *s_digit = 4 * l + j; *s_need = need - acc; *s_eq = h[j]; break; }
+        acc += h[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (acc + h[j] >= need) { *s_digit = 4 * l + j; *s_need = need - acc; *s_eq = h[j]; break; }
+        acc += h[j];
+      }
+    }
+  }
+}
+
 // One workgroup per bin, over that bin's points only. out: [nbins][kcap][4]; kout[b] = k written.
-// k = max(1, int(n_b * top)) largest y; ties at the k-th value go to the smallest point indices
-// (= the reference's stable descending sort), found by a second radix select on the index.
+// Per-bin top-k by y (k = max(1, int(n_bin * top)), capped); ties at the k-th value go to the
+// smallest point indices (= the reference's stable descending sort): radix select (8 x 8 bits, MSB first) of the k-th largest y key, then -- only
+// when the ties at that key are not all taken -- radix select (4 x 8 bits) of the largest index
+// among the ties to keep. The bin's keys and ids are cached in LDS (up to GEO_LCAP points; larger
+// bins read the excess from global memory), so each pass is LDS traffic + one histogram.
+#define GEO_LCAP 4096
 __global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* __restrict__ pts,
                                                                  const int* __restrict__ npts_p, int nbins,
                                                                  double top, GeoBins gb, double* __restrict__ out,
                                                                  int kcap, int* __restrict__ kout, int min_points) {
   __shared__ unsigned hist[256];
-  __shared__ uint64_t s_prefix;
-  __shared__ int s_need;
-  __shared__ int s_cnt;
+  __shared__ uint64_t skey[GEO_LCAP];
+  __shared__ int sid[GEO_LCAP];
+  __shared__ int s_digit, s_need, s_eq, s_cnt;
   const int bin = blockIdx.x;
   const int n = npts_p[0];
   const int nb = gb.cnt[bin];
@@ -235,67 +274,62 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* _
   int k = (int)((double)nb * top);
   if (k < 1) k = 1;
   if (k > kcap) k = kcap;
-  // 1) radix select (8 x 8 bits, MSB first) of the k-th largest y key in the bin
-  if (threadIdx.x == 0) { s_prefix = 0; s_need = k; }
-  __syncthreads();
+  for (int i = threadIdx.x; i < nb && i < GEO_LCAP; i += GEO_THREADS) {
+    const int id = ids[i];
+    sid[i] = id;
+    skey[i] = dkey(pts[(size_t)id * 4 + 1]);
+  }
+  auto key_at = [&](int i) -> uint64_t { return i < GEO_LCAP ? skey[i] : dkey(pts[(size_t)ids[i] * 4 + 1]); };
+  auto id_at = [&](int i) -> int { return i < GEO_LCAP ? sid[i] : ids[i]; };
+  // 1) k-th largest key
+  uint64_t prefix = 0;
+  int need = k, eq = 0;
   for (int pass = 0; pass < 8; ++pass) {
     const int shift = 56 - 8 * pass;
-    for (int i = threadIdx.x; i < 256; i += GEO_THREADS) hist[i] = 0;
+    hist[threadIdx.x] = 0;  // GEO_THREADS == 256
     __syncthreads();
-    const uint64_t prefix = s_prefix;
     const uint64_t pmask = pass == 0 ? 0ull : (~0ull << (64 - 8 * pass));
     for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
-      const uint64_t key = dkey(pts[(size_t)ids[i] * 4 + 1]);
+      const uint64_t key = key_at(i);
       if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int need = s_need, d = 255;
-      for (; d > 0; --d) {
-        if ((int)hist[d] >= need) break;
-        need -= hist[d];
-      }
-      s_need = need;
-      s_prefix = prefix | ((uint64_t)d << shift);
-    }
+    if (threadIdx.x < 64) geo_pick_digit<true>(hist, need, &s_digit, &s_need, &s_eq);
     __syncthreads();
+    prefix |= (uint64_t)s_digit << shift;
+    need = s_need;
+    eq = s_eq;
   }
-  const uint64_t kth = s_prefix;
-  const int need_eq = s_need;  // ties at kth to take, by smallest point index
-  // 2) radix select (4 x 8 bits) of the need_eq-th smallest index among the ties
-  if (threadIdx.x == 0) { s_prefix = 0; s_need = need_eq; }
-  __syncthreads();
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 24 - 8 * pass;
-    for (int i = threadIdx.x; i < 256; i += GEO_THREADS) hist[i] = 0;
-    __syncthreads();
-    const uint32_t prefix = (uint32_t)s_prefix;
-    const uint32_t pmask = pass == 0 ? 0u : (~0u << (32 - 8 * pass));
-    for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
-      const int id = ids[i];
-      if (dkey(pts[(size_t)id * 4 + 1]) == kth && ((uint32_t)id & pmask) == prefix)
-        atomicAdd(&hist[((uint32_t)id >> shift) & 255], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int need = s_need, d = 0;
-      for (; d < 255; ++d) {  // smallest digits first
-        if ((int)hist[d] >= need) break;
-        need -= hist[d];
+  const uint64_t kth = prefix;
+  // 2) ties at kth: take the `need` smallest indices (all of them when need == #ties)
+  uint32_t last_id = 0xffffffffu;
+  if (need < eq) {
+    uint32_t ip = 0;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      __syncthreads();
+      hist[threadIdx.x] = 0;
+      __syncthreads();
+      const uint32_t pmask = pass == 0 ? 0u : (~0u << (32 - 8 * pass));
+      for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
+        const uint32_t id = (uint32_t)id_at(i);
+        if (key_at(i) == kth && (id & pmask) == ip) atomicAdd(&hist[(id >> shift) & 255], 1u);
       }
-      s_need = need;
-      s_prefix = prefix | ((uint32_t)d << shift);
+      __syncthreads();
+      if (threadIdx.x < 64) geo_pick_digit<false>(hist, need, &s_digit, &s_need, &s_eq);
+      __syncthreads();
+      ip |= (uint32_t)s_digit << shift;
+      need = s_need;
     }
-    __syncthreads();
+    last_id = ip;
   }
-  const uint32_t last_id = (uint32_t)s_prefix;  // largest index among the selected ties
-  // 3) write: y key > kth, or == kth with index <= last_id (exactly k points)
+  // 3) write: key > kth, or == kth with index <= last_id (exactly k points)
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   double* ob = out + (size_t)bin * kcap * 4;
   for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
-    const int id = ids[i];
-    const uint64_t key = dkey(pts[(size_t)id * 4 + 1]);
+    const uint64_t key = key_at(i);
+    const int id = id_at(i);
     if (key > kth || (key == kth && (uint32_t)id <= last_id)) {
       const int o = atomicAdd(&s_cnt, 1);
       if (o < kcap)
