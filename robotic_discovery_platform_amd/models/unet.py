@@ -408,6 +408,12 @@ class UNetExecutor:
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
         self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
+        # Measured dead ends on this side stream (bs64, one MI355X): the whole step serialised on one
+        # stream is only ~0.5% slower (2801 vs 2816 img/s) -- the step is throughput-bound -- so
+        # (a) the skip half of each Up conv's input gradient moved here off the main stream's critical
+        # path was 1% SLOWER (2717 vs 2740; 4% at bs4), (b) a CU-masked side stream
+        # (hipExtStreamCreateWithCUMask, 25-87.5% of the CUs) was 8% slower, (c) a high-priority main
+        # stream was neutral. Removing work helps; moving it between streams does not.
         # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS)
         # (measured at bs32 with the side-stream overlap: 1024 -> 2025, 2048 -> 2086, 4096 -> 2068 img/s)
         self.wgrad_blocks = int(os.environ.get("RDP_WGRAD_BLOCKS", "2048"))
