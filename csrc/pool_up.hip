@@ -181,8 +181,10 @@ __global__ __launch_bounds__(256) void bn_relu_apply_pool_kernel(const u16* __re
 
 // dx = maxpool_bwd(dp) (+ dskip), then partial[blk] = [sum_g | sum_g*xhat] per channel with
 // g = dx * (y*scale + shift > 0), xhat = (y - mean) * invstd (bn_relu_bwd_reduce's partial format).
+// The pool's argmax comes from the activation recomputed from y (read anyway for the reduction), so
+// the stored activation is not read at all.
 __global__ __launch_bounds__(256) void maxpool2_bwd_bn_reduce_kernel(
-    const u16* __restrict__ dp, int dppitch, const u16* __restrict__ x, int xpitch, const u16* __restrict__ dskip,
+    const u16* __restrict__ dp, int dppitch, const u16* __restrict__ dskip,
     int dspitch, u16* __restrict__ dx, int dxpitch, const u16* __restrict__ y, int ypitch,
     const float* __restrict__ coef, int N, int H, int W, int C, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [rows][C][2]
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bn_reduce_kernel(
     const bool pooled = hc < Ho && wc < Wo;
     bool ok[4];
     long px[4];
-    uint4 vs[4], vy[4], vx[4], vd;
+    uint4 vs[4], vy[4], vd;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int h = 2 * hc + (q >> 1), w = 2 * wc + (q & 1);
@@ -214,16 +216,23 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bn_reduce_kernel(
       if (ok[q]) {
         vy[q] = *(const uint4*)(y + px[q] * ypitch + c);
         vs[q] = dskip ? *(const uint4*)(dskip + px[q] * dspitch + c) : make_uint4(0, 0, 0, 0);
-        if (pooled) vx[q] = *(const uint4*)(x + px[q] * xpitch + c);
       }
     }
     if (pooled) vd = *(const uint4*)(dp + (((long)n * Ho + hc) * Wo + wc) * dppitch + c);
     int idx[8];
     float d[8];
     if (pooled) {
+      // the forward pool's inputs, recomputed bit-exactly from y (bn_relu_apply_pool's arithmetic)
+      // instead of re-reading the stored activation
       float v[4][8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) unpack8f(vx[q], v[q]);
+      for (int q = 0; q < 4; ++q) {
+        float f[8];
+        unpack8f(vy[q], f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], ss[k], hh[k]), 0.f);
+        unpack8f(pack8f(f), v[q]);
+      }
       unpack8f(vd, d);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -552,6 +561,7 @@ int rdp_bn_relu_apply_pool(const void* y, int ypitch, void* a, int apitch, void*
   return 0;
 }
 // returns the number of partial rows written (T for bn_bwd_finalize), -1 if not applicable
+// x: the stored activation (pitch check only: the argmax is recomputed from y)
 int rdp_maxpool2_bwd_bn_reduce(const void* dp, int dppitch, const void* x, int xpitch, const void* dskip, int dspitch,
                                void* dx, int dxpitch, const void* y, int ypitch, const float* coef, int N, int H, int W,
                                int C, float* partial, int max_blocks, hipStream_t s) {
@@ -561,7 +571,7 @@ int rdp_maxpool2_bwd_bn_reduce(const void* dp, int dppitch, const void* x, int x
   const int grid = (int)std::max<long>(1, std::min<long>((nwin + 4 * rpb - 1) / (4 * rpb), max_blocks));
   const size_t lds = (size_t)rpb * C * 2 * sizeof(float);
   hipLaunchKernelGGL(maxpool2_bwd_bn_reduce_kernel, dim3(grid), dim3(256), lds, s, (const u16*)dp, dppitch,
-                     (const u16*)x, xpitch, (const u16*)dskip, dspitch, (u16*)dx, dxpitch, (const u16*)y, ypitch, coef,
+                     (const u16*)dskip, dspitch, (u16*)dx, dxpitch, (const u16*)y, ypitch, coef,
                      N, H, W, C, partial);
   return grid;
 }
