@@ -34,6 +34,10 @@ __global__ void colsum_kernel(const float* __restrict__ in, int T, int K, int rp
   if (ty == 0 && col < K) out[(size_t)blockIdx.y * K + col] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
+// Measured dead end: one launch per BN pass (each block reduces a row chunk, the last block to
+// arrive -- agent-scope fences + a system-scope counter -- runs the finalize) was 7% SLOWER at bs64
+// and 40% at bs4 than colsum + finalize: every block's release fence is a full per-XCD L2 writeback
+// (buffer_wbl2), far more than the ~6 us kernel boundary it saves.
 // reduce [T][K] rows to <= 64 rows in `ws` if needed; returns (pointer, rows)
 static const float* shrink_rows(const float* in, int T, int K, float* ws, int& rows, hipStream_t s) {
   if (T <= 64 || ws == nullptr) { rows = T; return in; }
