@@ -18,6 +18,7 @@ when a registry alias moves.
 """
 from __future__ import annotations
 
+import collections
 import logging
 import os
 import queue
@@ -116,7 +117,8 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         self._pool = futures.ThreadPoolExecutor(max_workers=decode_workers, thread_name_prefix="rdp-decode")
 
     def _decoded(self, request_iterator):
-        """Yield (t0, colour, depth) in request order; decoding runs ahead on the codec pool."""
+        """Yield (t0, colour, depth, more) in request order; decoding runs ahead on the codec pool.
+        ``more()`` tells whether the client has already sent the next frame."""
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         END = object()
 
@@ -140,7 +142,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             if item[3] is not None:
                 raise item[3]
             t, fc, fd, _ = item
-            yield t, fc.result(), fd.result()
+            yield t, fc.result(), fd.result(), lambda: q.qsize() > 0
 
     def close(self) -> None:
         """Stop the codec pool (its threads must not outlive the gRPC server at interpreter exit)."""
@@ -148,9 +150,22 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
 
     def analyze_frame(self, color: np.ndarray, depth: np.ndarray, t0: Optional[float] = None):
         t0 = time.perf_counter() if t0 is None else t0
+        resp, r = self._respond(self._process(color, depth), t0)
+        self._log(resp, r)
+        return resp
+
+    def _process(self, color: np.ndarray, depth: np.ndarray):
         if depth.dtype != np.uint16:
             depth = depth.astype(np.uint16)
-        r = self.engine.process(color, depth)
+        return self.engine.process(color, depth)
+
+    def _log(self, resp, r):
+        if self.metrics is not None:
+            self.metrics.write(resp.mean_curvature, resp.max_curvature, r.coverage)
+        self.frames += 1
+
+    def _respond(self, r, t0: float):
+        """FrameResult -> AnalysisResponse (PNG-encoded mask); runs on the codec pool when streaming."""
         c = r.curvature
         resp = pb.AnalysisResponse(mean_curvature=c.mean_curvature, max_curvature=c.max_curvature, status=c.status,
                                    mask_coverage=r.coverage)
@@ -158,19 +173,29 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             resp.spline_points.extend([pb.Point3D(x=p.x, y=p.y, z=p.z) for p in c.spline_points])
         resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1)
         resp.proc_time_ms = (time.perf_counter() - t0) * 1e3
-        if self.metrics is not None:
-            self.metrics.write(resp.mean_curvature, resp.max_curvature, r.coverage)
-        self.frames += 1
-        return resp
+        return resp, r
 
     def AnalyzeActuatorPerformance(self, request_iterator, context):
+        """Per-stream pipeline: decode (codec pool, runs ahead) -> engine (this thread, in order) ->
+        response encode (codec pool). Responses leave in request order; one that is ready -- or any,
+        when the client has not sent the next frame yet (lock-step clients) -- is never held back."""
         import grpc
         log.info("new analysis stream")
-        try:
-            for t0, color, depth in self._decoded(request_iterator):
-                with trace.range("serve.rpc.frame"):
-                    resp = self.analyze_frame(color, depth, t0)
+        inflight: "collections.deque" = collections.deque()
+
+        def ready(force: bool):
+            while inflight and (force or inflight[0].done() or len(inflight) > self.prefetch):
+                resp, r = inflight.popleft().result()
+                self._log(resp, r)
                 yield resp
+
+        try:
+            for t0, color, depth, more in self._decoded(request_iterator):
+                with trace.range("serve.rpc.frame"):
+                    r = self._process(color, depth)
+                inflight.append(self._pool.submit(self._respond, r, t0))
+                yield from ready(force=not more())
+            yield from ready(force=True)
         except Exception as e:
             log.error("unhandled exception during analysis: %s", e)
             context.set_code(grpc.StatusCode.INTERNAL)

@@ -1,9 +1,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export RDP_NO_BUILD=1
 R=$GRAFT_REPO_ROOT
-timeout -k 10 500 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
-cat gpurun_out/bench_default.json
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train -o train --output-format csv -- python3 $R/bench.py --batch 64 --steps 4 --warmup 3 --serve 0 > $R/gpurun_out/prof_train.log 2>&1 || { tail -20 $R/gpurun_out/prof_train.log; exit 1; }
-RDP_WGRAD_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/prof_serial -o serial --output-format csv -- python3 $R/bench.py --batch 64 --steps 4 --warmup 3 --serve 0 > $R/gpurun_out/prof_serial.log 2>&1 || { tail -20 $R/gpurun_out/prof_serial.log; exit 1; }
-PYTHONPATH=$R timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_serve -o serve --output-format csv -- python3 -m robotic_discovery_platform_amd.serve.bench_serve --frames 200 --warmup 20 --train-steps 20 > $R/gpurun_out/prof_serve.log 2>&1 || { tail -20 $R/gpurun_out/prof_serve.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_serve_gpu.py tests/test_serve_cpu.py > gpurun_out/t_s.log 2>&1 || { tail -30 gpurun_out/t_s.log; exit 1; }
+tail -1 gpurun_out/t_s.log
+for i in 1 2; do
+timeout -k 10 300 python -m robotic_discovery_platform_amd.serve.bench_serve > gpurun_out/serve.json 2> gpurun_out/serve.err || { tail -20 gpurun_out/serve.err; exit 1; }
+tail -1 gpurun_out/serve.json
+done
