@@ -186,6 +186,15 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
   // them in issue order, so stage g has landed once at most that many ops are outstanding (a plain
   // vmcnt(0) would also wait for the output stores of every tile before its next K step)
   int pend = 0;
+  // Training BN statistics accumulate over ALL of this block's tiles: with the persistent grid a
+  // multiple of tilesN (host-checked), block lid always has channel tile tn = lid % tilesN, so one
+  // slab row per (lid / tilesN, wm) -- grid * WAVES_M / tilesN rows instead of one per M-tile
+  // (65536 at 256^2 x 64 ch, bs 64), written once after the last tile.
+  float s1[NJ][4], s2[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
   for (int g = 0; g < total; ++g) {
     if (pend == 0 || !a.store_aware) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else if (pend == 2 * NJ) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NJ) : "memory");
@@ -240,11 +249,6 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
     const int tile = item;
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
-    float s1[NJ][4], s2[NJ][4];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
     // Widened stores: a lane holds 4 couts (16 j + 4 g + r, g = lane >> 4) of one pixel per
     // fragment. v_permlane16_swap of fragment pair (j, j+1) gives every lane 8 consecutive couts
     // (lanes g: 0 -> 0..7, 1 -> 16..23, 2 -> 8..15, 3 -> 24..31 of the pair) = one 16-B store, and a
@@ -293,26 +297,27 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
         bstore16(d2 ? ry2 : ry1, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
       }
     }
-    if (a.stats) {
-      // reduce over the 16 pixel lanes (lane & 15) sharing a channel group; one slab row per (tile, wm)
+    pend = 2 * NJ;  // 2 NJ output stores
+  }
+  if (a.stats && a.ksplit == 1 && total > 0) {
+    // reduce over the 16 pixel lanes (lane & 15) sharing a channel group; one slab row per (block group, wm)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s1[j][r] = row16_sum(s1[j][r]);
-          s2[j][r] = row16_sum(s2[j][r]);
-        }
-      if ((lane & 15) == 0) {
-        float* row = a.stats + (size_t)(tm * WAVES_M + wm) * 2 * a.Cout;
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] = row16_sum(s1[j][r]);
+        s2[j][r] = row16_sum(s2[j][r]);
+      }
+    if ((lane & 15) == 0) {
+      const int tn = (int)lid % a.tilesN;
+      float* row = a.stats + (size_t)(((int)lid / a.tilesN) * WAVES_M + wm) * 2 * a.Cout;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int c = n0 + wn * WNT + j * 16 + 4 * (lane >> 4);
-          *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
-          *(float4*)(row + a.Cout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
-        }
+      for (int j = 0; j < NJ; ++j) {
+        const int c = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
+        *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+        *(float4*)(row + a.Cout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
       }
     }
-    pend = a.stats ? 4 * NJ : 2 * NJ;  // 2 NJ output stores (+ 2 NJ stats-row stores)
   }
 }
 
@@ -420,8 +425,10 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
     return nblk;
   }
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
+  // the per-block stats rows need every block to keep one channel tile (see the kernel)
+  if (a.stats && grid % a.tilesN) return -1;
   hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
-  return tilesM * (BM / 64);
+  return grid / a.tilesN * (BM / 64);
 }
 
 // Returns the number of stats-slab rows written, or -1 on unsupported shape.
