@@ -46,7 +46,8 @@ int rdp_upT_unshuffle(const void*, int, void*, int, int, int, int, int, int, int
 int rdp_colsum_bf16(const void*, int, long, int, int, float*, float*, int, hipStream_t);
 int rdp_head_partial_blocks(long);
 int rdp_head_fwd(const void*, int, const float*, const float*, const float*, float*, float*, float*, float*, int, float,
-                 float, const float*, hipStream_t);
+                 float, const float*, float*, float*, float, hipStream_t);
+int rdp_head_grad_finalize(const float*, int, float*, float*, hipStream_t);
 int rdp_head_bwd(const void*, int, const float*, const float*, const float*, const float*, void*, int, float*, float*,
                  float*, int, float, float, float, const float*, float*, hipStream_t);
 int rdp_head_bn_bwd_apply(const void*, int, const float*, const float*, const float*, const float*, const float*,
@@ -351,9 +352,12 @@ void colsum_bf16(torch::Tensor x, int groups, torch::Tensor partial, torch::Tens
 int head_partial_blocks(long M) { return rdp_head_partial_blocks(M); }
 
 // coef (training, optional): `a` is the last conv's pre-BN output y and coef its BN coefficients
+// gpart + bnpart (with coef, dice_w == 0): the forward also emits the backward partials
+// (gpart [nb][65] head grads, bnpart [nb][128] BN-backward rows; nb = head_partial_blocks(M))
 void head_fwd(torch::Tensor a, torch::Tensor w, torch::Tensor b, torch::Tensor target, torch::Tensor logits,
               torch::Tensor partial, torch::Tensor sums, torch::Tensor loss, double dice_w, double dice_eps,
-              c10::optional<torch::Tensor> coef) {
+              c10::optional<torch::Tensor> coef, c10::optional<torch::Tensor> gpart,
+              c10::optional<torch::Tensor> bnpart, double gscale) {
   Act x = act(a, "a");
   TORCH_CHECK(x.C == 64, "head expects 64 channels");
   const long M = (long)x.N * x.H * x.W;
@@ -364,9 +368,28 @@ void head_fwd(torch::Tensor a, torch::Tensor w, torch::Tensor b, torch::Tensor t
     TORCH_CHECK(coef->numel() >= 4 * 64 && coef->scalar_type() == torch::kFloat, "head coef");
     cf = coef->data_ptr<float>();
   }
-  rdp_head_fwd(x.ptr, x.pitch, w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<float>(),
-               logits.data_ptr<float>(), partial.data_ptr<float>(), sums.data_ptr<float>(), loss.data_ptr<float>(), M,
-               (float)dice_w, (float)dice_eps, cf, cur_stream());
+  float* gp = nullptr;
+  float* bp = nullptr;
+  if (gpart) {
+    const long nb = rdp_head_partial_blocks(M);
+    TORCH_CHECK(cf && bnpart && dice_w == 0.0, "head_fwd grad partials need coef, bnpart and dice_w == 0");
+    check_f32(*gpart, "gpart");
+    check_f32(*bnpart, "bnpart");
+    TORCH_CHECK(gpart->numel() >= nb * 65 && bnpart->numel() >= nb * 128, "head_fwd grad partials too small");
+    gp = gpart->data_ptr<float>();
+    bp = bnpart->data_ptr<float>();
+  }
+  TORCH_CHECK(rdp_head_fwd(x.ptr, x.pitch, w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<float>(),
+                           logits.data_ptr<float>(), partial.data_ptr<float>(), sums.data_ptr<float>(),
+                           loss.data_ptr<float>(), M, (float)dice_w, (float)dice_eps, cf, gp, bp, (float)gscale,
+                           cur_stream()) > 0, "head_fwd");
+}
+
+void head_grad_finalize(torch::Tensor gpart, long M, torch::Tensor gw, torch::Tensor gb) {
+  check_f32(gpart, "gpart");
+  TORCH_CHECK(gpart.numel() >= (long)rdp_head_partial_blocks(M) * 65 && gw.numel() == 64 && gb.numel() == 1,
+              "head_grad_finalize sizes");
+  rdp_head_grad_finalize(gpart.data_ptr<float>(), (int)M, gw.data_ptr<float>(), gb.data_ptr<float>(), cur_stream());
 }
 
 // coef + bnpart given: BN-fused backward (da not written, returns the BN partial row count);
@@ -577,7 +600,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_partial_blocks", &head_partial_blocks);
   m.def("head_fwd", &head_fwd, py::arg("a"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("logits"),
         py::arg("partial"), py::arg("sums"), py::arg("loss"), py::arg("dice_w"), py::arg("dice_eps"),
-        py::arg("coef") = py::none());
+        py::arg("coef") = py::none(), py::arg("gpart") = py::none(), py::arg("bnpart") = py::none(),
+        py::arg("gscale") = 1.0);
+  m.def("head_grad_finalize", &head_grad_finalize);
   m.def("head_bwd", &head_bwd, py::arg("a"), py::arg("w"), py::arg("logits"), py::arg("target"), py::arg("sums"),
         py::arg("da"), py::arg("partial"), py::arg("gw"), py::arg("gb"), py::arg("dice_w"), py::arg("dice_eps"),
         py::arg("gscale"), py::arg("coef") = py::none(), py::arg("bnpart") = py::none());

@@ -34,6 +34,8 @@ RDP_DEV float dot8(const uint4& v, const float* w) {
   return s;
 }
 
+RDP_DEV float bfround(float f) { return __uint_as_float(((uint32_t)f2bf(f)) << 16); }
+
 RDP_DEV float sum8lanes(float v) {  // reduce across the 8 lanes of a pixel group
   v += __shfl_xor(v, 1, 64);
   v += __shfl_xor(v, 2, 64);
@@ -55,38 +57,74 @@ RDP_DEV uint4 bn_relu8(const uint4& v, const float* ss, const float* hh) {
   return o;
 }
 
-template <bool BN>
+// GRAD (training, BN-fused, BCE only -- d loss / d logit is then local, (sigmoid(x) - t) / M): the
+// forward pass also produces everything head_bwd_kernel<true> would, from the same read of y: head
+// weight/bias gradient partials gpart[blk][65] and the last conv's BN-backward partials
+// bnpart[blk][128]. The backward then only finalizes (no second pass over y).
+template <bool BN, bool GRAD>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const u16* __restrict__ a, int apitch,
                                                        const float* __restrict__ w, const float* __restrict__ b,
                                                        const float* __restrict__ target, float* __restrict__ logits,
                                                        float* __restrict__ partial, int M,
-                                                       const float* __restrict__ coef) {
+                                                       const float* __restrict__ coef, float* __restrict__ gpart,
+                                                       float* __restrict__ bnpart, float gscale) {
   __shared__ float red[4][4];
+  __shared__ float gred[GRAD ? 4 : 1][GRAD ? 3 * HEAD_C + 1 : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane & 7;
-  float wl[8], ss[8], hh[8];
+  float wl[8], ss[8], hh[8], mu[8], iv[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     wl[k] = w[sub * 8 + k];
     if (BN) { ss[k] = coef[2 * HEAD_C + sub * 8 + k]; hh[k] = coef[3 * HEAD_C + sub * 8 + k]; }
+    if (GRAD) { mu[k] = coef[sub * 8 + k]; iv[k] = coef[HEAD_C + sub * 8 + k]; }
   }
   const float bias = b[0];
+  const float gs = gscale / (float)M;
   float sb = 0.f, si = 0.f, sp = 0.f, st = 0.f;
+  float gw[8], sg[8], sgx[8], gb = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { gw[k] = 0.f; sg[k] = 0.f; sgx[k] = 0.f; }
   // HPX pixels in flight per 8-lane group (16-B loads issued back to back)
   const long stride = (long)gridDim.x * 32;  // 32 pixel groups per block
   for (long p0 = blockIdx.x * 32l + (threadIdx.x >> 3); p0 < M; p0 += stride * HPX) {
     uint4 v[HPX];
+    float tq[HPX];
 #pragma unroll
     for (int u = 0; u < HPX; ++u) {
       const long p = p0 + u * stride;
-      if (p < M) v[u] = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+      if (p < M) {
+        v[u] = *(const uint4*)(a + (size_t)p * apitch + sub * 8);
+        if (GRAD) tq[u] = target[p];
+      }
     }
     float xs[HPX];
 #pragma unroll
     for (int u = 0; u < HPX; ++u) xs[u] = dot8(BN ? bn_relu8(v[u], ss, hh) : v[u], wl);  // (garbage if p >= M)
 #pragma unroll
     for (int u = 0; u < HPX; ++u) xs[u] = sum8lanes(xs[u]);
-    // every lane of the group now holds the HPX logits: lane `sub` finishes pixel `sub`
+    if (GRAD) {  // every lane holds the HPX logits: gradients of its 8 channels for all of them
+#pragma unroll
+      for (int u = 0; u < HPX; ++u) {
+        if (p0 + u * stride >= M) break;
+        const float x = xs[u] + bias;
+        const float e = __expf(-fabsf(x));
+        const float sgm = x >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+        const float dx = (sgm - tq[u]) * gs;
+        float fy[8];
+        unpack8h(v[u], fy);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = fmaf(fy[k], ss[k], hh[k]);
+          gw[k] = fmaf(dx, bfround(fmaxf(z, 0.f)), gw[k]);
+          const float g = z > 0.f ? bfround(dx * wl[k]) : 0.f;
+          sg[k] += g;
+          sgx[k] += g * (fy[k] - mu[k]) * iv[k];
+        }
+        if (sub == 0) gb += dx;
+      }
+    }
+    // lane `sub` finishes pixel `sub`'s logit and loss terms
     float x = xs[0];
 #pragma unroll
     for (int u = 1; u < HPX; ++u) x = sub == u ? xs[u] : x;
@@ -97,18 +135,49 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const u16* __restrict__ a
       const float t = target[p];
       const float e = __expf(-fabsf(x));
       sb += fmaxf(x, 0.f) - x * t + log1pf(e);
-      const float sg = x >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
-      si += sg * t;
-      sp += sg;
+      const float sgm = x >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+      si += sgm * t;
+      sp += sgm;
       st += t;
     }
   }
   sb = wave_sum(sb); si = wave_sum(si); sp = wave_sum(sp); st = wave_sum(st);
   if (lane == 0) { red[wave][0] = sb; red[wave][1] = si; red[wave][2] = sp; red[wave][3] = st; }
+  if (GRAD) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // over the 8 pixel groups of the wave sharing `sub`
+      float v0 = gw[k], v1 = sg[k], v2 = sgx[k];
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        v0 += __shfl_xor(v0, o, 64);
+        v1 += __shfl_xor(v1, o, 64);
+        v2 += __shfl_xor(v2, o, 64);
+      }
+      gw[k] = v0; sg[k] = v1; sgx[k] = v2;
+    }
+    gb = wave_sum(gb);
+    if (lane < 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        gred[wave][lane * 8 + k] = gw[k];
+        gred[wave][HEAD_C + lane * 8 + k] = sg[k];
+        gred[wave][2 * HEAD_C + lane * 8 + k] = sgx[k];
+      }
+    }
+    if (lane == 0) gred[wave][3 * HEAD_C] = gb;
+  }
   __syncthreads();
   if (threadIdx.x < 4) {
     const int q = threadIdx.x;
     partial[blockIdx.x * 4 + q] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+  }
+  if (GRAD) {
+    for (int c = threadIdx.x; c < 3 * HEAD_C + 1; c += 256) {
+      const float tot = gred[0][c] + gred[1][c] + gred[2][c] + gred[3][c];
+      if (c < HEAD_C) gpart[blockIdx.x * (HEAD_C + 1) + c] = tot;
+      else if (c == 3 * HEAD_C) gpart[blockIdx.x * (HEAD_C + 1) + HEAD_C] = tot;
+      else bnpart[(size_t)blockIdx.x * 2 * HEAD_C + (c - HEAD_C)] = tot;
+    }
   }
 }
 
@@ -152,8 +221,6 @@ RDP_DEV float head_dlogit(float x, float t, float invM, float dice_w, float I, f
   }
   return dx * gscale;
 }
-
-RDP_DEV float bfround(float f) { return __uint_as_float(((uint32_t)f2bf(f)) << 16); }
 
 // BN = false: da[p][c] = bf16(dlogit*w[c]) is written for the consumer's BN backward.
 // BN = true : `a` is the pre-BN y of the last conv and da is never materialised. The block instead
@@ -378,20 +445,31 @@ static int blocks_for(long M) { return (int)std::max<long>(1, std::min<long>((M 
 extern "C" {
 int rdp_head_partial_blocks(long M) { return blocks_for(M); }
 
-// coef != nullptr: `a` is the last conv's pre-BN output; BN+ReLU are applied on the fly
+// coef != nullptr: `a` is the last conv's pre-BN output; BN+ReLU are applied on the fly.
+// gpart/bnpart != nullptr (needs coef, dice_w == 0): also the backward partials (head_fwd_kernel GRAD).
 int rdp_head_fwd(const void* a, int apitch, const float* w, const float* b, const float* target, float* logits,
                  float* partial, float* sums, float* loss, int M, float dice_w, float dice_eps, const float* coef,
-                 hipStream_t s) {
+                 float* gpart, float* bnpart, float gscale, hipStream_t s) {
   if (apitch % 8) return -1;
+  if (gpart && (!coef || !bnpart || dice_w != 0.f)) return -1;
   const int nb = blocks_for(M);
-  if (coef)
-    hipLaunchKernelGGL(head_fwd_kernel<true>, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target, logits,
-                       partial, M, coef);
+  if (gpart)
+    hipLaunchKernelGGL((head_fwd_kernel<true, true>), dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target,
+                       logits, partial, M, coef, gpart, bnpart, gscale);
+  else if (coef)
+    hipLaunchKernelGGL((head_fwd_kernel<true, false>), dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target,
+                       logits, partial, M, coef, gpart, bnpart, gscale);
   else
-    hipLaunchKernelGGL(head_fwd_kernel<false>, dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b, target, logits,
-                       partial, M, coef);
+    hipLaunchKernelGGL((head_fwd_kernel<false, false>), dim3(nb), dim3(256), 0, s, (const u16*)a, apitch, w, b,
+                       target, logits, partial, M, coef, gpart, bnpart, gscale);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partial, nb, M, dice_w, dice_eps, sums, loss);
   return nb;
+}
+
+// head weight / bias gradient from the [nb][65] partials of a GRAD forward
+int rdp_head_grad_finalize(const float* gpart, int M, float* gw, float* gb, hipStream_t s) {
+  hipLaunchKernelGGL(head_grad_finalize_kernel, dim3(HEAD_C + 1), dim3(256), 0, s, gpart, blocks_for(M), gw, gb);
+  return 0;
 }
 
 // coef != nullptr: BN-fused variant (da unused; bnpart receives the BN backward partial rows).

@@ -375,6 +375,13 @@ class UNetExecutor:
         self.M = M
         self.logits = torch.zeros(M, dtype=torch.float32, device=dev)
         self.head_partial = torch.zeros(C.head_partial_blocks(M) * 65, dtype=torch.float32, device=dev)
+        # BCE-only training with the BN-fused head: the forward pass also emits the head's backward
+        # partials (d loss / d logit is local), so backward only finalizes them (no second read of y)
+        self.head_grads_in_fwd = self.fuse_head and self.dice_w == 0.0
+        self.head_gscale = 1.0  # loss scale assumed by those partials (backward falls back if it differs)
+        self._head_fwd_grads = False
+        self.head_gpart = (torch.zeros(C.head_partial_blocks(M) * 65, dtype=torch.float32, device=dev)
+                           if self.head_grads_in_fwd else None)
         self.loss_sums = torch.zeros(4, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(2, dtype=torch.float32, device=dev)
         # stats slab (reused by every conv; finalize runs right after each conv)
@@ -414,9 +421,15 @@ class UNetExecutor:
         # path was 1% SLOWER (2717 vs 2740; 4% at bs4), (b) a CU-masked side stream
         # (hipExtStreamCreateWithCUMask, 25-87.5% of the CUs) was 8% slower, (c) a high-priority main
         # stream was neutral. Removing work helps; moving it between streams does not.
-        # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS)
-        # (measured at bs32 with the side-stream overlap: 1024 -> 2025, 2048 -> 2086, 4096 -> 2068 img/s)
-        self.wgrad_blocks = int(os.environ.get("RDP_WGRAD_BLOCKS", "2048"))
+        # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS). Fewer
+        # splits = less fp32 slab traffic (written by the wgrad, re-read by the reduction), more =
+        # more parallelism. Re-measured after the epilogue/fusion work (img/s): bs64 256 -> 2334,
+        # 512 -> 2926 / 2890, 768 -> 2912, 1024 -> 2879, 2048 -> 2880 / 2864, 4096 -> 2882;
+        # bs32 512 -> 2809 vs 2048 -> 2738; bs4 512 -> 1477 vs 2048 -> 1462 (the cliff is below 512);
+        # same-box repeat at bs64: 512 -> 2882 / 2902, 768 -> 2872 / 2872, 1024 -> 2845 / 2842,
+        # 2048 -> 2841 / 2839. (Serialised, the wgrads alone prefer more splits: the side stream's
+        # wgrads overlap the main stream, so a lighter slab wins.)
+        self.wgrad_blocks = int(os.environ.get("RDP_WGRAD_BLOCKS", "512"))
         N = self.N
         D = self.m.depth
 
@@ -563,8 +576,14 @@ class UNetExecutor:
         head_b = self.m.store.view("outc.conv.bias")
         if self.fuse_head:
             lb = self.up_layers[-1][1] if D else self.down_layers[0][1]
-            C.head_fwd(lb.y, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums, self.loss,
-                       self.dice_w, self.dice_eps, lb.coef)
+            if self.head_grads_in_fwd:
+                C.head_fwd(lb.y, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums,
+                           self.loss, self.dice_w, self.dice_eps, lb.coef, self.head_gpart, self.bn_partial,
+                           self.head_gscale)
+                self._head_fwd_grads = True
+            else:
+                C.head_fwd(lb.y, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums,
+                           self.loss, self.dice_w, self.dice_eps, lb.coef)
         else:
             C.head_fwd(self.final, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums,
                        self.loss, self.dice_w, self.dice_eps)
@@ -632,7 +651,11 @@ class UNetExecutor:
         last = self.up_layers[-1][1] if D else self.down_layers[0][1]
         hgw, hgb = st.flat_slice("outc.conv.weight", st.grad), st.flat_slice("outc.conv.bias", st.grad)
         head_gscale = None
-        if self.fuse_head:
+        if self.fuse_head and self._head_fwd_grads and gscale == self.head_gscale:
+            C.head_grad_finalize(self.head_gpart, self.M, hgw, hgb)  # partials came with the forward
+            last.bwd_rows = C.head_partial_blocks(self.M)
+            head_gscale = gscale
+        elif self.fuse_head:
             last.bwd_rows = C.head_bwd(last.y, head_w, self.logits, self.target, self.loss_sums, None,
                                        self.head_partial, hgw, hgb, self.dice_w, self.dice_eps, gscale, last.coef,
                                        self.bn_partial)
@@ -640,6 +663,7 @@ class UNetExecutor:
         else:
             C.head_bwd(self.final, head_w, self.logits, self.target, self.loss_sums, last.da, self.head_partial, hgw,
                        hgb, self.dice_w, self.dice_eps, gscale)
+        self._head_fwd_grads = False
         for i in range(D, 0, -1):
             la, lb = self.up_layers[i - 1]
             self._conv_bwd(C, lb, grad_hook, head_gscale if i == D else None)

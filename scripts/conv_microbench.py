@@ -18,6 +18,7 @@ from robotic_discovery_platform_amd.ops import native  # noqa: E402
 SHAPES = [  # (H, Cin1, Cin2, Cout)   spatial = H x H
     (256, 64, 0, 64), (128, 64, 0, 128), (128, 128, 0, 128), (64, 256, 0, 256), (32, 512, 0, 512),
     (16, 512, 0, 512), (32, 512, 512, 256), (64, 256, 256, 128), (128, 128, 128, 64), (256, 64, 64, 64),
+    (128, 128, 0, 64),
 ]
 
 

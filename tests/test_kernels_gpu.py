@@ -643,3 +643,15 @@ def test_head_bn_fused(C, dice_w):
     assert relerr(db, exact_db) < 1e-3 and relerr(dg, exact_dg) < 1e-3
     dy_exact = gamma * inv * (g - exact_db / M - xh * exact_dg / M)
     assert relerr(dy, dy_exact) < 1e-2
+    if dice_w == 0.0:  # BCE only: the forward can emit the backward partials itself
+        lg2, part2 = torch.zeros(M, device=dev), torch.zeros(nb * 65, device=dev)
+        sums2, loss2 = torch.zeros(4, device=dev), torch.zeros(2, device=dev)
+        gp, bp2 = torch.zeros(nb * 65, device=dev), torch.zeros(nb * 128, device=dev)
+        C.head_fwd(y, wt, b, t, lg2, part2, sums2, loss2, 0.0, 1.0, coef, gp, bp2, gs)
+        assert torch.equal(lg2, lg) and torch.equal(loss2, loss)
+        gw2, gb2 = torch.zeros(64, device=dev), torch.zeros(1, device=dev)
+        C.head_grad_finalize(gp, M, gw2, gb2)
+        assert relerr(gw2, gw) < 1e-5 and relerr(gb2, gb) < 1e-5
+        got = bp2.view(nb, 2, Ch).double().sum(0)
+        ref = bp.view(nb, 2, Ch).double().sum(0)
+        assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
