@@ -55,8 +55,8 @@ def main():
                    run_tool("graph_gaps.py", trace), "```"]
         if serial:
             md += ["", "## Same step with every kernel serialised on one stream (`RDP_WGRAD_OVERLAP=0`)", "",
-                   "Clean per-kernel cost (no contention). The overlapped schedule is only ~0.5% faster than this:",
-                   "the step is throughput-bound, so removing work is what moves the number.", "", "```",
+                   "Clean per-kernel cost (no contention); compare the wall time with the default schedule above",
+                   "for what the side-stream overlap buys.", "", "```",
                    run_tool("graph_gaps.py", serial), "```", "", "One step, per kernel (serialised | default):", "",
                    "```", run_tool("trace_breakdown.py", serial, "4", trace) if trace else "", "```", "",
                    "## Per-layer conv kernels (serialised step; TF/s = 2*N*H*W*9*Cin*Cout / time)", "", "```",
