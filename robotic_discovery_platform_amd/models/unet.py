@@ -415,12 +415,11 @@ class UNetExecutor:
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
         self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
-        # Measured dead ends on this side stream (bs64, one MI355X): the whole step serialised on one
-        # stream is only ~0.5% slower (2801 vs 2816 img/s) -- the step is throughput-bound -- so
-        # (a) the skip half of each Up conv's input gradient moved here off the main stream's critical
-        # path was 1% SLOWER (2717 vs 2740; 4% at bs4), (b) a CU-masked side stream
-        # (hipExtStreamCreateWithCUMask, 25-87.5% of the CUs) was 8% slower, (c) a high-priority main
-        # stream was neutral. Removing work helps; moving it between streams does not.
+        # Measured dead ends on this side stream (bs64, one MI355X): (a) the skip half of each Up conv's
+        # input gradient moved here off the main stream's critical path: 1% slower with the old
+        # 2048-block wgrad grid (2717 vs 2740 img/s), 5% slower with the 512-block grid (2790 vs 2940;
+        # 4% at bs4); (b) a CU-masked side stream (hipExtStreamCreateWithCUMask, 25-87.5% of the CUs):
+        # 8% slower; (c) a high-priority main stream: neutral.
         # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS). Fewer
         # splits = less fp32 slab traffic (written by the wgrad, re-read by the reduction), more =
         # more parallelism. Re-measured after the epilogue/fusion work (img/s): bs64 256 -> 2334,
