@@ -460,7 +460,9 @@ class UNetExecutor:
             self.dups.append(du)
             la.dx1 = self.dskips[lv]
             la.dx2 = du
-        # wgrad split-K choice + shared slab
+        # wgrad split-K choice + shared slab (one grid target for every layer: giving the first encoder
+        # level -- the last side-stream work of the step -- the wide 2048-block grid to shorten the
+        # tail measured 1.3% slower, 2900 / 2909 vs 2938 / 2950 img/s at bs64)
         slab = 0
         for L in self.layers:
             n, h, w, _ = L.x1.shape

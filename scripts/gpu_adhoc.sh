@@ -6,11 +6,10 @@ run() {  # name, env..., args
   env "${e[@]}" timeout -k 10 300 python bench.py --serve 0 "$@" > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || { tail -20 gpurun_out/ab_$n.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/ab_$n.json'));print('$n',d['value'],d['ms_per_step'],d['config']['hipgraph'])"
 }
-RDP_SKIP_DGRAD_SIDE=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_unet_native_gpu.py > gpurun_out/t_u.log 2>&1 || { tail -30 gpurun_out/t_u.log; exit 1; }
-tail -1 gpurun_out/t_u.log
 for r in 1 2; do
-run side0_$r RDP_SKIP_DGRAD_SIDE=0 --steps 40
-run side1_$r RDP_SKIP_DGRAD_SIDE=1 --steps 40
+run t512_$r RDP_WGRAD_TAIL_BLOCKS=512 --steps 40
+run t2048_$r RDP_WGRAD_TAIL_BLOCKS=2048 --steps 40
+run t4096_$r RDP_WGRAD_TAIL_BLOCKS=4096 --steps 40
 done
-run b4side0 RDP_SKIP_DGRAD_SIDE=0 --steps 40 --batch 4
-run b4side1 RDP_SKIP_DGRAD_SIDE=1 --steps 40 --batch 4
+run b4t512 RDP_WGRAD_TAIL_BLOCKS=512 --steps 40 --batch 4
+run b4t2048 RDP_WGRAD_TAIL_BLOCKS=2048 --steps 40 --batch 4
