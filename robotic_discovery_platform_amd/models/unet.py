@@ -483,6 +483,18 @@ class UNetExecutor:
             # roles swapped in conv_wgrad: "x" = dyT (4*cout ch), "dy" = the ConvT input (cin ch)
             slab = max(slab, C.wgrad_slab_elems(n, h, w, 4 * us.cout, us.cin, 1, 0, sp_))
         self.slab = torch.zeros(slab, dtype=torch.float32, device=dev)
+        # The first layer's wgrad is the step's last gradient; the side stream is still working off
+        # its backlog then while the main stream idles, so it runs on the main stream with its own slab
+        # (RDP_LAST_WGRAD_MAIN=0: on the side stream like the others)
+        self.last_wgrad_main = self.side is not None and os.environ.get("RDP_LAST_WGRAD_MAIN", "1") != "0"
+        self.slab_main = None
+        if self.last_wgrad_main:
+            L0 = self.down_layers[0][0]
+            n, h, w, _ = L0.x1.shape
+            cin = L0.spec.cin if not L0.spec.packed else 8
+            self.slab_main = torch.zeros(C.wgrad_slab_elems(n, h, w, cin, L0.spec.cout, L0.spec.taps,
+                                                            int(L0.spec.packed), L0.splits),
+                                         dtype=torch.float32, device=dev)
         if self.m.up_specs:
             self.colsum_ws = torch.zeros(1024 * max(4 * us.cout for us in self.m.up_specs), dtype=torch.float32,
                                          device=dev)
@@ -625,8 +637,11 @@ class UNetExecutor:
         gw = st.flat_slice(sp.name + ".weight", st.grad)
         # wgrad (latency-bound on x / dY streams) overlaps the main stream's dgrad + next BN backward;
         # all wgrads share the slab, so they stay serialized on the one side stream
-        self._on_side(lambda: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab, gw,
-                                           0, L.splits, 0))
+        if self.slab_main is not None and L is self.down_layers[0][0]:
+            C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab_main, gw, 0, L.splits, 0)
+        else:
+            self._on_side(lambda: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab,
+                                               gw, 0, L.splits, 0))
         if L.dx1 is not None:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:

@@ -6,10 +6,11 @@ run() {  # name, env..., args
   env "${e[@]}" timeout -k 10 300 python bench.py --serve 0 "$@" > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || { tail -20 gpurun_out/ab_$n.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/ab_$n.json'));print('$n',d['value'],d['ms_per_step'],d['config']['hipgraph'])"
 }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_unet_native_gpu.py tests/test_ddp_native_gpu.py > gpurun_out/t_u.log 2>&1 || { tail -30 gpurun_out/t_u.log; exit 1; }
+tail -1 gpurun_out/t_u.log
 for r in 1 2; do
-run t512_$r RDP_WGRAD_TAIL_BLOCKS=512 --steps 40
-run t2048_$r RDP_WGRAD_TAIL_BLOCKS=2048 --steps 40
-run t4096_$r RDP_WGRAD_TAIL_BLOCKS=4096 --steps 40
+run lm0_$r RDP_LAST_WGRAD_MAIN=0 --steps 40
+run lm1_$r RDP_LAST_WGRAD_MAIN=1 --steps 40
 done
-run b4t512 RDP_WGRAD_TAIL_BLOCKS=512 --steps 40 --batch 4
-run b4t2048 RDP_WGRAD_TAIL_BLOCKS=2048 --steps 40 --batch 4
+run b4lm0 RDP_LAST_WGRAD_MAIN=0 --steps 40 --batch 4
+run b4lm1 RDP_LAST_WGRAD_MAIN=1 --steps 40 --batch 4
