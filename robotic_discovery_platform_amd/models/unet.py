@@ -485,7 +485,8 @@ class UNetExecutor:
         self.slab = torch.zeros(slab, dtype=torch.float32, device=dev)
         # The first layer's wgrad is the step's last gradient; the side stream is still working off
         # its backlog then while the main stream idles, so it runs on the main stream with its own slab
-        # (RDP_LAST_WGRAD_MAIN=0: on the side stream like the others)
+        # (RDP_LAST_WGRAD_MAIN=0: on the side stream like the others; also moving the second-to-last
+        # layer's wgrad to the main stream measured 1.3% slower, 2913 / 2869 vs 2947 / 2912 img/s)
         self.last_wgrad_main = self.side is not None and os.environ.get("RDP_LAST_WGRAD_MAIN", "1") != "0"
         self.slab_main = None
         if self.last_wgrad_main:

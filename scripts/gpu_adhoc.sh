@@ -9,8 +9,8 @@ run() {  # name, env..., args
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_unet_native_gpu.py tests/test_ddp_native_gpu.py > gpurun_out/t_u.log 2>&1 || { tail -30 gpurun_out/t_u.log; exit 1; }
 tail -1 gpurun_out/t_u.log
 for r in 1 2; do
-run lm0_$r RDP_LAST_WGRAD_MAIN=0 --steps 40
+run lm2_$r RDP_LAST_WGRAD_MAIN=2 --steps 40
 run lm1_$r RDP_LAST_WGRAD_MAIN=1 --steps 40
 done
-run b4lm0 RDP_LAST_WGRAD_MAIN=0 --steps 40 --batch 4
+run b4lm2 RDP_LAST_WGRAD_MAIN=2 --steps 40 --batch 4
 run b4lm1 RDP_LAST_WGRAD_MAIN=1 --steps 40 --batch 4
