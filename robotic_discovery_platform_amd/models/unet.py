@@ -739,7 +739,10 @@ class UNetExecutor:
 
 
 class NativeAdam:
-    """torch.optim.Adam semantics over the flat store, one fused launch (+ derived-weight rebuild)."""
+    """torch.optim.Adam semantics over the flat store, one fused launch (+ derived-weight rebuild).
+
+    (Measured dead end: per-layer Adam segments on the weight-gradient side stream as each layer's
+    gradient became final -- neutral at bs64, 3% slower at bs4 from the 18 extra launches.)"""
 
     def __init__(self, model: UNetNative, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0):
