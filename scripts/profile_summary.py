@@ -63,6 +63,18 @@ def main():
                    run_tool("analyze_trace.py", serial, "64"), "```"]
         open(os.path.join(ROOT, "profiles", "train_step_kernels.md"), "w").write("\n".join(md) + "\n")
         print("wrote profiles/train_step_kernels.md")
+    tt = find("prof_tr/**/tr_kernel_stats.csv")
+    if tt:
+        md = ["# Native training step, transposed-conv decoder (fixed), bs 64: kernel time (rocprofv3)", "",
+              "`rocprofv3 --kernel-trace --stats -- python3 bench.py --decoder transposed --batch 64 --steps 4 "
+              "--warmup 3 --serve 0` on one MI355X (7 steps in the totals). 31.04M params, 96.3 GFLOP/img "
+              "forward (1.2x the bilinear model).", "", stats_table(tt)]
+        trace = find("prof_tr/**/tr_kernel_trace.csv")
+        if trace:
+            md += ["", "## Wall / busy / idle per step", "", "```", run_tool("graph_gaps.py", trace), "```", "",
+                   "## One step, per kernel", "", "```", run_tool("trace_breakdown.py", trace, "4"), "```"]
+        open(os.path.join(ROOT, "profiles", "train_step_transposed.md"), "w").write("\n".join(md) + "\n")
+        print("wrote profiles/train_step_transposed.md")
     sv = find("prof_serve/**/serve_kernel_stats.csv")
     if sv:
         shutil.copy(sv, os.path.join(ROOT, "profiles", "serve_kernel_stats.csv"))
