@@ -12,6 +12,9 @@ extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
                    float*, long, hipStream_t);
+int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
+                     float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
+                     hipStream_t);
 long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
@@ -208,6 +211,27 @@ void bn_relu_apply(torch::Tensor y, torch::Tensor out, torch::Tensor coef, int r
   TORCH_CHECK(coef.numel() >= 4 * a.C, "coef");
   TORCH_CHECK(rdp_bn_relu_apply(a.ptr, a.pitch, o.ptr, o.pitch, coef.data_ptr<float>(), a.N * a.H * a.W, a.C, relu,
                                 cur_stream()) == 0, "bn_relu_apply");
+}
+
+// 3x3 dgrad (row-ring kernel) whose epilogue also writes the BN-backward partial rows of the layer that
+// owns dx (y_bn: its pre-BN output, coef: its [mean|invstd|scale|shift]; ReLU). Returns the partial
+// rows for bn_bwd_finalize, or -1 if the ring kernel does not apply (caller falls back to
+// conv_fwd + bn_relu_bwd_reduce; nothing was launched).
+int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch::Tensor y_bn, torch::Tensor coef,
+                     torch::Tensor partial) {
+  Act a = act(dy, "dy"), o = act(dx, "dx"), b = act(y_bn, "y_bn");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && b.N == a.N && b.H == a.H && b.W == a.W && b.C == o.C,
+              "conv_dgrad_bnred: shape mismatch");
+  TORCH_CHECK(w.size(0) == o.C, "w rows != Cout");
+  check_f32(coef, "coef");
+  check_f32(partial, "partial");
+  TORCH_CHECK(coef.numel() >= 4l * o.C, "coef must hold 4*C floats");
+  // ring grid <= 256 blocks x 4 pixel groups (64 couts) or 2 (128): <= 1024 rows of 2*C
+  TORCH_CHECK(partial.numel() >= 1024l * 2 * o.C, "partial too small");
+  return rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
+                          o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
+                          0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), cur_stream());
 }
 
 int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, int relu, torch::Tensor partial) {
@@ -585,6 +609,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_relu_apply", &bn_relu_apply);
   m.def("bn_relu_bwd_reduce", &bn_relu_bwd_reduce);
+  m.def("conv_dgrad_bnred", &conv_dgrad_bnred);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_relu_bwd_apply", &bn_relu_bwd_apply);
   m.def("maxpool2_fwd", &maxpool2_fwd);

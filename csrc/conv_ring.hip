@@ -40,6 +40,11 @@ struct RingArgs {
   const float* escale;
   const float* eshift;
   int erelu;
+  // dgrad epilogue fused with the next BN backward reduction (stats != nullptr): per channel
+  // sum(g) and sum(g * xhat), g = relu'(bny * scale + shift) * out; bncoef = [mean|invstd|scale|shift]
+  const u16* bny;
+  int bnypitch;
+  const float* bncoef;
   int H, W, WS;  // WS = W / 64 segments per image row
   int nrows;     // N * WS * H: input rows in column order (R = column * H + h)
   int npairs;    // nrows / 2: steps (two output rows each)
@@ -52,7 +57,9 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 // ABL (ablation builds for the microbenchmark, RDP_RING_ABL): 1 = no ring DMA after the prologue,
 // 2 = no MFMA, 4 = no epilogue stores
 // COUT = 64: 8 waves = 2 channel groups x 4 pixel groups (32 px); COUT = 128: 4 x 2 (64 px).
-template <int COUT, int ABL = 0>
+// BNR: dgrad epilogue fused with the owner layer's BN-backward reduction (a separate instantiation:
+// its y registers would otherwise cost every other variant 12 VGPRs -- spills at COUT = 128)
+template <int COUT, int ABL = 0, bool BNR = false>
 __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
   constexpr int PXW = 128 / NPG, NI = PXW / 16;  // pixels per wave (one output row half or whole)
@@ -60,7 +67,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NX = 8;           // ring slots: 4 rows in use + 2 steps x 2 rows in flight
   constexpr int PIECES = 18;      // 1-KiB DMA pieces per step (2 rows x 9)
   constexpr int MINPW = PIECES / 8;
-  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 2 * COUT * 4];  // + zero slot, BN fold
+  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 4 * COUT * 4];  // + zero slot, BN fold / BN-bwd coefs
   float* const efold = (float*)(ring + (NX + 1) * XREG);  // eval BN fold [scale | shift] (LDS, not VGPRs)
 
   const int lane = threadIdx.x & 63;
@@ -155,6 +162,9 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   if (a.escale) {
     for (int c = threadIdx.x; c < COUT; c += 512) { efold[c] = a.escale[c]; efold[COUT + c] = a.eshift[c]; }
   }
+  if constexpr (BNR) {
+    for (int c = threadIdx.x; c < 4 * COUT; c += 512) efold[c] = a.bncoef[c];
+  }
 
   // slot NX stays zero: the padding row read by a column's first / last output row, so the tap loop
   // has no branches and the compiler can overlap one tap's fragment reads with the previous MFMAs
@@ -186,7 +196,24 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     raw_barrier();
-    if (!(ABL & 1) && ks + 2 < nks) issue(P + 2);
+    // BN-backward fusion: the owner layer's pre-BN activations at this step's outputs, loaded before
+    // the stage P + 2 DMAs so their latency hides under the taps. (hipcc cannot see the DMAs, so its
+    // vmcnt(0) before the first use also waits for stage P + 2; keeping the loads invisible to it with
+    // inline asm + a hand-counted vmcnt is unsafe: it may copy the destination registers before the wait.)
+    uint2 yb[NI][2];
+    if constexpr (BNR) {
+      int ym0, yw0;
+      row_base(2 * P + orow, ym0, yw0);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const u16* pa = a.bny + (size_t)(ym0 + px0 + 16 * i + (lane & 15)) * a.bnypitch + 32 * cg + 16 * j + 4 * gq;
+          yb[i][j] = *(const uint2*)pa;
+        }
+    }
+    const bool dma_next = !(ABL & 1) && ks + 2 < nks;
+    if (dma_next) issue(P + 2);
 
     const int R0 = 2 * P + orow;  // this wave's output row (column order)
     const int h = R0 - (int)rdiv((uint32_t)R0, a.fh_m, a.fh_s) * a.H;
@@ -279,10 +306,24 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
         if (a.stats) {
           const float q0 = __uint_as_float(v[j].x << 16), q1 = __uint_as_float(v[j].x & 0xffff0000u);
           const float q2 = __uint_as_float(v[j].y << 16), q3 = __uint_as_float(v[j].y & 0xffff0000u);
-          s1[j][0] += q0; s2[j][0] += q0 * q0;
-          s1[j][1] += q1; s2[j][1] += q1 * q1;
-          s1[j][2] += q2; s2[j][2] += q2 * q2;
-          s1[j][3] += q3; s2[j][3] += q3 * q3;
+          if constexpr (BNR) {
+            const int c = 32 * cg + 16 * j + 4 * gq;
+            const float4 mu = *(const float4*)(efold + c), iv = *(const float4*)(efold + COUT + c);
+            const float4 sc = *(const float4*)(efold + 2 * COUT + c), sh = *(const float4*)(efold + 3 * COUT + c);
+            const float y0 = __uint_as_float(yb[i][j].x << 16), y1 = __uint_as_float(yb[i][j].x & 0xffff0000u);
+            const float y2 = __uint_as_float(yb[i][j].y << 16), y3 = __uint_as_float(yb[i][j].y & 0xffff0000u);
+            const float g0 = fmaf(y0, sc.x, sh.x) > 0.f ? q0 : 0.f, g1 = fmaf(y1, sc.y, sh.y) > 0.f ? q1 : 0.f;
+            const float g2 = fmaf(y2, sc.z, sh.z) > 0.f ? q2 : 0.f, g3 = fmaf(y3, sc.w, sh.w) > 0.f ? q3 : 0.f;
+            s1[j][0] += g0; s2[j][0] += g0 * (y0 - mu.x) * iv.x;
+            s1[j][1] += g1; s2[j][1] += g1 * (y1 - mu.y) * iv.y;
+            s1[j][2] += g2; s2[j][2] += g2 * (y2 - mu.z) * iv.z;
+            s1[j][3] += g3; s2[j][3] += g3 * (y3 - mu.w) * iv.w;
+          } else {
+            s1[j][0] += q0; s2[j][0] += q0 * q0;
+            s1[j][1] += q1; s2[j][1] += q1 * q1;
+            s1[j][2] += q2; s2[j][2] += q2 * q2;
+            s1[j][3] += q3; s2[j][3] += q3 * q3;
+          }
         }
       }
       const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
@@ -317,10 +358,29 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
 // Applicability of the ring kernel (3x3, one 64-channel source, 64 or 128 outputs -- split at a
 // multiple of 32 into two destinations --, W % 64 == 0, even H); returns the stats rows it writes,
 // or -1 when not applicable.
+extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                                void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
+                                int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
+                                int erelu, int max_blocks, const void* bn_y_, int bn_ypitch, const float* bn_coef,
+                                hipStream_t s);
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
                              void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                              int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                              int erelu, int max_blocks, hipStream_t s) {
+  return rdp_conv_ring_ex(x, xbytes, C, pitch, w, wbytes, ldw, y, ybytes, ypitch, y2, ybytes2, ypitch2, Cy1, Cout,
+                          stats, N, H, W, escale, eshift, erelu, max_blocks, nullptr, 0, nullptr, s);
+}
+
+// Row-ring dgrad whose epilogue also produces the BN-backward partial rows of the layer that owns
+// the output (bn_y: its pre-BN activations, bn_coef: its [mean|invstd|scale|shift]; ReLU applied):
+// replaces a separate bn_relu_bwd_reduce pass over (da, y). Returns the partial rows, or -1.
+extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                                void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
+                                int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
+                                int erelu, int max_blocks, const void* bn_y_, int bn_ypitch, const float* bn_coef,
+                                hipStream_t s) {
+  const u16* bn_y = (const u16*)bn_y_;
+  if (bn_y && (!stats || escale || y2 || bn_ypitch % 4 || Cout != 64)) return -1;
   if (C != 64 || (Cout != 64 && Cout != 128) || W % 64 || H % 2 || ldw < 576 || Cy1 % 32) return -1;
   if (y2 == nullptr && Cy1 != Cout) return -1;
   if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || ybytes2 >= (1l << 31) || wbytes >= (1l << 31)) return -1;
@@ -331,6 +391,7 @@ extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const
   a.y2 = (u16*)(y2 ? y2 : y); a.ybytes2 = y2 ? (uint32_t)ybytes2 : 0u; a.ypitch2 = y2 ? ypitch2 : ypitch;
   a.Cy1 = Cy1;
   a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  a.bny = bn_y; a.bnypitch = bn_ypitch; a.bncoef = bn_coef;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -346,6 +407,10 @@ extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const
   if (Cout == 128) {
     hipLaunchKernelGGL((conv_ring_kernel<128>), dim3(grid), dim3(512), 0, s, a);
     return grid * 2;
+  }
+  if (bn_y) {
+    hipLaunchKernelGGL((conv_ring_kernel<64, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    return grid * 4;
   }
   switch (abl) {
     case 1: hipLaunchKernelGGL((conv_ring_kernel<64, 1>), dim3(grid), dim3(512), 0, s, a); break;

@@ -288,6 +288,7 @@ class _Layer:
     da: Optional[torch.Tensor] = None  # gradient w.r.t. a (filled by the consumer)
     dy: Optional[torch.Tensor] = None
     dx1: Optional[torch.Tensor] = None  # dgrad destinations (None => no dgrad)
+    dx1_owner: Optional["_Layer"] = None  # layer whose BN input gradient dx1 is (None: a pool / concat grad)
     dx2: Optional[torch.Tensor] = None
     splits: int = 1
     bwd_rows: int = 0  # BN-backward partial rows already produced by a fused producer of da
@@ -429,6 +430,9 @@ class UNetExecutor:
         # 2048 -> 2841 / 2839. (Serialised, the wgrads alone prefer more splits: the side stream's
         # wgrads overlap the main stream, so a lighter slab wins.)
         self.wgrad_blocks = int(os.environ.get("RDP_WGRAD_BLOCKS", "512"))
+        # dgrad into the da of a BN layer: where the row-ring kernel runs it (64 -> 64 channels), its
+        # epilogue also produces that layer's BN-backward partial sums (no bn_relu_bwd_reduce pass)
+        self.dgrad_bnred = os.environ.get("RDP_DGRAD_BNRED", "1") != "0"
         N = self.N
         D = self.m.depth
 
@@ -443,11 +447,13 @@ class UNetExecutor:
         # inc: conv1 has no dgrad; conv2 -> inc conv1 da
         (l0, l1) = enc_layers[0]
         l1.dx1 = l0.da
+        l1.dx1_owner = l0
         self.dpools: List[torch.Tensor] = []
         self.dskips: List[torch.Tensor] = [like(s) for s in self.skips[:D]]  # grads from the decoder concat
         for i in range(1, D + 1):
             la, lb = enc_layers[i]
             lb.dx1 = la.da
+            lb.dx1_owner = la
             dp = like(self.pools[i - 1])
             self.dpools.append(dp)
             la.dx1 = dp
@@ -456,6 +462,7 @@ class UNetExecutor:
             lv = D - i
             la, lb = self.up_layers[i - 1]
             lb.dx1 = la.da
+            lb.dx1_owner = la
             du = like(self.ups[i - 1])
             self.dups.append(du)
             la.dx1 = self.dskips[lv]
@@ -643,7 +650,13 @@ class UNetExecutor:
         else:
             self._on_side(lambda: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab,
                                                gw, 0, L.splits, 0))
-        if L.dx1 is not None:
+        owner = L.dx1_owner if self.dgrad_bnred else None
+        if owner is not None and L.dx2 is None and sp.taps == 9 and not owner.bwd_rows:
+            rows = C.conv_dgrad_bnred(L.dy, self.m.dgrad_weight(sp), L.dx1, owner.y, owner.coef, self.bn_partial)
+            if rows > 0:
+                owner.bwd_rows = rows
+                owner = True
+        if L.dx1 is not None and owner is not True:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:
             self._on_side(lambda: hooks(sp))  # the bucket's all-reduce waits for the wgrad too

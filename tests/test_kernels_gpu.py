@@ -241,6 +241,41 @@ def test_bn_relu_train_fwd_bwd(C):
     assert relerr(dg, bn.weight.grad) < 1e-3 and relerr(db, bn.bias.grad) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,W,Cout", [(2, 64, 64, 64), (1, 32, 128, 64), (2, 16, 64, 128)])
+def test_conv_dgrad_bnred(C, N, H, W, Cout):
+    """Row-ring dgrad with the next BN's backward reduction in its epilogue: dx identical to the
+    unfused dgrad; the partial sums match torch fp32 sum(g), sum(g * xhat) of the bf16 dx."""
+    torch.manual_seed(17)
+    dev = "cuda"
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    w = bf(torch.randn(Cout, 64, 3, 3, device=dev) * 0.05)
+    wk = ohwi(w).contiguous()
+    y = bf(torch.randn(N, H, W, Cout, device=dev) * 2 + 0.3)
+    M = N * H * W
+    mean = y.float().mean((0, 1, 2))
+    inv = 1.0 / (y.float().var((0, 1, 2), unbiased=False) + 1e-5).sqrt()
+    scale = (torch.rand(Cout, device=dev) + 0.5) * inv
+    shift = torch.randn(Cout, device=dev) * 0.1 - mean * scale
+    coef = torch.cat([mean, inv, scale, shift]).contiguous()
+    dx = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    part = torch.zeros(1024 * 2 * Cout, device=dev)
+    rows = C.conv_dgrad_bnred(dy, wk, dx, y, coef, part)
+    if Cout != 64:  # only the 64-output ring kernel has the fused variant: -1, nothing launched
+        assert rows == -1
+        return
+    assert rows > 0
+    dx_ref = torch.empty_like(dx)
+    C.conv_fwd(dy, None, wk, 9, 0, dx_ref, None, None, 6, None, 0)  # same ring kernel, no fusion
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_ref)
+    conv = F.conv2d(nchw(dy).float(), w.float(), padding=1)
+    assert relerr(nchw(dx), conv) < 1e-2
+    g = torch.where(y.float() * scale + shift > 0, dx.float(), torch.zeros((), device=dev))
+    p = part[: rows * 2 * Cout].view(rows, 2, Cout).sum(0)
+    assert relerr(p[0], g.sum((0, 1, 2))) < 1e-3
+    assert relerr(p[1], (g * (y.float() - mean) * inv).sum((0, 1, 2))) < 1e-3
+
+
 def test_maxpool_fwd_bwd_with_skip(C):
     torch.manual_seed(6)
     dev = "cuda"
