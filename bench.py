@@ -50,6 +50,7 @@ def parse():
                    help="capture the native step in a hipGraph (1), eager launches (0), -1: auto by batch size")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--loss", choices=["bce", "bce_dice"], default="bce")
+    p.add_argument("--sync-bn", type=int, default=0, help="1: SyncBatchNorm across ranks (not the reference's BN)")
     p.add_argument("--serve", type=int, default=-1,
                    help="also measure e2e serving FPS / p50 latency (default: on for single-GPU runs)")
     return p.parse_args()
@@ -114,7 +115,8 @@ def make_eager_step(args, dev, world):
 def make_native_step(args, dev, world):
     from robotic_discovery_platform_amd.train.engine import build_bench_step
     return build_bench_step(batch=args.batch, size=args.size, decoder=args.decoder, device=dev,
-                            world=world, graph="auto" if args.graph < 0 else bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss)
+                            world=world, graph="auto" if args.graph < 0 else bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss,
+                            sync_bn=bool(args.sync_bn))
 
 
 class _Progress:
@@ -189,6 +191,7 @@ def main():
                 "impl": args.impl,
                 "optimizer": "Adam(lr=1e-4)",
                 "loss": args.loss,
+                "sync_bn": bool(args.sync_bn) and world > 1,
                 "hipgraph": used_graph,
             },
             "baseline_note": "vs_baseline = value / 2.14 img/s (BASELINE.md: reference bs4 fp32 on CPU; "

@@ -63,6 +63,7 @@ class TrainConfig:
     synthetic_if_missing: bool = True
     synthetic_samples: int = 64
     grad_bucket_mb: float = 16.0
+    sync_bn: bool = False  # share BN batch statistics across DDP ranks (SyncBatchNorm semantics)
     graph: bool = False  # hipGraph-capture the train step (measured slower than eager launches, engine.py)
     model_depth: int = 4  # U-Net levels (reference: 4; the plumbing config uses 2)
     bilinear: bool = True  # decoder: bilinear upsample (reference default) or transposed conv (fixed)

@@ -389,6 +389,11 @@ class UNetExecutor:
         max_rows = max(C.conv_stats_rows(L.x1.shape[0] * L.x1.shape[1] * L.x1.shape[2], L.spec.cout, 0) * 2 * L.spec.cout
                        for L in self.layers)
         self.stats = torch.zeros(max_rows, dtype=torch.float32, device=dev)
+        # SyncBatchNorm (optional): process group whose ranks share batch statistics.
+        # The per-block partial rows are folded to one [2][C] row, all-reduced (one 2C-float call per
+        # layer, forward and backward) and finalized with the global pixel count.
+        self.sync_group = None
+        self.sync_world = 1
         self.red_ws = torch.zeros(64 * 2 * max(L.spec.cout for L in self.layers), dtype=torch.float32, device=dev)
         # split-K workspace (fp32 partial tiles) for the convs whose tile grid alone underfills the
         # chip (deep layers at small batch, e.g. serving at N=1); shared: convs run in sequence
@@ -537,6 +542,8 @@ class UNetExecutor:
         b = m.store.view(sp.bn + ".bias")
         if self.training:
             M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
+            if self.sync_world > 1:
+                rows, M = self._sync_rows(self.stats, rows, sp.cout), M * self.sync_world
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
                           m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
         if pool is not None and self.fuse_pool:
@@ -620,14 +627,43 @@ class UNetExecutor:
         # the reduction already ran inside the pool/head backward that produced L.da (fused), or runs now
         T = L.bwd_rows if L.bwd_rows else C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
         L.bwd_rows = 0
-        C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
-                          st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
-                          self.red_ws)
+        if self.sync_world > 1:
+            # gamma/beta gradients stay local (DDP averages them like any weight); the input-gradient
+            # coefficients use the globally reduced sums, as torch.nn.SyncBatchNorm does
+            C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
+                              st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
+                              self.red_ws)
+            T, M = self._sync_rows(self.bn_partial, T, sp.cout), M * self.sync_world
+            C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef, None, None, L.coef2,
+                              self.red_ws)
+        else:
+            C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
+                              st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
+                              self.red_ws)
         if head_gscale is not None:  # fused head: g recomputed from the logits, no da
             C.head_bn_bwd_apply(L.y, st.view("outc.conv.weight").reshape(-1), self.logits, self.target,
                                 self.loss_sums, L.coef, L.coef2, L.dy, self.dice_w, self.dice_eps, head_gscale)
         else:
             C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
+
+    def set_sync_bn(self, group=None, enabled: bool = True):
+        """Share BN batch statistics across the ranks of ``group`` (default: WORLD) in training."""
+        import torch.distributed as dist
+        if enabled and dist.is_available() and dist.is_initialized():
+            self.sync_group, self.sync_world = group, dist.get_world_size(group)
+        else:
+            self.sync_group, self.sync_world = None, 1
+
+    def _sync_rows(self, buf: torch.Tensor, rows: int, c: int) -> int:
+        """Fold ``rows`` partial [2][C] rows of ``buf`` into row 0 (fp64 sum), all-reduce it over the
+        sync group and return 1 (the row count the finalize kernels then read)."""
+        import torch.distributed as dist
+        tot = buf[: rows * 2 * c].view(rows, 2 * c).sum(0, dtype=torch.float64)
+        if dist.get_backend(self.sync_group) == "gloo":  # host round trip (gloo tests: ranks share a GPU)
+            tot = tot.cpu()
+        dist.all_reduce(tot, group=self.sync_group)
+        buf[: 2 * c].copy_(tot)
+        return 1
 
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream

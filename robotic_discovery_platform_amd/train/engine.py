@@ -42,7 +42,7 @@ class NativeTrainer:
     GRAPH_AUTO_MAX_PIXELS = 0
 
     def __init__(self, model: UNetNative, batch: int, h: int, w: int, lr: float = 1e-4, loss: str = "bce",
-                 dice_weight: float = 1.0, graph="auto", bucket_mb: float = 16.0):
+                 dice_weight: float = 1.0, graph="auto", bucket_mb: float = 16.0, sync_bn: bool = False):
         self.model = model
         self.ex = model.executor(batch, h, w, training=True, loss=loss, dice_weight=dice_weight)
         self.opt = NativeAdam(model, lr=lr)
@@ -55,6 +55,7 @@ class NativeTrainer:
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
             self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb)
             self._layer_params = {sp.name: sp.param_names() for sp in list(model.specs) + list(model.up_specs)}
+            self.ex.set_sync_bn(enabled=sync_bn)
         if graph == "auto":
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
         self.use_graph = bool(graph) and self.world == 1 and torch.cuda.is_available()
@@ -191,13 +192,13 @@ class EagerTrainer:
 
 
 def build_bench_step(batch: int, size: int, decoder: str, device: torch.device, world: int, graph: bool,
-                     bucket_mb: float, loss: str = "bce"):
+                     bucket_mb: float, loss: str = "bce", sync_bn: bool = False):
     """bench.py hook: returns a zero-arg callable running one full native training step."""
     bilinear = decoder == "bilinear"
     torch.manual_seed(0)
     ref = UNetRef(3, 1, bilinear=bilinear)
     model = UNetNative(3, 1, bilinear=bilinear, device=device, init_from=ref)
-    tr = NativeTrainer(model, batch, size, size, loss=loss, graph=graph, bucket_mb=bucket_mb)
+    tr = NativeTrainer(model, batch, size, size, loss=loss, graph=graph, bucket_mb=bucket_mb, sync_bn=sync_bn)
     g = torch.Generator(device="cpu").manual_seed(1234 + tr.rank)
     x = torch.rand(batch, 3, size, size, generator=g).to(device)
     y = (torch.rand(batch, 1, size, size, generator=g) > 0.5).float().to(device)

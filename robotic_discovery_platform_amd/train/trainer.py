@@ -64,7 +64,8 @@ class _NativeRunner:
         key = (n, h, w)
         if key not in self._trainers:
             tr = self._cls(self.model, n, h, w, lr=self.cfg.learning_rate, loss=self.cfg.loss,
-                           dice_weight=self.cfg.dice_weight, graph=self.cfg.graph, bucket_mb=self.cfg.grad_bucket_mb)
+                           dice_weight=self.cfg.dice_weight, graph=self.cfg.graph, bucket_mb=self.cfg.grad_bucket_mb,
+                           sync_bn=self.cfg.sync_bn)
             tr.opt = self._shared_opt
             self._trainers[key] = tr
         return self._trainers[key]
@@ -167,6 +168,8 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
         runner = _NativeRunner(model, cfg)
     else:
         model = ref.to(dev)
+        if cfg.sync_bn and dev.type == "cuda" and dist_info()[1] > 1:  # torch's SyncBatchNorm is GPU-only
+            model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
         runner = _EagerRunner(model, cfg, dev)
 
     start_epoch, best_val = 0, float("inf")
