@@ -72,6 +72,31 @@ def test_flat_bucketer_allreduce(tmp_path):
     assert json.load(open(out))["nbuckets"] > 1
 
 
+# ----------------------------------------------------------------------------- SyncBN row fold
+def _syncbn_rows_worker(rank, world):
+    """UNetExecutor._sync_rows: T partial [2][C] rows per rank -> row 0 = sum over rows and ranks."""
+    from types import SimpleNamespace
+    from robotic_discovery_platform_amd.models.unet import UNetExecutor
+    C, T = 8, 5
+    ex = SimpleNamespace(sync_group=None, sync_world=world)
+    buf = torch.zeros(64 * 2 * C)
+    rows = torch.arange(T * 2 * C, dtype=torch.float32).view(T, 2 * C) * (rank + 1)
+    buf[: T * 2 * C] = rows.reshape(-1)
+    assert UNetExecutor._sync_rows(ex, buf, T, C) == 1
+    exp = rows.sum(0) / (rank + 1) * sum(r + 1 for r in range(world))
+    assert torch.equal(buf[: 2 * C], exp)
+    # set_sync_bn picks the world size of the initialised group; disabled -> local statistics
+    ex2 = SimpleNamespace()
+    UNetExecutor.set_sync_bn(ex2)
+    assert ex2.sync_world == world
+    UNetExecutor.set_sync_bn(ex2, enabled=False)
+    assert ex2.sync_world == 1 and ex2.sync_group is None
+
+
+def test_syncbn_row_fold_allreduce():
+    _run(_syncbn_rows_worker, 3)
+
+
 # ----------------------------------------------------------------------------- gradient equivalence
 def _make(seed):
     from robotic_discovery_platform_amd.models.unet_ref import UNetRef
