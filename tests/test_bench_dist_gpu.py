@@ -1,0 +1,38 @@
+"""bench.py's multi-rank contract, end to end: torch.distributed.run launches 2 ranks (sharing the one
+GPU of the test box over gloo; the driver's real N-GPU runs use RCCL), rank 0 prints ONE JSON line
+whose value aggregates both ranks. Also exercises --sync-bn through the launcher."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("sync_bn", [0, 1])
+def test_bench_two_ranks_json_contract(sync_bn):
+    env = dict(os.environ, RDP_DIST_BACKEND="gloo", RDP_NO_BUILD="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "2", "--size", "64", "--sync-bn", str(sync_bn)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    assert d["config"]["sync_bn"] is bool(sync_bn)
+    assert d["value"] > 0 and abs(d["value"] - 4 * 1000.0 / d["ms_per_step"]) / d["value"] < 0.02
