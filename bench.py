@@ -51,6 +51,10 @@ def parse():
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--loss", choices=["bce", "bce_dice"], default="bce")
     p.add_argument("--sync-bn", type=int, default=0, help="1: SyncBatchNorm across ranks (not the reference's BN)")
+    p.add_argument("--grad-comm", choices=["fp32", "bf16"], default="fp32",
+                   help="gradient all-reduce dtype (bf16: half the xGMI bytes, fp32 accumulate in Adam)")
+    p.add_argument("--ddp-force", type=int, default=0,
+                   help="1: run the DDP path (RCCL process group, bucketed all-reduce hooks) even at world 1")
     p.add_argument("--serve", type=int, default=-1,
                    help="also measure e2e serving FPS / p50 latency (default: on for single-GPU runs)")
     return p.parse_args()
@@ -68,11 +72,18 @@ def setup_dist(args):
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    if world > 1 or args.ddp_force:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            from robotic_discovery_platform_amd.utils.launch import _free_port
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         # nccl == RCCL on ROCm (xGMI); RDP_DIST_BACKEND=gloo lets several ranks share one GPU in tests
         backend = os.environ.get("RDP_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
-        dist.init_process_group(backend=backend, device_id=dev if dev.type == "cuda" and backend == "nccl" else None)
+        from robotic_discovery_platform_amd.utils.launch import dist_timeout
+        dist.init_process_group(backend=backend, timeout=dist_timeout(),
+                                device_id=dev if dev.type == "cuda" and backend == "nccl" else None)
     return rank, world, dev
 
 
@@ -116,7 +127,7 @@ def make_native_step(args, dev, world):
     from robotic_discovery_platform_amd.train.engine import build_bench_step
     return build_bench_step(batch=args.batch, size=args.size, decoder=args.decoder, device=dev,
                             world=world, graph="auto" if args.graph < 0 else bool(args.graph), bucket_mb=args.bucket_mb, loss=args.loss,
-                            sync_bn=bool(args.sync_bn))
+                            sync_bn=bool(args.sync_bn), grad_comm=args.grad_comm, ddp_force=bool(args.ddp_force))
 
 
 class _Progress:
@@ -191,15 +202,16 @@ def main():
                 "impl": args.impl,
                 "optimizer": "Adam(lr=1e-4)",
                 "loss": args.loss,
-                "sync_bn": bool(args.sync_bn) and world > 1,
+                "sync_bn": bool(args.sync_bn) and world > 1 and args.impl == "native",
                 "hipgraph": used_graph,
+                "grad_comm": args.grad_comm if (world > 1 or args.ddp_force) else None,
             },
             "baseline_note": "vs_baseline = value / 2.14 img/s (BASELINE.md: reference bs4 fp32 on CPU; "
                              "no published GPU number exists)",
         }
         out.update(extra)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return bool(serve) and rank == 0
 

@@ -63,6 +63,8 @@ class TrainConfig:
     synthetic_if_missing: bool = True
     synthetic_samples: int = 64
     grad_bucket_mb: float = 16.0
+    grad_comm: str = "fp32"  # gradient all-reduce dtype: "fp32" or "bf16" (fp32 accumulate in Adam)
+    dist_timeout_s: float = 600.0  # process-group timeout: a hung collective fails the job instead of hanging
     sync_bn: bool = False  # share BN batch statistics across DDP ranks (SyncBatchNorm semantics)
     graph: bool = False  # hipGraph-capture the train step (measured slower than eager launches, engine.py)
     model_depth: int = 4  # U-Net levels (reference: 4; the plumbing config uses 2)
@@ -83,6 +85,8 @@ class ServeConfig:
     mask_threshold: float = 0.5
     backend: str = "auto"
     graph: bool = True
+    devices: str = ""  # comma-separated GPU indices for per-GPU replicas ("" = current device only; "all")
+    replicas_per_device: int = 2  # independent stream pipelines (hipGraph + buffers) per GPU
     hot_reload_alias: Optional[str] = None  # e.g. "staging": reload when alias moves
 
 

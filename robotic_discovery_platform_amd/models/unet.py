@@ -543,7 +543,7 @@ class UNetExecutor:
         if self.training:
             M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
             if self.sync_world > 1:
-                rows, M = self._sync_rows(self.stats, rows, sp.cout), M * self.sync_world
+                rows, M = self._sync_rows(self.stats, rows, sp.cout, (L.y.shape[1], L.y.shape[2]))
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
                           m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
         if pool is not None and self.fuse_pool:
@@ -633,7 +633,7 @@ class UNetExecutor:
             C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
                               st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
                               self.red_ws)
-            T, M = self._sync_rows(self.bn_partial, T, sp.cout), M * self.sync_world
+            T, M = self._sync_rows(self.bn_partial, T, sp.cout, (L.y.shape[1], L.y.shape[2]))
             C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef, None, None, L.coef2,
                               self.red_ws)
         else:
@@ -647,23 +647,50 @@ class UNetExecutor:
             C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
 
     def set_sync_bn(self, group=None, enabled: bool = True):
-        """Share BN batch statistics across the ranks of ``group`` (default: WORLD) in training."""
+        """Share BN batch statistics across the ranks of ``group`` in training.
+
+        Default group: a dedicated copy of WORLD created once per model (collective: every rank calls
+        this in the same order), so the small per-layer statistics all-reduces get their own RCCL
+        communicator and never queue behind the gradient buckets issued from the wgrad side stream.
+        The ranks' (N, H, W) are all-gathered once here: the global pixel count of every BN layer is
+        static, so ranks with different batch shapes get exact global moments (as torch's
+        SyncBatchNorm, which gathers per-rank counts) without a per-layer host round trip."""
         import torch.distributed as dist
         if enabled and dist.is_available() and dist.is_initialized():
+            if group is None:
+                group = self.m.__dict__.get("_sync_bn_group")
+                if group is None:
+                    group = dist.new_group()
+                    self.m.__dict__["_sync_bn_group"] = group
             self.sync_group, self.sync_world = group, dist.get_world_size(group)
+            shp = torch.tensor([self.N, self.H, self.W], dtype=torch.int64)
+            if dist.get_backend(group) != "gloo":
+                shp = shp.to(self.dev)
+            shapes = [torch.zeros_like(shp) for _ in range(self.sync_world)]
+            dist.all_gather(shapes, shp, group=group)
+            self._sync_m = {}
+            for lvl, (h, w) in enumerate(self.sizes):
+                tot = 0
+                for t in shapes:
+                    n, hh, ww = (int(v) for v in t.tolist())
+                    for _ in range(lvl):
+                        hh, ww = hh // 2, ww // 2
+                    tot += n * hh * ww
+                self._sync_m[(h, w)] = tot
         else:
             self.sync_group, self.sync_world = None, 1
 
-    def _sync_rows(self, buf: torch.Tensor, rows: int, c: int) -> int:
+    def _sync_rows(self, buf: torch.Tensor, rows: int, c: int, hw: Tuple[int, int]) -> Tuple[int, int]:
         """Fold ``rows`` partial [2][C] rows of ``buf`` into row 0 (fp64 sum), all-reduce it over the
-        sync group and return 1 (the row count the finalize kernels then read)."""
+        sync group and return (1, global pixel count at spatial size ``hw``): the row count the
+        finalize kernels then read and the pixels the reduced sums cover."""
         import torch.distributed as dist
         tot = buf[: rows * 2 * c].view(rows, 2 * c).sum(0, dtype=torch.float64)
         if dist.get_backend(self.sync_group) == "gloo":  # host round trip (gloo tests: ranks share a GPU)
             tot = tot.cpu()
         dist.all_reduce(tot, group=self.sync_group)
         buf[: 2 * c].copy_(tot)
-        return 1
+        return 1, self._sync_m[hw]
 
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream

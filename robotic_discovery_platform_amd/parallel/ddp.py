@@ -15,6 +15,10 @@ Design (MI355X-first):
     ring all-reduce moves 2(n-1)/n of the bucket per GPU, so ~16 MB buckets (≈4-5 per step) keep
     every bucket well above the latency-bound regime while still giving backward-overlap.
   * The 1/world averaging is folded into the fused Adam kernel (gscale), not a separate pass.
+  * ``comm_dtype=torch.bfloat16`` (SURVEY.md §7.4 option): each ready bucket is cast into a bf16
+    mirror of the gradient buffer on the producing stream and all-reduced there (half the xGMI bytes:
+    34.5 MB instead of 69 MB per step for the bilinear U-Net); ``finish()`` widens the reduced sums
+    back into the fp32 buffer, so Adam still accumulates its moments and the master in fp32.
 """
 from __future__ import annotations
 
@@ -34,10 +38,13 @@ class FlatBucketer:
     """Reverse-order contiguous gradient buckets over a flat buffer."""
 
     def __init__(self, grad_flat: torch.Tensor, param_ranges: Sequence[Tuple[str, int, int]],
-                 bucket_mb: float = 16.0, group=None):
+                 bucket_mb: float = 16.0, group=None, comm_dtype: Optional[torch.dtype] = None):
         self.grad = grad_flat
         self.group = group
-        elt = grad_flat.element_size()
+        self.comm_dtype = comm_dtype if comm_dtype not in (None, grad_flat.dtype) else None
+        # bf16 mirror of the whole gradient buffer (buckets are slices of it, like of ``grad``)
+        self.comm = torch.empty_like(grad_flat, dtype=self.comm_dtype) if self.comm_dtype is not None else None
+        elt = (self.comm if self.comm is not None else grad_flat).element_size()
         cap = max(1, int(bucket_mb * 1024 * 1024 / elt))
         # walk parameters in reverse registration order, cutting at parameter boundaries
         self.buckets: List[Tuple[int, int]] = []
@@ -79,24 +86,31 @@ class FlatBucketer:
         self.pending = [len(p) for p in self.bucket_params]
         self.handles = []
 
+    def _launch(self, b: int):
+        lo, hi = self.buckets[b]
+        buf = self.grad[lo:hi]
+        if self.comm is not None:
+            buf = self.comm[lo:hi]
+            buf.copy_(self.grad[lo:hi])  # narrowing cast on the stream that produced the gradients
+        self.handles.append((b, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
+
     def mark_ready(self, names: Iterable[str]):
         for n in names:
             b = self.param_bucket[n]
             self.pending[b] -= 1
             if self.pending[b] == 0:
-                lo, hi = self.buckets[b]
-                self.handles.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                                    async_op=True))
+                self._launch(b)
 
     def finish(self):
         for b, p in enumerate(self.pending):  # anything never marked (unused params) goes now
             if p > 0:
-                lo, hi = self.buckets[b]
                 self.pending[b] = 0
-                self.handles.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                                    async_op=True))
-        for h in self.handles:
-            h.wait()
+                self._launch(b)
+        for b, h in self.handles:
+            h.wait()  # the caller's stream now waits for the collective (RCCL: no host block)
+            if self.comm is not None:
+                lo, hi = self.buckets[b]
+                self.grad[lo:hi].copy_(self.comm[lo:hi])  # widen the reduced sums back to fp32
         self.handles = []
 
 

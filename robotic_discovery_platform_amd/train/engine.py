@@ -42,23 +42,36 @@ class NativeTrainer:
     GRAPH_AUTO_MAX_PIXELS = 0
 
     def __init__(self, model: UNetNative, batch: int, h: int, w: int, lr: float = 1e-4, loss: str = "bce",
-                 dice_weight: float = 1.0, graph="auto", bucket_mb: float = 16.0, sync_bn: bool = False):
+                 dice_weight: float = 1.0, graph="auto", bucket_mb: float = 16.0, sync_bn: bool = False,
+                 grad_comm: Optional[str] = None, ddp_force: Optional[bool] = None):
         self.model = model
         self.ex = model.executor(batch, h, w, training=True, loss=loss, dice_weight=dice_weight)
         self.opt = NativeAdam(model, lr=lr)
         self.rank, self.world = dist_info()
         self.bucketer = None
-        if self.world > 1:
+        # DDP machinery (broadcast, bucketer, side-stream hooks, gscale) also at world == 1 when forced
+        # (RDP_DDP_FORCE=1): exercises the RCCL path on a single GPU (all_reduce over one rank)
+        if ddp_force is None:
+            ddp_force = os.environ.get("RDP_DDP_FORCE", "0") != "0"
+        # gradient all-reduce dtype: "fp32" (default) or "bf16" (half the bytes; fp32 accumulate in Adam)
+        grad_comm = grad_comm or os.environ.get("RDP_GRAD_COMM", "fp32")
+        if grad_comm not in ("fp32", "bf16"):
+            raise ValueError(f"grad_comm must be 'fp32' or 'bf16', got {grad_comm!r}")
+        self.grad_comm = grad_comm
+        import torch.distributed as dist
+        self.ddp = self.world > 1 or (bool(ddp_force) and dist.is_available() and dist.is_initialized())
+        if self.ddp:
             st = model.store
             broadcast_module_state([st.flat] + [b for _, b in model.named_buffers()])
             model.refresh_weights()
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
-            self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb)
+            self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb,
+                                         comm_dtype=torch.bfloat16 if grad_comm == "bf16" else None)
             self._layer_params = {sp.name: sp.param_names() for sp in list(model.specs) + list(model.up_specs)}
             self.ex.set_sync_bn(enabled=sync_bn)
         if graph == "auto":
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
-        self.use_graph = bool(graph) and self.world == 1 and torch.cuda.is_available()
+        self.use_graph = bool(graph) and not self.ddp and torch.cuda.is_available()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.stream = None
         if torch.cuda.is_available() and model.store.device.type == "cuda" and \
@@ -192,13 +205,15 @@ class EagerTrainer:
 
 
 def build_bench_step(batch: int, size: int, decoder: str, device: torch.device, world: int, graph: bool,
-                     bucket_mb: float, loss: str = "bce", sync_bn: bool = False):
+                     bucket_mb: float, loss: str = "bce", sync_bn: bool = False, grad_comm: str = "fp32",
+                     ddp_force: bool = False):
     """bench.py hook: returns a zero-arg callable running one full native training step."""
     bilinear = decoder == "bilinear"
     torch.manual_seed(0)
     ref = UNetRef(3, 1, bilinear=bilinear)
     model = UNetNative(3, 1, bilinear=bilinear, device=device, init_from=ref)
-    tr = NativeTrainer(model, batch, size, size, loss=loss, graph=graph, bucket_mb=bucket_mb, sync_bn=sync_bn)
+    tr = NativeTrainer(model, batch, size, size, loss=loss, graph=graph, bucket_mb=bucket_mb, sync_bn=sync_bn,
+                       grad_comm=grad_comm, ddp_force=ddp_force)
     g = torch.Generator(device="cpu").manual_seed(1234 + tr.rank)
     x = torch.rand(batch, 3, size, size, generator=g).to(device)
     y = (torch.rand(batch, 1, size, size, generator=g) > 0.5).float().to(device)

@@ -65,7 +65,7 @@ class _NativeRunner:
         if key not in self._trainers:
             tr = self._cls(self.model, n, h, w, lr=self.cfg.learning_rate, loss=self.cfg.loss,
                            dice_weight=self.cfg.dice_weight, graph=self.cfg.graph, bucket_mb=self.cfg.grad_bucket_mb,
-                           sync_bn=self.cfg.sync_bn)
+                           sync_bn=self.cfg.sync_bn, grad_comm=self.cfg.grad_comm)
             tr.opt = self._shared_opt
             self._trainers[key] = tr
         return self._trainers[key]
@@ -164,7 +164,7 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
     ref = UNetRef(3, 1, bilinear=cfg.bilinear, depth=cfg.model_depth)
     if backend == "native":
         from ..models.unet import UNetNative
-        model = UNetNative(3, 1, depth=cfg.model_depth, device=dev, init_from=ref)
+        model = UNetNative(3, 1, bilinear=cfg.bilinear, depth=cfg.model_depth, device=dev, init_from=ref)
         runner = _NativeRunner(model, cfg)
     else:
         model = ref.to(dev)

@@ -8,6 +8,7 @@ Errors are re-raised tagged with the rank so a failing replica is identifiable i
 from __future__ import annotations
 
 import contextlib
+import datetime
 import os
 from typing import Optional, Tuple
 
@@ -15,7 +16,19 @@ import torch
 import torch.distributed as dist
 
 
-def init_distributed(backend: Optional[str] = None) -> Tuple[int, int, torch.device]:
+def dist_timeout(seconds: Optional[float] = None) -> datetime.timedelta:
+    """Process-group timeout (``RDP_DIST_TIMEOUT_S``, default 600 s): a rank that dies or hangs makes
+    the others' collectives fail with an error after this long instead of blocking forever (the
+    torchrun agent then tears the job down and ``--resume auto`` relaunches from the checkpoint)."""
+    if seconds is None:
+        seconds = float(os.environ.get("RDP_DIST_TIMEOUT_S", "600"))
+    return datetime.timedelta(seconds=float(seconds))
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None,
+                     force: bool = False) -> Tuple[int, int, torch.device]:
+    """Join the job's process group. ``force=True`` also initialises a 1-rank group (world == 1), so
+    the RCCL code paths (bucketed all-reduce, stream semantics) run on a single GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -24,11 +37,24 @@ def init_distributed(backend: Optional[str] = None) -> Tuple[int, int, torch.dev
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         be = backend or os.environ.get("RDP_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
-        dist.init_process_group(backend=be, device_id=dev if be == "nccl" else None)
+        with rank_tagged_errors():
+            dist.init_process_group(backend=be, rank=rank, world_size=world, timeout=dist_timeout(timeout_s),
+                                    device_id=dev if be == "nccl" else None)
     return rank, world, dev
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def shutdown_distributed() -> None:

@@ -72,25 +72,65 @@ def test_flat_bucketer_allreduce(tmp_path):
     assert json.load(open(out))["nbuckets"] > 1
 
 
+def _bucketer_bf16_worker(rank, world, out):
+    """bf16 comm mirror: buckets are narrowed to bf16, summed over the ranks, widened back."""
+    from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer
+    sizes = [5, 300, 17, 1024, 64, 3, 700]
+    ranges, off = [], 0
+    for i, n in enumerate(sizes):
+        ranges.append((f"p{i}", off, off + n))
+        off += n
+    gen = torch.Generator().manual_seed(rank)
+    src = torch.randn(off, generator=gen)
+    g = src.clone()
+    b = FlatBucketer(g, ranges, bucket_mb=1200 * 2 / 2 ** 20, comm_dtype=torch.bfloat16)
+    assert b.comm is not None and b.comm.dtype == torch.bfloat16
+    b.reset()
+    for n, _, _ in reversed(ranges):
+        b.mark_ready([n])
+    b.finish()
+    assert g.dtype == torch.float32
+    allsrc = [torch.zeros_like(src) for _ in range(world)]
+    dist.all_gather(allsrc, src)
+    exact = sum(allsrc)
+    # each rank's share is rounded to bf16 once, the sum once more (2 ranks)
+    mag = sum(a.abs() for a in allsrc)
+    assert ((g - exact).abs() <= 2 ** -7 * mag + 1e-6).all(), (g - exact).abs().max()
+    assert torch.equal(g, sum(a.bfloat16().float() for a in allsrc).bfloat16().float())
+    if rank == 0:
+        json.dump({"nbuckets": len(b.buckets)}, open(out, "w"))
+
+
+def test_flat_bucketer_bf16_comm(tmp_path):
+    out = str(tmp_path / "r.json")
+    _run(_bucketer_bf16_worker, 2, out)
+    assert json.load(open(out))["nbuckets"] > 1
+
+
 # ----------------------------------------------------------------------------- SyncBN row fold
 def _syncbn_rows_worker(rank, world):
-    """UNetExecutor._sync_rows: T partial [2][C] rows per rank -> row 0 = sum over rows and ranks."""
+    """UNetExecutor._sync_rows: T partial [2][C] rows per rank -> row 0 = sum over rows and ranks;
+    set_sync_bn gathers the ranks' (N, H, W) once, so unequal per-rank batches get exact counts."""
     from types import SimpleNamespace
     from robotic_discovery_platform_amd.models.unet import UNetExecutor
     C, T = 8, 5
-    ex = SimpleNamespace(sync_group=None, sync_world=world)
+    # set_sync_bn: rank r runs batch r + 1 (unequal), 8x8 input, two levels
+    ex = SimpleNamespace(m=SimpleNamespace(), N=rank + 1, H=8, W=8, sizes=[(8, 8), (4, 4)], dev="cpu")
+    UNetExecutor.set_sync_bn(ex)
+    assert ex.sync_world == world and ex.sync_group is not None
+    nsum = sum(r + 1 for r in range(world))
+    assert ex._sync_m == {(8, 8): 64 * nsum, (4, 4): 16 * nsum}
+    grp = ex.sync_group
+    UNetExecutor.set_sync_bn(ex)  # the dedicated group is created once per model
+    assert ex.sync_group is grp
     buf = torch.zeros(64 * 2 * C)
     rows = torch.arange(T * 2 * C, dtype=torch.float32).view(T, 2 * C) * (rank + 1)
     buf[: T * 2 * C] = rows.reshape(-1)
-    assert UNetExecutor._sync_rows(ex, buf, T, C) == 1
-    exp = rows.sum(0) / (rank + 1) * sum(r + 1 for r in range(world))
+    assert UNetExecutor._sync_rows(ex, buf, T, C, (4, 4)) == (1, 16 * nsum)
+    exp = rows.sum(0) / (rank + 1) * nsum
     assert torch.equal(buf[: 2 * C], exp)
-    # set_sync_bn picks the world size of the initialised group; disabled -> local statistics
-    ex2 = SimpleNamespace()
-    UNetExecutor.set_sync_bn(ex2)
-    assert ex2.sync_world == world
-    UNetExecutor.set_sync_bn(ex2, enabled=False)
-    assert ex2.sync_world == 1 and ex2.sync_group is None
+    UNetExecutor.set_sync_bn(ex, enabled=False)
+    assert ex.sync_world == 1 and ex.sync_group is None
 
 
 def test_syncbn_row_fold_allreduce():

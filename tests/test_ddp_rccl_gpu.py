@@ -1,0 +1,119 @@
+"""The native DDP path under the real RCCL backend (``nccl`` on ROCm) on one GPU.
+
+gpurun gives one MI355X, and RCCL refuses two ranks per device, so the 2/4/8-GPU runs are the
+driver's. What CAN run here is a 1-rank ``nccl`` process group with the DDP machinery forced on
+(``ddp_force``): broadcast, the FlatBucketer's async bucket all-reduces issued from the wgrad side
+stream, ``h.wait()`` stream semantics, the bf16 comm mirror and gscale folded into Adam. With one
+rank the all-reduce is an identity, so the result must equal the non-DDP step bit for bit (fp32
+comm) or the bf16-rounded gradients (bf16 comm) -- any stream-ordering bug (a bucket reduced before
+its wgrad finished, Adam reading before the wait) shows up as a mismatch.
+
+Each case runs in a spawned child so the process group never leaks into other tests.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n=4, hw=64, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(n, 3, hw, hw, generator=g), (torch.rand(n, 1, hw, hw, generator=g) > 0.6).float()
+
+
+def _worker(rank, port, comm, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        from robotic_discovery_platform_amd.models.unet import UNetNative
+        from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+        from robotic_discovery_platform_amd.train.engine import NativeTrainer
+        torch.manual_seed(7)
+        nat = UNetNative(3, 1, device=dev, init_from=UNetRef(3, 1))
+        tr = NativeTrainer(nat, 4, 64, 64, lr=1e-3, graph=False, bucket_mb=4.0, ddp_force=True, grad_comm=comm)
+        assert tr.ddp and tr.bucketer is not None and len(tr.bucketer.buckets) >= 4
+        assert tr.ex.side is not None  # hooks fire from the wgrad side stream
+        x, t = _data()
+        tr.set_batch(x.to(dev), t.to(dev))
+        grads = []
+        for _ in range(3):
+            tr.step()
+            grads.append(nat.store.grad.clone())
+        torch.cuda.synchronize()
+        torch.save({"flat": nat.store.flat.cpu(), "grads": [g.cpu() for g in grads]}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _plain(comm):
+    """Same 3 steps without DDP; for bf16 comm the gradient is rounded to bf16 before each Adam."""
+    from robotic_discovery_platform_amd.models.unet import NativeAdam, UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(7)
+    nat = UNetNative(3, 1, device=dev, init_from=UNetRef(3, 1))
+    ex = nat.executor(4, 64, 64, training=True)
+    opt = NativeAdam(nat, lr=1e-3)
+    x, t = _data()
+    ex.set_input(x.to(dev), t.to(dev))
+    grads = []
+    for _ in range(3):
+        ex.forward()
+        ex.backward()
+        if comm == "bf16":
+            nat.store.grad.copy_(nat.store.grad.to(torch.bfloat16).float())
+        grads.append(nat.store.grad.clone())
+        opt.step()
+    torch.cuda.synchronize()
+    return nat.store.flat.cpu(), [g.cpu() for g in grads]
+
+
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_rccl_world1_ddp_step_matches_plain_step(tmp_path, comm):
+    out = str(tmp_path / f"ddp_{comm}.pt")
+    mp.spawn(_worker, args=(_free_port(), comm, out), nprocs=1, join=True)
+    got = torch.load(out, weights_only=True)
+    flat, grads = _plain(comm)
+    for i, (a, b) in enumerate(zip(got["grads"], grads)):
+        assert torch.equal(a, b), f"step {i}: grads differ (max {float((a - b).abs().max()):.3g})"
+    assert torch.equal(got["flat"], flat)
+
+
+def _bench_worker(rank, port, out):
+    """bench.py's own --ddp-force path: 1-rank nccl group, bf16 comm, JSON line reports it."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_PORT=str(port), RDP_NO_BUILD="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--batch", "4", "--steps", "3", "--warmup",
+                        "1", "--serve", "0", "--ddp-force", "1", "--grad-comm", "bf16"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    with open(out, "w") as f:
+        f.write(r.stdout + "\n__RC__%d\n" % r.returncode + r.stderr[-2000:])
+
+
+def test_bench_ddp_force_reports_rccl_path(tmp_path):
+    import json
+    out = str(tmp_path / "bench.txt")
+    _bench_worker(0, _free_port(), out)
+    txt = open(out).read()
+    assert "__RC__0" in txt, txt
+    line = [ln for ln in txt.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["config"]["grad_comm"] == "bf16" and res["n_gpus"] == 1 and res["value"] > 0
