@@ -64,6 +64,9 @@ int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
 double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
+int rdp_geo_spline_res_len(int);
+int rdp_geo_spline(const double*, int, int, const int*, const int*, const int*, double*, int*, double*, int, double,
+                   int, int, double, int, int, double*, hipStream_t);
 }
 
 namespace {
@@ -567,6 +570,28 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
   TORCH_CHECK(r >= 0, "geo_edges: nbins must be in [1, 128]");
 }
 
+// on-device spline stage: per-bin sort of the edge points (out/kout from geo_edges) + FITPACK-equivalent
+// fit + nsamp-point evaluation and curvature into res (rdp_geo_spline_res_len(nsamp) doubles)
+void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor hdr, torch::Tensor npts, torch::Tensor sorted,
+                torch::Tensor gperm, torch::Tensor u, torch::Tensor res, double s, int k, int nsamp, double eps,
+                int min_points, int min_edge) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(2) == 4 &&
+              out.is_contiguous(), "out [nbins][kcap][4] f64");
+  TORCH_CHECK(kout.scalar_type() == torch::kInt32 && kout.numel() >= out.size(0), "kout");
+  TORCH_CHECK(hdr.scalar_type() == torch::kInt32 && npts.scalar_type() == torch::kInt32, "hdr/npts int32");
+  TORCH_CHECK(sorted.scalar_type() == torch::kFloat64 && sorted.dim() == 2 && sorted.size(1) == 3 &&
+              sorted.is_contiguous(), "sorted [ecap][3] f64");
+  const int ecap = sorted.size(0);
+  TORCH_CHECK(gperm.scalar_type() == torch::kInt32 && gperm.numel() >= 2L * ecap, "gperm: 2*ecap int32");
+  TORCH_CHECK(u.scalar_type() == torch::kFloat64 && u.numel() >= ecap, "u: ecap f64");
+  TORCH_CHECK(res.scalar_type() == torch::kFloat64 && res.numel() >= rdp_geo_spline_res_len(nsamp), "res");
+  const int r = rdp_geo_spline(out.data_ptr<double>(), out.size(0), out.size(1), kout.data_ptr<int>(),
+                               hdr.data_ptr<int>(), npts.data_ptr<int>(), sorted.data_ptr<double>(),
+                               gperm.data_ptr<int>(), u.data_ptr<double>(), ecap, s, k, nsamp, eps, min_points,
+                               min_edge, res.data_ptr<double>(), cur_stream());
+  TORCH_CHECK(r == 0, "geo_spline: k must be in [1, 5], nsamp in [1, 256]");
+}
+
 int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
 long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 
@@ -640,6 +665,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("parcur", &parcur);
   m.def("geo_edges", &geo_edges);
   m.def("geo_nblocks", &geo_nblocks);
+  m.def("geo_spline", &geo_spline);
+  m.def("geo_spline_res_len", &rdp_geo_spline_res_len);
   m.def("geo_work_ints", &geo_work_ints);
   m.def("preprocess", &preprocess);
   m.def("mask_upsample", &mask_upsample);

@@ -7,11 +7,12 @@ dataclasses, same early-exit and failure semantics), executed MI355X-first:
   GPU (csrc/geometry.hip, graph-capturable):  masked-depth deprojection + row-major stream
       compaction (fp64) -> x min/max -> 50-bin top-5 %-by-y edge selection (radix select, exact
       tie-breaking) -> packed edge points
-  host (csrc/spline.cpp):  sort by x, FITPACK-equivalent parametric smoothing spline (s = 0.1,
-      k = 3), 100-sample curvature |r' x r''| / |r'|^3 and spline points
-
-The spline stage has <= ~15 coefficients per dimension: it is latency-bound on
-any GPU, so it runs on the host right after the (small) edge-point read-back.
+  GPU (csrc/geo_spline.hip, graph-capturable):  per-bin sort by x, FITPACK-equivalent parametric
+      smoothing spline (s = 0.1, k = 3; banded normal equations reduced over the points in
+      parallel, FITPACK's knot / smoothing-parameter control flow on one thread), 100-sample
+      splev + curvature |r' x r''| / |r'|^3 -> a 308-double result (status, kappa mean/max, points)
+  host (csrc/spline.cpp):  the exact FITPACK port -- the CPU path, the test oracle, and the
+      fallback for the rare fit that needs more than the device's 64 coefficients per dimension
 """
 from __future__ import annotations
 
@@ -63,6 +64,25 @@ def fit_edges(pts_sorted: np.ndarray, cfg: GeometryConfig, n_points: int) -> Cur
                            n_points, E)
 
 
+# device result status codes (csrc/geo_spline.hip)
+_DEV_STATUS = {0: "ok", 1: "too_few_points", 2: "too_few_edge_points", 3: "fit_failed"}
+DEV_NEEDS_HOST = 4
+
+
+def result_from_device(res: np.ndarray, cfg: GeometryConfig) -> Optional[CurvatureResult]:
+    """CurvatureResult from the device result vector; None when the fit must finish on the host."""
+    st = int(res[0])
+    if st == DEV_NEEDS_HOST:
+        return None
+    E, npts = int(res[6]), int(res[7])
+    if st != 0:
+        return CurvatureResult(status=_DEV_STATUS.get(st, "fit_failed"), n_points=npts,
+                               n_edge_points=E if st != 1 else 0)
+    p = res[8:8 + 3 * cfg.num_samples].reshape(-1, 3)
+    return CurvatureResult(float(res[4]), float(res[5]), [Point(float(a), float(b), float(c)) for a, b, c in p],
+                           "ok", npts, E)
+
+
 def edges_numpy(mask, depth, K, scale, cfg: GeometryConfig) -> Tuple[np.ndarray, int]:
     """CPU edge extraction with the kernels' exact semantics (used where no GPU is present)."""
     v, u = np.nonzero(mask > 0)
@@ -111,6 +131,11 @@ class GeometryEngine:
         ecap = ecap or (self.cfg.num_bins + int(H * W * self.cfg.top_k_percent) + 1)
         self.edges = torch.zeros(ecap, 4, dtype=torch.float64, device=device)
         self.hdr = torch.zeros(1, dtype=torch.int32, device=device)
+        # on-device spline stage: x-sorted edge points, merge scratch, chord parameters, result
+        self.sorted = torch.zeros(ecap, 3, dtype=torch.float64, device=device)
+        self.gperm = torch.zeros(2 * ecap, dtype=torch.int32, device=device)
+        self.u = torch.zeros(ecap, dtype=torch.float64, device=device)
+        self.res = torch.zeros(self.C.geo_spline_res_len(self.cfg.num_samples), dtype=torch.float64, device=device)
 
     def launch(self, mask_dev: torch.Tensor, depth_dev: torch.Tensor, K: np.ndarray, scale: float):
         """Enqueue the edge extraction on the current stream (no host sync; graph-capturable)."""
@@ -118,6 +143,21 @@ class GeometryEngine:
         self.C.geo_edges(mask_dev, depth_dev, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]),
                          float(scale), self.work_i, self.work_d, self.pts, self.npts, self.out, self.kout, c.num_bins,
                          c.top_k_percent, c.min_points, self.edges, self.hdr)
+
+    def launch_spline(self):
+        """Enqueue the on-device spline stage after ``launch`` (no host sync; graph-capturable)."""
+        c = self.cfg
+        self.C.geo_spline(self.out, self.kout, self.hdr, self.npts, self.sorted, self.gperm, self.u, self.res,
+                          c.smoothing, c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points)
+
+    def finish_device(self, res_host: np.ndarray) -> CurvatureResult:
+        """Result of ``launch_spline`` (``res`` read back); a fit beyond the device capacity is redone
+        on the host from the device-sorted edge points (synchronous read-back, rare)."""
+        r = result_from_device(res_host, self.cfg)
+        if r is not None:
+            return r
+        E, npts = int(res_host[6]), int(res_host[7])
+        return fit_edges(self.sorted[:E].cpu().numpy(), self.cfg, npts)
 
     def finish(self, edges_host: np.ndarray, E: int, n_points: int) -> CurvatureResult:
         if n_points < self.cfg.min_points:
@@ -127,8 +167,10 @@ class GeometryEngine:
 
 def compute_curvature_profile(mask: np.ndarray, depth_image: np.ndarray, intrinsics: np.ndarray,
                               depth_scale: float, cfg: Optional[GeometryConfig] = None,
-                              device: Optional[torch.device] = None) -> CurvatureResult:
-    """Reference-signature entry point (numpy in, CurvatureResult out)."""
+                              device: Optional[torch.device] = None, spline: str = "device") -> CurvatureResult:
+    """Reference-signature entry point (numpy in, CurvatureResult out). On a GPU the spline stage
+    runs on the device (``spline="device"``) or on the host from the device's edge points
+    (``spline="host"``, the FITPACK-exact oracle path)."""
     cfg = cfg or GeometryConfig()
     K = np.asarray(intrinsics, dtype=np.float64)
     use_gpu = torch.cuda.is_available() if device is None else torch.device(device).type == "cuda"
@@ -143,6 +185,9 @@ def compute_curvature_profile(mask: np.ndarray, depth_image: np.ndarray, intrins
     m = torch.from_numpy(np.ascontiguousarray(mask.astype(np.uint8))).to(dev)
     d = torch.from_numpy(np.ascontiguousarray(depth_image.astype(np.uint16)).view(np.int16)).to(dev)
     eng.launch(m, d, K, depth_scale)
+    if spline == "device":
+        eng.launch_spline()
+        return eng.finish_device(eng.res.cpu().numpy())
     n = int(eng.npts.item())
     E = int(eng.hdr.item())
     return eng.finish(eng.edges[:min(E, eng.edges.shape[0])].cpu().numpy(), E, n)

@@ -10,8 +10,9 @@ resize -> numpy/scipy geometry -> coverage) with one device program per frame:
     head_mask       1x1 head + (logit > 0) -> u8 256x256        csrc/head_loss.hip
     mask_upsample   nearest -> HxW u8 + nnz count               csrc/serve_kernels.hip
     geo_edges       deproject + compaction + 50-bin top-5 %     csrc/geometry.hip
-    pinned D2H (mask, edge points, counters)
-    host            x-sort + FITPACK-equivalent spline + curvature    csrc/spline.cpp
+    geo_spline      per-bin x-sort, FITPACK-equivalent spline fit, 100-sample splev + curvature
+                                                                csrc/geo_spline.hip
+    pinned D2H (mask, 308-double curvature result, counters)
 
 The device part between the copies is captured once into a hipGraph (torch.cuda.CUDAGraph) and
 replayed per frame, so a frame costs one graph launch plus three copies instead of ~90 kernel
@@ -115,7 +116,7 @@ class FramePipeline:
         self.h_color = torch.empty(H, W, 3, dtype=torch.uint8, pin_memory=True)
         self.h_depth = torch.empty(H, W, dtype=torch.int16, pin_memory=True)
         self.h_mask = torch.empty(H, W, dtype=torch.uint8, pin_memory=True)
-        self.h_edges = torch.empty(ecap, 4, dtype=torch.float64, pin_memory=True)
+        self.h_res = torch.empty(self.geo.res.numel(), dtype=torch.float64, pin_memory=True)
         self.h_meta = torch.empty(4, dtype=torch.int32, pin_memory=True)
         self.ev0 = torch.cuda.Event(enable_timing=True)
         self.ev1 = torch.cuda.Event(enable_timing=True)
@@ -135,6 +136,7 @@ class FramePipeline:
                     self.thr_logit, self.m256)
         C.mask_upsample(self.m256.view(self.S, self.S), self.mask, self.meta[0:1])
         self.geo.launch(self.mask, self.d_depth, self.K, self.scale)
+        self.geo.launch_spline()
         self.meta[1:2].copy_(self.geo.hdr)
         self.meta[2:3].copy_(self.geo.npts)
 
@@ -172,7 +174,7 @@ class FramePipeline:
             else:
                 self._device_program()
             self.h_mask.copy_(self.mask, non_blocking=True)
-            self.h_edges.copy_(self.geo.edges, non_blocking=True)
+            self.h_res.copy_(self.geo.res, non_blocking=True)
             self.h_meta.copy_(self.meta, non_blocking=True)
             self.ev1.record(s)
 
@@ -181,9 +183,9 @@ class FramePipeline:
         with trace.range("serve.frame.wait_gpu"):
             self.ev1.synchronize()
         t1 = time.perf_counter()
-        count, E, npts = (int(v) for v in self.h_meta.numpy()[:3])
-        with trace.range("serve.frame.spline_fit"):
-            res = self.geo.finish(self.h_edges.numpy(), E, npts)
+        count = int(self.h_meta.numpy()[0])
+        with trace.range("serve.frame.spline_fit"):  # device result -> CurvatureResult (host fit only as fallback)
+            res = self.geo.finish_device(self.h_res.numpy())
         t2 = time.perf_counter()
         cov = 100.0 * count / (self.H * self.W)
         return FrameResult(self.h_mask.numpy().copy(), cov, res,

@@ -120,9 +120,18 @@ def test_geometry_kernels_match_oracle(seed):
     eo = eo[np.argsort(eo[:, 0], kind="stable")]
     got = sort_edges(eng.edges[:E].cpu().numpy())
     assert E == eo.shape[0] and np.array_equal(got, eo)
-    r = compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001, device="cuda")
+    r = compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001, device="cuda")  # on-device spline
+    h = compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001, device="cuda", spline="host")
     x = ref.compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001)
-    assert r.status == x.status and r.mean_curvature == pytest.approx(x.mean_curvature, rel=1e-7)
+    for got in (r, h):
+        assert got.status == x.status and got.mean_curvature == pytest.approx(x.mean_curvature, rel=1e-7)
+        assert got.max_curvature == pytest.approx(x.max_curvature, rel=1e-7)
+        assert len(got.spline_points) == len(x.spline_points)
+        if x.spline_points:
+            a = np.array([[q.x, q.y, q.z] for q in got.spline_points])
+            b = np.array([[q.x, q.y, q.z] for q in x.spline_points])
+            assert np.abs(a - b).max() < 1e-9
+    assert r.n_edge_points == E and r.n_points == n
 
 
 def test_geometry_early_exits():
