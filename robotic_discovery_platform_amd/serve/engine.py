@@ -23,6 +23,7 @@ hosts without a GPU and for the loopback tests.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import math
 import queue
@@ -207,9 +208,20 @@ class CpuFramePipeline:
         self.H, self.W, self.S, self.thr = H, W, size, threshold
         self.cfg = geo_cfg or GeometryConfig()
         self.lock = threading.Lock()
+        self._pending = None
 
     def refresh_weights(self):
         pass  # the torch module reads its parameters directly
+
+    def submit(self, color_bgr: np.ndarray, depth: np.ndarray):
+        if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
+            raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
+        self._pending = (color_bgr, depth)
+
+    def collect(self) -> FrameResult:
+        color_bgr, depth = self._pending
+        self._pending = None
+        return self.process(color_bgr, depth)
 
     def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
         import torch.nn.functional as F
@@ -228,47 +240,92 @@ class CpuFramePipeline:
                                              "fit_ms": (time.perf_counter() - t1) * 1e3})
 
 
+def replicate_model(model, device: torch.device):
+    """A copy of ``model`` on ``device`` (same architecture, weights and BN statistics)."""
+    if _is_native(model):
+        from ..models.unet import UNetNative
+        rep = UNetNative(model.n_channels, model.n_classes, bilinear=model.bilinear, base_width=model.base_width,
+                         depth=model.depth, device=device)
+        rep.load_state_dict({k: v.detach() for k, v in model.state_dict().items()})
+        return rep.eval()
+    import copy
+    return copy.deepcopy(model).to(device).eval()
+
+
 class EnginePool:
-    """N per-frame pipelines shared by the server's worker threads (one checked out per frame)."""
+    """Per-frame pipelines for the server's streams, with one model replica per GPU.
+
+    * ``devices`` (SURVEY.md §2.4 serving concurrency): one replica of the weights per listed GPU,
+      each with its own ``n`` pipelines (executor buffers, HIP stream, hipGraph) per frame size.
+      Streams are assigned to replicas round-robin when they open (``session()``); replicas never
+      communicate, so N GPUs serve N times the streams.
+    * ``session()`` gives a stream double-buffering: frame i+1 is staged and replayed on a second
+      pipeline (own stream) while frame i's result is still on the device, so H2D, graph and D2H of
+      consecutive frames overlap and the host tail of frame i overlaps the GPU work of frame i+1.
+    """
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
-                 threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None):
+                 threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
+                 devices=None):
         self.model = model
         self.args = dict(K=K, depth_scale=depth_scale, size=size, threshold=threshold, geo_cfg=geo_cfg)
         self.graph = graph
-        self.n = n
+        self.n = max(1, n)
         self.gpu = _is_native(model)
+        home = _model_device(model)
+        devs = [torch.device(d) for d in (devices or [home])]
+        self.devices = devs
+        self.replicas = [model if devs[i] == home and i == 0 else replicate_model(model, devs[i])
+                         for i in range(len(devs))]
         self._pools = {}
         self._mk_lock = threading.Lock()
-        self._get(H, W)
+        self._rr = 0
+        self.sessions_opened = [0] * len(self.replicas)
+        for r in range(len(self.replicas)):
+            self._get(r, H, W)
 
-    def _new(self, H, W):
+    def _new(self, r: int, H, W):
+        m = self.replicas[r]
         if self.gpu:
-            return FramePipeline(self.model, H=H, W=W, graph=self.graph, **self.args)
-        return CpuFramePipeline(self.model, H=H, W=W, **self.args)
+            return FramePipeline(m, H=H, W=W, graph=self.graph, device=self.devices[r], **self.args)
+        return CpuFramePipeline(m, H=H, W=W, **self.args)
 
-    def _get(self, H, W) -> "queue.Queue":
+    def _get(self, r: int, H, W) -> "queue.Queue":
         with self._mk_lock:
-            q = self._pools.get((H, W))
+            q = self._pools.get((r, H, W))
             if q is None:
                 q = queue.Queue()
                 for _ in range(self.n):
-                    q.put(self._new(H, W))
-                self._pools[(H, W)] = q
+                    q.put(self._new(r, H, W))
+                self._pools[(r, H, W)] = q
             return q
+
+    def session(self) -> "EngineSession":
+        """A per-stream handle bound to the next replica (round-robin)."""
+        with self._mk_lock:
+            r = self._rr % len(self.replicas)
+            self._rr += 1
+            self.sessions_opened[r] += 1
+        return EngineSession(self, r)
 
     @contextlib.contextmanager
     def exclusive(self):
-        """Hold every pipeline (no frame in flight), e.g. while weights are swapped in place;
-        yields the held pipelines."""
+        """Hold every pipeline of every replica (no frame in flight), e.g. while weights are swapped
+        in place; yields the held pipelines."""
         with self._mk_lock:
-            qs = list(self._pools.values())
-            held = [(q, q.get()) for q in qs for _ in range(self.n)]
+            held = [(q, q.get()) for q in self._pools.values() for _ in range(self.n)]
             try:
                 yield [p for _, p in held]
             finally:
                 for q, p in held:
                     q.put(p)
+
+    def load_state_dict(self, sd):
+        """Hot reload: copy new weights into every replica (call inside ``exclusive()``)."""
+        for m in self.replicas:
+            m.load_state_dict(sd)
+            if hasattr(m, "refresh_weights"):
+                m.refresh_weights()
 
     @staticmethod
     def refresh_weights(pipelines):
@@ -277,12 +334,69 @@ class EnginePool:
             p.refresh_weights()
 
     def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
-        q = self._get(*depth.shape[:2])
-        p = q.get()
+        """One frame, synchronously, on the next replica."""
+        s = self.session()
+        s.submit(color_bgr, depth)
+        return s.drain()[0][1]
+
+
+class EngineSession:
+    """One stream's view of the pool: up to ``depth`` frames in flight on its replica's pipelines.
+
+    ``submit`` never blocks while this session holds a pipeline: if none is free it first collects
+    its own oldest frame (returned to the caller), so concurrent sessions cannot deadlock."""
+
+    def __init__(self, pool: EnginePool, replica: int, depth: int = 2):
+        self.pool, self.replica, self.depth = pool, replica, max(1, depth)
+        self.inflight: "collections.deque" = collections.deque()
+
+    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, tag=None) -> list:
+        """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect."""
+        out = []
+        while len(self.inflight) >= self.depth:
+            out.append(self._collect_one())
+        q = self.pool._get(self.replica, *depth.shape[:2])
         try:
-            return p.process(color_bgr, depth)
+            p = q.get_nowait()
+        except queue.Empty:
+            while self.inflight:  # free our own pipelines before waiting on others'
+                out.append(self._collect_one())
+            p = q.get()
+        try:
+            p.submit(color_bgr, depth)
+        except Exception as e:
+            q.put(p)
+            out.append((tag, e))
+            return out
+        self.inflight.append((tag, p, q))
+        return out
+
+    def _collect_one(self):
+        tag, p, q = self.inflight.popleft()
+        try:
+            return tag, p.collect()
+        except Exception as e:  # a failed frame must not take the pipeline with it
+            return tag, e
         finally:
             q.put(p)
+
+    def collect_oldest(self) -> list:
+        return [self._collect_one()] if self.inflight else []
+
+    def drain(self) -> list:
+        out = []
+        while self.inflight:
+            out.append(self._collect_one())
+        return out
+
+
+def _model_device(model) -> torch.device:
+    if _is_native(model):
+        return model.store.device
+    try:
+        return next(model.parameters()).device
+    except (StopIteration, AttributeError):
+        return torch.device("cpu")
 
 
 def _is_native(model) -> bool:

@@ -106,28 +106,49 @@ def registry_version(store, uri: str) -> Optional[str]:
 
 
 class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
+    """Per-stream pipeline: decode (codec pool, runs ahead) -> engine session (double-buffered on one
+    GPU replica) -> response encode (codec pool), responses in request order.
+
+    Failure semantics: the reference ends the stream with ``StatusCode.INTERNAL`` + one empty
+    response on any exception (server.py:154-158); that stays the behaviour for transport errors and
+    with ``frame_errors="abort"``. With the default ``frame_errors="degrade"`` a frame that cannot be
+    decoded or analysed (truncated PNG, corrupt JPEG, size mismatch, ...) gets a response with
+    ``status="error: ..."`` and zero curvature, and the stream goes on. ``faults`` is an optional
+    ``FaultInjector`` (tests / chaos runs) that corrupts requests before decoding.
+    """
+
     def __init__(self, engine: EnginePool, metrics: Optional[MetricsLog] = None, prefetch: int = 4,
-                 decode_workers: int = 8):
+                 decode_workers: int = 8, frame_errors: str = "degrade", faults=None):
         self.engine = engine
         self.metrics = metrics
         self.prefetch = prefetch
+        self.frame_errors = frame_errors
+        self.faults = faults
         self.frames = 0
+        self.frame_failures = 0
+        self._stats_lock = threading.Lock()
+        self.queue_ms: "collections.deque" = collections.deque(maxlen=4096)  # request read -> processing start
+        self.proc_ms: "collections.deque" = collections.deque(maxlen=4096)  # processing start -> response ready
         # shared host-codec pool: JPEG / 16-bit PNG decodes release the GIL, so colour and depth of a
         # frame, and up to `prefetch` frames of a stream, decode concurrently
         self._pool = futures.ThreadPoolExecutor(max_workers=decode_workers, thread_name_prefix="rdp-decode")
 
     def _decoded(self, request_iterator):
-        """Yield (t0, colour, depth, more) in request order; decoding runs ahead on the codec pool.
+        """Yield (t_read, colour, depth, error, more) in request order; decoding runs ahead on the
+        codec pool. ``error`` is the decode exception of a bad frame (colour/depth None then);
         ``more()`` tells whether the client has already sent the next frame."""
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         END = object()
 
         def reader():
             try:
-                for req in request_iterator:
+                for i, req in enumerate(request_iterator):
                     t = time.perf_counter()
-                    fc = self._pool.submit(decode_image, req.color_image.data, True)
-                    fd = self._pool.submit(decode_image, req.depth_image.data, False)
+                    cb, db = req.color_image.data, req.depth_image.data
+                    if self.faults is not None:
+                        cb, db = self.faults.corrupt_request(i, cb, db)
+                    fc = self._pool.submit(decode_image, cb, True)
+                    fd = self._pool.submit(decode_image, db, False)
                     q.put((t, fc, fd, None))
             except Exception as e:  # surface transport errors in the handler thread
                 q.put((None, None, None, e))
@@ -142,7 +163,13 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             if item[3] is not None:
                 raise item[3]
             t, fc, fd, _ = item
-            yield t, fc.result(), fd.result(), lambda: q.qsize() > 0
+            try:
+                color, depth = fc.result(), fd.result()
+                err = None
+            except Exception as e:
+                color = depth = None
+                err = e
+            yield t, color, depth, err, lambda: q.qsize() > 0
 
     def close(self) -> None:
         """Stop the codec pool (its threads must not outlive the gRPC server at interpreter exit)."""
@@ -150,38 +177,68 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
 
     def analyze_frame(self, color: np.ndarray, depth: np.ndarray, t0: Optional[float] = None):
         t0 = time.perf_counter() if t0 is None else t0
-        resp, r = self._respond(self._process(color, depth), t0)
+        resp, r = self._respond(self._process(color, depth), (t0, t0))
         self._log(resp, r)
         return resp
 
+    @staticmethod
+    def _as_u16(depth: np.ndarray) -> np.ndarray:
+        return depth if depth.dtype == np.uint16 else depth.astype(np.uint16)
+
     def _process(self, color: np.ndarray, depth: np.ndarray):
-        if depth.dtype != np.uint16:
-            depth = depth.astype(np.uint16)
-        return self.engine.process(color, depth)
+        return self.engine.process(color, self._as_u16(depth))
 
     def _log(self, resp, r):
-        if self.metrics is not None:
+        if self.metrics is not None and r is not None:
             self.metrics.write(resp.mean_curvature, resp.max_curvature, r.coverage)
         self.frames += 1
 
-    def _respond(self, r, t0: float):
-        """FrameResult -> AnalysisResponse (PNG-encoded mask); runs on the codec pool when streaming."""
-        c = r.curvature
-        resp = pb.AnalysisResponse(mean_curvature=c.mean_curvature, max_curvature=c.max_curvature, status=c.status,
-                                   mask_coverage=r.coverage)
-        if c.spline_points:
-            resp.spline_points.extend([pb.Point3D(x=p.x, y=p.y, z=p.z) for p in c.spline_points])
-        resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1)
-        resp.proc_time_ms = (time.perf_counter() - t0) * 1e3
+    def _respond(self, r, t):
+        """FrameResult (or the frame's exception) -> AnalysisResponse; runs on the codec pool when
+        streaming. ``t`` = (request read, processing start): proc_time_ms is the server's processing
+        time of this frame (decode wait excluded), the queueing before it is kept separately."""
+        t_read, t_start = t
+        if isinstance(r, Exception):
+            resp = pb.AnalysisResponse(status=f"error: {type(r).__name__}: {r}"[:200])
+            r = None
+        else:
+            c = r.curvature
+            resp = pb.AnalysisResponse(mean_curvature=c.mean_curvature, max_curvature=c.max_curvature,
+                                       status=c.status, mask_coverage=r.coverage)
+            if c.spline_points:
+                resp.spline_points.extend([pb.Point3D(x=p.x, y=p.y, z=p.z) for p in c.spline_points])
+            resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1)
+        now = time.perf_counter()
+        resp.proc_time_ms = (now - t_start) * 1e3
+        with self._stats_lock:
+            self.queue_ms.append((t_start - t_read) * 1e3)
+            self.proc_ms.append((now - t_start) * 1e3)
         return resp, r
 
+    def latency_stats(self) -> dict:
+        with self._stats_lock:
+            q, p = list(self.queue_ms), list(self.proc_ms)
+        pct = (lambda v, k: float(np.percentile(v, k)) if v else float("nan"))
+        return {"queue_p50_ms": pct(q, 50), "proc_p50_ms": pct(p, 50), "proc_p99_ms": pct(p, 99),
+                "frames": self.frames, "frame_failures": self.frame_failures}
+
     def AnalyzeActuatorPerformance(self, request_iterator, context):
-        """Per-stream pipeline: decode (codec pool, runs ahead) -> engine (this thread, in order) ->
-        response encode (codec pool). Responses leave in request order; one that is ready -- or any,
-        when the client has not sent the next frame yet (lock-step clients) -- is never held back."""
+        """Responses leave in request order; one that is ready -- or any, when the client has not
+        sent the next frame yet (lock-step clients) -- is never held back."""
         import grpc
         log.info("new analysis stream")
-        inflight: "collections.deque" = collections.deque()
+        inflight: "collections.deque" = collections.deque()  # encode futures, request order
+        sess = self.engine.session()
+        times = {}
+
+        def encode(results):
+            for tag, r in results:
+                if isinstance(r, Exception):
+                    if self.frame_errors == "abort":
+                        raise r
+                    self.frame_failures += 1
+                    log.warning("frame failed (%s: %s): degraded response", type(r).__name__, r)
+                inflight.append(self._pool.submit(self._respond, r, times.pop(tag)))
 
         def ready(force: bool):
             while inflight and (force or inflight[0].done() or len(inflight) > self.prefetch):
@@ -190,11 +247,19 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                 yield resp
 
         try:
-            for t0, color, depth, more in self._decoded(request_iterator):
-                with trace.range("serve.rpc.frame"):
-                    r = self._process(color, depth)
-                inflight.append(self._pool.submit(self._respond, r, t0))
+            for i, (t_read, color, depth, err, more) in enumerate(self._decoded(request_iterator)):
+                t_start = time.perf_counter()
+                times[i] = (t_read, t_start)
+                if err is not None:
+                    encode(sess.drain())  # keep request order: older frames first
+                    encode([(i, err)])
+                else:
+                    with trace.range("serve.rpc.frame"):
+                        encode(sess.submit(color, self._as_u16(depth), tag=i))
+                    if not more():  # lock-step client: finish this frame now
+                        encode(sess.drain())
                 yield from ready(force=not more())
+            encode(sess.drain())
             yield from ready(force=True)
         except Exception as e:
             log.error("unhandled exception during analysis: %s", e)
@@ -227,9 +292,7 @@ class ModelWatcher(threading.Thread):
             return False
         _, sd = mlpt.load_state(uri, self.cfg.mlruns_dir)
         with self.engine.exclusive() as pipelines:
-            self.model.load_state_dict(sd)
-            if hasattr(self.model, "refresh_weights"):
-                self.model.refresh_weights()
+            self.engine.load_state_dict(sd)  # every per-GPU replica
             self.engine.refresh_weights(pipelines)
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
@@ -243,17 +306,31 @@ class ModelWatcher(threading.Thread):
             self.check_once()
 
 
-def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_size: int = 2, port: Optional[int] = None):
+def serving_devices(spec: str, default: Optional[torch.device] = None):
+    """``ServeConfig.devices``: "" -> [default], "all" -> every visible GPU, "0,2" -> those GPUs."""
+    spec = (spec or "").strip()
+    if not spec:
+        return None if default is None else [default]
+    if spec == "all":
+        return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    return [torch.device(d) if not d.strip().isdigit() else torch.device("cuda", int(d)) for d in spec.split(",")]
+
+
+def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_size: Optional[int] = None,
+                 port: Optional[int] = None, faults=None):
     """Create (server, service, watcher, bound_port); None if resources are missing (reference abort)."""
     import grpc
+    devices = serving_devices(cfg.devices)
+    if devices and device is None:
+        device = devices[0]
     model, K, ds, version = load_resources(cfg, device)
     if model is None or K is None or ds is None:
         log.error("FATAL: could not load all required resources")
         return None
     metrics = MetricsLog(cfg.metrics_log)
-    engine = EnginePool(model, K, ds, n=pool_size, threshold=cfg.mask_threshold, graph=cfg.graph,
-                        size=cfg.model_img_size)
-    service = VisionAnalysisService(engine, metrics)
+    engine = EnginePool(model, K, ds, n=pool_size or cfg.replicas_per_device, threshold=cfg.mask_threshold,
+                        graph=cfg.graph, size=cfg.model_img_size, devices=devices)
+    service = VisionAnalysisService(engine, metrics, frame_errors=cfg.frame_errors, faults=faults)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.max_workers))
     pb.add_VisionAnalysisServiceServicer_to_server(service, server)
     bound = server.add_insecure_port(f"{cfg.host}:{cfg.port if port is None else port}")
@@ -265,7 +342,8 @@ def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_s
 
 def serve(cfg: Optional[ServeConfig] = None, block: bool = True):
     cfg = cfg or ServeConfig()
-    out = build_server(cfg)
+    from .faults import from_env
+    out = build_server(cfg, faults=from_env())
     if out is None:
         return None
     server, service, watcher, port = out

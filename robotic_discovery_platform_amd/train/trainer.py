@@ -184,7 +184,9 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
         log.info("Resumed from epoch %d (best val %.4f)", start_epoch, best_val)
 
     history = []
+    from ..utils.launch import maybe_crash
     for epoch in range(start_epoch, cfg.epochs):
+        maybe_crash(epoch, rank)
         t0 = time.time()
         sampler.set_epoch(epoch)
         order = torch.tensor(list(iter(sampler)), dtype=torch.long)

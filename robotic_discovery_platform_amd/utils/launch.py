@@ -69,3 +69,20 @@ def rank_tagged_errors():
         yield
     except Exception as e:
         raise RuntimeError(f"[rank {rank}] {type(e).__name__}: {e}") from e
+
+
+def maybe_crash(epoch: int, rank: Optional[int] = None) -> None:
+    """Fault injection for relaunch tests: ``RDP_FAULT_CRASH="<rank>:<epoch>"`` makes that rank die
+    (``os._exit(17)``, no cleanup, like a killed process) when it reaches the start of that epoch.
+    The surviving ranks then fail their next collective (peer gone / process-group timeout), the
+    launcher tears the job down, and a relaunch with ``--resume auto`` continues from the last
+    epoch checkpoint."""
+    spec = os.environ.get("RDP_FAULT_CRASH", "")
+    if not spec:
+        return
+    r, _, e = spec.partition(":")
+    me = int(os.environ.get("RANK", "0")) if rank is None else rank
+    if int(r) == me and int(e) == epoch:
+        import sys
+        print(f"[rank {me}] RDP_FAULT_CRASH: exiting at epoch {epoch}", file=sys.stderr, flush=True)
+        os._exit(17)

@@ -5,6 +5,10 @@ process, find the newest version in stage "None" with ``get_latest_versions``, t
 ``set_registered_model_alias(name, "staging", version)``. Exceptions are logged (and returned),
 not raised, like the reference. Additions: an optional drift gate (only retrain when the drift
 detector fires) and a ``promote`` callback used to notify a running server (hot reload).
+
+Under torchrun every rank calls this (``train_model`` is collective), but only rank 0 evaluates the
+drift gate (its decision is broadcast so all ranks agree on whether to train) and touches the
+registry alias; the other ranks return after training.
 """
 from __future__ import annotations
 
@@ -25,16 +29,27 @@ def run_retraining_pipeline(cfg: Optional[TrainConfig] = None, alias: str = PROM
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
     log.info("Starting automated retraining pipeline...")
     out = {"promoted": False}
+    from ..parallel.ddp import dist_info
+    rank, world = dist_info()
     try:
         if only_if_drift:
-            from ..monitoring.drift import analyze_drift
-            rep = analyze_drift(only_if_drift, make_plot=False)
+            rep = None
+            if rank == 0:
+                from ..monitoring.drift import analyze_drift
+                rep = analyze_drift(only_if_drift, make_plot=False)
+            if world > 1:
+                import torch.distributed as dist
+                box = [rep]
+                dist.broadcast_object_list(box, src=0)
+                rep = box[0]
             out["drift"] = rep
             if not rep.get("drift_detected"):
                 log.info("No drift detected: skipping retraining.")
                 return out
         res = train_model(cfg)
         out["train"] = res
+        if rank != 0:  # registry writes are rank 0's (train_model already registered there)
+            return out
         uri = cfg.mlruns_dir
         client = mlstore.MlflowClient(uri if "://" in uri else __import__("os").path.abspath(uri))
         latest = client.get_latest_versions(cfg.registered_model_name, stages=["None"])

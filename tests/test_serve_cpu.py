@@ -131,12 +131,14 @@ def test_server_aborts_without_calibration(tmp_path):
     assert build_server(cfg, torch.device("cpu")) is None
 
 
-def test_bad_frame_yields_internal_error(tmp_path):
+def test_bad_frame_abort_mode_is_reference_semantics(tmp_path):
+    """frame_errors="abort": any per-frame exception -> INTERNAL + one empty response, stream ends
+    (/root/reference/services/vision_analysis/server.py:154-158)."""
     import grpc
     from robotic_discovery_platform_amd.proto import vision as pb
     from robotic_discovery_platform_amd.serve.server import build_server
     _setup_store(tmp_path)
-    cfg = _serve_cfg(tmp_path)
+    cfg = _serve_cfg(tmp_path, frame_errors="abort")
     server, _, _, port = build_server(cfg, torch.device("cpu"), pool_size=1)
     server.start()
     try:
@@ -152,6 +154,87 @@ def test_bad_frame_yields_internal_error(tmp_path):
             assert ei.value.code() == grpc.StatusCode.INTERNAL
     finally:
         server.stop(0)
+
+
+def test_fault_injection_degrades_frames_and_stream_survives(tmp_path):
+    """Default frame_errors="degrade": injected bad frames get an error status (or the degenerate-
+    geometry status), the good frames around them are analysed normally, order is preserved."""
+    import grpc
+    from robotic_discovery_platform_amd.proto import vision as pb
+    from robotic_discovery_platform_amd.serve.client import make_request
+    from robotic_discovery_platform_amd.serve.faults import FaultInjector
+    from robotic_discovery_platform_amd.serve.server import build_server
+    _setup_store(tmp_path)
+    cfg = _serve_cfg(tmp_path)
+    fi = FaultInjector({"truncated_png": [1], "empty_color": [2], "zero_depth": [3], "size_mismatch": [4],
+                        "corrupt_jpeg": [6]})
+    server, service, _, port = build_server(cfg, torch.device("cpu"), pool_size=2, faults=fi)
+    server.start()
+    sc = make_scene(1)
+    req = make_request(sc.color, sc.depth)
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+            stub = pb.VisionAnalysisServiceStub(ch)
+            out = list(stub.AnalyzeActuatorPerformance(iter([req] * 8)))
+    finally:
+        server.stop(0)
+    assert len(out) == 8
+    good = out[0].status
+    assert not good.startswith("error")
+    assert out[1].status.startswith("error") and out[2].status.startswith("error")
+    assert out[3].status == "too_few_points" and out[3].mean_curvature == 0 and not out[3].spline_points
+    assert out[4].status.startswith("error: ValueError")
+    assert out[5].status == good and out[7].status == good  # stream kept going
+    assert out[5].mean_curvature == out[0].mean_curvature and out[5].mask == out[0].mask
+    assert fi.injected["truncated_png"] == 1 and fi.injected["corrupt_jpeg"] == 1
+    st = service.latency_stats()
+    assert st["frame_failures"] >= 3 and st["proc_p50_ms"] > 0 and st["queue_p50_ms"] >= 0
+
+
+def test_engine_replicas_round_robin_and_hot_reload():
+    """ServeConfig.devices: one replica per device, streams assigned round-robin, weight reloads reach
+    every replica. (CPU "devices" stand in for GPUs: the pool logic is device-agnostic.)"""
+    from robotic_discovery_platform_amd.serve.engine import EnginePool
+    sc = make_scene(3)
+    m256 = resize_nearest((sc.mask > 0).astype(np.uint8), (256, 256))
+    model = OracleSegmenter(m256)
+    pool = EnginePool(model, DEFAULT_K, 0.001, n=1, devices=["cpu", "cpu", "cpu"])
+    assert len(pool.replicas) == 3 and pool.replicas[0] is model and pool.replicas[1] is not model
+    sess = [pool.session() for _ in range(7)]
+    assert [s.replica for s in sess] == [0, 1, 2, 0, 1, 2, 0] and pool.sessions_opened == [3, 2, 2]
+    ref = sess[0].submit(sc.color, sc.depth, tag="a") + sess[0].drain()
+    for s in sess[1:3]:
+        got = s.submit(sc.color, sc.depth, tag="b") + s.drain()
+        assert np.array_equal(got[0][1].mask, ref[0][1].mask)
+    with pool.exclusive() as held:
+        assert len(held) == 3
+        pool.load_state_dict({"m": torch.zeros(256, 256), "p": torch.ones(1)})
+    assert all(float(r.p) == 1.0 and float(r.m.sum()) == 0 for r in pool.replicas)
+
+
+def test_engine_session_double_buffering_order_and_no_deadlock():
+    from robotic_discovery_platform_amd.serve.engine import EnginePool
+    scenes = [make_scene(i) for i in range(4)]
+    m256 = resize_nearest((scenes[0].mask > 0).astype(np.uint8), (256, 256))
+    pool = EnginePool(OracleSegmenter(m256), DEFAULT_K, 0.001, n=1)  # one pipeline shared by 2 sessions
+    results = {}
+
+    def run(name):
+        s = pool.session()
+        got = []
+        for i in range(6):
+            sc = scenes[i % 4]
+            got += s.submit(sc.color, sc.depth, tag=i)
+        got += s.drain()
+        results[name] = got
+
+    th = [threading.Thread(target=run, args=(k,)) for k in ("x", "y")]
+    [t.start() for t in th]
+    [t.join(timeout=120) for t in th]
+    assert not any(t.is_alive() for t in th)
+    for k in ("x", "y"):
+        assert [t for t, _ in results[k]] == list(range(6))
+        assert all(not isinstance(r, Exception) for _, r in results[k])
 
 
 def test_hot_reload_on_alias_move(tmp_path):
