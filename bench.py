@@ -55,6 +55,9 @@ def parse():
                    help="gradient all-reduce dtype (bf16: half the xGMI bytes, fp32 accumulate in Adam)")
     p.add_argument("--ddp-force", type=int, default=0,
                    help="1: run the DDP path (RCCL process group, bucketed all-reduce hooks) even at world 1")
+    p.add_argument("--extras", type=int, default=-1,
+                   help="also report ref_batch_imgs_per_s (bs 4 step) and train_model_imgs_per_s (train_model on an "
+                        "on-disk synthetic PNG dataset, incl. data gather/H2D); default: on for 1-GPU native runs")
     p.add_argument("--serve", type=int, default=-1,
                    help="also measure e2e serving FPS / p50 latency (default: on for single-GPU runs)")
     return p.parse_args()
@@ -130,6 +133,45 @@ def make_native_step(args, dev, world):
                             sync_bn=bool(args.sync_bn), grad_comm=args.grad_comm, ddp_force=bool(args.ddp_force))
 
 
+def measure_ref_batch(args, dev, steps: int = 50, warmup: int = 10) -> dict:
+    """The reference's batch (bs 4, train_segmenter.py:46) through the same native step."""
+    from robotic_discovery_platform_amd.train.engine import build_bench_step
+    step = build_bench_step(batch=4, size=args.size, decoder=args.decoder, device=dev, world=1, graph="auto",
+                            bucket_mb=args.bucket_mb, loss=args.loss)
+    for _ in range(warmup):
+        step()
+    sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync(dev)
+    dt = time.perf_counter() - t0
+    return {"ref_batch_imgs_per_s": round(4 * steps / dt, 2), "ref_batch_ms_per_step": round(dt / steps * 1e3, 3)}
+
+
+def measure_train_model(args, dev, samples: int = 160, epochs: int = 3) -> dict:
+    """``train_model`` (the train_segmenter.py entry point) on an on-disk synthetic PNG dataset at the
+    reference's batch 4: device-resident data build, per-epoch shuffled batches gathered on the GPU,
+    native steps, eval-mode validation, checkpoints and registry writes. Reports the last epoch's
+    training throughput (validation excluded) and the epoch wall time."""
+    import logging
+    import tempfile
+    from robotic_discovery_platform_amd.config import TrainConfig
+    from robotic_discovery_platform_amd.data.synthetic import write_dataset
+    from robotic_discovery_platform_amd.train.trainer import train_model
+    root = tempfile.mkdtemp(prefix="rdp_bench_tm_")
+    write_dataset(os.path.join(root, "data"), samples, seed=0)
+    logging.getLogger("rdp.train").setLevel(logging.WARNING)
+    cfg = TrainConfig(epochs=epochs, batch_size=4, image_size=args.size, bilinear=args.decoder == "bilinear",
+                      dataset_dir=os.path.join(root, "data"), mlruns_dir=os.path.join(root, "mlruns"),
+                      model_output_dir=os.path.join(root, "models"), backend="native")
+    res = train_model(cfg)
+    last = res["history"][-1]
+    return {"train_model_imgs_per_s": round(last["train_imgs_per_s"], 2),
+            "train_model_epoch_s": round(last["epoch_s"], 4),
+            "train_model_config": f"bs4, {samples} on-disk PNG scenes (80/20 split), epoch {epochs} of {epochs}"}
+
+
 class _Progress:
     """Prints the current phase to stderr every 30 s until the timed region is done (rank 0)."""
 
@@ -170,13 +212,22 @@ def main():
     ms = dt / args.steps * 1e3
     imgs = args.batch * world * args.steps / dt
     extra = {}
+    extras = args.extras if args.extras >= 0 else int(world == 1 and args.impl == "native" and dev.type == "cuda")
+    if extras and rank == 0:
+        progress.phase = "extras (reference batch, train_model)"
+        for fn in (measure_ref_batch, measure_train_model):
+            try:  # never let it break the training result line
+                extra.update(fn(args, dev))
+            except Exception as e:  # pragma: no cover - reported in the JSON
+                extra[fn.__name__ + "_error"] = f"{type(e).__name__}: {e}"
     serve = args.serve if args.serve >= 0 else int(world == 1 and args.impl == "native" and dev.type == "cuda")
     if serve and rank == 0:
+        progress.phase = "serving"
         try:  # second half of the metric; never let it break the training result line
             from robotic_discovery_platform_amd.serve.bench_serve import measure_serving
-            extra = measure_serving(dev)
+            extra.update(measure_serving(dev))
         except Exception as e:  # pragma: no cover - reported in the JSON
-            extra = {"serve_error": f"{type(e).__name__}: {e}"}
+            extra["serve_error"] = f"{type(e).__name__}: {e}"
     if rank == 0:
         out = {
             "metric": METRIC,

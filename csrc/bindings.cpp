@@ -65,6 +65,9 @@ int rdp_parcur(int, int, const double*, const double*, double, int, int, double*
 double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
 int rdp_geo_spline_res_len(int);
+int rdp_area_maxtap();
+int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
+                       const double*, int, int, int, void*, hipStream_t);
 int rdp_geo_spline(const double*, int, int, const int*, const int*, const int*, double*, int*, double*, int, double,
                    int, int, double, int, int, double*, hipStream_t);
 }
@@ -592,6 +595,22 @@ void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor hdr, torch:
   TORCH_CHECK(r == 0, "geo_spline: k must be in [1, 5], nsamp in [1, 256]");
 }
 
+// INTER_AREA resize of one u8 HxWxC image on the device (tables from data/device_data.py)
+void resize_area_u8(torch::Tensor in, torch::Tensor ys, torch::Tensor yn, torch::Tensor yw, torch::Tensor xs,
+                    torch::Tensor xn, torch::Tensor xw, int swap_rb, torch::Tensor out) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == torch::kUInt8 && in.dim() == 3 && in.is_contiguous(), "in u8 HxWxC");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kUInt8 && out.dim() == 3 && out.is_contiguous() &&
+              out.size(2) == in.size(2), "out u8 HxWxC");
+  const int H = out.size(0), W = out.size(1), T = rdp_area_maxtap();
+  TORCH_CHECK(ys.numel() == H && yn.numel() == H && yw.numel() == (long)H * T && xs.numel() == W &&
+              xn.numel() == W && xw.numel() == (long)W * T, "area tables");
+  TORCH_CHECK(ys.scalar_type() == torch::kInt32 && yw.scalar_type() == torch::kFloat64, "table dtypes");
+  const int r = rdp_resize_area_u8(in.data_ptr(), in.size(0), in.size(1), in.size(2), ys.data_ptr<int>(),
+                                   yn.data_ptr<int>(), yw.data_ptr<double>(), xs.data_ptr<int>(), xn.data_ptr<int>(),
+                                   xw.data_ptr<double>(), H, W, swap_rb, out.data_ptr(), cur_stream());
+  TORCH_CHECK(r == 0, "resize_area_u8: C must be 1..4");
+}
+
 int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
 long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 
@@ -666,6 +685,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("geo_edges", &geo_edges);
   m.def("geo_nblocks", &geo_nblocks);
   m.def("geo_spline", &geo_spline);
+  m.def("resize_area_u8", &resize_area_u8);
+  m.def("area_maxtap", &rdp_area_maxtap);
   m.def("geo_spline_res_len", &rdp_geo_spline_res_len);
   m.def("geo_work_ints", &geo_work_ints);
   m.def("preprocess", &preprocess);

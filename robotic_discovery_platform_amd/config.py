@@ -63,6 +63,7 @@ class TrainConfig:
     synthetic_if_missing: bool = True
     synthetic_samples: int = 64
     grad_bucket_mb: float = 16.0
+    device_data: bool = True  # GPU: build the processed dataset once on the device (u8), batches gathered there
     grad_comm: str = "fp32"  # gradient all-reduce dtype: "fp32" or "bf16" (fp32 accumulate in Adam)
     dist_timeout_s: float = 600.0  # process-group timeout: a hung collective fails the job instead of hanging
     sync_bn: bool = False  # share BN batch statistics across DDP ranks (SyncBatchNorm semantics)

@@ -30,6 +30,11 @@ class SegmentationDataset(Dataset):
     def __len__(self) -> int:
         return len(self.ids)
 
+    def raw_arrays(self, idx: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(colour BGR u8 at file size, mask u8 at file size): input of the device-side resizes."""
+        name = self.ids[idx]
+        return imread(os.path.join(self.image_dir, name), color=True), imread_gray(os.path.join(self.mask_dir, name))
+
     def load_arrays(self, idx: int) -> Tuple[np.ndarray, np.ndarray]:
         name = self.ids[idx]
         img = imread(os.path.join(self.image_dir, name), color=True)
@@ -54,6 +59,10 @@ class SyntheticSegmentationDataset(Dataset):
 
     def __len__(self) -> int:
         return self.n
+
+    def raw_arrays(self, idx: int) -> Tuple[np.ndarray, np.ndarray]:
+        s = make_scene(self.seed + idx)
+        return s.color, s.mask
 
     def __getitem__(self, idx: int):
         s = make_scene(self.seed + idx)

@@ -67,9 +67,39 @@ def measure_engine(model, scenes, frames: int = 200, warmup: int = 20):
             gpu.append(r.timings["gpu_ms"])
             fit.append(r.timings["fit_ms"])
             ok += r.curvature.status == "ok"
-    return {"engine_fps": round(1e3 * len(lat) / sum(lat), 1), "engine_p50_ms": round(_pct(lat, 50), 3),
-            "engine_p99_ms": round(_pct(lat, 99), 3), "engine_gpu_p50_ms": round(_pct(gpu, 50), 3),
-            "engine_fit_p50_ms": round(_pct(fit, 50), 3), "engine_ok_frac": ok / max(1, len(lat))}
+    out = {"engine_fps": round(1e3 * len(lat) / sum(lat), 1), "engine_p50_ms": round(_pct(lat, 50), 3),
+           "engine_p99_ms": round(_pct(lat, 99), 3), "engine_gpu_p50_ms": round(_pct(gpu, 50), 3),
+           "engine_fit_p50_ms": round(_pct(fit, 50), 3), "engine_ok_frac": ok / max(1, len(lat))}
+    out.update(measure_engine_pipelined(model, scenes, frames, warmup))
+    return out
+
+
+def measure_engine_pipelined(model, scenes, frames: int = 200, warmup: int = 20, streams: int = 1):
+    """Frames back to back through double-buffered stream sessions (EnginePool.session): frame i+1's
+    H2D + graph overlap frame i's tail. ``streams`` concurrent sessions share the GPU."""
+    from ..data.synthetic import DEFAULT_K
+    from .engine import EnginePool
+    pool = EnginePool(model, DEFAULT_K, 0.001, n=2 * streams, graph=True)
+    res = {}
+
+    def run(k):
+        s = pool.session()
+        for i in range(warmup):
+            sc = scenes[i % len(scenes)]
+            s.submit(sc.color, sc.depth, tag=i)
+        s.drain()
+        t0 = time.perf_counter()
+        for i in range(frames):
+            sc = scenes[i % len(scenes)]
+            s.submit(sc.color, sc.depth, tag=i)
+        s.drain()
+        res[k] = time.perf_counter() - t0
+
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(streams)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    return {f"engine_pipelined_fps{'' if streams == 1 else f'_{streams}streams'}":
+            round(frames * streams / max(res.values()), 1)}
 
 
 def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2):
@@ -112,7 +142,9 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
                     proc.append(resp.proc_time_ms)
             t_end = time.perf_counter()
             out["e2e_fps"] = round(frames / (t_end - t_start), 1)
-            out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)
+            out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)  # processing only (proc_time_ms)
+            st = svc.latency_stats()
+            out["e2e_server_queue_p50_ms"] = round(st["queue_p50_ms"], 3)  # request read -> processing start
             _progress(f"streamed: {out}")
             # lock-step round trip
             q: "queue.Queue" = queue.Queue()

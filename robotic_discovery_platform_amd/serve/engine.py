@@ -353,6 +353,10 @@ class EngineSession:
     def submit(self, color_bgr: np.ndarray, depth: np.ndarray, tag=None) -> list:
         """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect."""
         out = []
+        if color_bgr.ndim != 3 or color_bgr.shape[2] != 3 or color_bgr.shape[:2] != depth.shape[:2]:
+            out += self.drain()  # results stay in submission order
+            out.append((tag, ValueError(f"colour {color_bgr.shape} and depth {depth.shape} frame sizes differ")))
+            return out
         while len(self.inflight) >= self.depth:
             out.append(self._collect_one())
         q = self.pool._get(self.replica, *depth.shape[:2])
@@ -366,6 +370,7 @@ class EngineSession:
             p.submit(color_bgr, depth)
         except Exception as e:
             q.put(p)
+            out += self.drain()
             out.append((tag, e))
             return out
         self.inflight.append((tag, p, q))

@@ -113,10 +113,19 @@ class _EagerRunner:
         self.tr.opt.load_state_dict(sd)
 
 
-def _batches(x: torch.Tensor, y: torch.Tensor, order, bs: int):
+def _batches(x: torch.Tensor, y: torch.Tensor, order, bs: int, dev):
+    """Batches (float NCHW image, float N1HW mask) in ``order``; u8 device-resident data is gathered
+    and converted on the device."""
+    if x.dtype == torch.uint8:
+        from ..data.device_data import batch_to_float
+        order = order.to(x.device)
+        for i in range(0, len(order), bs):
+            idx = order[i:i + bs]
+            yield batch_to_float(x.index_select(0, idx), y.index_select(0, idx))
+        return
     for i in range(0, len(order), bs):
         idx = order[i:i + bs]
-        yield x[idx], y[idx]
+        yield x[idx].to(dev, non_blocking=True), y[idx].to(dev, non_blocking=True)
 
 
 def build_dataset(cfg: TrainConfig):
@@ -152,12 +161,23 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
                             "device": str(dev), "architecture": "UNet", "backend": backend, "world_size": world,
                             "loss": cfg.loss, "dtype": cfg.dtype})
 
-    # ---- data (host tensors; the whole processed dataset fits easily) ----
+    # ---- data ----
+    # GPU: the processed dataset is built once on the device (u8 NHWC; INTER_AREA / nearest resizes
+    # as kernels) and batches are gathered there -- no per-step host work or H2D copy. CPU: host
+    # float tensors (the reference's item format).
     ds = build_dataset(cfg)
     train_set, val_set = split_dataset(ds, cfg.validation_split, cfg.seed)
-    xtr, ytr = preload(ds, train_set.indices)
-    xva, yva = preload(ds, val_set.indices) if len(val_set) else (None, None)
-    log.info("Dataset: %d training, %d validation samples", len(train_set), len(val_set))
+    size = (cfg.image_size, cfg.image_size)
+    device_data = cfg.device_data and dev.type == "cuda" and hasattr(ds, "raw_arrays")
+    if device_data:
+        from ..data.device_data import build_device_dataset
+        xtr, ytr = build_device_dataset(ds, train_set.indices, dev, size)
+        xva, yva = build_device_dataset(ds, val_set.indices, dev, size) if len(val_set) else (None, None)
+    else:
+        xtr, ytr = preload(ds, train_set.indices)
+        xva, yva = preload(ds, val_set.indices) if len(val_set) else (None, None)
+    log.info("Dataset: %d training, %d validation samples (%s)", len(train_set), len(val_set),
+             "device-resident u8" if device_data else "host")
     sampler = DistributedShardSampler(len(train_set), rank, world, shuffle=True, seed=cfg.seed)
 
     # ---- model / engine ----
@@ -192,9 +212,12 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
         order = torch.tensor(list(iter(sampler)), dtype=torch.long)
         tl = torch.zeros((), device=dev)
         nb = 0
-        for xb, yb in _batches(xtr, ytr, order, cfg.batch_size):
-            tl += runner.train_step(xb.to(dev, non_blocking=True), yb.to(dev, non_blocking=True)).float()
+        for xb, yb in _batches(xtr, ytr, order, cfg.batch_size, dev):
+            tl += runner.train_step(xb, yb).float()
             nb += 1
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t_train = time.time() - t0
         if world > 1:
             stats = torch.stack([tl, torch.tensor(float(nb), device=dev)])
             dist.all_reduce(stats)
@@ -202,17 +225,18 @@ def train_model(cfg: Optional[TrainConfig] = None, resume: Optional[str] = None)
         avg_train = float(tl.item()) / max(nb, 1)
         vl, nv = torch.zeros((), device=dev), 0
         if xva is not None and len(xva):
-            for i in range(0, len(xva), cfg.batch_size):
-                vl += runner.eval_loss(xva[i:i + cfg.batch_size].to(dev), yva[i:i + cfg.batch_size].to(dev)).float()
+            for xb, yb in _batches(xva, yva, torch.arange(len(xva)), cfg.batch_size, dev):
+                vl += runner.eval_loss(xb, yb).float()
                 nv += 1
         avg_val = float(vl.item()) / max(nv, 1) if nv else avg_train
         dt = time.time() - t0
-        history.append({"epoch": epoch, "train_loss": avg_train, "val_loss": avg_val, "epoch_s": dt})
+        history.append({"epoch": epoch, "train_loss": avg_train, "val_loss": avg_val, "epoch_s": dt,
+                        "train_s": t_train, "train_imgs_per_s": len(order) * world / max(t_train, 1e-9)})
         if is_main:
             mlstore.log_metric("train_loss", avg_train, step=epoch)
             mlstore.log_metric("val_loss", avg_val, step=epoch)
             mlstore.log_metric("epoch_time_s", dt, step=epoch)
-            mlstore.log_metric("train_imgs_per_s", len(order) * world / max(dt, 1e-9), step=epoch)
+            mlstore.log_metric("train_imgs_per_s", len(order) * world / max(t_train, 1e-9), step=epoch)
             log.info("Epoch %d/%d: train %.4f val %.4f (%.1fs)", epoch + 1, cfg.epochs, avg_train, avg_val, dt)
             if avg_val < best_val:
                 best_val = avg_val
