@@ -110,6 +110,22 @@ def build_device_dataset(ds, indices: Sequence[int], device: torch.device, size:
     return x, y
 
 
+_LUT = {}
+
+
+def _u8_lut(device) -> torch.Tensor:
+    """v / 255 for v in 0..255, divided in fp64 and rounded to fp32 -- exactly the reference's
+    ``image / 255.0`` (numpy float64) followed by ``.float()`` (a GPU tensor division by a scalar
+    multiplies by the reciprocal and can be 1 ulp off)."""
+    key = str(device)
+    if key not in _LUT:
+        _LUT[key] = (torch.arange(256, dtype=torch.float64) / 255.0).to(torch.float32).to(device)
+    return _LUT[key]
+
+
 def batch_to_float(xb: torch.Tensor, yb: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """u8 NHWC RGB + u8 NHW mask -> (float NCHW /255, float N1HW /255): the reference's item format."""
-    return xb.permute(0, 3, 1, 2).float().div_(255.0), yb.unsqueeze(1).float().div_(255.0)
+    lut = _u8_lut(xb.device)
+    x = lut.index_select(0, xb.reshape(-1).int()).view(xb.shape).permute(0, 3, 1, 2)
+    y = lut.index_select(0, yb.reshape(-1).int()).view(yb.shape).unsqueeze(1)
+    return x, y
