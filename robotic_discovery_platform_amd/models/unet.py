@@ -409,6 +409,8 @@ class UNetExecutor:
             ws = max(ws, C.conv_ws_elems(n, h, w, us.cin, 0, 4 * us.cout, 1, 0, 0))
             if training:
                 ws = max(ws, C.conv_ws_elems(n, h, w, 4 * us.cout, 0, us.cin, 1, 0, 0))
+        if os.environ.get("RDP_SPLITK", "1") == "0":  # A/B knob: no split-K (every conv one pass)
+            ws = 0
         self.kws = torch.zeros(ws, dtype=torch.float32, device=dev) if ws else None
         if training:
             self._alloc_backward(C)

@@ -180,15 +180,16 @@ def _progress(msg):
 
 
 def measure_serving(dev: Optional[torch.device] = None, frames: int = 200, warmup: int = 20,
-                    train_steps: int = 200) -> dict:
+                    train_steps: int = 200, e2e: bool = True) -> dict:
     dev = dev or torch.device("cuda")
     model, scenes = prepare_model(dev, train_steps)
     _progress("model ready")
     res = {"serve_frame": "640x480 RGB-D -> 256x256 U-Net", "serve_weights": f"trained {train_steps} steps on synthetic"}
     res.update({"serve_" + k: v for k, v in measure_engine(model, scenes, frames, warmup).items()})
     _progress(f"engine done: {res}")
-    res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup).items()})
-    _progress("e2e done")
+    if e2e:
+        res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup).items()})
+        _progress("e2e done")
     return res
 
 
@@ -199,5 +200,7 @@ if __name__ == "__main__":
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--train-steps", type=int, default=200)
+    ap.add_argument("--e2e", type=int, default=1)
     a = ap.parse_args()
-    print(json.dumps(measure_serving(torch.device("cuda"), a.frames, a.warmup, a.train_steps)), flush=True)
+    print(json.dumps(measure_serving(torch.device("cuda"), a.frames, a.warmup, a.train_steps, bool(a.e2e))),
+          flush=True)
