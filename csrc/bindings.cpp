@@ -20,7 +20,7 @@ int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
 int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
                   double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, hipStream_t);
-int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*,
+int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*, int,
                    int, int, void*, hipStream_t);
 int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
@@ -65,6 +65,10 @@ int rdp_parcur(int, int, const double*, const double*, double, int, int, double*
 double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
 int rdp_geo_spline_res_len(int);
+int rdp_png_info(const uint8_t*, long, int*, int*, int*);
+int rdp_png_decode(const uint8_t*, long, uint8_t*, long);
+long rdp_png_encode_gray8(const uint8_t*, int, int, int, uint8_t*, long);
+long rdp_png_encode_bound(int, int);
 int rdp_area_maxtap();
 int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
                        const double*, int, int, int, void*, hipStream_t);
@@ -611,11 +615,45 @@ void resize_area_u8(torch::Tensor in, torch::Tensor ys, torch::Tensor yn, torch:
   TORCH_CHECK(r == 0, "resize_area_u8: C must be 1..4");
 }
 
+// grayscale 8/16-bit PNG -> u8 / int16 (u16 bits) CPU tensor, decoded without the GIL; None when the
+// PNG is not one this reader handles (or is corrupt): the caller falls back to PIL
+py::object png_decode(py::bytes data) {
+  char* buf = nullptr;
+  Py_ssize_t n = 0;
+  if (PyBytes_AsStringAndSize(data.ptr(), &buf, &n) != 0) throw py::error_already_set();
+  int w = 0, h = 0, bd = 0;
+  if (rdp_png_info((const uint8_t*)buf, n, &w, &h, &bd) != 0) return py::none();
+  auto t = torch::empty({h, w}, torch::TensorOptions().dtype(bd == 16 ? torch::kInt16 : torch::kUInt8));
+  int r;
+  {
+    py::gil_scoped_release nogil;
+    r = rdp_png_decode((const uint8_t*)buf, n, (uint8_t*)t.data_ptr(), (long)t.numel() * t.element_size());
+  }
+  if (r != 0) return py::none();
+  return py::cast(t);
+}
+
+// u8 [H, W] CPU tensor -> 8-bit grayscale PNG bytes (deflate level), encoded without the GIL
+py::bytes png_encode_gray8(torch::Tensor img, int level) {
+  TORCH_CHECK(!img.is_cuda() && img.scalar_type() == torch::kUInt8 && img.dim() == 2 && img.is_contiguous(),
+              "u8 HxW contiguous CPU tensor");
+  const int h = img.size(0), w = img.size(1);
+  std::string out((size_t)rdp_png_encode_bound(w, h), '\0');
+  long len;
+  {
+    py::gil_scoped_release nogil;
+    len = rdp_png_encode_gray8(img.data_ptr<uint8_t>(), w, h, level, (uint8_t*)&out[0], (long)out.size());
+  }
+  TORCH_CHECK(len > 0, "png encode failed");
+  out.resize((size_t)len);
+  return py::bytes(out);
+}
+
 int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
 long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 
 void preprocess(torch::Tensor bgr, torch::Tensor ystart, torch::Tensor ysize, torch::Tensor yw, torch::Tensor xstart,
-                torch::Tensor xsize, torch::Tensor xw, torch::Tensor out) {
+                torch::Tensor xsize, torch::Tensor xw, torch::Tensor out, int rgb) {
   TORCH_CHECK(bgr.is_cuda() && bgr.scalar_type() == torch::kUInt8 && bgr.dim() == 3 && bgr.size(2) == 3 &&
               bgr.is_contiguous(), "bgr u8 HxWx3");
   Act o = act(out, "out");
@@ -624,7 +662,7 @@ void preprocess(torch::Tensor bgr, torch::Tensor ystart, torch::Tensor ysize, to
               xw.numel() == (long)o.W * 16, "aa tables");
   rdp_preprocess(bgr.data_ptr(), bgr.size(0), bgr.size(1), ystart.data_ptr<int>(), ysize.data_ptr<int>(),
                  yw.data_ptr<float>(), xstart.data_ptr<int>(), xsize.data_ptr<int>(), xw.data_ptr<float>(), o.H, o.W,
-                 o.ptr, cur_stream());
+                 rgb, o.ptr, cur_stream());
 }
 
 void mask_upsample(torch::Tensor m, torch::Tensor out, torch::Tensor count) {
@@ -685,11 +723,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("geo_edges", &geo_edges);
   m.def("geo_nblocks", &geo_nblocks);
   m.def("geo_spline", &geo_spline);
+  m.def("png_decode", &png_decode);
+  m.def("png_encode_gray8", &png_encode_gray8);
   m.def("resize_area_u8", &resize_area_u8);
   m.def("area_maxtap", &rdp_area_maxtap);
   m.def("geo_spline_res_len", &rdp_geo_spline_res_len);
   m.def("geo_work_ints", &geo_work_ints);
-  m.def("preprocess", &preprocess);
+  m.def("preprocess", &preprocess, py::arg("bgr"), py::arg("ystart"), py::arg("ysize"), py::arg("yw"),
+        py::arg("xstart"), py::arg("xsize"), py::arg("xw"), py::arg("out"), py::arg("rgb") = 0);
   m.def("mask_upsample", &mask_upsample);
   m.def("splev", &splev);
   m.def("fit_curvature", &fit_curvature);

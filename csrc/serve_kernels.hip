@@ -1,6 +1,7 @@
 // Serving-path pre/post-processing kernels (per frame, graph-capturable).
 //
-// preprocess: replaces torchvision ToTensor() + Resize((256,256), antialias=True) + BGR->RGB of
+// preprocess: replaces torchvision ToTensor() + Resize((256,256), antialias=True) + BGR->RGB (or RGB
+//   input as decoded by the server, rgb = 1) of
 //   /root/reference/services/vision_analysis/server.py:107-110,120-121: u8 BGR HWC -> /255 ->
 //   antialiased bilinear (triangle filter, support = scale, normalized weights, torch
 //   _upsample_bilinear2d_aa semantics; weight tables precomputed on the host) -> bf16 NHWC with
@@ -20,7 +21,7 @@ struct AATable {  // per output index: first input index, number of taps, weight
 __global__ void preprocess_kernel(const uint8_t* __restrict__ bgr, int H, int W, const int* __restrict__ ystart,
                                   const int* __restrict__ ysize, const float* __restrict__ yw,
                                   const int* __restrict__ xstart, const int* __restrict__ xsize,
-                                  const float* __restrict__ xw, int OH, int OW, u16* __restrict__ out) {
+                                  const float* __restrict__ xw, int OH, int OW, int rgb, u16* __restrict__ out) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= OH * OW) return;
   const int oy = o / OW, ox = o - oy * OW;
@@ -39,6 +40,11 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ bgr, int H, int W,
     r += wy * rr;
     g += wy * gg;
     b += wy * bb;
+  }
+  if (rgb) {  // input already RGB (the server decodes JPEG straight to RGB): channels 0 / 2 swap roles
+    const float t = r;
+    r = b;
+    b = t;
   }
   const float inv = 1.0f / 255.0f;
   uint4 v;
@@ -78,10 +84,11 @@ __global__ void zero_u32_kernel(unsigned* p, int n) {
 
 extern "C" {
 int rdp_preprocess(const void* bgr, int H, int W, const int* ystart, const int* ysize, const float* yw,
-                   const int* xstart, const int* xsize, const float* xw, int OH, int OW, void* out, hipStream_t s) {
+                   const int* xstart, const int* xsize, const float* xw, int OH, int OW, int rgb, void* out,
+                   hipStream_t s) {
   const int n = OH * OW;
   hipLaunchKernelGGL(preprocess_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)bgr, H, W, ystart,
-                     ysize, yw, xstart, xsize, xw, OH, OW, (u16*)out);
+                     ysize, yw, xstart, xsize, xw, OH, OW, rgb, (u16*)out);
   return 0;
 }
 

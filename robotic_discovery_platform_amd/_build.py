@@ -87,7 +87,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     if force or tasks or not os.path.exists(OUT) or os.path.getmtime(OUT) < _newest(objs):
         link = ["g++", "-shared", "-o", OUT] + objs + [
             f"-L{tlib}", f"-L{os.path.join(ROCM, 'lib')}", f"-Wl,-rpath,{tlib}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}",
-            "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
+            "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lz"]
         _run(link)
         if verbose:
             print(f"[rdp build] linked {OUT}", flush=True)

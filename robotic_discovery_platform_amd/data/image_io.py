@@ -6,8 +6,9 @@ Reference uses of OpenCV:
     ``cv2.imencode('.png', mask*255)`` (server.py:142).
   * ``cv2.resize(INTER_AREA)`` for training images, ``INTER_NEAREST`` for masks
     (train_segmenter.py:86,90) and for the served mask (server.py:125).
-Codecs go through PIL (JPEG/PNG incl. 16-bit PNG). Arrays keep OpenCV's conventions: colour
-images are HxWx3 uint8 **BGR**, depth is HxW uint16.
+Codecs: grayscale 8/16-bit PNG (depth in, mask out: the per-frame serving codecs) go through the
+native zlib codec (csrc/codecs.cpp, no GIL held); JPEG and every other PNG flavour through PIL.
+Arrays keep OpenCV's conventions: colour images are HxWx3 uint8 **BGR**, depth is HxW uint16.
 """
 from __future__ import annotations
 
@@ -26,8 +27,24 @@ def encode_jpeg(bgr: np.ndarray, quality: int = 95) -> bytes:
     return buf.getvalue()
 
 
+_PNG_SIG = b"\x89PNG\r\n\x1a\n"
+
+
+def _native():
+    try:
+        from ..ops import native
+        return native()
+    except Exception:  # pragma: no cover - no extension: PIL only
+        return None
+
+
 def encode_png(arr: np.ndarray, compress_level: int = 6) -> bytes:
     """PNG of uint8 gray, uint8 BGR (stored as RGB) or uint16 gray (lossless 16-bit)."""
+    if arr.ndim == 2 and arr.dtype == np.uint8:
+        C = _native()
+        if C is not None:
+            import torch
+            return C.png_encode_gray8(torch.from_numpy(np.ascontiguousarray(arr)), int(compress_level))
     buf = io.BytesIO()
     kw = dict(format="PNG", compress_level=compress_level)
     if arr.dtype == np.uint16:
@@ -39,11 +56,20 @@ def encode_png(arr: np.ndarray, compress_level: int = 6) -> bytes:
     return buf.getvalue()
 
 
-def decode_image(data: bytes, color: bool = True) -> np.ndarray:
-    """IMREAD_COLOR -> HxWx3 uint8 BGR; color=False -> IMREAD_UNCHANGED (uint8 or uint16 gray)."""
+def decode_image(data: bytes, color: bool = True, order: str = "BGR") -> np.ndarray:
+    """IMREAD_COLOR -> HxWx3 uint8 BGR (``order="RGB"``: RGB, skipping the channel flip for consumers
+    that take either order); color=False -> IMREAD_UNCHANGED (uint8 or uint16 gray)."""
+    if not color and data[:8] == _PNG_SIG:
+        C = _native()
+        t = C.png_decode(bytes(data)) if C is not None else None
+        if t is not None:
+            a = t.numpy()
+            return a.view(np.uint16) if a.dtype == np.int16 else a
     im = Image.open(io.BytesIO(data))
     if color:
-        return np.asarray(im.convert("RGB"))[..., ::-1].copy()
+        im.load()
+        rgb = np.asarray(im if im.mode == "RGB" else im.convert("RGB"))
+        return rgb if order == "RGB" else rgb[..., ::-1].copy()
     if im.mode in ("I;16", "I;16B", "I;16L", "I"):
         return np.asarray(im, dtype=np.uint16).copy() if im.mode != "I" else np.asarray(im).astype(np.uint16)
     if im.mode == "L":

@@ -121,17 +121,19 @@ class FramePipeline:
         self.h_meta = torch.empty(4, dtype=torch.int32, pin_memory=True)
         self.ev0 = torch.cuda.Event(enable_timing=True)
         self.ev1 = torch.cuda.Event(enable_timing=True)
-        self.graph = None
+        self.graphs = {}  # channel order of the staged colour frame (0 BGR, 1 RGB) -> hipGraph
+        self.use_graph = graph
         self.lock = threading.Lock()
+        self._rgb = 0
         if graph:
-            self._capture()
+            self._capture(0)
         else:
             self.refresh_weights()
 
     # ---------------------------------------------------------------- device program
-    def _device_program(self):
+    def _device_program(self, rgb: int = 0):
         C, ex, m = self.C, self.ex, self.model
-        C.preprocess(self.d_color, *self.tab, ex.x_in)
+        C.preprocess(self.d_color, *self.tab, ex.x_in, rgb)
         ex.forward(head=False, refresh_eval=False)  # BN-fold coefficients: see refresh_weights()
         C.head_mask(ex.final, m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
                     self.thr_logit, self.m256)
@@ -148,19 +150,25 @@ class FramePipeline:
             self.ex.prepare_eval()
         self.stream.synchronize()
 
-    def _capture(self):
-        self.refresh_weights()
+    @property
+    def graph(self):
+        return self.graphs.get(0)
+
+    def _capture(self, rgb: int):
+        if not self.graphs:
+            self.refresh_weights()
         with torch.cuda.stream(self.stream):
-            self._device_program()  # warm-up (lazy allocations, kernel loading)
+            self._device_program(rgb)  # warm-up (lazy allocations, kernel loading)
         self.stream.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
-            self._device_program()
-        self.graph = g
+            self._device_program(rgb)
+        self.graphs[rgb] = g
 
     # ---------------------------------------------------------------- per frame
-    def submit(self, color_bgr: np.ndarray, depth: np.ndarray):
-        """Stage a frame and enqueue its device work; returns immediately (call ``collect``)."""
+    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, rgb: bool = False):
+        """Stage a frame and enqueue its device work; returns immediately (call ``collect``).
+        ``rgb``: the colour frame is RGB (as the server decodes it), not OpenCV's BGR."""
         if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
         self.h_color.numpy()[...] = color_bgr
@@ -170,10 +178,14 @@ class FramePipeline:
             self.ev0.record(s)
             self.d_color.copy_(self.h_color, non_blocking=True)
             self.d_depth.copy_(self.h_depth, non_blocking=True)
-            if self.graph is not None:
-                self.graph.replay()
+            if self.use_graph:
+                g = self.graphs.get(int(rgb))
+                if g is None:  # first frame in this channel order: capture its graph (stream-ordered)
+                    self._capture(int(rgb))
+                    g = self.graphs[int(rgb)]
+                g.replay()
             else:
-                self._device_program()
+                self._device_program(int(rgb))
             self.h_mask.copy_(self.mask, non_blocking=True)
             self.h_res.copy_(self.geo.res, non_blocking=True)
             self.h_meta.copy_(self.meta, non_blocking=True)
@@ -213,10 +225,10 @@ class CpuFramePipeline:
     def refresh_weights(self):
         pass  # the torch module reads its parameters directly
 
-    def submit(self, color_bgr: np.ndarray, depth: np.ndarray):
+    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, rgb: bool = False):
         if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
-        self._pending = (color_bgr, depth)
+        self._pending = (color_bgr[..., ::-1] if rgb else color_bgr, depth)
 
     def collect(self) -> FrameResult:
         color_bgr, depth = self._pending
@@ -350,8 +362,9 @@ class EngineSession:
         self.pool, self.replica, self.depth = pool, replica, max(1, depth)
         self.inflight: "collections.deque" = collections.deque()
 
-    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, tag=None) -> list:
-        """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect."""
+    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, tag=None, rgb: bool = False) -> list:
+        """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect.
+        ``rgb``: the colour frame is in RGB order (else OpenCV BGR)."""
         out = []
         if color_bgr.ndim != 3 or color_bgr.shape[2] != 3 or color_bgr.shape[:2] != depth.shape[:2]:
             out += self.drain()  # results stay in submission order
@@ -367,7 +380,7 @@ class EngineSession:
                 out.append(self._collect_one())
             p = q.get()
         try:
-            p.submit(color_bgr, depth)
+            p.submit(color_bgr, depth, rgb)
         except Exception as e:
             q.put(p)
             out += self.drain()

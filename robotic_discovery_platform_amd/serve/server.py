@@ -147,7 +147,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     cb, db = req.color_image.data, req.depth_image.data
                     if self.faults is not None:
                         cb, db = self.faults.corrupt_request(i, cb, db)
-                    fc = self._pool.submit(decode_image, cb, True)
+                    fc = self._pool.submit(decode_image, cb, True, "RGB")  # no BGR flip: the engine takes RGB
                     fd = self._pool.submit(decode_image, db, False)
                     q.put((t, fc, fd, None))
             except Exception as e:  # surface transport errors in the handler thread
@@ -255,7 +255,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     encode([(i, err)])
                 else:
                     with trace.range("serve.rpc.frame"):
-                        encode(sess.submit(color, self._as_u16(depth), tag=i))
+                        encode(sess.submit(color, self._as_u16(depth), tag=i, rgb=True))
                     if not more():  # lock-step client: finish this frame now
                         encode(sess.drain())
                 yield from ready(force=not more())
