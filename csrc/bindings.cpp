@@ -19,7 +19,8 @@ long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
 int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
-                  double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, hipStream_t);
+                  double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, const void*, int, int,
+                  int*, hipStream_t);
 int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*, int,
                    int, int, void*, hipStream_t);
 int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
@@ -72,8 +73,8 @@ long rdp_png_encode_bound(int, int);
 int rdp_area_maxtap();
 int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
                        const double*, int, int, int, void*, hipStream_t);
-int rdp_geo_spline(const double*, int, int, const int*, const int*, const int*, double*, int*, double*, int, double,
-                   int, int, double, int, int, double*, hipStream_t);
+int rdp_geo_spline(const double*, int, int, const int*, const int*, double*, int*, double*, int, double, int, int,
+                   double, int, int, const int*, int, double*, hipStream_t);
 }
 
 namespace {
@@ -555,9 +556,12 @@ py::tuple fit_curvature(torch::Tensor pts, double s, int k, int nsamp, double ep
 }
 
 // geometry: mask u8 [H,W], depth u16-as-int16 [H,W] (GPU) -> packed edge points; returns E via hdr (device)
+// m256 (serving form): mask is an OUTPUT (nearest upsample of the model mask) and cov[nblk] gets the
+// per-row-block coverage counts; edges None: no packed edge list (hdr untouched)
 void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, double cx, double cy, double scale,
                torch::Tensor work_i, torch::Tensor work_d, torch::Tensor pts, torch::Tensor npts, torch::Tensor out,
-               torch::Tensor kout, int nbins, double top, int min_points, torch::Tensor edges, torch::Tensor hdr) {
+               torch::Tensor kout, int nbins, double top, int min_points, c10::optional<torch::Tensor> edges,
+               c10::optional<torch::Tensor> hdr, c10::optional<torch::Tensor> m256, c10::optional<torch::Tensor> cov) {
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == torch::kUInt8 && mask.dim() == 2 && mask.is_contiguous(), "mask");
   TORCH_CHECK(depth.is_cuda() && depth.element_size() == 2 && depth.sizes() == mask.sizes() && depth.is_contiguous(),
               "depth u16");
@@ -568,34 +572,61 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
   TORCH_CHECK(work_d.numel() >= 2 * nblk && work_d.scalar_type() == torch::kFloat64, "work_d");
   TORCH_CHECK(pts.scalar_type() == torch::kFloat64 && pts.numel() >= (long)H * W * 4, "pts cap");
   TORCH_CHECK(out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(0) >= nbins && out.size(2) == 4, "out");
-  TORCH_CHECK(edges.scalar_type() == torch::kFloat64 && edges.dim() == 2 && edges.size(1) == 4, "edges");
+  const bool pack = edges && edges->defined();
+  if (pack) {
+    TORCH_CHECK(edges->scalar_type() == torch::kFloat64 && edges->dim() == 2 && edges->size(1) == 4, "edges");
+    TORCH_CHECK(hdr && hdr->defined() && hdr->scalar_type() == torch::kInt32, "hdr int32");
+  }
+  const void* mp = nullptr;
+  int mh = 0, mw = 0;
+  int* covp = nullptr;
+  if (m256 && m256->defined()) {
+    TORCH_CHECK(m256->is_cuda() && m256->scalar_type() == torch::kUInt8 && m256->dim() == 2 && m256->is_contiguous(),
+                "m256 u8 2-D");
+    TORCH_CHECK(cov && cov->defined() && cov->scalar_type() == torch::kInt32 && cov->numel() >= nblk,
+                "cov: geo_nblocks(H) int32");
+    mp = m256->data_ptr();
+    mh = m256->size(0);
+    mw = m256->size(1);
+    covp = cov->data_ptr<int>();
+  }
   const int r = rdp_geo_edges(mask.data_ptr(), depth.data_ptr(), H, W, fx, fy, cx, cy, scale, work_i.data_ptr<int>(),
                               work_d.data_ptr<double>(), work_d.data_ptr<double>() + nblk, pts.data_ptr<double>(), H * W,
                               npts.data_ptr<int>(), out.data_ptr<double>(), out.size(1), kout.data_ptr<int>(), nbins,
-                              top, min_points, edges.data_ptr<double>(), edges.size(0), hdr.data_ptr<int>(),
-                              cur_stream());
+                              top, min_points, pack ? edges->data_ptr<double>() : nullptr, pack ? edges->size(0) : 0,
+                              pack ? hdr->data_ptr<int>() : nullptr, mp, mh, mw, covp, cur_stream());
   TORCH_CHECK(r >= 0, "geo_edges: nbins must be in [1, 128]");
 }
 
+int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
+long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
+
 // on-device spline stage: per-bin sort of the edge points (out/kout from geo_edges) + FITPACK-equivalent
 // fit + nsamp-point evaluation and curvature into res (rdp_geo_spline_res_len(nsamp) doubles)
-void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor hdr, torch::Tensor npts, torch::Tensor sorted,
-                torch::Tensor gperm, torch::Tensor u, torch::Tensor res, double s, int k, int nsamp, double eps,
-                int min_points, int min_edge) {
+void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch::Tensor sorted, torch::Tensor gperm,
+                torch::Tensor u, torch::Tensor res, double s, int k, int nsamp, double eps, int min_points,
+                int min_edge, c10::optional<torch::Tensor> cov) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(2) == 4 &&
               out.is_contiguous(), "out [nbins][kcap][4] f64");
   TORCH_CHECK(kout.scalar_type() == torch::kInt32 && kout.numel() >= out.size(0), "kout");
-  TORCH_CHECK(hdr.scalar_type() == torch::kInt32 && npts.scalar_type() == torch::kInt32, "hdr/npts int32");
+  TORCH_CHECK(npts.scalar_type() == torch::kInt32, "npts int32");
   TORCH_CHECK(sorted.scalar_type() == torch::kFloat64 && sorted.dim() == 2 && sorted.size(1) == 3 &&
               sorted.is_contiguous(), "sorted [ecap][3] f64");
   const int ecap = sorted.size(0);
   TORCH_CHECK(gperm.scalar_type() == torch::kInt32 && gperm.numel() >= 2L * ecap, "gperm: 2*ecap int32");
   TORCH_CHECK(u.scalar_type() == torch::kFloat64 && u.numel() >= ecap, "u: ecap f64");
   TORCH_CHECK(res.scalar_type() == torch::kFloat64 && res.numel() >= rdp_geo_spline_res_len(nsamp), "res");
+  const int* covp = nullptr;
+  int ncov = 0;
+  if (cov && cov->defined()) {
+    TORCH_CHECK(cov->scalar_type() == torch::kInt32, "cov int32");
+    covp = cov->data_ptr<int>();
+    ncov = cov->numel();
+  }
   const int r = rdp_geo_spline(out.data_ptr<double>(), out.size(0), out.size(1), kout.data_ptr<int>(),
-                               hdr.data_ptr<int>(), npts.data_ptr<int>(), sorted.data_ptr<double>(),
-                               gperm.data_ptr<int>(), u.data_ptr<double>(), ecap, s, k, nsamp, eps, min_points,
-                               min_edge, res.data_ptr<double>(), cur_stream());
+                               npts.data_ptr<int>(), sorted.data_ptr<double>(), gperm.data_ptr<int>(),
+                               u.data_ptr<double>(), ecap, s, k, nsamp, eps, min_points, min_edge, covp, ncov,
+                               res.data_ptr<double>(), cur_stream());
   TORCH_CHECK(r == 0, "geo_spline: k must be in [1, 5], nsamp in [1, 256]");
 }
 
@@ -649,8 +680,6 @@ py::bytes png_encode_gray8(torch::Tensor img, int level) {
   return py::bytes(out);
 }
 
-int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
-long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 
 void preprocess(torch::Tensor bgr, torch::Tensor ystart, torch::Tensor ysize, torch::Tensor yw, torch::Tensor xstart,
                 torch::Tensor xsize, torch::Tensor xw, torch::Tensor out, int rgb) {
@@ -720,9 +749,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wprep", &wprep);
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
-  m.def("geo_edges", &geo_edges);
+  m.def("geo_edges", &geo_edges, py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),
+        py::arg("cy"), py::arg("scale"), py::arg("work_i"), py::arg("work_d"), py::arg("pts"), py::arg("npts"),
+        py::arg("out"), py::arg("kout"), py::arg("nbins"), py::arg("top"), py::arg("min_points"),
+        py::arg("edges") = py::none(), py::arg("hdr") = py::none(), py::arg("m256") = py::none(),
+        py::arg("cov") = py::none());
   m.def("geo_nblocks", &geo_nblocks);
-  m.def("geo_spline", &geo_spline);
+  m.def("geo_spline", &geo_spline, py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
+        py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
+        py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none());
   m.def("png_decode", &png_decode);
   m.def("png_encode_gray8", &png_encode_gray8);
   m.def("resize_area_u8", &resize_area_u8);

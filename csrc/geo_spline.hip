@@ -32,7 +32,8 @@
 //
 // res layout (doubles): [0] status (0 ok, 1 too few points, 2 too few edge points, 3 fit failed =
 // FITPACK invalid input, 4 needs host: beyond the device knot capacity), [1] ier, [2] n knots,
-// [3] fp, [4] mean kappa, [5] max kappa, [6] E edge points, [7] valid points, [8..] nsamp x 3 points.
+// [3] fp, [4] mean kappa, [5] max kappa, [6] E edge points, [7] valid points, [8..] nsamp x 3 points,
+// [8 + 3 nsamp] mask coverage count (serving form; -1 without coverage input).
 #include "common.h"
 #include <stdint.h>
 
@@ -441,15 +442,29 @@ RDP_DEV double splev_dev(const double* t1, int lo, int nn, const double* cd, int
 
 template <int K>
 __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __restrict__ P, double* __restrict__ U,
-                                                              const int* __restrict__ hdr,
+                                                              const int* __restrict__ kout, int nbins, int kcap,
                                                               const int* __restrict__ npts_p, int ecap, double s,
                                                               int nsamp, double eps, int min_points, int min_edge,
+                                                              const int* __restrict__ cov, int ncov,
                                                               double* __restrict__ res) {
   constexpr int K1 = K + 1, K2 = K + 2, nmin = 2 * K1;
   constexpr int NCAP = SPL_NK + K1;  // max knots: nk1 = n - K1 <= SPL_NK coefficients
   __shared__ SplSh S;
   const int tid = threadIdx.x;
-  const int m = min(hdr[0], ecap), np = npts_p[0];
+  if (tid == 0) {  // edge-point count = the packed length of the per-bin slabs; coverage = sum of row blocks
+    int e = 0;
+    for (int b = 0; b < nbins; ++b) e += min(kout[b], kcap);
+    S.n = e;
+    long c = -1;
+    if (cov) {
+      c = 0;
+      for (int b = 0; b < ncov; ++b) c += cov[b];
+    }
+    res[8 + 3 * nsamp] = (double)c;
+  }
+  __syncthreads();
+  const int m = min(S.n, ecap), np = npts_p[0];
+  __syncthreads();
   auto finish_status = [&](int st, int ier, int n, double fp) {
     if (tid == 0) {
       res[0] = st; res[1] = ier; res[2] = n; res[3] = fp; res[4] = 0.0; res[5] = 0.0; res[6] = m; res[7] = np;
@@ -726,17 +741,17 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
 }
 
 extern "C" {
-int rdp_geo_spline_res_len(int nsamp) { return 8 + 3 * nsamp; }
+int rdp_geo_spline_res_len(int nsamp) { return 9 + 3 * nsamp; }
 
 // sort the per-bin edge points (out [nbins][kcap][4], kout) into sorted [ecap][3] and fit/evaluate.
-int rdp_geo_spline(const double* out, int nbins, int kcap, const int* kout, const int* hdr, const int* npts,
-                   double* sorted, int* gperm, double* u, int ecap, double s, int k, int nsamp, double eps,
-                   int min_points, int min_edge, double* res, hipStream_t st) {
+int rdp_geo_spline(const double* out, int nbins, int kcap, const int* kout, const int* npts, double* sorted,
+                   int* gperm, double* u, int ecap, double s, int k, int nsamp, double eps, int min_points,
+                   int min_edge, const int* cov, int ncov, double* res, hipStream_t st) {
   if (k < 1 || k > SPL_KMAX || nsamp < 1 || nsamp > SPL_THREADS) return -1;
   hipLaunchKernelGGL(geo_sort_kernel, dim3(nbins), dim3(256), 0, st, out, kcap, kout, sorted, gperm, ecap);
 #define RDP_FIT(KK)                                                                                                \
-  hipLaunchKernelGGL(geo_fit_kernel<KK>, dim3(1), dim3(SPL_THREADS), 0, st, sorted, u, hdr, npts, ecap, s, nsamp, \
-                     eps, min_points, min_edge, res)
+  hipLaunchKernelGGL(geo_fit_kernel<KK>, dim3(1), dim3(SPL_THREADS), 0, st, sorted, u, kout, nbins, kcap, npts, \
+                     ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res)
   switch (k) {
     case 1: RDP_FIT(1); break;
     case 2: RDP_FIT(2); break;

@@ -44,18 +44,46 @@ RDP_DEV int block_scan_excl(int v, int* sh, int& total) {
   return wsum + x - v;
 }
 
+// Serving form (m256 != nullptr): the full-resolution mask is derived here from the model-resolution
+// mask by cv2 INTER_NEAREST (src = min(floor(dst * in/out), in - 1), double math as the reference's
+// cv2.resize, server.py:125) and written out (it is the PNG-encoded response mask), and the coverage
+// count (nnz of the mask, server.py:133) is produced per row block -- no separate upsample kernel and
+// no global atomics. Block 0 also zeroes the binning counters used two kernels later.
+struct GeoSrc {
+  const uint8_t* m256;  // nullptr: `mask` is an input
+  int mh, mw;
+  double sy, sx;
+  uint8_t* mask_out;
+  int* cov;  // [nblk] coverage counts (serving form)
+  int* zero;  // [nzero] ints zeroed by block 0
+  int nzero;
+};
+
+RDP_DEV uint8_t src_mask(const GeoSrc& g, const uint8_t* mask, int p, int W) {
+  if (!g.m256) return mask[p];
+  const int y = p / W, x = p - y * W;
+  const int iy = min((int)floor((double)y * g.sy), g.mh - 1), ix = min((int)floor((double)x * g.sx), g.mw - 1);
+  return g.m256[iy * g.mw + ix];
+}
+
 __global__ __launch_bounds__(GEO_THREADS) void geo_count_kernel(const uint8_t* __restrict__ mask,
                                                                 const uint16_t* __restrict__ depth, int H, int W,
                                                                 GeoCam cam, int* __restrict__ counts,
-                                                                double* __restrict__ xmin, double* __restrict__ xmax) {
+                                                                double* __restrict__ xmin, double* __restrict__ xmax,
+                                                                GeoSrc gs) {
   __shared__ double smin[GEO_THREADS / 64], smax[GEO_THREADS / 64];
-  __shared__ int scnt[GEO_THREADS / 64];
+  __shared__ int scnt[GEO_THREADS / 64], scov[GEO_THREADS / 64];
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < gs.nzero; i += GEO_THREADS) gs.zero[i] = 0;
   const int r0 = blockIdx.x * GEO_ROWS_PER_BLOCK;
   const int r1 = min(H, r0 + GEO_ROWS_PER_BLOCK);
-  int cnt = 0;
+  int cnt = 0, cov = 0;
   double lo = 1e300, hi = -1e300;
   for (int p = r0 * W + threadIdx.x; p < r1 * W; p += GEO_THREADS) {
-    if (pix_valid(mask, depth, p)) {
+    const uint8_t mv = src_mask(gs, mask, p, W);
+    if (gs.m256) gs.mask_out[p] = mv;
+    cov += mv != 0;
+    if (mv > 0 && depth[p] > 0) {
       ++cnt;
       const int u = p % W;
       const double z = (double)depth[p] * cam.scale;
@@ -68,18 +96,20 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_count_kernel(const uint8_t* _
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     cnt += __shfl_xor(cnt, o, 64);
+    cov += __shfl_xor(cov, o, 64);
     lo = fmin(lo, __shfl_xor(lo, o, 64));
     hi = fmax(hi, __shfl_xor(hi, o, 64));
   }
-  if (lane == 0) { scnt[wave] = cnt; smin[wave] = lo; smax[wave] = hi; }
+  if (lane == 0) { scnt[wave] = cnt; scov[wave] = cov; smin[wave] = lo; smax[wave] = hi; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int c = 0;
+    int c = 0, v = 0;
     double a = 1e300, b = -1e300;
-    for (int w = 0; w < GEO_THREADS / 64; ++w) { c += scnt[w]; a = fmin(a, smin[w]); b = fmax(b, smax[w]); }
+    for (int w = 0; w < GEO_THREADS / 64; ++w) { c += scnt[w]; v += scov[w]; a = fmin(a, smin[w]); b = fmax(b, smax[w]); }
     counts[blockIdx.x] = c;
     xmin[blockIdx.x] = a;
     xmax[blockIdx.x] = b;
+    if (gs.cov) gs.cov[blockIdx.x] = v;
   }
 }
 
@@ -371,10 +401,13 @@ long rdp_geo_work_ints(int H, int W) { return (long)rdp_geo_nblocks(H) + 2L * H 
 
 // work_i: [nblk] counts | [cap] bin_of | [cap] bidx | [128] cnt | [128] cursor ; work_d: xmin/xmax
 // pts [cap][4]; out [nbins][kcap][4]
+// m256 != nullptr (serving form): `mask` is an OUTPUT, derived from the mh x mw model mask by
+// nearest upsampling, and cov[nblk] receives per-row-block coverage counts. edges == nullptr: no
+// packed edge list (the on-device spline reads the per-bin slabs directly).
 int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, double fy, double cx, double cy,
                   double scale, int* counts, double* xmin, double* xmax, double* pts, int cap, int* npts,
                   double* out, int kcap, int* kout, int nbins, double top, int min_points, double* edges,
-                  int ecap, int* hdr, hipStream_t s) {
+                  int ecap, int* hdr, const void* m256, int mh, int mw, int* cov, hipStream_t s) {
   if (nbins > 128 || nbins < 1) return -1;
   const int nblk = rdp_geo_nblocks(H);
   GeoCam cam{fx, fy, cx, cy, scale};
@@ -383,9 +416,18 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
   gb.bidx = gb.bin_of + cap;
   gb.cnt = gb.bidx + cap;
   gb.cursor = gb.cnt + 128;
-  hipLaunchKernelGGL(geo_zero_kernel, dim3(1), dim3(256), 0, s, gb.cnt, 256);
+  GeoSrc gs;
+  gs.m256 = (const uint8_t*)m256;
+  gs.mh = mh;
+  gs.mw = mw;
+  gs.sy = m256 ? 1.0 / ((double)H / (double)mh) : 0.0;  // as cv::resize INTER_NEAREST (serve_kernels.hip)
+  gs.sx = m256 ? 1.0 / ((double)W / (double)mw) : 0.0;
+  gs.mask_out = (uint8_t*)mask;
+  gs.cov = cov;
+  gs.zero = gb.cnt;  // cnt + cursor (256 ints), consumed two kernels later
+  gs.nzero = 256;
   hipLaunchKernelGGL(geo_count_kernel, dim3(nblk), dim3(GEO_THREADS), 0, s, (const uint8_t*)mask,
-                     (const uint16_t*)depth, H, W, cam, counts, xmin, xmax);
+                     (const uint16_t*)depth, H, W, cam, counts, xmin, xmax, gs);
   hipLaunchKernelGGL(geo_write_kernel, dim3(nblk), dim3(GEO_THREADS), 0, s, (const uint8_t*)mask,
                      (const uint16_t*)depth, H, W, cam, counts, nblk, pts, cap, npts);
   const int pblocks = (cap + GEO_THREADS * 4 - 1) / (GEO_THREADS * 4);
@@ -394,7 +436,7 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
   hipLaunchKernelGGL(geo_bin_scatter_kernel, dim3(pblocks), dim3(GEO_THREADS), 0, s, npts, nbins, gb);
   hipLaunchKernelGGL(geo_select_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, nbins, top, gb, out, kcap,
                      kout, min_points);
-  hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
+  if (edges) hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
   return nblk;
 }
 }

@@ -69,6 +69,11 @@ _DEV_STATUS = {0: "ok", 1: "too_few_points", 2: "too_few_edge_points", 3: "fit_f
 DEV_NEEDS_HOST = 4
 
 
+def coverage_from_device(res: np.ndarray, cfg: GeometryConfig) -> int:
+    """Mask pixel count carried in the device result (serving form; -1 if not produced)."""
+    return int(res[8 + 3 * cfg.num_samples])
+
+
 def result_from_device(res: np.ndarray, cfg: GeometryConfig) -> Optional[CurvatureResult]:
     """CurvatureResult from the device result vector; None when the fit must finish on the host."""
     st = int(res[0])
@@ -136,6 +141,7 @@ class GeometryEngine:
         self.gperm = torch.zeros(2 * ecap, dtype=torch.int32, device=device)
         self.u = torch.zeros(ecap, dtype=torch.float64, device=device)
         self.res = torch.zeros(self.C.geo_spline_res_len(self.cfg.num_samples), dtype=torch.float64, device=device)
+        self.cov = torch.zeros(nblk, dtype=torch.int32, device=device)
 
     def launch(self, mask_dev: torch.Tensor, depth_dev: torch.Tensor, K: np.ndarray, scale: float):
         """Enqueue the edge extraction on the current stream (no host sync; graph-capturable)."""
@@ -143,12 +149,25 @@ class GeometryEngine:
         self.C.geo_edges(mask_dev, depth_dev, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]),
                          float(scale), self.work_i, self.work_d, self.pts, self.npts, self.out, self.kout, c.num_bins,
                          c.top_k_percent, c.min_points, self.edges, self.hdr)
+        self._serving_form = False
+
+    def launch_frame(self, m256_dev: torch.Tensor, mask_out: torch.Tensor, depth_dev: torch.Tensor, K: np.ndarray,
+                     scale: float):
+        """Serving form: ``mask_out`` (H x W) is produced here by nearest-upsampling the model-resolution
+        mask ``m256_dev`` (no separate upsample kernel), with the coverage count per row block, and no
+        packed edge list; follow with ``launch_spline()`` (its result then carries the coverage)."""
+        c = self.cfg
+        self.C.geo_edges(mask_out, depth_dev, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]),
+                         float(scale), self.work_i, self.work_d, self.pts, self.npts, self.out, self.kout, c.num_bins,
+                         c.top_k_percent, c.min_points, None, None, m256_dev, self.cov)
+        self._serving_form = True
 
     def launch_spline(self):
         """Enqueue the on-device spline stage after ``launch`` (no host sync; graph-capturable)."""
         c = self.cfg
-        self.C.geo_spline(self.out, self.kout, self.hdr, self.npts, self.sorted, self.gperm, self.u, self.res,
-                          c.smoothing, c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points)
+        self.C.geo_spline(self.out, self.kout, self.npts, self.sorted, self.gperm, self.u, self.res, c.smoothing,
+                          c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points,
+                          self.cov if getattr(self, "_serving_form", False) else None)
 
     def finish_device(self, res_host: np.ndarray) -> CurvatureResult:
         """Result of ``launch_spline`` (``res`` read back); a fit beyond the device capacity is redone

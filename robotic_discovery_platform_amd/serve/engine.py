@@ -8,11 +8,11 @@ resize -> numpy/scipy geometry -> coverage) with one device program per frame:
     preprocess      u8 BGR -> AA resize -> bf16 NHWC8          csrc/serve_kernels.hip
     UNet forward    18 implicit-GEMM convs, BN folded in epilogues   csrc/conv_igemm.hip
     head_mask       1x1 head + (logit > 0) -> u8 256x256        csrc/head_loss.hip
-    mask_upsample   nearest -> HxW u8 + nnz count               csrc/serve_kernels.hip
-    geo_edges       deproject + compaction + 50-bin top-5 %     csrc/geometry.hip
+    geo_edges       nearest upsample -> HxW u8 mask + coverage, deproject + compaction + 50-bin
+                    top-5 %                                     csrc/geometry.hip
     geo_spline      per-bin x-sort, FITPACK-equivalent spline fit, 100-sample splev + curvature
                                                                 csrc/geo_spline.hip
-    pinned D2H (mask, 308-double curvature result, counters)
+    pinned D2H (mask, 309-double result: curvature, points, coverage, counts)
 
 The device part between the copies is captured once into a hipGraph (torch.cuda.CUDAGraph) and
 replayed per frame, so a frame costs one graph launch plus three copies instead of ~90 kernel
@@ -110,7 +110,6 @@ class FramePipeline:
         self.d_depth = torch.empty(H, W, dtype=torch.int16, device=dev)
         self.m256 = torch.empty(size * size, dtype=torch.uint8, device=dev)
         self.mask = torch.empty(H, W, dtype=torch.uint8, device=dev)
-        self.meta = torch.zeros(4, dtype=torch.int32, device=dev)
         ecap = self.cfg.num_bins + int(H * W * self.cfg.top_k_percent) + 1
         self.geo = GeometryEngine(H, W, dev, self.cfg, ecap=ecap)
         # pinned host staging
@@ -118,7 +117,6 @@ class FramePipeline:
         self.h_depth = torch.empty(H, W, dtype=torch.int16, pin_memory=True)
         self.h_mask = torch.empty(H, W, dtype=torch.uint8, pin_memory=True)
         self.h_res = torch.empty(self.geo.res.numel(), dtype=torch.float64, pin_memory=True)
-        self.h_meta = torch.empty(4, dtype=torch.int32, pin_memory=True)
         self.ev0 = torch.cuda.Event(enable_timing=True)
         self.ev1 = torch.cuda.Event(enable_timing=True)
         self.graphs = {}  # channel order of the staged colour frame (0 BGR, 1 RGB) -> hipGraph
@@ -137,11 +135,8 @@ class FramePipeline:
         ex.forward(head=False, refresh_eval=False)  # BN-fold coefficients: see refresh_weights()
         C.head_mask(ex.final, m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
                     self.thr_logit, self.m256)
-        C.mask_upsample(self.m256.view(self.S, self.S), self.mask, self.meta[0:1])
-        self.geo.launch(self.mask, self.d_depth, self.K, self.scale)
+        self.geo.launch_frame(self.m256.view(self.S, self.S), self.mask, self.d_depth, self.K, self.scale)
         self.geo.launch_spline()
-        self.meta[1:2].copy_(self.geo.hdr)
-        self.meta[2:3].copy_(self.geo.npts)
 
     def refresh_weights(self):
         """Recompute the BN-fold coefficients from the current weights / running stats (after a
@@ -188,7 +183,6 @@ class FramePipeline:
                 self._device_program(int(rgb))
             self.h_mask.copy_(self.mask, non_blocking=True)
             self.h_res.copy_(self.geo.res, non_blocking=True)
-            self.h_meta.copy_(self.meta, non_blocking=True)
             self.ev1.record(s)
 
     def collect(self) -> FrameResult:
@@ -196,7 +190,8 @@ class FramePipeline:
         with trace.range("serve.frame.wait_gpu"):
             self.ev1.synchronize()
         t1 = time.perf_counter()
-        count = int(self.h_meta.numpy()[0])
+        from ..geometry.curvature import coverage_from_device
+        count = coverage_from_device(self.h_res.numpy(), self.cfg)
         with trace.range("serve.frame.spline_fit"):  # device result -> CurvatureResult (host fit only as fallback)
             res = self.geo.finish_device(self.h_res.numpy())
         t2 = time.perf_counter()

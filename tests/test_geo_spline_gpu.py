@@ -45,10 +45,9 @@ def _device_fit(p, s, k=3, shuffle_seed=None, nbins=1):
     ecap = m + 8
     sorted_ = torch.zeros(ecap, 3, dtype=torch.float64, device=dev)
     res = torch.zeros(C.geo_spline_res_len(NSAMP), dtype=torch.float64, device=dev)
-    C.geo_spline(torch.from_numpy(out).to(dev), kout, torch.tensor([m], dtype=torch.int32, device=dev),
-                 torch.tensor([10 ** 6], dtype=torch.int32, device=dev), sorted_,
-                 torch.zeros(2 * ecap, dtype=torch.int32, device=dev), torch.zeros(ecap, dtype=torch.float64, device=dev),
-                 res, s, k, NSAMP, 1e-6, 100, 20)
+    C.geo_spline(torch.from_numpy(out).to(dev), kout, torch.tensor([10 ** 6], dtype=torch.int32, device=dev),
+                 sorted_, torch.zeros(2 * ecap, dtype=torch.int32, device=dev),
+                 torch.zeros(ecap, dtype=torch.float64, device=dev), res, s, k, NSAMP, 1e-6, 100, 20)
     torch.cuda.synchronize()
     return res.cpu().numpy(), sorted_[:m].cpu().numpy()
 
@@ -81,6 +80,7 @@ def test_device_spline_matches_scipy(kind, s, seed):
     assert res[4] == pytest.approx(rm, rel=1e-6) and res[5] == pytest.approx(rx, rel=1e-6)
     ref_pts = np.array(splev(np.linspace(0, 1, NSAMP), tck)).T
     assert np.abs(res[8:8 + 3 * NSAMP].reshape(-1, 3) - ref_pts).max() < 1e-8
+    assert res[8 + 3 * NSAMP] == -1  # no coverage input
 
 
 def test_device_spline_matches_host_port_and_is_deterministic():
@@ -92,7 +92,7 @@ def test_device_spline_matches_host_port_and_is_deterministic():
     ier, mk, xk, pts, fp, n = native().fit_curvature(torch.from_numpy(np.ascontiguousarray(p)), 0.01, 3, NSAMP, 1e-6)
     assert int(a[1]) == ier and int(a[2]) == n
     assert a[4] == pytest.approx(mk, rel=1e-7) and a[5] == pytest.approx(xk, rel=1e-7)
-    assert np.abs(a[8:].reshape(-1, 3) - pts.numpy()).max() < 1e-9
+    assert np.abs(a[8:8 + 3 * NSAMP].reshape(-1, 3) - pts.numpy()).max() < 1e-9
 
 
 def test_device_spline_degenerate_inputs():
