@@ -90,10 +90,13 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
   const auto rw = make_rsrc(a.w, a.wbytes);
 
   // ---- DMA-side state of the tile currently being staged ----
-  // per pixel row: linear pixel index and a 9-bit mask of the taps whose source pixel is in the
-  // image (bit t set <=> row valid and (h+dr, w+ds) in bounds), computed once per tile.
-  int pm[NROW];
-  uint32_t tmask[NROW];
+  // per pixel row (computed once per tile): byte offset of this lane's 16-B chunk of the pixel in
+  // each source (pb1 / pb2), and the INVERTED 9-bit tap mask (bit t set <=> row invalid or
+  // (h+dr, w+ds) outside the image). The per-K-step address is then 3 full-rate VALU ops per DMA:
+  // v_bfe (tap bit) + v_add (uniform tap/channel offset) + v_lshl_or (bit 31 = out of range, which
+  // the buffer descriptor turns into zeros) -- no multiply or compare in the K loop.
+  uint32_t pb1[NROW], pb2[NROW];
+  uint32_t nmask[NROW];
   uint32_t woff[WPIECES];
   int itap = 0, icc = 0;  // (tap, 64-channel chunk) of the stage being issued (generic mode)
   int ks0 = 0;  // first global K step of the work item being staged (split-K)
@@ -121,8 +124,9 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
       msk |= (rok & 2u) ? (cok << 3) : 0u;
       msk |= (rok & 4u) ? (cok << 6) : 0u;
       if (a.taps == 1) msk = 1u;
-      tmask[r] = valid ? msk : 0u;
-      pm[r] = (int)mm;
+      nmask[r] = valid ? ~msk : ~0u;
+      pb1[r] = (mm * (uint32_t)a.pitch1 + (uint32_t)gch * 8u) * 2u;
+      pb2[r] = (mm * (uint32_t)a.pitch2 + (uint32_t)gch * 8u) * 2u;
     }
 #pragma unroll
     for (int f = 0; f < WPIECES; ++f) {
@@ -134,11 +138,11 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
   auto issue = [&](int ks, char* buf) {
     if (a.packed) {
       const int tap = ks * 8 + gch;  // per lane; taps >= 9 have no mask bit -> zeros
-      const int toff = (tap_dr(tap) * a.W + tap_ds(tap)) * a.pitch1;
+      const int toff = (tap_dr(tap) * a.W + tap_ds(tap)) * a.pitch1 * 2 - gch * 16;
 #pragma unroll
       for (int r = 0; r < NROW; ++r) {
-        const bool ok = (tmask[r] >> tap) & 1u;
-        const uint32_t off = ok ? (uint32_t)(pm[r] * a.pitch1 + toff) * 2u : RDP_OOB;
+        const uint32_t bad = tap < 9 ? (nmask[r] >> tap) & 1u : 1u;
+        const uint32_t off = (bad << 31) | (uint32_t)((int)pb1[r] + toff);
         dma16(rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
       }
     } else {
@@ -146,12 +150,12 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
       const bool s2 = c0 >= a.C1;
       const int pitch = s2 ? a.pitch2 : a.pitch1;
       const int tap_lin = a.taps == 9 ? tap_dr(itap) * a.W + tap_ds(itap) : 0;
-      const int soff = tap_lin * pitch + (s2 ? c0 - a.C1 : c0) + gch * 8;  // uniform except gch
+      const int soff = (tap_lin * pitch + (s2 ? c0 - a.C1 : c0)) * 2;  // wave-uniform (SGPR)
       const int bit = a.taps == 9 ? itap : 0;
 #pragma unroll
       for (int r = 0; r < NROW; ++r) {
-        const bool ok = (tmask[r] >> bit) & 1u;
-        const uint32_t off = ok ? (uint32_t)(pm[r] * pitch + soff) * 2u : RDP_OOB;
+        const uint32_t bad = __builtin_amdgcn_ubfe(nmask[r], (uint32_t)bit, 1u);
+        const uint32_t off = (bad << 31) | (uint32_t)((int)(s2 ? pb2[r] : pb1[r]) + soff);
         dma16(s2 ? rx2 : rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
       }
       if (++icc == a.cpt) { icc = 0; ++itap; if (itap == a.taps) itap = 0; }

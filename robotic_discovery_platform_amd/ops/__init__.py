@@ -23,6 +23,14 @@ def native(build_if_missing: bool = True):
         if _mod is not None:
             return _mod
         import torch  # noqa: F401  (loads libtorch before the extension)
+        alt = os.environ.get("RDP_NATIVE_SO")  # A/B runs: load another build of the same library
+        if alt:
+            from importlib import machinery, util
+            loader = machinery.ExtensionFileLoader("robotic_discovery_platform_amd._C", alt)
+            spec = util.spec_from_file_location("robotic_discovery_platform_amd._C", alt, loader=loader)
+            _mod = util.module_from_spec(spec)
+            loader.exec_module(_mod)
+            return _mod
         try:
             _mod = importlib.import_module("robotic_discovery_platform_amd._C")
         except ImportError as e:

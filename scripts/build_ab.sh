@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build an A/B baseline library: the current objects, with the named sources taken from a git rev.
+# usage: scripts/build_ab.sh <rev> <src.hip> [...]   -> ab/_C_base.so  (load with RDP_NATIVE_SO)
+set -e
+cd "$(dirname "$0")/.."
+rev=$1; shift
+python -m robotic_discovery_platform_amd._build > /dev/null
+mkdir -p ab build/ab
+objs=""
+for o in build/obj/*.o; do objs="$objs $o"; done
+for src in "$@"; do
+  git show "$rev:csrc/$src" > build/ab/$src
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -munsafe-fp-atomics -I csrc -c build/ab/$src -o build/ab/$src.o
+  objs=$(echo $objs | sed "s|build/obj/$src.o|build/ab/$src.o|")
+done
+TL=$(python -c "import torch,os;print(os.path.join(os.path.dirname(torch.__file__),'lib'))")
+g++ -shared -o ab/_C_base.so $objs -L$TL -L/opt/rocm/lib -Wl,-rpath,$TL -Wl,-rpath,/opt/rocm/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip -ltorch_python -lamdhip64 -lz
+echo "built ab/_C_base.so from $rev: $*"
