@@ -130,6 +130,10 @@ class FramePipeline:
 
     # ---------------------------------------------------------------- device program
     def _device_program(self, rgb: int = 0):
+        # Measured dead end: the H2D / D2H copies captured INTO this graph, depth H2D and mask D2H
+        # on a forked branch -- the memcpy nodes replay as blit kernels (20.7 + 17.7 us for colour /
+        # depth instead of DMA-engine copies), the fork adds a ~67 us cross-queue gap, and two
+        # pipelines no longer overlap: GPU p50 0.622 -> 0.648 ms, pipelined 2307 -> 1502 FPS.
         C, ex, m = self.C, self.ex, self.model
         C.preprocess(self.d_color, *self.tab, ex.x_in, rgb)
         ex.forward(head=False, refresh_eval=False)  # BN-fold coefficients: see refresh_weights()
