@@ -423,6 +423,14 @@ class UNetExecutor:
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
         self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
+        # RDP_WGRAD_STREAMS > 1: weight gradients round-robin over that many side streams, each with
+        # its own slab (consecutive layers' wgrads run concurrently, not queued behind each other).
+        # Measured dead end (same box, 2 rounds): bs4 1499 / 1451 / 1444 img/s and bs64 2994-2998 /
+        # 2949-2964 / 2944-2962 for 1 / 2 / 3 streams -- every extra stream lands on another hardware
+        # queue and the contention costs more than the added concurrency (cf. graph replay, engine.py)
+        nside = max(1, int(os.environ.get("RDP_WGRAD_STREAMS", "1"))) if self.side is not None else 1
+        self.sides = [self.side] + [torch.cuda.Stream(dev) for _ in range(nside - 1)] if self.side is not None else []
+        self._side_rr = 0
         # Measured dead ends on this side stream (bs64, one MI355X): (a) the skip half of each Up conv's
         # input gradient moved here off the main stream's critical path: 1% slower with the old
         # 2048-block wgrad grid (2717 vs 2740 img/s), 5% slower with the 512-block grid (2790 vs 2940;
@@ -497,6 +505,8 @@ class UNetExecutor:
             # roles swapped in conv_wgrad: "x" = dyT (4*cout ch), "dy" = the ConvT input (cin ch)
             slab = max(slab, C.wgrad_slab_elems(n, h, w, 4 * us.cout, us.cin, 1, 0, sp_))
         self.slab = torch.zeros(slab, dtype=torch.float32, device=dev)
+        self.slabs = [self.slab] + [torch.zeros(slab, dtype=torch.float32, device=dev)
+                                    for _ in range(max(0, len(self.sides) - 1))]
         # The first layer's wgrad is the step's last gradient; the side stream is still working off
         # its backlog then while the main stream idles, so it runs on the main stream with its own slab
         # (RDP_LAST_WGRAD_MAIN=0: on the side stream like the others; also moving the second-to-last
@@ -694,6 +704,23 @@ class UNetExecutor:
         buf[: 2 * c].copy_(tot)
         return 1, self._sync_m[hw]
 
+    def _join_sides_into_side(self):
+        """Make the first side stream wait for the others (before a DDP bucket hook: the bucket's
+        all-reduce must see every wgrad issued so far, whichever side stream ran it)."""
+        for st in self.sides[1:]:
+            self.side.wait_stream(st)
+
+    def _on_wgrad_stream(self, fn):
+        """Run ``fn(slab)`` (a weight gradient) on the next side stream with that stream's slab."""
+        if len(self.sides) <= 1:
+            return self._on_side(lambda: fn(self.slab))
+        k = self._side_rr % len(self.sides)
+        self._side_rr += 1
+        st = self.sides[k]
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            return fn(self.slabs[k])
+
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream
         (fork); without a side stream it runs inline."""
@@ -713,8 +740,8 @@ class UNetExecutor:
         if self.slab_main is not None and L is self.down_layers[0][0]:
             C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab_main, gw, 0, L.splits, 0)
         else:
-            self._on_side(lambda: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab,
-                                               gw, 0, L.splits, 0))
+            self._on_wgrad_stream(lambda slab: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real,
+                                                            slab, gw, 0, L.splits, 0))
         owner = L.dx1_owner if self.dgrad_bnred else None
         if owner is not None and L.dx2 is None and sp.taps == 9 and not owner.bwd_rows:
             rows = C.conv_dgrad_bnred(L.dy, self.m.dgrad_weight(sp), L.dx1, owner.y, owner.coef, self.bn_partial)
@@ -724,6 +751,7 @@ class UNetExecutor:
         if L.dx1 is not None and owner is not True:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:
+            self._join_sides_into_side()
             self._on_side(lambda: hooks(sp))  # the bucket's all-reduce waits for the wgrad too
 
     def backward(self, grad_hook=None, gscale: float = 1.0):
@@ -739,7 +767,8 @@ class UNetExecutor:
             self._backward(C, D, st, grad_hook, gscale)
         finally:
             if main is not None:
-                main.wait_stream(self.side)  # join
+                for side in self.sides:
+                    main.wait_stream(side)  # join
 
     def _backward(self, C, D, st, grad_hook, gscale):
         head_w = st.view("outc.conv.weight").reshape(-1)
@@ -779,12 +808,13 @@ class UNetExecutor:
                 dyT = self.dyTs[i - 1]
                 C.upT_unshuffle(du, dyT, oy, ox)
                 C.colsum_bf16(dyT, 4, self.colsum_ws, st.flat_slice(us.name + ".bias", st.grad), 0)
-                self._on_side(lambda: C.conv_wgrad(dyT, None, low_layer.a, 1, 0, 4 * us.cout, self.slab,
-                                                   st.flat_slice(us.name + ".weight", st.grad), 0,
-                                                   self.upT_splits[i - 1], 0))
+                self._on_wgrad_stream(lambda slab: C.conv_wgrad(dyT, None, low_layer.a, 1, 0, 4 * us.cout, slab,
+                                                                st.flat_slice(us.name + ".weight", st.grad), 0,
+                                                                self.upT_splits[i - 1], 0))
                 C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
                            self.kws)
                 if grad_hook is not None:
+                    self._join_sides_into_side()
                     self._on_side(lambda: grad_hook(us))
         for i in range(D, 0, -1):
             la, lb = self.down_layers[i]

@@ -6,7 +6,8 @@ Two measurements on 640x480 synthetic RGB-D frames (the reference camera format,
              server.py:117-133 without codecs/transport.
   * e2e:     the full gRPC service over loopback (client-encoded JPEG colour + 16-bit PNG depth,
              server decode, engine, PNG mask encode, metrics CSV, response) -- one stream, streamed
-             (throughput FPS) and lock-step (round-trip p50/p99).
+             (throughput FPS) and lock-step (round-trip p50/p99); the load generator runs in its own
+             process like the reference's client.py.
 
 Weights: the reference U-Net architecture, briefly trained on synthetic scenes (so masks look like
 an actuator and the geometry stage sees realistic point counts), unless ``train_steps=0``.
@@ -102,13 +103,63 @@ def measure_engine_pipelined(model, scenes, frames: int = 200, warmup: int = 20,
             round(frames * streams / max(res.values()), 1)}
 
 
-def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2):
+def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8) -> dict:
+    """The load generator: one client stream (the reference client's encodings: JPEG colour, 16-bit
+    PNG depth), streamed throughput then lock-step round trips. Runs in its own process."""
     import grpc
-    from ..camera import write_calibration
-    from ..config import ServeConfig
-    from ..data.synthetic import DEFAULT_K
+    from ..data.synthetic import make_scene
     from ..proto import vision as pb
     from .client import make_request
+    reqs = [make_request(sc.color, sc.depth) for sc in (make_scene(i) for i in range(n_scenes))]
+    out = {}
+    with grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_receive_message_length", 64 << 20),
+                                                               ("grpc.max_send_message_length", 64 << 20)]) as ch:
+        stub = pb.VisionAnalysisServiceStub(ch)
+        n = warmup + frames
+
+        def gen():
+            for i in range(n):
+                yield reqs[i % len(reqs)]
+
+        t_start = None
+        proc = []
+        for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen())):
+            if i == warmup - 1:
+                t_start = time.perf_counter()
+            if i >= warmup:
+                proc.append(resp.proc_time_ms)
+        t_end = time.perf_counter()
+        out["e2e_fps"] = round(frames / (t_end - t_start), 1)
+        out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)  # processing only (proc_time_ms)
+        q: "queue.Queue" = queue.Queue()
+        sent = []
+
+        def gen_ls():
+            for i in range(n):
+                sent.append(time.perf_counter())
+                yield reqs[i % len(reqs)]
+                q.get()
+
+        rtt = []
+        for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen_ls())):
+            now = time.perf_counter()
+            if i >= warmup:
+                rtt.append((now - sent[i]) * 1e3)
+            q.put(1)
+        out["e2e_p50_ms"] = round(_pct(rtt, 50), 3)
+        out["e2e_p99_ms"] = round(_pct(rtt, 99), 3)
+    return out
+
+
+def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2):
+    """Server in this process, load generator in a separate client process (the reference's
+    topology: client.py and server.py are different processes), over loopback gRPC."""
+    import grpc
+    import json
+    import subprocess
+    import sys
+    from ..data.synthetic import DEFAULT_K
+    from ..proto import vision as pb
     from .engine import EnginePool
     from .server import MetricsLog, VisionAnalysisService
     from concurrent import futures
@@ -119,51 +170,21 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
     pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
     port = server.add_insecure_port("127.0.0.1:0")
     server.start()
-    reqs = [make_request(s.color, s.depth) for s in scenes]
     out = {}
     try:
-        with grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_receive_message_length", 64 << 20),
-                                                                   ("grpc.max_send_message_length", 64 << 20)]) as ch:
-            stub = pb.VisionAnalysisServiceStub(ch)
-            # streamed throughput
-            n = warmup + frames
-            t_first = [None]
-
-            def gen():
-                for i in range(n):
-                    yield reqs[i % len(reqs)]
-
-            t_start = None
-            proc = []
-            for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen())):
-                if i == warmup - 1:
-                    t_start = time.perf_counter()
-                if i >= warmup:
-                    proc.append(resp.proc_time_ms)
-            t_end = time.perf_counter()
-            out["e2e_fps"] = round(frames / (t_end - t_start), 1)
-            out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)  # processing only (proc_time_ms)
-            st = svc.latency_stats()
-            out["e2e_server_queue_p50_ms"] = round(st["queue_p50_ms"], 3)  # request read -> processing start
-            _progress(f"streamed: {out}")
-            # lock-step round trip
-            q: "queue.Queue" = queue.Queue()
-            sent = []
-
-            def gen_ls():
-                for i in range(n):
-                    sent.append(time.perf_counter())
-                    yield reqs[i % len(reqs)]
-                    q.get()
-
-            rtt = []
-            for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen_ls())):
-                now = time.perf_counter()
-                if i >= warmup:
-                    rtt.append((now - sent[i]) * 1e3)
-                q.put(1)
-            out["e2e_p50_ms"] = round(_pct(rtt, 50), 3)
-            out["e2e_p99_ms"] = round(_pct(rtt, 99), 3)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                   HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")  # the client never touches the GPU
+        r = subprocess.run([sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve", "--client-port",
+                            str(port), "--frames", str(frames), "--warmup", str(warmup)], env=env,
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"client process failed: {r.stderr[-1500:]}")
+        out.update(json.loads(r.stdout.strip().splitlines()[-1]))
+        st = svc.latency_stats()
+        out["e2e_server_queue_p50_ms"] = round(st["queue_p50_ms"], 3)  # request read -> processing start
+        out["e2e_client"] = "separate process"
+        _progress(f"e2e: {out}")
     finally:
         # wait for the gRPC core to finish shutting down before its objects are collected: a
         # server torn down at interpreter exit aborts the process ("terminate called without an
@@ -201,6 +222,10 @@ if __name__ == "__main__":
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--train-steps", type=int, default=200)
     ap.add_argument("--e2e", type=int, default=1)
+    ap.add_argument("--client-port", type=int, default=0, help="internal: run as the e2e load-generator process")
     a = ap.parse_args()
+    if a.client_port:
+        print(json.dumps(run_client_load(a.client_port, a.frames, a.warmup)), flush=True)
+        raise SystemExit(0)
     print(json.dumps(measure_serving(torch.device("cuda"), a.frames, a.warmup, a.train_steps, bool(a.e2e))),
           flush=True)

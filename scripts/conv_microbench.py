@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--out", default=None)
     ap.add_argument("--shapes", default=None, help="comma list of shape indices")
+    ap.add_argument("--wgrad-blocks", type=int, default=2048,
+                    help="split-K grid target of the wgrad kernels (the training step uses 512, RDP_WGRAD_BLOCKS)")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda")
@@ -50,7 +52,7 @@ def main():
         if a.wgrad:
             dy = torch.randn(N, H, H, Co, device=dev).to(torch.bfloat16)
             tiles = ((9 * Cin + 255) // 256) * (Co // 64)
-            splits = max(1, min((2048 + tiles - 1) // tiles, N * H * H // 2048))
+            splits = max(1, min((a.wgrad_blocks + tiles - 1) // tiles, N * H * H // 2048))
             slab = torch.zeros(C.wgrad_slab_elems(N, H, H, Cin, Co, 9, 0, splits), device=dev)
             out = torch.zeros(Co * 9 * Cin, device=dev)
 
@@ -76,6 +78,9 @@ def main():
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / a.reps)
         row = {"shape": f"{N}x{H}x{H} {C1}+{C2}->{Co}", "kind": "wgrad" if a.wgrad else "fwd"}
+        if a.wgrad:
+            row["splits"] = splits
+            row["wgrad_blocks"] = a.wgrad_blocks
         for v in variants:
             med = statistics.median(times[v])
             row[f"v{v}_us"] = round(med * 1e3, 1)
