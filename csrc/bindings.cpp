@@ -42,7 +42,8 @@ int rdp_maxpool2_bwd(const void*, int, const void*, int, const void*, int, void*
 int rdp_bn_relu_apply_pool(const void*, int, void*, int, void*, int, const float*, int, int, int, int, hipStream_t);
 int rdp_maxpool2_bwd_bn_reduce(const void*, int, const void*, int, const void*, int, void*, int, const void*, int,
                                const float*, int, int, int, int, float*, int, hipStream_t);
-int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, const float*,
+                      hipStream_t);
 int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, const void*, int,
                       const float*, float*, int, hipStream_t);
 int rdp_upT_shuffle(const void*, int, const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -320,11 +321,18 @@ int maxpool2_bwd_bn_reduce(torch::Tensor dp, torch::Tensor x, c10::optional<torc
   return T;
 }
 
-void upsample2_fwd(torch::Tensor x, torch::Tensor out, int oy, int ox) {
+// coef (optional, fp32 [4C] = mean|invstd|scale|shift): x is pre-BN; BN + ReLU applied on the fly
+void upsample2_fwd(torch::Tensor x, torch::Tensor out, int oy, int ox, c10::optional<torch::Tensor> coef) {
   Act a = act(x, "x"), o = act(out, "out");
   TORCH_CHECK(o.N == a.N && o.C == a.C, "upsample shape");
   TORCH_CHECK(2 * a.H + oy <= o.H && 2 * a.W + ox <= o.W && oy >= 0 && ox >= 0, "upsample fwd placement");
-  TORCH_CHECK(rdp_upsample2_fwd(a.ptr, a.pitch, o.ptr, o.pitch, a.N, a.H, a.W, o.H, o.W, oy, ox, a.C, cur_stream()) == 0,
+  const float* cp = nullptr;
+  if (coef && coef->defined()) {
+    TORCH_CHECK(coef->is_cuda() && coef->scalar_type() == torch::kFloat32 && coef->numel() >= 4 * a.C, "coef [4C] f32");
+    cp = coef->data_ptr<float>();
+  }
+  TORCH_CHECK(rdp_upsample2_fwd(a.ptr, a.pitch, o.ptr, o.pitch, a.N, a.H, a.W, o.H, o.W, oy, ox, a.C, cp,
+                                cur_stream()) == 0,
               "upsample fwd: channels must be 2^k in [8, 2048], pitches multiples of 8");
 }
 
@@ -727,7 +735,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2_bwd", &maxpool2_bwd);
   m.def("bn_relu_apply_pool", &bn_relu_apply_pool);
   m.def("maxpool2_bwd_bn_reduce", &maxpool2_bwd_bn_reduce);
-  m.def("upsample2_fwd", &upsample2_fwd);
+  m.def("upsample2_fwd", &upsample2_fwd, py::arg("x"), py::arg("out"), py::arg("oy"), py::arg("ox"),
+        py::arg("coef") = py::none());
   m.def("upT_shuffle", &upT_shuffle);
   m.def("upT_unshuffle", &upT_unshuffle);
   m.def("colsum_bf16", &colsum_bf16);

@@ -293,9 +293,17 @@ RDP_DEV void up_src(int u, int in, float r, int& i0, int& i1, float& l1) {
 // (bwd) image row segment of 256 (pixel, 8-channel group) pairs: the row's source rows and weights
 // are block-uniform (scalar), channel groups are a power of two, so the per-thread indexing is shifts
 // and masks (no 64-bit division), and every access is a 16-B, line-coalesced vector.
+// coef != nullptr: x is the producing layer's PRE-BN output; its training BN + ReLU (coef =
+// [mean|invstd|scale|shift]) is applied to each tap and rounded to bf16 exactly as bn_relu_apply would
+// store it, so the post-activation tensor of the layer below every Up block is never materialised.
+RDP_DEV void bn_relu8(float* v, const float* sc, const float* sh) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = bf2f(f2bf(fmaxf(fmaf(v[k], sc[k], sh[k]), 0.f)));
+}
+
 __global__ __launch_bounds__(256) void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch,
                                                             u16* __restrict__ out, int opitch, UpGeom g, int lcg,
-                                                            int nchunk) {
+                                                            int nchunk, const float* __restrict__ coef) {
   const int CG = 1 << lcg;
   const int items = g.N * g.Hout * nchunk;
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
@@ -320,6 +328,12 @@ __global__ __launch_bounds__(256) void upsample2_fwd_kernel(const u16* __restric
       unpack8f(*(const uint4*)(x + ((base + y0) * g.win + x1) * xpitch + c), b);
       unpack8f(*(const uint4*)(x + ((base + y1) * g.win + x0) * xpitch + c), cc);
       unpack8f(*(const uint4*)(x + ((base + y1) * g.win + x1) * xpitch + c), d);
+      if (coef) {
+        float sc[8], sh[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { sc[k] = coef[2 * g.C + c + k]; sh[k] = coef[3 * g.C + c + k]; }
+        bn_relu8(a, sc, sh); bn_relu8(b, sc, sh); bn_relu8(cc, sc, sh); bn_relu8(d, sc, sh);
+      }
       const float hy = 1.f - ly, hx = 1.f - lx;
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = hy * (hx * a[k] + lx * b[k]) + ly * (hx * cc[k] + lx * d[k]);
@@ -595,13 +609,13 @@ static int ilog2(int v) {
   return l;
 }
 int rdp_upsample2_fwd(const void* x, int xpitch, void* out, int opitch, int N, int hin, int win, int Hout, int Wout,
-                      int oy, int ox, int C, hipStream_t s) {
+                      int oy, int ox, int C, const float* coef, hipStream_t s) {
   if (!pow2c(C) || xpitch % 8 || opitch % 8) return -1;
   UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
   const int lcg = ilog2(C / 8), nchunk = (int)(((long)Wout * (C / 8) + 255) / 256);
   const long items = (long)N * Hout * nchunk;
   hipLaunchKernelGGL(upsample2_fwd_kernel, dim3((int)std::min<long>(items, 8192)), dim3(256), 0, s, (const u16*)x,
-                     xpitch, (u16*)out, opitch, g, lcg, nchunk);
+                     xpitch, (u16*)out, opitch, g, lcg, nchunk, coef);
   return 0;
 }
 // y/coef/partial given: fused BN-backward reduction of dx's consumer BN; returns the partial rows

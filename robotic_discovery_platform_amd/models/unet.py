@@ -312,6 +312,11 @@ class UNetExecutor:
         # backward partials and dy from the logits (backward), so the 64-ch activation and its gradient
         # are never materialised (RDP_FUSE_HEAD=0: separate kernels, for A/B measurements)
         self.fuse_head = training and os.environ.get("RDP_FUSE_HEAD", "1") != "0"
+        # training, bilinear decoder: the BN+ReLU of the layer under each Up block (down4.conv2,
+        # up1..3.conv2) is applied by the upsample kernel as it reads the pre-BN tensor, so those
+        # post-activation tensors are never written (their only reader is the upsample; backward
+        # works from the pre-BN tensor). RDP_FUSE_UP_BN=0: separate apply kernels (A/B).
+        self.fuse_up_bn = training and model.bilinear and os.environ.get("RDP_FUSE_UP_BN", "1") != "0"
         C = _native()
         D = model.depth
         bf = torch.bfloat16
@@ -591,14 +596,18 @@ class UNetExecutor:
                 C.maxpool2_fwd(self.skips[i - 1], self.pools[i - 1])
             la, lb = self.down_layers[i]
             self._conv_bn_relu(C, la)
-            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None)
+            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None,
+                                        apply=not (i == D and self.fuse_up_bn))
         low = self.skips[D]
+        low_layer = self.down_layers[D][1]
         for i in range(1, D + 1):
             lv = D - i
             u = self.ups[i - 1]
             oy = (u.shape[1] - 2 * low.shape[1]) // 2
             ox = (u.shape[2] - 2 * low.shape[2]) // 2
-            if self.m.bilinear:
+            if self.m.bilinear and self.fuse_up_bn:
+                C.upsample2_fwd(low_layer.y, u, oy, ox, low_layer.coef)  # BN + ReLU of low_layer on the fly
+            elif self.m.bilinear:
                 C.upsample2_fwd(low, u, oy, ox)
             else:
                 us = self.m.up_specs[i - 1]
@@ -608,8 +617,8 @@ class UNetExecutor:
             la, lb = self.up_layers[i - 1]
             self._conv_bn_relu(C, la)
             last = i == D
-            self._conv_bn_relu(C, lb, apply=not (last and self.fuse_head and head))
-            low = lb.a
+            self._conv_bn_relu(C, lb, apply=not ((last and self.fuse_head and head) or (not last and self.fuse_up_bn)))
+            low, low_layer = lb.a, lb
         if not head:
             return
         head_w = self.m.store.view("outc.conv.weight").reshape(-1)

@@ -327,6 +327,14 @@ def test_upsample_fwd_bwd(C, hin, win, H2, W2):
     gg = dx.float() * ((y.float() * ss + (beta - mean * ss)) > 0)
     exact = torch.stack([gg.sum((0, 1, 2)), (gg * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
     assert torch.allclose(got, exact, rtol=1e-3, atol=1e-3)
+    # forward fused with the producer's training BN + ReLU: identical to apply-then-upsample
+    a = torch.empty_like(y)
+    C.bn_relu_apply(y, a, coef, 1)
+    ref_out = torch.empty_like(out)
+    C.upsample2_fwd(a, ref_out, dY // 2, dX // 2)
+    fused = torch.empty_like(out)
+    C.upsample2_fwd(y, fused, dY // 2, dX // 2, coef)
+    assert torch.equal(fused, ref_out)
 
 
 @pytest.mark.parametrize("dice_w", [0.0, 1.0])
