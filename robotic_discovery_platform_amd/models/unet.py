@@ -315,8 +315,10 @@ class UNetExecutor:
         # training, bilinear decoder: the BN+ReLU of the layer under each Up block (down4.conv2,
         # up1..3.conv2) is applied by the upsample kernel as it reads the pre-BN tensor, so those
         # post-activation tensors are never written (their only reader is the upsample; backward
-        # works from the pre-BN tensor). RDP_FUSE_UP_BN=0: separate apply kernels (A/B).
-        self.fuse_up_bn = training and model.bilinear and os.environ.get("RDP_FUSE_UP_BN", "1") != "0"
+        # works from the pre-BN tensor). Off by default: measured 0.3-0.5 % SLOWER at bs 64 (2966 / 2965
+        # vs 2981 / 2973 img/s, same box, interleaved) -- the upsample re-applies BN to each of the 4
+        # taps of every output (4x the input elements) and these tensors are small. RDP_FUSE_UP_BN=1 on.
+        self.fuse_up_bn = training and model.bilinear and os.environ.get("RDP_FUSE_UP_BN", "0") != "0"
         C = _native()
         D = model.depth
         bf = torch.bfloat16
