@@ -303,36 +303,86 @@ RDP_DEV void resid_pass(SplSh& S, const double* __restrict__ P, const double* __
   __syncthreads();
 }
 
-// banded Cholesky (bandwidth KB) of S.A (A[i][d] = (i, i+d)) into S.R, then S.c = A^-1 Z.
-// Thread 0 only. Returns false on a non-positive pivot.
-template <int KB>
-RDP_DEV bool chol_solve(SplSh& S, int nk1) {
-  double (*c)[SPL_NK] = S.c;
+// Banded Cholesky + both triangular solves for the system A = G + p2i * BtB (band KB; G has band
+// K1 <= KB, BtB = B^T B of the fpdisc rows when smoothing, p2i = p^-2), A c = Z for 3 right-hand
+// sides; c -> S.c. Thread 0 only, but the row recurrences run in registers: a sliding window of the
+// last KB rows of R (compile-time indexed) and of the forward-substitution values, so each row costs
+// ~KB^2/2 register FMAs plus its KB loads of G / BtB / Z -- no LDS round trip inside the
+// dependency chain (the LDS-latency-bound form took ~30 us per solve). R rows are stored once for
+// the back substitution, which also keeps its c window in registers. false: non-positive pivot.
+template <int KB, int K1>
+RDP_DEV bool chol_solve(SplSh& S, int nk1, double p2i) {
+  double win[KB][KB];  // win[q]: R row (i - (KB-1) + q), entries d = 0..KB-1 (rows < 0: zeros)
+  double yw[3][KB];
+#pragma unroll
+  for (int q = 0; q < KB; ++q) {
+#pragma unroll
+    for (int d = 0; d < KB; ++d) win[q][d] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) yw[k][q] = 0.0;
+  }
   for (int i = 0; i < nk1; ++i) {
+#pragma unroll
+    for (int q = 0; q < KB - 1; ++q) {
+#pragma unroll
+      for (int d = 0; d < KB; ++d) win[q][d] = win[q + 1][d];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) yw[k][q] = yw[k][q + 1];
+    }
+    double a[KB];
+#pragma unroll
     for (int d = 0; d < KB; ++d) {
-      const int j = i + d;
-      if (j >= nk1) break;
-      double s = S.A[i][d];
-      for (int p = max(0, j - (KB - 1)); p < i; ++p) s -= S.R[p][i - p] * S.R[p][j - p];
+      const bool in = i + d < nk1;
+      double v = (d < K1 && in) ? S.G[i][d] : 0.0;
+      if (p2i != 0.0 && in) v += p2i * S.A[i][d];  // S.A holds B^T B while smoothing
+      a[d] = v;
+    }
+    double r0 = 0.0, inv = 0.0;
+#pragma unroll
+    for (int d = 0; d < KB; ++d) {
+      double sacc = a[d];
+#pragma unroll
+      for (int q = d; q < KB - 1; ++q) sacc -= win[q][KB - 1 - q] * win[q][KB - 1 - q + d];
       if (d == 0) {
-        if (!(s > 0.0)) return false;
-        S.R[i][0] = sqrt(s);
+        if (!(sacc > 0.0)) return false;
+        r0 = sqrt(sacc);
+        inv = 1.0 / r0;
+        win[KB - 1][0] = r0;
       } else {
-        S.R[i][d] = s / S.R[i][0];
+        win[KB - 1][d] = (i + d < nk1) ? sacc * inv : 0.0;
       }
     }
-  }
-  for (int dim = 0; dim < 3; ++dim) {
-    double* y = S.y[dim];
-    for (int i = 0; i < nk1; ++i) {
-      double s = S.Z[i][dim];
-      for (int p = max(0, i - (KB - 1)); p < i; ++p) s -= S.R[p][i - p] * y[p];
-      y[i] = s / S.R[i][0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double sacc = S.Z[i][k];
+#pragma unroll
+      for (int q = 0; q < KB - 1; ++q) sacc -= win[q][KB - 1 - q] * yw[k][q];
+      yw[k][KB - 1] = sacc * inv;
+      S.y[k][i] = yw[k][KB - 1];
     }
-    for (int i = nk1 - 1; i >= 0; --i) {
-      double s = y[i];
-      for (int d = 1; d < KB && i + d < nk1; ++d) s -= S.R[i][d] * c[dim][i + d];
-      c[dim][i] = s / S.R[i][0];
+#pragma unroll
+    for (int d = 0; d < KB; ++d) S.R[i][d] = win[KB - 1][d];
+  }
+  double cw[3][KB];  // cw[k][d] = c_{i + 1 + d}
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int d = 0; d < KB; ++d) cw[k][d] = 0.0;
+  for (int i = nk1 - 1; i >= 0; --i) {
+    double r[KB];
+#pragma unroll
+    for (int d = 0; d < KB; ++d) r[d] = S.R[i][d];
+    const double inv = 1.0 / r[0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double sacc = S.y[k][i];
+#pragma unroll
+      for (int d = 1; d < KB; ++d) sacc -= r[d] * cw[k][d - 1];
+      const double ci = sacc * inv;
+#pragma unroll
+      for (int d = KB - 1; d > 0; --d) cw[k][d] = cw[k][d - 1];
+      cw[k][0] = ci;
+      S.c[k][i] = ci;
     }
   }
   return true;
@@ -451,16 +501,25 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
   constexpr int NCAP = SPL_NK + K1;  // max knots: nk1 = n - K1 <= SPL_NK coefficients
   __shared__ SplSh S;
   const int tid = threadIdx.x;
-  if (tid == 0) {  // edge-point count = the packed length of the per-bin slabs; coverage = sum of row blocks
-    int e = 0;
-    for (int b = 0; b < nbins; ++b) e += min(kout[b], kcap);
-    S.n = e;
-    long c = -1;
-    if (cov) {
-      c = 0;
-      for (int b = 0; b < ncov; ++b) c += cov[b];
+  {  // edge-point count = the packed length of the per-bin slabs; coverage = sum of the row blocks
+    int e = 0, c = 0;
+    for (int b = tid; b < nbins; b += SPL_THREADS) e += min(kout[b], kcap);
+    if (cov)
+      for (int b = tid; b < ncov; b += SPL_THREADS) c += cov[b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      e += __shfl_xor(e, o, 64);
+      c += __shfl_xor(c, o, 64);
     }
-    res[8 + 3 * nsamp] = (double)c;
+    if ((tid & 63) == 0) {
+      S.kval[tid >> 6] = e;
+      S.kval[4 + (tid >> 6)] = c;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      S.n = S.kval[0] + S.kval[1] + S.kval[2] + S.kval[3];
+      res[8 + 3 * nsamp] = cov ? (double)(S.kval[4] + S.kval[5] + S.kval[6] + S.kval[7]) : -1.0;
+    }
   }
   __syncthreads();
   const int m = min(S.n, ecap), np = npts_p[0];
@@ -488,17 +547,23 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     }
     U[i] = run;
   }
-  S.scan[tid] = run;
-  __syncthreads();
-  if (tid == 0) {
-    double acc = 0.0;
-    for (int i = 0; i < SPL_THREADS; ++i) {
-      const double v = S.scan[i];
-      S.scan[i] = acc;
-      acc += v;
+  {  // exclusive block scan of the chunk lengths: wave shfl scans + the 4 wave totals (fixed order)
+    const int lane = tid & 63, w = tid >> 6;
+    double incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
     }
-    S.fp = acc;  // total chord length
-    S.bad = 0;
+    if (lane == 63) S.scan[w] = incl;
+    if (tid == 0) S.bad = 0;
+    __syncthreads();
+    double wbase = 0.0;
+    for (int q = 0; q < w; ++q) wbase += S.scan[q];
+    const double total_all = ((S.scan[0] + S.scan[1]) + S.scan[2]) + S.scan[3];
+    __syncthreads();
+    S.scan[tid] = wbase + incl - run;  // exclusive prefix of this thread's chunk
+    if (tid == 0) S.fp = total_all;    // total chord length
   }
   __syncthreads();
   const double base = S.scan[tid], total = S.fp;
@@ -545,11 +610,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     gram_pass<K>(S, P, U, m, nk1);
     if (tid == 0) {
       double sd = 0.0;
-      for (int i = 0; i < nk1; ++i) {
-#pragma unroll
-        for (int d = 0; d < K1; ++d) S.A[i][d] = S.G[i][d];
-      }
-      if (!chol_solve<K1>(S, nk1)) S.phase = PH_HOST;
+      if (!chol_solve<K1, K1>(S, nk1, 0.0)) S.phase = PH_HOST;
       for (int i = 0; i < nk1; ++i) sd += S.R[i][0];
       S.sumdiag = sd;
     }
@@ -613,21 +674,21 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
       S.phase = PH_SMOOTH;
     }
     __syncthreads();
+    // B^T B (band K2) once for all p: A[i][d] = sum_a B[i-a][a] * B[i-a][a+d], in parallel
+    for (int e = tid; e < nk1 * K2; e += SPL_THREADS) {
+      const int i = e / K2, d = e - (e / K2) * K2;
+      double v = 0.0;
+      for (int a = 0; a + d < K2; ++a) {
+        const int r = i - a;
+        if (r >= 0 && r < n8 && i + d < nk1) v += S.B[r][a] * S.B[r][a + d];
+      }
+      S.A[i][d] = v;
+    }
+    __syncthreads();
     for (int iter = 1; iter <= maxit; ++iter) {
       if (tid == 0) {
         const double pinv = 1.0 / p, p2i = pinv * pinv;
-        for (int i = 0; i < nk1; ++i) {
-#pragma unroll
-          for (int d = 0; d < K1; ++d) S.A[i][d] = S.G[i][d];
-          S.A[i][K1] = 0.0;
-        }
-        for (int r = 0; r < n8; ++r)
-#pragma unroll
-          for (int a = 0; a < K2; ++a)
-#pragma unroll
-            for (int bb = a; bb < K2; ++bb)
-              if (r + bb < nk1) S.A[r + a][bb - a] += p2i * S.B[r][a] * S.B[r][bb];
-        if (!chol_solve<K2>(S, nk1)) S.phase = PH_HOST;
+        if (!chol_solve<K2, K1>(S, nk1, p2i)) S.phase = PH_HOST;
       }
       __syncthreads();
       if (S.phase == PH_HOST) break;
@@ -720,15 +781,28 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     S.kap[tid] = nd > eps ? sqrt(cx * cx + cy * cy + cz * cz) / (nd * nd * nd) : 0.0;
   }
   __syncthreads();
-  if (tid == 0) {  // sample order, like the host loop
-    double ksum = 0.0, kmax = 0.0;
-    int cnt = 0;
-    for (int i = 0; i < nsamp; ++i)
-      if (S.kval[i]) {
-        ksum += S.kap[i];
-        kmax = cnt ? fmax(kmax, S.kap[i]) : S.kap[i];
-        ++cnt;
-      }
+  {  // mean / max over the samples with |r'| > eps: wave reductions, waves combined in order
+    const bool v = tid < nsamp && S.kval[tid];
+    double ks = v ? S.kap[tid] : 0.0, km = v ? S.kap[tid] : 0.0;
+    int kc = v ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ks += __shfl_xor(ks, o, 64);
+      km = fmax(km, __shfl_xor(km, o, 64));
+      kc += __shfl_xor(kc, o, 64);
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) {
+      S.kap[tid >> 6] = ks;
+      S.kap[4 + (tid >> 6)] = km;
+      S.kval[tid >> 6] = kc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double ksum = ((S.kap[0] + S.kap[1]) + S.kap[2]) + S.kap[3];
+    const double kmax = fmax(fmax(S.kap[4], S.kap[5]), fmax(S.kap[6], S.kap[7]));
+    const int cnt = S.kval[0] + S.kval[1] + S.kval[2] + S.kval[3];
     res[0] = SPL_OK;
     res[1] = ier;
     res[2] = n;

@@ -109,9 +109,11 @@ def micro_table(paths):
 
 
 def micro_main():
+    # profiles/conv_microbench.md is written by scripts/micro_report.py (one labelled column per run);
+    # this legacy path merged every micro_*.log into duplicate unlabelled rows, so it only prints now
     paths = sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "micro_*.log")))
     t = micro_table(paths)
-    if t:
+    if t and os.environ.get("RDP_LEGACY_MICRO_MD"):
         md = ["# Conv kernels per U-Net layer shape (scripts/conv_microbench.py, bs 32, median of rounds)", "",
               "fwd variants: v0 = auto dispatch, v1 = halo-tile kernel, v128/v256 = implicit-GEMM tiles; "
               "wgrad: v0 = default (BK=64, 2 stages). TF/s counts 2*N*H*W*9*Cin*Cout.", "", t]
