@@ -15,6 +15,8 @@ int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, con
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
                      hipStream_t);
+void rdp_conv_set_fixup_kb(long);
+void rdp_conv_set_stages(int);
 long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
@@ -717,6 +719,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
         py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
         py::arg("ws") = py::none());
+  m.def("conv_set_fixup_kb", &rdp_conv_set_fixup_kb, "split-K in-kernel fixup bound in KB (0 = reduce kernel)");
+  m.def("conv_set_stages", &rdp_conv_set_stages, "igemm K-pipeline depth: 0 = auto, 2-4 = forced");
   m.def("conv_ws_elems", [](int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
     return rdp_conv_ws_elems(N, H, W, C1, C2, Cout, taps, packed, bm_pref);
   });

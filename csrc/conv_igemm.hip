@@ -51,6 +51,8 @@ struct ConvArgs {
   int cpt;  // 64-channel chunks per tap (generic mode)
   int ksplit;    // > 1: split-K, work item = (tile, split), fp32 partial tiles go to kslab
   float* kslab;  // [ksplit][M][Cout] fp32
+  uint32_t* kcnt;  // split-K arrival counter per output tile (zero between launches)
+  int fixup;       // split-K: 1 = the tile's last-arriving block reduces + runs the epilogue in-kernel
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
   int store_aware;  // 1: the per-step vmcnt leaves the previous epilogue's stores in flight
@@ -64,8 +66,23 @@ extern "C" void rdp_conv_set_debug_flags(int f) { g_conv_debug_flags = f; }
 RDP_DEV int tap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
 RDP_DEV int tap_ds(int tap) { return tap - 3 * ((tap * 11) >> 5) - 1; }
 
-template <int BM, int BN, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs a) {
+template <int N>
+RDP_DEV void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+// wait until at most B + (epilogue stores issued since) vector-memory ops are outstanding
+template <int B, int P1, int P2>
+RDP_DEV void vm_wait_p(int pend) {
+  if (pend == 0) vm_wait<B>();
+  else if (pend == P1) vm_wait<B + P1>();
+  else vm_wait<B + P2>();
+}
+
+// NST: K-pipeline stages (LDS buffers). 2 = double buffering at 2 blocks / CU (default: the
+// co-resident block hides the DMA latency); 3-4 = a deeper ring at 1 block / CU (A/B option for
+// grids that put at most one block on each CU; measured no faster, see conv_stages()).
+template <int BM, int BN, int NWV = 4, bool FIX = false, int NST = 2>
+__global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int WAVES_M = BM / 64;
   constexpr int WAVES_N = NWV / WAVES_M;
   constexpr int WNT = BN / WAVES_N;  // couts per wave (64, or 32 with 8-wave blocks)
@@ -73,7 +90,12 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
   constexpr int P_BYTES = BM * 128, W_BYTES = BN * 128, BUF = P_BYTES + W_BYTES;
   constexpr int NROW = BM / 8 / NWV;     // pixel-row DMA pieces per wave per K step
   constexpr int WPIECES = BN / 8 / NWV;  // weight-row DMA pieces per wave per K step
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  constexpr int DMA_OPS = NROW + WPIECES;  // vector-memory ops per wave per stage
+  static_assert(NST >= 2 && NST <= 4, "pipeline depth");
+  // + 16 B: the split-K "last arriver" word (kept in the one LDS array: a second __shared__ object
+  // can make hipcc wait vmcnt(0) before every fragment read, cdna_hip_programming.md §5 item 4a)
+  // (only in the fixup variant: 2 x 40 KB + 16 B would drop the 256 x 64 tile to 1 block / CU)
+  __shared__ __attribute__((aligned(16))) char smem[NST * BUF + (FIX ? 16 : 0)];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -180,12 +202,23 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  int ks = 0, t = 0;    // compute position (K step within tile, tile index)
+  int iks = 0, it = 0;  // issue position (K step within tile, tile index) of the newest stage
+  int ig = 0;           // global index of the newest issued stage
+  int ibuf = 0, cbuf = 0;  // LDS buffer of the newest issued stage / of the stage being computed
   if (total > 0) {
     set_tile(0);
     issue(0, smem);
+#pragma unroll
+    for (int p = 1; p < NST - 1; ++p) {  // deeper pipelines: fill stages 1 .. NST-2 up front
+      if (p < total) {
+        if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
+        issue(iks, smem + p * BUF);
+        ig = p;
+        ibuf = p;
+      }
+    }
   }
-  int ks = 0, t = 0;    // compute position (K step within tile, tile index)
-  int iks = 0, it = 0;  // issue position of the stage in flight
   // vector-memory stores the previous step's epilogue issued after stage g's DMA: vmcnt counts
   // them in issue order, so stage g has landed once at most that many ops are outstanding (a plain
   // vmcnt(0) would also wait for the output stores of every tile before its next K step)
@@ -200,16 +233,26 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
   for (int g = 0; g < total; ++g) {
-    if (pend == 0 || !a.store_aware) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else if (pend == 2 * NJ) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NJ) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * NJ) : "memory");
+    // stage g has landed once at most (stages issued after it) x DMA_OPS + (epilogue stores issued
+    // after it) ops are outstanding (in-order completion); older stores are not counted, which only
+    // makes the wait stricter
+    {
+      const int ahead = ig - g;  // 0 .. NST-2
+      const int pd = a.store_aware ? pend : 0;
+      if (NST <= 2 || ahead == 0) vm_wait_p<0, 2 * NJ, 4 * NJ>(pd);
+      else if (NST <= 3 || ahead == 1) vm_wait_p<(NST > 2 ? DMA_OPS : 0), 2 * NJ, 4 * NJ>(pd);
+      else vm_wait_p<(NST > 3 ? 2 * DMA_OPS : 0), 2 * NJ, 4 * NJ>(pd);
+    }
     pend = 0;
     raw_barrier();
-    if (g + 1 < total) {
+    if (ig + 1 < total) {  // the buffer computed at step g-1: every wave is past it (barrier above)
       if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
-      issue(iks, smem + ((g + 1) & 1) * BUF);
+      ibuf = ibuf + 1 == NST ? 0 : ibuf + 1;
+      issue(iks, smem + ibuf * BUF);
+      ++ig;
     }
-    const char* pb = smem + (g & 1) * BUF;
+    const char* pb = smem + cbuf * BUF;
+    cbuf = cbuf + 1 == NST ? 0 : cbuf + 1;
     const char* wb = pb + P_BYTES;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -229,11 +272,14 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
     ks = 0;
     const int item = (int)lid + t * (int)G;
     ++t;
-    if (a.ksplit > 1) {  // fp32 partial tile -> slab[split][m][n]; epilogue runs in the reduce
+    int tile = item;
+    if (a.ksplit > 1) {  // fp32 partial tile -> slab[split][m][n]
       const int tiles1 = a.ntiles / a.ksplit;
-      const int tile = item % tiles1, split = item / tiles1;
+      tile = item % tiles1;
+      const int split = item / tiles1;
       const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
       const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
+      // in-kernel fixup: slabs stored write-through (sc1), so no release fence is needed
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
@@ -243,14 +289,50 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
           const f32x4 o = acc[j][i];
           acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
           const uint32_t off = m < a.M ? (uint32_t)(((long)split * a.M + m) * a.Cout + n) * 4u : RDP_OOB;
-          bstore16(rk, off, make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
-                                       __float_as_uint(o[3])));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rk, off, 0, FIX ? 16 : 0);
         }
       }
-      pend = 4 * NJ;  // NJ x 4 slab stores
-      continue;
+      if constexpr (!FIX) {  // the epilogue runs in conv_splitk_reduce_kernel
+        pend = 4 * NJ;  // NJ x 4 slab stores
+        continue;
+      }
+      // Publish / consume (cdna_hip_programming.md §6 Guideline 16, R1 counter form): every storing
+      // wave drains its write-through stores, the block barrier joins them, ONE lane takes a ticket on
+      // the tile's counter (agent scope); the block that draws ksplit-1 resets the counter, acquires
+      // (agent: drops this CU's stale L1 lines), drains, and after a barrier every wave reads the
+      // ksplit slabs with plain loads -- correct for any placement of the slices over XCDs / CUs.
+      wait_vm0();
+      __syncthreads();
+      volatile uint32_t* last_w = (volatile uint32_t*)(smem + NST * BUF);
+      if (threadIdx.x == 0) {
+        auto* c = (__attribute__((address_space(1))) uint32_t*)(a.kcnt + tile);
+        const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t last = old == (uint32_t)(a.ksplit - 1) ? 1u : 0u;
+        if (last) {
+          __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          wait_vm0();
+        }
+        *last_w = last;
+      }
+      __syncthreads();
+      pend = 0;
+      if (*last_w == 0u) continue;
+      // sum the slabs in split order (bitwise independent of which slice arrived last)
+      for (int sp = 0; sp < a.ksplit; ++sp) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = tm * BM + wm * 64 + i * 16 + (lane & 15);
+            const uint32_t off = m < a.M ? (uint32_t)(((long)sp * a.M + m) * a.Cout + n) * 4u : RDP_OOB;
+            acc[j][i] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 0));
+          }
+        }
+      }
+      // fall through: the epilogue of the reduced tile
     }
-    const int tile = item;
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
     // Widened stores: a lane holds 4 couts (16 j + 4 g + r, g = lane >> 4) of one pixel per
@@ -302,6 +384,31 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
       }
     }
     pend = 2 * NJ;  // 2 NJ output stores
+    if (FIX && a.stats) {
+      // fixup: this block reduced tile (tm, tn) -- its BN partial sums go to stats row (tm, wm)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float q1 = row16_sum(s1[j][r]), q2 = row16_sum(s2[j][r]);
+          s1[j][r] = q1;
+          s2[j][r] = q2;
+        }
+      if ((lane & 15) == 0) {
+        float* row = a.stats + (size_t)(tm * WAVES_M + wm) * 2 * a.Cout;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
+          *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+          *(float4*)(row + a.Cout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+      pend += NJ * 2;  // stats stores (lanes 0/16/32/48)
+    }
   }
   if (a.stats && a.ksplit == 1 && total > 0) {
     // reduce over the 16 pixel lanes (lane & 15) sharing a channel group; one slab row per (block group, wm)
@@ -395,6 +502,26 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
   }
 }
 
+// split-K workspace layout: [KCNT_WORDS] u32 arrival counters (zero-initialised by the caller, left
+// zero by every launch) followed by the fp32 slab
+#define KCNT_WORDS 256
+
+// In-kernel split-K fixup (the tile's last-arriving block reduces) vs the separate reduce launch.
+// Measured dead end (serving frame, N = 1, one MI355X): each fixed-up conv took 9-11 us longer
+// (drain of the write-through slab stores + ticket + agent acquire + the reducer's serial slab reads
+// from HBM) than the 6-7 us reduce launch it replaced, so the default bound is 0 (always the reduce
+// kernel). RDP_SPLITK_FIXUP_KB (or rdp_conv_set_fixup_kb) enables it for ksplit x BM x BN x 4 bytes
+// up to that size; kept tested (tests/test_kernels_gpu.py) for the A/B.
+static long g_fixup_kb = -1;
+extern "C" void rdp_conv_set_fixup_kb(long kb) { g_fixup_kb = kb; }
+static long fixup_max_bytes() {
+  if (g_fixup_kb < 0) {
+    const char* e = getenv("RDP_SPLITK_FIXUP_KB");
+    g_fixup_kb = e ? atol(e) : 0L;
+  }
+  return g_fixup_kb * 1024L;
+}
+
 // Split-K when the tile grid leaves most CUs idle: the smallest divisor of the K steps that gives
 // >= 256 work items with >= 4 K steps each, as long as the fp32 slab fits `ws_elems`.
 static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long ws_elems) {
@@ -410,6 +537,39 @@ static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long 
   return ks;
 }
 
+// K-pipeline depth. Measured dead end (serving frame at N = 1, one MI355X, same box A/B): the 4-stage
+// ring at 1 block / CU for grids of <= 256 blocks made every such conv 0.3-1 us SLOWER (e.g. 128^2
+// 128->128 13.4 -> 14.4 us, 64^2 256->256 17.5 -> 18.3 us; GPU p50 0.600 -> 0.614 ms): those convs
+// are bound by their fixed launch / prologue / epilogue cost, not by the per-step DMA round trip.
+// Default 2; RDP_CONV_STAGES (or rdp_conv_set_stages) = 3 / 4 forces the deep ring (1 block / CU) for
+// A/B runs (tests/test_kernels_gpu.py keeps all depths bitwise equal).
+static int g_conv_stages = -1;
+extern "C" void rdp_conv_set_stages(int n) { g_conv_stages = n; }
+static int conv_stages(int grid, int buf_bytes) {
+  if (g_conv_stages < 0) {
+    const char* e = getenv("RDP_CONV_STAGES");
+    g_conv_stages = e ? atoi(e) : 0;
+  }
+  (void)grid;
+  int nst = g_conv_stages > 2 ? g_conv_stages : 2;
+  while (nst > 2 && nst * buf_bytes + 16 > 160 * 1024) --nst;  // LDS per workgroup (+ fixup word)
+  return nst < 2 ? 2 : (nst > 4 ? 4 : nst);
+}
+
+template <int BM, int BN, int NWV, bool FIX>
+static void launch_depth(const ConvArgs& a, int grid, hipStream_t s) {
+  constexpr int BUF = (BM + BN) * 128;
+  const int nst = conv_stages(grid, BUF);
+  if constexpr (4 * BUF + 16 <= 160 * 1024) {
+    if (nst == 4) {
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV, FIX, 4>), dim3(grid), dim3(64 * NWV), 0, s, a);
+      return;
+    }
+  }
+  if (nst >= 3) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV, FIX, 3>), dim3(grid), dim3(64 * NWV), 0, s, a);
+  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV, FIX, 2>), dim3(grid), dim3(64 * NWV), 0, s, a);
+}
+
 template <int BM, int BN, int NWV = 4>
 static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) {
   const int tilesM = (a.M + BM - 1) / BM;
@@ -417,10 +577,15 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
   a.ntiles = tilesM * a.tilesN;
   a.ksplit = a.kslab ? choose_ksplit(a.ntiles, a.nks, a.M, a.Cout, a.packed, ws_elems) : 1;
   if (a.ksplit > 1) {
+    a.fixup = (long)a.ksplit * BM * BN * 4 <= fixup_max_bytes() && a.ntiles <= KCNT_WORDS;
     a.nks /= a.ksplit;
     a.ntiles *= a.ksplit;
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
+    if (a.fixup) {
+      launch_depth<BM, BN, NWV, true>(a, grid, s);
+      return tilesM * (BM / 64);  // stats rows (tm, wave row), written by the reducers
+    }
+    launch_depth<BM, BN, NWV, false>(a, grid, s);
     const int rpb = 256 / (a.Cout / 8);
     int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
@@ -431,7 +596,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
   // the per-block stats rows need every block to keep one channel tile (see the kernel)
   if (a.stats && grid % a.tilesN) return -1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
+  launch_depth<BM, BN, NWV, false>(a, grid, s);
   return grid / a.tilesN * (BM / 64);
 }
 
@@ -470,9 +635,14 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   }
   ConvArgs a;
   a.escale = escale; a.eshift = eshift; a.erelu = erelu;
-  a.kslab = ws;
+  // ws = [KCNT_WORDS counters | slab] (rdp_conv_ws_elems)
+  const bool has_ws = ws != nullptr && ws_elems > KCNT_WORDS;
+  a.kcnt = has_ws ? (uint32_t*)ws : nullptr;
+  a.kslab = has_ws ? ws + KCNT_WORDS : nullptr;
   a.ksplit = 1;
-  const long wse = ws_elems < (1L << 29) ? ws_elems : (1L << 29);  // slab bytes < 2 GiB (buffer offsets)
+  a.fixup = 0;
+  long wse = has_ws ? ws_elems - KCNT_WORDS : 0;
+  wse = wse < (1L << 29) ? wse : (1L << 29);  // slab bytes < 2 GiB (buffer offsets)
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
   a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
   a.C1 = C1; a.C2 = C2; a.pitch1 = pitch1; a.pitch2 = pitch2;
@@ -530,5 +700,5 @@ extern "C" long rdp_conv_ws_elems(int N, int H, int W, int C1, int C2, int Cout,
   const int BM = ((pref == 128 || pref == 0) && Cout % 128 == 0) ? 128 : 256, BN = BM == 128 ? 128 : 64;
   const int ntiles = (M + BM - 1) / BM * (Cout / BN);
   const int d = choose_ksplit(ntiles, nks, M, Cout, packed, 1L << 29);
-  return d > 1 ? (long)d * M * Cout : 0;
+  return d > 1 ? (long)d * M * Cout + KCNT_WORDS : 0;
 }

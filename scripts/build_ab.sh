@@ -13,6 +13,13 @@ for src in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -munsafe-fp-atomics -I csrc -c build/ab/$src -o build/ab/$src.o
   objs=$(echo $objs | sed "s|build/obj/$src.o|build/ab/$src.o|")
 done
+# symbols the current bindings need that the old sources lack: weak no-op stubs (AB_STUBS="name ...")
+if [ -n "$AB_STUBS" ]; then
+  : > build/ab/stubs.c
+  for f in $AB_STUBS; do echo "__attribute__((weak)) void $f(long x) { (void)x; }" >> build/ab/stubs.c; done
+  gcc -c -fPIC build/ab/stubs.c -o build/ab/stubs.o
+  objs="$objs build/ab/stubs.o"
+fi
 TL=$(python -c "import torch,os;print(os.path.join(os.path.dirname(torch.__file__),'lib'))")
 g++ -shared -o ab/_C_base.so $objs -L$TL -L/opt/rocm/lib -Wl,-rpath,$TL -Wl,-rpath,/opt/rocm/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip -ltorch_python -lamdhip64 -lz
 echo "built ab/_C_base.so from $rev: $*"

@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Kernel timeline of one serving-engine frame from a rocprofv3 kernel trace.
 
-Frames are delimited by ``preprocess_kernel`` (one per frame); the second-to-last complete frame is
-printed (start offset, duration, grid, kernel) with the summed kernel time.
+Frames are delimited by ``preprocess_kernel`` (one per frame). Prints, per kernel position of the
+frame, the start offset and duration of the second-to-last complete frame plus the median duration
+over the last (up to) 50 frames with the same kernel sequence, and the summed kernel time.
 usage: serve_frame.py <kernel_trace.csv>
 """
 import csv
+import statistics
 import sys
 
 
@@ -15,15 +17,22 @@ def main(path):
     if len(idx) < 3:
         print("fewer than 3 frames in the trace")
         return
-    i0, i1 = idx[-3], idx[-2]
-    t0 = int(rows[i0]["Start_Timestamp"])
-    tot = 0
-    print(f"{'start us':>9} {'dur us':>7} {'grid':>8} kernel")
-    for r in rows[i0:i1]:
+    frames = [rows[a:b] for a, b in zip(idx[:-1], idx[1:])]
+    ref = frames[-2]
+    sig = [r["Kernel_Name"] for r in ref]
+    same = [f for f in frames[-51:-1] if [r["Kernel_Name"] for r in f] == sig]
+    t0 = int(ref[0]["Start_Timestamp"])
+    tot = tmed = 0.0
+    print(f"{'start us':>9} {'dur us':>7} {'med us':>7} {'grid':>8} kernel   (median over {len(same)} frames)")
+    for k, r in enumerate(ref):
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        tot += e - s
-        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:7.1f} {r['Grid_Size_X']:>8} {r['Kernel_Name'].split('(')[0][:60]}")
-    print(f"kernel sum {tot / 1e3:.1f} us")
+        med = statistics.median(int(f[k]["End_Timestamp"]) - int(f[k]["Start_Timestamp"]) for f in same) / 1e3
+        tot += (e - s) / 1e3
+        tmed += med
+        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:7.1f} {med:7.1f} {r['Grid_Size_X']:>8} "
+              f"{r['Kernel_Name'].split('(')[0][:60]}")
+    span = (int(ref[-1]["End_Timestamp"]) - t0) / 1e3
+    print(f"kernel sum {tot:.1f} us (median-frame sum {tmed:.1f} us), first start -> last end {span:.1f} us")
 
 
 if __name__ == "__main__":

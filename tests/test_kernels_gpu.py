@@ -431,9 +431,25 @@ def test_conv_transpose2x2(C, N, h, w, Cin, Cout, H2, W2):
 
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(1, 16, 16, 512, 0, 512), (1, 8, 8, 256, 256, 256),
-                                              (2, 7, 9, 128, 0, 64), (1, 32, 32, 256, 0, 128)])
-def test_conv_splitk(C, N, H, W, C1, C2, Cout):
-    """Split-K path (small M, large K) with the stats epilogue, the BN-fold epilogue and split output."""
+                                              (2, 7, 9, 128, 0, 64), (1, 32, 32, 256, 0, 128),
+                                              (1, 64, 64, 128, 0, 256), (1, 64, 64, 256, 0, 256),
+                                              (1, 128, 128, 128, 128, 64)])
+@pytest.mark.parametrize("fixup_kb", [0, 256])
+def test_conv_splitk(C, N, H, W, C1, C2, Cout, fixup_kb):
+    """Split-K path (small M, large K) with the stats epilogue, the BN-fold epilogue and split output.
+
+    Deep splits (>= 9 slices of 128x128 tiles) reduce in conv_splitk_reduce_kernel; the serving
+    shapes with 2-4 slices (64^2 x 128/256 -> 256, 128^2 x 256 -> 64) take the in-kernel fixup
+    (last-arriving block reduces) when enabled (fixup_kb): same numerics, bitwise reproducible,
+    counters left at zero."""
+    C.conv_set_fixup_kb(fixup_kb)
+    try:
+        _splitk_case(C, N, H, W, C1, C2, Cout)
+    finally:
+        C.conv_set_fixup_kb(0)
+
+
+def _splitk_case(C, N, H, W, C1, C2, Cout):
     torch.manual_seed(6)
     dev = "cuda"
     x1 = bf(torch.randn(N, H, W, C1, device=dev))
@@ -451,6 +467,10 @@ def test_conv_splitk(C, N, H, W, C1, C2, Cout):
     r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, stats, 0, None, 0, ws)
     assert 0 < r <= rows
     assert relerr(nchw(y), ref) < 1e-2
+    assert torch.count_nonzero(ws[:256]) == 0  # split-K arrival counters are reset by the last arriver
+    yb = torch.empty_like(y)
+    C.conv_fwd(x1, x2, wk, 9, 0, yb, None, None, 0, None, 0, ws)
+    assert torch.equal(yb, y)  # slices summed in split order whichever arrives last
     yq = nchw(y).float()
     s = stats.view(rows, 2, Cout)[:r].sum(0)
     assert torch.allclose(s[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
@@ -468,6 +488,41 @@ def test_conv_splitk(C, N, H, W, C1, C2, Cout):
     y2 = torch.empty(N, H, W, Cout // 2, dtype=torch.bfloat16, device=dev)
     C.conv_fwd(x1, x2, wk, 9, 0, y1, y2, None, 0, None, 0, ws)
     assert relerr(torch.cat([nchw(y1), nchw(y2)], 1), ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [(1, 64, 64, 256, 0, 256, 0), (1, 16, 16, 512, 0, 512, 0),
+                                                   (4, 256, 256, 64, 0, 128, 0), (2, 33, 47, 64, 64, 64, 0),
+                                                   (1, 64, 64, 128, 0, 128, 128), (1, 64, 64, 128, 0, 64, 256)])
+def test_conv_pipeline_depth_bitwise(C, N, H, W, C1, C2, Cout, pref):
+    """The K pipeline at 2 / 3 / 4 stages (auto picks 4 for grids of <= 256 blocks) computes the same
+    MFMA sequence: outputs and BN partial sums bitwise equal across depths, and correct. Covers the
+    split-K reduce, persistent blocks walking several tiles (4 x 256^2: the deep ring crosses tile
+    boundaries) and the forced 4-wave tiles."""
+    torch.manual_seed(8)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    n_ws = C.conv_ws_elems(N, H, W, C1, C2, Cout, 9, 0, pref)
+    ws = torch.zeros(max(n_ws, 1), device=dev) if n_ws else None
+    rows = C.conv_stats_rows(N * H * W, Cout, pref)
+    outs = []
+    try:
+        for st in (2, 3, 4):
+            C.conv_set_stages(st)
+            y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+            stats = torch.zeros(rows * 2 * Cout, device=dev)
+            r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, stats, pref, None, 0, ws)
+            outs.append((y, stats.view(rows, 2, Cout)[:r].sum(0)))
+    finally:
+        C.conv_set_stages(0)
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.conv2d(xin, w.float(), padding=1)
+    assert relerr(nchw(outs[0][0]), ref) < 1e-2
+    for y, s in outs[1:]:
+        assert torch.equal(y, outs[0][0])
+        assert torch.allclose(s, outs[0][1], rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(2, 16, 16, 128, 0, 128), (1, 9, 13, 64, 64, 256)])
