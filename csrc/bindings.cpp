@@ -123,8 +123,9 @@ float* ws_ptr(const c10::optional<torch::Tensor>& ws, int K) {
 // stats slab rows written by conv_fwd: one per (M tile, wave row)
 int conv_stats_rows(long M, int Cout, int bm_pref) {
   bm_pref %= 1000;
-  if (bm_pref == 128 && Cout % 128 == 0) return (M + 127) / 128 * 2;
-  if (bm_pref == 256) return (M + 255) / 256 * 4;
+  // forced tiles: one row per (M tile, wave row), or up to 512 rows when split-K reduces them
+  if (bm_pref == 128 && Cout % 128 == 0) return (int)std::max<long>((M + 127) / 128 * 2, 512);
+  if (bm_pref == 256) return (int)std::max<long>((M + 255) / 256 * 4, 512);
   // auto / halo: upper bound over every tile choice (halo: up to 8 wave rows per 256-pixel tile)
   // split-K reduce: up to 512 rows
   const long a = (M + 127) / 128 * 2, b = (M + 255) / 256 * 8;

@@ -443,56 +443,61 @@ extern "C" int rdp_conv_halo(const void* x1, const void* x2, long xbytes1, long 
                              int Cout, const float* escale, const float* eshift, int erelu, hipStream_t s);
 
 // Split-K reduction + epilogue: y[m][n] = epi(sum_s slab[s][m][n]); optional BN-stats rows (one per
-// block). Thread = fixed 8-channel group (epilogue coefficients in registers), rows grid-strided.
+// block). Thread = fixed 4-channel group (epilogue coefficients in registers), rows grid-strided.
+// The slices are read 8 at a time as independent 16-B buffer loads (slices past ksplit read zeros
+// from an out-of-range offset: no branch around the loads) into 4 accumulators summed in a fixed
+// order: a dependent load per slice made this kernel one L2 round trip per slice (7-8 us at 18
+// slices at N = 1; the serving convs reduce 2-18 slices).
 __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs a, int nrow_blocks) {
-  extern __shared__ float sst[];  // [rows][2][8 per thread-group] stats staging
-  const int CG = a.Cout >> 3, RPB = 256 / CG;  // Cout power of two, <= 2048
+  extern __shared__ float sst[];  // [rows][2][Cout] stats staging
+  const int CG = a.Cout >> 2, RPB = 256 / CG;  // Cout power of two, 64 <= Cout <= 1024
   const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
-  const int n = g * 8;
-  float sc[8], sh[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { sc[k] = a.escale ? a.escale[n + k] : 1.f; sh[k] = a.eshift ? a.eshift[n + k] : 0.f; }
+  const int n = g * 4;
+  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.escale) sc = *(const float4*)(a.escale + n);
+  if (a.eshift) sh = *(const float4*)(a.eshift + n);
   const bool d2 = n >= a.Cy1;
   const int nn = d2 ? n - a.Cy1 : n;
   u16* const y = d2 ? a.y2 : a.y1;
   const int yp = d2 ? a.ypitch2 : a.ypitch1;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
+  const uint32_t sstride = (uint32_t)a.M * (uint32_t)a.Cout * 4u;  // bytes between slices
+  f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
   for (int m = blockIdx.x * RPB + r; m < a.M; m += nrow_blocks * RPB) {
-    float v[8];
+    f32x4 acc[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = 0.f;
-    for (int sp = 0; sp < a.ksplit; ++sp) {
-      const float* p = a.kslab + ((long)sp * a.M + m) * a.Cout + n;
-      const float4 p0 = *(const float4*)p, p1 = *(const float4*)(p + 4);
-      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
-      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
-    }
+    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t base = ((uint32_t)m * (uint32_t)a.Cout + (uint32_t)n) * 4u;
+    for (int sp0 = 0; sp0 < a.ksplit; sp0 += 8) {
+      f32x4 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      v[k] = fmaf(v[k], sc[k], sh[k]);
-      if (a.erelu) v[k] = fmaxf(v[k], 0.f);
-    }
-    uint4 o;
-    o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]); o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
-    *(uint4*)(y + (long)m * yp + nn) = o;
-    if (a.stats) {
-      const uint32_t w[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float q0 = __uint_as_float(w[k] << 16), q1 = __uint_as_float(w[k] & 0xffff0000u);
-        s1[2 * k] += q0; s2[2 * k] += q0 * q0;
-        s1[2 * k + 1] += q1; s2[2 * k + 1] += q1 * q1;
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t off = sp0 + u < a.ksplit ? base + (uint32_t)(sp0 + u) * sstride : RDP_OOB;
+        v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 0));
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u & 3] += v[u];
+    }
+    f32x4 o = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+    o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+    if (a.erelu) {
+      o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
+    }
+    const uint2 w = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+    *(uint2*)(y + (long)m * yp + nn) = w;
+    if (a.stats) {
+      const float q0 = __uint_as_float(w.x << 16), q1 = __uint_as_float(w.x & 0xffff0000u);
+      const float q2 = __uint_as_float(w.y << 16), q3 = __uint_as_float(w.y & 0xffff0000u);
+      s1[0] += q0; s2[0] += q0 * q0;
+      s1[1] += q1; s2[1] += q1 * q1;
+      s1[2] += q2; s2[2] += q2 * q2;
+      s1[3] += q3; s2[3] += q3 * q3;
     }
   }
   if (!a.stats) return;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sst[(r * 2 + 0) * a.Cout + n + k] = s1[k];
-    sst[(r * 2 + 1) * a.Cout + n + k] = s2[k];
-  }
+  *(float4*)(sst + (r * 2 + 0) * a.Cout + n) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  *(float4*)(sst + (r * 2 + 1) * a.Cout + n) = make_float4(s2[0], s2[1], s2[2], s2[3]);
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * a.Cout; c += 256) {
     const int half = c / a.Cout, ch = c - half * a.Cout;
@@ -525,7 +530,7 @@ static long fixup_max_bytes() {
 // Split-K when the tile grid leaves most CUs idle: the smallest divisor of the K steps that gives
 // >= 256 work items with >= 4 K steps each, as long as the fp32 slab fits `ws_elems`.
 static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long ws_elems) {
-  const bool pow2 = Cout >= 8 && Cout <= 2048 && (Cout & (Cout - 1)) == 0;
+  const bool pow2 = Cout >= 64 && Cout <= 1024 && (Cout & (Cout - 1)) == 0;  // reduce kernel's groups
   int ks = 1;
   if (!pow2 || packed || ntiles >= 192) return 1;
   for (int d = 2; d <= nks / 4; ++d) {
@@ -586,7 +591,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
       return tilesM * (BM / 64);  // stats rows (tm, wave row), written by the reducers
     }
     launch_depth<BM, BN, NWV, false>(a, grid, s);
-    const int rpb = 256 / (a.Cout / 8);
+    const int rpb = 256 / (a.Cout / 4);
     int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
     const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
