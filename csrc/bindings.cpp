@@ -11,7 +11,7 @@
 extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
-                   float*, long, hipStream_t);
+                   float*, long, void*, int, int*, hipStream_t);
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
                      hipStream_t);
@@ -77,7 +77,7 @@ int rdp_area_maxtap();
 int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
                        const double*, int, int, int, void*, hipStream_t);
 int rdp_geo_spline(const double*, int, int, const int*, const int*, double*, int*, double*, int, double, int, int,
-                   double, int, int, const int*, int, double*, hipStream_t);
+                   double, int, int, const int*, int, double*, double*, hipStream_t);
 }
 
 namespace {
@@ -136,7 +136,8 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)
 int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, int taps, int packed,
              torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref,
-             c10::optional<torch::Tensor> affine, int relu, c10::optional<torch::Tensor> ws) {
+             c10::optional<torch::Tensor> affine, int relu, c10::optional<torch::Tensor> ws,
+             c10::optional<torch::Tensor> pool) {
   Act a1 = act(x1, "x1"), a2;
   if (x2) {
     a2 = act(*x2, "x2");
@@ -165,12 +166,25 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     esh = affine->data_ptr<float>() + 3 * Cout;
   }
   if (ws) check_f32(*ws, "ws");
+  // pool (eval): MaxPool2d(2) of y1 -> pool [N][H/2][W/2][Cout]; fused into the split-K reduce when
+  // that path runs, else a maxpool2_fwd launch after the conv
+  Act po;
+  if (pool) {
+    po = act(*pool, "pool");
+    TORCH_CHECK(!y2 && !stats && po.N == o1.N && po.H == o1.H / 2 && po.W == o1.W / 2 && po.C == o1.C,
+                "pool: eval conv with one destination, [N][H/2][W/2][Cout]");
+  }
+  int pooled = 0;
   const int r = rdp_conv_igemm(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
                                a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1), o1.ptr,
                                y2 ? o2.ptr : nullptr, o1.bytes, y2 ? o2.bytes : 0, o1.C, o1.pitch, y2 ? o2.pitch : 0,
                                sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu,
-                               ws ? ws->data_ptr<float>() : nullptr, ws ? (long)ws->numel() : 0L, cur_stream());
+                               ws ? ws->data_ptr<float>() : nullptr, ws ? (long)ws->numel() : 0L,
+                               pool ? po.ptr : nullptr, pool ? po.pitch : 0, pool ? &pooled : nullptr, cur_stream());
   TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
+  if (pool && !pooled)
+    TORCH_CHECK(rdp_maxpool2_fwd(o1.ptr, o1.pitch, po.ptr, po.pitch, o1.N, o1.H, o1.W, o1.C, cur_stream()) == 0,
+                "conv_fwd: maxpool");
   return r;
 }
 
@@ -616,7 +630,7 @@ long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 // fit + nsamp-point evaluation and curvature into res (rdp_geo_spline_res_len(nsamp) doubles)
 void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch::Tensor sorted, torch::Tensor gperm,
                 torch::Tensor u, torch::Tensor res, double s, int k, int nsamp, double eps, int min_points,
-                int min_edge, c10::optional<torch::Tensor> cov) {
+                int min_edge, c10::optional<torch::Tensor> cov, c10::optional<torch::Tensor> dbg) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(2) == 4 &&
               out.is_contiguous(), "out [nbins][kcap][4] f64");
   TORCH_CHECK(kout.scalar_type() == torch::kInt32 && kout.numel() >= out.size(0), "kout");
@@ -634,10 +648,15 @@ void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch
     covp = cov->data_ptr<int>();
     ncov = cov->numel();
   }
+  double* dbgp = nullptr;  // optional phase profile (20 doubles, see geo_fit_kernel)
+  if (dbg && dbg->defined()) {
+    TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kFloat64 && dbg->numel() >= 20, "dbg: >= 20 f64");
+    dbgp = dbg->data_ptr<double>();
+  }
   const int r = rdp_geo_spline(out.data_ptr<double>(), out.size(0), out.size(1), kout.data_ptr<int>(),
                                npts.data_ptr<int>(), sorted.data_ptr<double>(), gperm.data_ptr<int>(),
                                u.data_ptr<double>(), ecap, s, k, nsamp, eps, min_points, min_edge, covp, ncov,
-                               res.data_ptr<double>(), cur_stream());
+                               res.data_ptr<double>(), dbgp, cur_stream());
   TORCH_CHECK(r == 0, "geo_spline: k must be in [1, 5], nsamp in [1, 256]");
 }
 
@@ -719,7 +738,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "rdp MI355X (gfx950) HIP kernels";
   m.def("conv_fwd", &conv_fwd, py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
         py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
-        py::arg("ws") = py::none());
+        py::arg("ws") = py::none(), py::arg("pool") = py::none());
   m.def("conv_set_fixup_kb", &rdp_conv_set_fixup_kb, "split-K in-kernel fixup bound in KB (0 = reduce kernel)");
   m.def("conv_set_stages", &rdp_conv_set_stages, "igemm K-pipeline depth: 0 = auto, 2-4 = forced");
   m.def("conv_ws_elems", [](int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
@@ -771,7 +790,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("geo_nblocks", &geo_nblocks);
   m.def("geo_spline", &geo_spline, py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
-        py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none());
+        py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none());
   m.def("png_decode", &png_decode);
   m.def("png_encode_gray8", &png_encode_gray8);
   m.def("resize_area_u8", &resize_area_u8);

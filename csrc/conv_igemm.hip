@@ -53,6 +53,8 @@ struct ConvArgs {
   float* kslab;  // [ksplit][M][Cout] fp32
   uint32_t* kcnt;  // split-K arrival counter per output tile (zero between launches)
   int fixup;       // split-K: 1 = the tile's last-arriving block reduces + runs the epilogue in-kernel
+  u16* pool;       // split-K reduce only: also write MaxPool2d(2) of the output (eval), [M/4][ppitch]
+  int ppitch;
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
   int store_aware;  // 1: the per-step vmcnt leaves the previous epilogue's stores in flight
@@ -463,7 +465,8 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
   const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
   const uint32_t sstride = (uint32_t)a.M * (uint32_t)a.Cout * 4u;  // bytes between slices
   f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
-  for (int m = blockIdx.x * RPB + r; m < a.M; m += nrow_blocks * RPB) {
+  // sum of the slices + epilogue for pixel m -> 4 bf16 (packed), stored to y
+  auto pixel = [&](int m) -> uint2 {
     f32x4 acc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -486,6 +489,34 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
     }
     const uint2 w = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
     *(uint2*)(y + (long)m * yp + nn) = w;
+    return w;
+  };
+  if (a.pool) {
+    // eval-mode MaxPool2d(2) of the output, fused: a thread owns 2x2 windows (H, W even)
+    const int Ho = a.H >> 1, Wo = a.W >> 1, nwin = a.M >> 2;
+    for (int wi = blockIdx.x * RPB + r; wi < nwin; wi += nrow_blocks * RPB) {
+      const int img = wi / (Ho * Wo), rem = wi - img * (Ho * Wo), ho = rem / Wo, wo = rem - ho * Wo;
+      const int m00 = (img * a.H + 2 * ho) * a.W + 2 * wo;
+      const uint2 q[4] = {pixel(m00), pixel(m00 + 1), pixel(m00 + a.W), pixel(m00 + a.W + 1)};
+      float mx[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t wd = k < 2 ? q[0].x : q[0].y;
+        mx[k] = __uint_as_float((k & 1) ? (wd & 0xffff0000u) : (wd << 16));
+      }
+#pragma unroll
+      for (int t = 1; t < 4; ++t)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t wd = k < 2 ? q[t].x : q[t].y;
+          mx[k] = fmaxf(mx[k], __uint_as_float((k & 1) ? (wd & 0xffff0000u) : (wd << 16)));
+        }
+      *(uint2*)(a.pool + (long)wi * a.ppitch + n) = make_uint2(pack2bf(mx[0], mx[1]), pack2bf(mx[2], mx[3]));
+    }
+    return;  // eval: no statistics
+  }
+  for (int m = blockIdx.x * RPB + r; m < a.M; m += nrow_blocks * RPB) {
+    const uint2 w = pixel(m);
     if (a.stats) {
       const float q0 = __uint_as_float(w.x << 16), q1 = __uint_as_float(w.x & 0xffff0000u);
       const float q2 = __uint_as_float(w.y << 16), q3 = __uint_as_float(w.y & 0xffff0000u);
@@ -576,7 +607,7 @@ static void launch_depth(const ConvArgs& a, int grid, hipStream_t s) {
 }
 
 template <int BM, int BN, int NWV = 4>
-static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) {
+static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, int* pooled = nullptr) {
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
   a.ntiles = tilesM * a.tilesN;
@@ -587,6 +618,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
     a.ntiles *= a.ksplit;
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
     if (a.fixup) {
+      a.pool = nullptr;
       launch_depth<BM, BN, NWV, true>(a, grid, s);
       return tilesM * (BM / 64);  // stats rows (tm, wave row), written by the reducers
     }
@@ -594,10 +626,16 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s) 
     const int rpb = 256 / (a.Cout / 4);
     int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
+    if (a.pool) {  // fused eval MaxPool2d(2): one work row per 2x2 window, no stats rows
+      nblk = (a.M / 4 + rpb - 1) / rpb;
+      nblk = nblk < 2048 ? nblk : 2048;
+      if (pooled) *pooled = 1;
+    }
     const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
     return nblk;
   }
+  a.pool = nullptr;  // the non-split epilogue does not pool (the caller launches maxpool2_fwd)
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
   // the per-block stats rows need every block to keep one channel tile (see the kernel)
   if (a.stats && grid % a.tilesN) return -1;
@@ -611,7 +649,10 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
                               long ybytes1, long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats,
                               int N, int H, int W, int Cout, int taps, int packed, int bm_pref,
                               const float* escale, const float* eshift, int erelu, float* ws, long ws_elems,
-                              hipStream_t s) {
+                              void* pool, int ppitch, int* pooled, hipStream_t s) {
+  // pool (eval, optional): MaxPool2d(2) of y1 fused into the split-K reduce when that path runs;
+  // *pooled = 1 if it was written (otherwise the caller pools)
+  if (pooled) *pooled = 0;
   // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 6 = force the row-ring kernel,
   // 128 / 256 (2 / 3: 8-wave) = force this kernel's tile
   {
@@ -646,6 +687,9 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   a.kslab = has_ws ? ws + KCNT_WORDS : nullptr;
   a.ksplit = 1;
   a.fixup = 0;
+  a.pool = (pool != nullptr && pooled != nullptr && stats == nullptr && y2 == nullptr && H % 2 == 0 && W % 2 == 0)
+               ? (u16*)pool : nullptr;
+  a.ppitch = ppitch;
   long wse = has_ws ? ws_elems - KCNT_WORDS : 0;
   wse = wse < (1L << 29) ? wse : (1L << 29);  // slab bytes < 2 GiB (buffer offsets)
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
@@ -686,12 +730,12 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // barrier + DMA latency, 1.5x the LDS fragment reads per MFMA) for the 128x128 / 256x64 tiles
   // (measured dead end: 256 x 256 / 256 x 128 tiles in this 2-phase structure, one 8-wave block
   // per CU -- 49 spilled VGPRs at 256 x 256; +6 % on 32^2 x 512 -> 512 only, -5..-40 % elsewhere)
-  if (bm_pref == 2 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s);
-  if (bm_pref == 3) return launch_cfg<256, 64, 8>(a, max_blocks, wse, s);
-  if (bm_pref == 128 && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s);
-  if (bm_pref == 0 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s);
-  if (bm_pref == 256) return launch_cfg<256, 64>(a, max_blocks, wse, s);
-  return launch_cfg<256, 64, 8>(a, max_blocks, wse, s);
+  if (bm_pref == 2 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s, pooled);
+  if (bm_pref == 3) return launch_cfg<256, 64, 8>(a, max_blocks, wse, s, pooled);
+  if (bm_pref == 128 && Cout % 128 == 0) return launch_cfg<128, 128>(a, max_blocks, wse, s, pooled);
+  if (bm_pref == 0 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s, pooled);
+  if (bm_pref == 256) return launch_cfg<256, 64>(a, max_blocks, wse, s, pooled);
+  return launch_cfg<256, 64, 8>(a, max_blocks, wse, s, pooled);
 }
 
 // fp32 workspace elements the auto dispatch would use for split-K on this shape (0 = no split)

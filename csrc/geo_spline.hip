@@ -134,8 +134,9 @@ struct SplSh {
   double scan[SPL_THREADS];
   double kap[SPL_THREADS];
   int kval[SPL_THREADS];
+  double ev[9][SPL_THREADS];               // samples: r, r', r'' x 3 dims
   double fp, sumdiag;
-  int n, phase, bad;
+  int n, phase, bad, smooth;
 };
 
 enum { PH_LSQ = 0, PH_SMOOTH = 1, PH_DONE = 2, PH_FAIL = 3, PH_HOST = 4 };
@@ -223,22 +224,40 @@ RDP_DEV void gram_pass(SplSh& S, const double* __restrict__ P, const double* __r
       x[2] = P[(size_t)it * 3 + 2];
     }
     const int lmin = wmin(act ? l : 0x7fffffff), lmax = wmax(act ? l : -1);
+    constexpr int NG = K1 * (K1 + 1) / 2, NV = NG + 3 * K1;  // band products + right-hand sides
     for (int v = lmin; v <= lmax; ++v) {
       const bool sel = act && l == v;
       if (!__any(sel)) continue;
       const int r0 = v - K1;  // 0-based row of the interval's first coefficient
+      // all NV products of this lane, then ONE step-major butterfly over them: the NV shuffle chains
+      // are independent, so their LDS-permute latencies overlap (value-major wsums serialised them:
+      // ~6.6 us per pass at 1 interval)
+      double q[NV];
+      {
+        int k = 0;
 #pragma unroll
-      for (int a = 0; a < K1; ++a) {
+        for (int a = 0; a < K1; ++a)
 #pragma unroll
-        for (int bb = a; bb < K1; ++bb) {
-          const double q = wsum(sel ? h[a + 1] * h[bb + 1] : 0.0);
-          if (lane == 0) S.Gw[w][r0 + a][bb - a] += q;
-        }
+          for (int bb = a; bb < K1; ++bb) q[k++] = sel ? h[a + 1] * h[bb + 1] : 0.0;
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const double q = wsum(sel ? h[a + 1] * x[d] : 0.0);
-          if (lane == 0) S.Zw[w][r0 + a][d] += q;
-        }
+        for (int a = 0; a < K1; ++a)
+#pragma unroll
+          for (int d = 0; d < 3; ++d) q[k++] = sel ? h[a + 1] * x[d] : 0.0;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) q[k] += __shfl_xor(q[k], o, 64);
+      if (lane == 0) {
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < K1; ++a)
+#pragma unroll
+          for (int bb = a; bb < K1; ++bb) S.Gw[w][r0 + a][bb - a] += q[k++];
+#pragma unroll
+        for (int a = 0; a < K1; ++a)
+#pragma unroll
+          for (int d = 0; d < 3; ++d) S.Zw[w][r0 + a][d] += q[k++];
       }
     }
   }
@@ -473,21 +492,26 @@ RDP_DEV double fprati_dev(double& p1, double& f1, double p2, double f2, double& 
   return p;
 }
 
-// value of a degree-KK spline (coefficients cd, knots t1 + lo, nn knots) at x, as rdp_splev1
+// the three coordinates of a degree-KK spline (coefficients cd, knots t1 + lo, nn knots) at x: one
+// interval search and basis, then per coordinate the arithmetic of rdp_splev1 (csrc/spline.cpp)
 template <int KK>
-RDP_DEV double splev_dev(const double* t1, int lo, int nn, const double* cd, int ncd, double x) {
-  const double* tt = t1 + lo;  // 1-based: tt[1] = t[lo + 1]
-  int l = KK;                  // 0-based interval as in spline.cpp: tt0[l] <= x < tt0[l+1]
+RDP_DEV void splev3_dev(const double* t1, int lo, int nn, const double (*cd)[SPL_NK], int ncd, double x,
+                        double (*out)[SPL_THREADS], int j) {
+  const double* tt = t1 + lo;
+  int l = KK;
   while (l < nn - KK - 2 && x >= tt[l + 2]) ++l;
   double h[KK + 2];
   bspl<KK>(tt, x, l + 1, h);
-  double s = 0.0;
 #pragma unroll
-  for (int j = 1; j <= KK + 1; ++j) {
-    const int ci = l - KK + j - 1;
-    if (ci >= 0 && ci < ncd) s += cd[ci] * h[j];
+  for (int d = 0; d < 3; ++d) {
+    double s = 0.0;
+#pragma unroll
+    for (int jj = 1; jj <= KK + 1; ++jj) {
+      const int ci = l - KK + jj - 1;
+      if (ci >= 0 && ci < ncd) s += cd[d][ci] * h[jj];
+    }
+    out[d][j] = s;
   }
-  return s;
 }
 
 template <int K>
@@ -496,11 +520,33 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
                                                               const int* __restrict__ npts_p, int ecap, double s,
                                                               int nsamp, double eps, int min_points, int min_edge,
                                                               const int* __restrict__ cov, int ncov,
-                                                              double* __restrict__ res) {
+                                                              double* __restrict__ res, double* __restrict__ dbg) {
   constexpr int K1 = K + 1, K2 = K + 2, nmin = 2 * K1;
   constexpr int NCAP = SPL_NK + K1;  // max knots: nk1 = n - K1 <= SPL_NK coefficients
   __shared__ SplSh S;
   const int tid = threadIdx.x;
+  // optional phase profile (dbg != nullptr, thread 0): 100 MHz realtime ticks per phase + counts.
+  // [0] m [1] LSQ iterations [2] smoothing iterations [3] total [4] setup [5] gram [6] chol LSQ
+  // [7] resid LSQ [8] knot control [9] BtB [10] chol smooth [11] resid smooth [12] eval [13] n
+  // [14..18] eval sub-phases: derivative coefficients, samples, curvature, reductions, result write
+  uint64_t t_last = 0;
+  double prof[20] = {0.0};
+  auto stamp = [&](int slot) {
+    if (dbg != nullptr && tid == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (slot >= 0) prof[slot] += (double)(now - t_last);
+      t_last = now;
+    }
+  };
+  stamp(-1);
+  const uint64_t t_start = t_last;
+  auto prof_flush = [&]() {
+    if (dbg != nullptr && tid == 0) {
+      stamp(12);
+      prof[3] = (double)(t_last - t_start);
+      for (int i = 0; i < 20; ++i) dbg[i] = prof[i];
+    }
+  };
   {  // edge-point count = the packed length of the per-bin slabs; coverage = sum of the row blocks
     int e = 0, c = 0;
     for (int b = tid; b < nbins; b += SPL_THREADS) e += min(kout[b], kcap);
@@ -584,7 +630,9 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
   const double ub = U[0], ue = U[m - 1];
   int ier = 0, nplus = 0;  // thread 0 only
   double fp0 = 0.0, fpold = 0.0, fpms = 0.0;
+  stamp(4);
   if (tid == 0) {
+    prof[0] = m;
     S.n = nmin;
     S.phase = PH_LSQ;
     S.nrdata[1] = m - 2;
@@ -607,16 +655,21 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
       }
     }
     __syncthreads();
+    stamp(8);
     gram_pass<K>(S, P, U, m, nk1);
+    stamp(5);
     if (tid == 0) {
       double sd = 0.0;
       if (!chol_solve<K1, K1>(S, nk1, 0.0)) S.phase = PH_HOST;
       for (int i = 0; i < nk1; ++i) sd += S.R[i][0];
       S.sumdiag = sd;
+      prof[1] += 1.0;
     }
     __syncthreads();
+    stamp(6);
     if (S.phase != PH_LSQ) break;
     resid_pass<K>(S, P, U, m, nk1, true);
+    stamp(7);
     if (tid == 0) {
       const double fp = S.fp;
       int nn = n;
@@ -658,10 +711,16 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
       }
     }
     __syncthreads();
+    stamp(8);
   }
   if (S.phase == PH_HOST) { finish_status(SPL_NEEDS_HOST, 0, S.n, 0.0); return; }
 
-  if (S.phase == PH_SMOOTH && ier != -2) {
+  // ier lives on thread 0: publish the block-uniform decision through LDS (a per-thread test here
+  // sent threads 1..255 through 20 idle smoothing iterations, ~27 us, whenever the polynomial fit
+  // already met s -- the common serving case)
+  if (tid == 0) S.smooth = S.phase == PH_SMOOTH && ier != -2;
+  __syncthreads();
+  if (S.smooth) {
     // ---- smoothing spline: p with fp(p) = s by rational interpolation ----
     const int n = S.n, nk1 = n - K1, n8 = n - nmin;
     double p1 = 0.0, f1 = 0.0, p3 = -1.0, f3 = 0.0, p = 0.0;
@@ -674,6 +733,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
       S.phase = PH_SMOOTH;
     }
     __syncthreads();
+    stamp(8);
     // B^T B (band K2) once for all p: A[i][d] = sum_a B[i-a][a] * B[i-a][a+d], in parallel
     for (int e = tid; e < nk1 * K2; e += SPL_THREADS) {
       const int i = e / K2, d = e - (e / K2) * K2;
@@ -685,14 +745,18 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
       S.A[i][d] = v;
     }
     __syncthreads();
+    stamp(9);
     for (int iter = 1; iter <= maxit; ++iter) {
       if (tid == 0) {
         const double pinv = 1.0 / p, p2i = pinv * pinv;
         if (!chol_solve<K2, K1>(S, nk1, p2i)) S.phase = PH_HOST;
+        prof[2] += 1.0;
       }
       __syncthreads();
+      stamp(10);
       if (S.phase == PH_HOST) break;
       resid_pass<K>(S, P, U, m, nk1, false);
+      stamp(11);
       if (tid == 0) {
         const double fp = S.fp;
         fpms = fp - s;
@@ -740,6 +804,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
         if (stop) S.phase = PH_DONE;
       }
       __syncthreads();
+      stamp(8);
       if (S.phase != PH_SMOOTH) break;
     }
     if (S.phase == PH_HOST) { finish_status(SPL_NEEDS_HOST, 0, S.n, 0.0); return; }
@@ -747,6 +812,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
 
   // ---- evaluation: r, r', r'' at nsamp parameters; kappa = |r' x r''| / |r'|^3 ----
   const int n = S.n, nk1 = n - K1;
+  if (tid == 0) prof[13] = n;
   for (int i = tid; i < 3 * nk1; i += SPL_THREADS) {  // first-derivative coefficients (splder)
     const int d = i / nk1, j = i % nk1;
     if (j < nk1 - 1) {
@@ -755,6 +821,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     }
   }
   __syncthreads();
+  stamp(14);
   for (int i = tid; i < 3 * nk1; i += SPL_THREADS) {  // second derivative
     const int d = i / nk1, j = i % nk1;
     if (j < nk1 - 2) {
@@ -763,16 +830,31 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     }
   }
   __syncthreads();
+  stamp(14);
+  // 3 x nsamp items (derivative order q, sample j): one interval search + basis per item for all three
+  // coordinates, spread over the block. (One thread per sample running the 9 evaluations inline made
+  // this phase ~30 us: a large cold code footprint executed once per launch.)
+  for (int it = tid; it < 3 * nsamp; it += SPL_THREADS) {
+    const int q = it / nsamp, j = it - q * nsamp;
+    const double x = nsamp > 1 ? (double)j / (double)(nsamp - 1) : 0.0;
+    if (q == 0) {
+      splev3_dev<K>(S.t, 0, n, S.c, nk1, x, S.ev, j);
+    } else if (q == 1) {
+      splev3_dev<K - 1>(S.t, 1, n - 2, S.cd1, nk1 - 1, x, S.ev + 3, j);
+    } else {
+      if constexpr (K >= 2) splev3_dev<K - 2>(S.t, 2, n - 4, S.cd2, nk1 - 2, x, S.ev + 6, j);
+      else S.ev[6][j] = S.ev[7][j] = S.ev[8][j] = 0.0;
+    }
+  }
+  __syncthreads();
+  stamp(15);
   if (tid < nsamp) {
-    const double x = nsamp > 1 ? (double)tid / (double)(nsamp - 1) : 0.0;
-    double r[3], d1[3], d2[3];
+    double d1[3], d2[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      r[d] = splev_dev<K>(S.t, 0, n, S.c[d], nk1, x);
-      d1[d] = splev_dev<K - 1>(S.t, 1, n - 2, S.cd1[d], nk1 - 1, x);
-      if constexpr (K >= 2) d2[d] = splev_dev<K - 2>(S.t, 2, n - 4, S.cd2[d], nk1 - 2, x);
-      else d2[d] = 0.0;
-      res[8 + (size_t)tid * 3 + d] = r[d];
+      res[8 + (size_t)tid * 3 + d] = S.ev[d][tid];
+      d1[d] = S.ev[3 + d][tid];
+      d2[d] = S.ev[6 + d][tid];
     }
     const double cx = d1[1] * d2[2] - d1[2] * d2[1], cy = d1[2] * d2[0] - d1[0] * d2[2],
                  cz = d1[0] * d2[1] - d1[1] * d2[0];
@@ -781,6 +863,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     S.kap[tid] = nd > eps ? sqrt(cx * cx + cy * cy + cz * cz) / (nd * nd * nd) : 0.0;
   }
   __syncthreads();
+  stamp(16);
   {  // mean / max over the samples with |r'| > eps: wave reductions, waves combined in order
     const bool v = tid < nsamp && S.kval[tid];
     double ks = v ? S.kap[tid] : 0.0, km = v ? S.kap[tid] : 0.0;
@@ -799,6 +882,7 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     }
     __syncthreads();
   }
+  stamp(17);
   if (tid == 0) {
     const double ksum = ((S.kap[0] + S.kap[1]) + S.kap[2]) + S.kap[3];
     const double kmax = fmax(fmax(S.kap[4], S.kap[5]), fmax(S.kap[6], S.kap[7]));
@@ -812,6 +896,8 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
     res[6] = m;
     res[7] = np;
   }
+  stamp(18);
+  prof_flush();
 }
 
 extern "C" {
@@ -820,12 +906,12 @@ int rdp_geo_spline_res_len(int nsamp) { return 9 + 3 * nsamp; }
 // sort the per-bin edge points (out [nbins][kcap][4], kout) into sorted [ecap][3] and fit/evaluate.
 int rdp_geo_spline(const double* out, int nbins, int kcap, const int* kout, const int* npts, double* sorted,
                    int* gperm, double* u, int ecap, double s, int k, int nsamp, double eps, int min_points,
-                   int min_edge, const int* cov, int ncov, double* res, hipStream_t st) {
+                   int min_edge, const int* cov, int ncov, double* res, double* dbg, hipStream_t st) {
   if (k < 1 || k > SPL_KMAX || nsamp < 1 || nsamp > SPL_THREADS) return -1;
   hipLaunchKernelGGL(geo_sort_kernel, dim3(nbins), dim3(256), 0, st, out, kcap, kout, sorted, gperm, ecap);
 #define RDP_FIT(KK)                                                                                                \
   hipLaunchKernelGGL(geo_fit_kernel<KK>, dim3(1), dim3(SPL_THREADS), 0, st, sorted, u, kout, nbins, kcap, npts, \
-                     ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res)
+                     ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res, dbg)
   switch (k) {
     case 1: RDP_FIT(1); break;
     case 2: RDP_FIT(2); break;

@@ -271,6 +271,10 @@ class UNetNative(nn.Module):
         return cache[key]
 
 
+# eval-mode MaxPool2d fused into the split-K conv reduce (serving); "0" = separate maxpool launches
+_FUSE_POOL_EVAL = os.environ.get("RDP_FUSE_POOL_EVAL", "1") != "0"
+
+
 def _native():
     from ..ops import native
     return native()
@@ -554,8 +558,12 @@ class UNetExecutor:
         m = self.m
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
-            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws)
-            return False
+            # with ``pool``: MaxPool2d(2) too (fused into the split-K reduce where that path runs;
+            # RDP_FUSE_POOL_EVAL=0: the separate maxpool launch, for A/B)
+            if pool is not None and not _FUSE_POOL_EVAL:
+                pool = None
+            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool)
+            return pool is not None
         rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
         g = m.store.view(sp.bn + ".weight")
         b = m.store.view(sp.bn + ".bias")

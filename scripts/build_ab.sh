@@ -10,7 +10,21 @@ objs=""
 for o in build/obj/*.o; do objs="$objs $o"; done
 for src in "$@"; do
   git show "$rev:csrc/$src" > build/ab/$src
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -munsafe-fp-atomics -I csrc -c build/ab/$src -o build/ab/$src.o
+  case $src in
+    *.hip) /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -munsafe-fp-atomics -I csrc -c build/ab/$src -o build/ab/$src.o ;;
+    *.cpp) python - "$src" <<'PY'
+import os, subprocess, sys, sysconfig
+from robotic_discovery_platform_amd import _build as b
+src = sys.argv[1]
+tinc, _, abi = b._torch_paths()
+cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+       "-I", b.CSRC, "-I", os.path.join(b.ROCM, "include")]
+if src == "bindings.cpp":
+    cmd += ["-DTORCH_EXTENSION_NAME=_C"] + sum((["-I", p] for p in tinc), []) + ["-I", sysconfig.get_paths()["include"]]
+subprocess.run(cmd + ["-c", f"build/ab/{src}", "-o", f"build/ab/{src}.o"], check=True)
+PY
+    ;;
+  esac
   objs=$(echo $objs | sed "s|build/obj/$src.o|build/ab/$src.o|")
 done
 # symbols the current bindings need that the old sources lack: weak no-op stubs (AB_STUBS="name ...")

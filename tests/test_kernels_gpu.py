@@ -490,6 +490,36 @@ def _splitk_case(C, N, H, W, C1, C2, Cout):
     assert relerr(torch.cat([nchw(y1), nchw(y2)], 1), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(1, 64, 64, 256, 0, 256), (1, 32, 32, 512, 0, 512),
+                                              (1, 128, 128, 128, 0, 128), (2, 16, 16, 256, 256, 512),
+                                              (1, 256, 256, 64, 0, 128)])
+def test_conv_eval_fused_pool(C, N, H, W, C1, C2, Cout):
+    """Eval conv (BN fold + ReLU) with ``pool=``: MaxPool2d(2) fused into the split-K reduce (deep
+    serving shapes) or launched after the conv (no split, last case) -- bitwise the pool of the output."""
+    torch.manual_seed(9)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    n_ws = C.conv_ws_elems(N, H, W, C1, C2, Cout, 9, 0, 0)
+    ws = torch.zeros(n_ws, device=dev) if n_ws else None
+    g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    a = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    p = torch.full((N, H // 2, W // 2, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, a, None, None, 0, coef, 1, ws, p)
+    a2 = torch.empty_like(a)
+    C.conv_fwd(x1, x2, wk, 9, 0, a2, None, None, 0, coef, 1, ws)
+    assert torch.equal(a, a2)
+    assert torch.equal(p, F.max_pool2d(nchw(a).float(), 2).to(torch.bfloat16).permute(0, 2, 3, 1))
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.relu(F.batch_norm(F.conv2d(xin, w.float(), padding=1), rm, rv, g, b, False, 0.0, 1e-5))
+    assert relerr(nchw(a), ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [(1, 64, 64, 256, 0, 256, 0), (1, 16, 16, 512, 0, 512, 0),
                                                    (4, 256, 256, 64, 0, 128, 0), (2, 33, 47, 64, 64, 64, 0),
                                                    (1, 64, 64, 128, 0, 128, 128), (1, 64, 64, 128, 0, 64, 256)])
