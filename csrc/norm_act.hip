@@ -34,13 +34,41 @@ __global__ void colsum_kernel(const float* __restrict__ in, int T, int K, int rp
   if (ty == 0 && col < K) out[(size_t)blockIdx.y * K + col] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
+#define FIN_DIRECT_ROWS 2048
+#define FIN_RG 16  // row groups per finalize block (blockDim = 64 * FIN_RG)
+
+// sum over rows t = ty, ty + FIN_RG, ... of p[t][c] and p[t][C + c] (row stride 2C), fp64
+RDP_DEV void fin_rows(const float* __restrict__ p, int T, int C, int c, int ty, double& s, double& q) {
+  double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+  int t = ty;
+  for (; t + 3 * FIN_RG < T; t += 4 * FIN_RG) {
+    const float a0 = p[(size_t)t * 2 * C + c], b0 = p[(size_t)t * 2 * C + C + c];
+    const float a1 = p[(size_t)(t + FIN_RG) * 2 * C + c], b1 = p[(size_t)(t + FIN_RG) * 2 * C + C + c];
+    const float a2 = p[(size_t)(t + 2 * FIN_RG) * 2 * C + c], b2 = p[(size_t)(t + 2 * FIN_RG) * 2 * C + C + c];
+    const float a3 = p[(size_t)(t + 3 * FIN_RG) * 2 * C + c], b3 = p[(size_t)(t + 3 * FIN_RG) * 2 * C + C + c];
+    s0 += (double)a0 + (double)a2;
+    s1 += (double)a1 + (double)a3;
+    q0 += (double)b0 + (double)b2;
+    q1 += (double)b1 + (double)b3;
+  }
+  for (; t < T; t += FIN_RG) {
+    s0 += (double)p[(size_t)t * 2 * C + c];
+    q0 += (double)p[(size_t)t * 2 * C + C + c];
+  }
+  s = s0 + s1;
+  q = q0 + q1;
+}
+
 // Measured dead end: one launch per BN pass (each block reduces a row chunk, the last block to
 // arrive -- agent-scope fences + a system-scope counter -- runs the finalize) was 7% SLOWER at bs64
 // and 40% at bs4 than colsum + finalize: every block's release fence is a full per-XCD L2 writeback
 // (buffer_wbl2), far more than the ~6 us kernel boundary it saves.
 // reduce [T][K] rows to <= 64 rows in `ws` if needed; returns (pointer, rows)
 static const float* shrink_rows(const float* in, int T, int K, float* ws, int& rows, hipStream_t s) {
-  if (T <= 64 || ws == nullptr) { rows = T; return in; }
+  // the finalize kernels sum up to FIN_DIRECT_ROWS rows themselves (16 row groups x 64 channels per
+  // block, 4 loads in flight per thread): one launch instead of colsum + finalize (bs 4 has 36 BN
+  // passes per step, each paying a kernel boundary for the shrink)
+  if (T <= FIN_DIRECT_ROWS || ws == nullptr) { rows = T; return in; }
   const int S = 64;
   const int rpc = (T + S - 1) / S;
   hipLaunchKernelGGL(colsum_kernel, dim3((K + 63) / 64, S), dim3(256), 0, s, in, T, K, rpc, ws);
@@ -49,26 +77,22 @@ static const float* shrink_rows(const float* in, int T, int K, float* ws, int& r
 }
 
 // coef layout: [0:C) mean, [C:2C) invstd, [2C:3C) scale = gamma*invstd, [3C:4C) shift = beta - mean*scale
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int T, int C, double count,
+__global__ __launch_bounds__(64 * FIN_RG) void bn_finalize_kernel(const float* __restrict__ stats, int T, int C, double count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ rmean, float* __restrict__ rvar, long long* nbt,
                                    float momentum, float eps, float* __restrict__ coef) {
-  __shared__ double red[2][4][64];
+  __shared__ double red[2][FIN_RG][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int t = ty; t < T; t += 4) {
-      s += (double)stats[(size_t)t * 2 * C + c];
-      q += (double)stats[(size_t)t * 2 * C + C + c];
-    }
-  }
+  if (c < C) fin_rows(stats, T, C, c, ty, s, q);
   red[0][ty][tx] = s;
   red[1][ty][tx] = q;
   __syncthreads();
   if (ty == 0 && c < C) {
-    s = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
-    q = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    s = 0.0;
+    q = 0.0;
+    for (int g = 0; g < FIN_RG; ++g) { s += red[0][g][tx]; q += red[1][g][tx]; }
     const double mean = s / count;
     double var = q / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -215,26 +239,22 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_kernel(const u16* __re
 
 // Backward finalize: dgamma, dbeta (written or accumulated into fp32 grads) and the apply
 // coefficients coef2 = [A | B | Cc]: dy = A*g + B*y + Cc.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int T, int C, double count,
+__global__ __launch_bounds__(64 * FIN_RG) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int T, int C, double count,
                                        const float* __restrict__ gamma, const float* __restrict__ coef,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
                                        float* __restrict__ coef2) {
-  __shared__ double red[2][4][64];
+  __shared__ double red[2][FIN_RG][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int t = ty; t < T; t += 4) {
-      s += (double)partial[(size_t)t * 2 * C + c];
-      q += (double)partial[(size_t)t * 2 * C + C + c];
-    }
-  }
+  if (c < C) fin_rows(partial, T, C, c, ty, s, q);
   red[0][ty][tx] = s;
   red[1][ty][tx] = q;
   __syncthreads();
   if (ty == 0 && c < C) {
-    s = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
-    q = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    s = 0.0;
+    q = 0.0;
+    for (int g = 0; g < FIN_RG; ++g) { s += red[0][g][tx]; q += red[1][g][tx]; }
     if (dbeta) dbeta[c] = (float)s;
     if (dgamma) dgamma[c] = (float)q;
     const double mean = coef[c], inv = coef[C + c], gm = gamma[c];
@@ -301,7 +321,7 @@ int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* g
                     float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef, float* ws,
                     hipStream_t s) {
   stats = shrink_rows(stats, T, 2 * C, ws, T, s);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, stats, T, C, (double)count, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
                      beta, rmean, rvar, nbt, momentum, eps, coef);
   return 0;
 }
@@ -336,7 +356,7 @@ int rdp_bn_relu_bwd_reduce(const void* da, int dapitch, const void* y, int ypitc
 int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const float* gamma, const float* coef,
                         float* dgamma, float* dbeta, float* coef2, float* ws, hipStream_t s) {
   partial = shrink_rows(partial, T, 2 * C, ws, T, s);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, partial, T, C, (double)count, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
                      coef, dgamma, dbeta, coef2);
   return 0;
 }
