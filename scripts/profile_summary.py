@@ -75,13 +75,24 @@ def main():
                    "## One step, per kernel", "", "```", run_tool("trace_breakdown.py", trace, "4"), "```"]
         open(os.path.join(ROOT, "profiles", "train_step_transposed.md"), "w").write("\n".join(md) + "\n")
         print("wrote profiles/train_step_transposed.md")
+    b4 = find("prof_bs4/**/bs4_kernel_trace.csv")
+    if b4:
+        md = ["# Native training step at the reference batch (bs 4, 256², bf16, Adam): kernel time (rocprofv3)", "",
+              "Default schedule (eager launches, wgrads on the side stream): `rocprofv3 --kernel-trace --stats -- "
+              "python3 bench.py --batch 4 --steps 20 --warmup 5 --serve 0` on one MI355X (the profiler adds "
+              "per-launch overhead; the unprofiled rate is `ref_batch_imgs_per_s` in the bench line).", "",
+              "## Wall / busy / idle per step (µs; sum > busy = the side-stream wgrads overlap the main stream)", "",
+              "```", run_tool("graph_gaps.py", b4), "```", "", "## Per-kernel totals for one step", "", "```",
+              run_tool("trace_breakdown.py", b4, "4"), "```"]
+        open(os.path.join(ROOT, "profiles", "train_step_bs4.md"), "w").write("\n".join(md) + "\n")
+        print("wrote profiles/train_step_bs4.md")
     sv = find("prof_serve/**/serve_kernel_stats.csv")
     if sv:
         shutil.copy(sv, os.path.join(ROOT, "profiles", "serve_kernel_stats.csv"))
         md = ["# Serving benchmark: kernel time (rocprofv3 --kernel-trace --stats)", "",
-              "`python -m robotic_discovery_platform_amd.serve.bench_serve --frames 200 --warmup 20 --train-steps 20` "
-              "(includes the 20 short training steps that produce realistic masks, then per-frame graph replays "
-              "of the engine and the gRPC e2e runs).", "", stats_table(sv, 40)]
+              "`python -m robotic_discovery_platform_amd.serve.bench_serve --frames 200 --warmup 20 --train-steps 200 --e2e 0` "
+              "(includes the 200 training steps that produce realistic masks, then per-frame graph replays "
+              "of the engine).", "", stats_table(sv, 40)]
         st = find("prof_serve/**/serve_kernel_trace.csv")
         if st:
             md += ["", "## One engine frame (graph replay), kernel timeline", "", "```",
