@@ -60,10 +60,10 @@ int rdp_head_bwd(const void*, int, const float*, const float*, const float*, con
 int rdp_head_bn_bwd_apply(const void*, int, const float*, const float*, const float*, const float*, const float*,
                           const float*, void*, int, int, float, float, float, hipStream_t);
 int rdp_head_mask(const void*, int, const float*, const float*, float, void*, int, hipStream_t);
-int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, int*,
+int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, int*, int,
              hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
-int rdp_wprep(const float*, void*, const void*, int, hipStream_t);
+int rdp_wprep(const float*, void*, const void*, int, int*, hipStream_t);
 int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
 double rdp_splev1(const double*, int, const double*, int, double, int);
@@ -506,7 +506,7 @@ void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_t
 }
 
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
-          double lr, double b1, double b2, double eps, double wd, double gscale, torch::Tensor step) {
+          double lr, double b1, double b2, double eps, double wd, double gscale, torch::Tensor step, bool inc) {
   check_f32(p, "p"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam numel");
   TORCH_CHECK(step.scalar_type() == torch::kInt32 && step.is_cuda(), "step int32");
@@ -517,7 +517,7 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c1
   }
   TORCH_CHECK(rdp_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sh, p.numel(),
                        (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale,
-                       (int*)step.data_ptr(), cur_stream()) == 0, "adam: numel must be a multiple of 4");
+                       (int*)step.data_ptr(), inc ? 1 : 0, cur_stream()) == 0, "adam: numel must be a multiple of 4");
 }
 
 void cast_bf16(torch::Tensor p, torch::Tensor out) {
@@ -526,11 +526,16 @@ void cast_bf16(torch::Tensor p, torch::Tensor out) {
   rdp_cast_bf16(p.data_ptr<float>(), out.data_ptr(), p.numel(), cur_stream());
 }
 
-void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg) {
+void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg, c10::optional<torch::Tensor> step) {
   check_f32(master, "master");
   TORCH_CHECK(out.scalar_type() == torch::kBFloat16, "wprep out bf16");
   TORCH_CHECK(segs.is_cuda() && segs.numel() * segs.element_size() >= (long)nseg * rdp_wseg_size(), "segs");
-  rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, cur_stream());
+  int* sp = nullptr;
+  if (step) {
+    TORCH_CHECK(step->scalar_type() == torch::kInt32 && step->is_cuda(), "step int32");
+    sp = (int*)step->data_ptr();
+  }
+  rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, sp, cur_stream());
 }
 
 void check_cpu_f64(const torch::Tensor& t, const char* name) {
@@ -777,9 +782,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale"), py::arg("coef") = py::none(), py::arg("bnpart") = py::none());
   m.def("head_bn_bwd_apply", &head_bn_bwd_apply);
   m.def("head_mask", &head_mask);
-  m.def("adam", &adam);
+  m.def("adam", &adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
+        py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
+        py::arg("inc") = true);
   m.def("cast_bf16", &cast_bf16);
-  m.def("wprep", &wprep);
+  m.def("wprep", &wprep, py::arg("master"), py::arg("out"), py::arg("segs"), py::arg("nseg"),
+        py::arg("step") = py::none());
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
   m.def("geo_edges", &geo_edges, py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),

@@ -61,10 +61,13 @@ struct WSeg {
 // kind 0 is a per-tap 2-D transpose ([cout][cin] -> [cin][cout]); it goes through a 64x64 LDS tile
 // so both the fp32 reads (along cin) and the bf16 writes (along cout) are coalesced. (The direct
 // element-wise gather read the masters with a stride of taps*cin floats: ~130 us per step.)
+// step != nullptr: also advance Adam's device step counter (the optimizer step just ran on the
+// same stream, so every Adam block has read it) -- one launch fewer than a separate increment
 __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ master, u16* __restrict__ out,
-                                                    const WSeg* __restrict__ segs) {
+                                                    const WSeg* __restrict__ segs, int* __restrict__ step) {
   const WSeg sg = segs[blockIdx.y];
   const int tid = threadIdx.x;
+  if (step && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) step[0] += 1;
   if (sg.kind == 0) {
     __shared__ u16 tile[64][66];
     const int tco = (sg.cout + 63) >> 6, tci = (sg.cin + 63) >> 6;
@@ -102,14 +105,15 @@ __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ ma
 }
 
 extern "C" {
+// inc = 0: the caller advances the step counter later on this stream (rdp_wprep with step)
 int rdp_adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2,
-             float eps, float wd, float gscale, int* step, hipStream_t s) {
+             float eps, float wd, float gscale, int* step, int inc, hipStream_t s) {
   if (n % 4) return -1;
   const long n4 = n / 4;
   const int grid = (int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 8192));
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, s, p, g, m, v, (u16*)shadow, n, lr, b1, b2, eps, wd, gscale,
                      step);
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  if (inc) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   return 0;
 }
 
@@ -120,9 +124,12 @@ int rdp_cast_bf16(const float* p, void* out, long n, hipStream_t s) {
 }
 
 // segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps} (32 bytes each)
-int rdp_wprep(const float* master, void* out, const void* segs, int nseg, hipStream_t s) {
-  if (nseg <= 0) return 0;
-  hipLaunchKernelGGL(wprep_kernel, dim3(128, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs);
+int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* step, hipStream_t s) {
+  if (nseg <= 0) {
+    if (step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+    return 0;
+  }
+  hipLaunchKernelGGL(wprep_kernel, dim3(128, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, step);
   return 0;
 }
 int rdp_wseg_size() { return (int)sizeof(WSeg); }

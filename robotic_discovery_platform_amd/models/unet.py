@@ -880,8 +880,8 @@ class NativeAdam:
         C = _native()
         st = self.m.store
         C.adam(st.flat, st.grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr, self.betas[0], self.betas[1], self.eps,
-               self.wd, gscale, st.step)
-        C.wprep(st.flat, self.m.derived, self.m._segs, self.m._nseg)
+               self.wd, gscale, st.step, False)
+        C.wprep(st.flat, self.m.derived, self.m._segs, self.m._nseg, st.step)  # + the step counter advance
 
     def state_dict(self):
         st = self.m.store
