@@ -715,7 +715,14 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
     h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
     const int nblk = tiles * h.splits;
-    if (variant == 0 && W % 64 == 0 && BN == 64) {  // row-ring variant: same split of the positions
+    // A/B: the row-ring variant also at BN = 128. Measured neutral in the overlapped step (bs 64
+    // 2892 / 2915 vs 2897 / 2916 img/s; bs 4 1539 / 1544 vs 1535 / 1538), as is the halo grid
+    // target (RDP_WGRAD_HALO_BLOCKS 256 / 512 / 1024: 2891 / 2881 / 2881, 2880 / 2890 / 2879).
+    static const int env_ring128 = [] {
+      const char* e = getenv("RDP_WGRAD_RING128");
+      return e ? atoi(e) : 0;
+    }();
+    if (variant == 0 && W % 64 == 0 && (BN == 64 || env_ring128)) {  // row-ring variant: same split of the positions
       WgradRingArgs g;
       g.x1 = h.x1; g.x2 = h.x2; g.xbytes1 = h.xbytes1; g.xbytes2 = h.xbytes2;
       g.C1 = C1; g.C2 = C2; g.pitch1 = pitch1; g.pitch2 = pitch2;
