@@ -40,6 +40,8 @@ int rdp_bn_bwd_finalize(const float*, int, int, long, const float*, const float*
 int rdp_bn_relu_bwd_apply(const void*, int, const void*, int, const float*, const float*, void*, int, int, int, int,
                           hipStream_t);
 int rdp_maxpool2_fwd(const void*, int, void*, int, int, int, int, int, hipStream_t);
+int rdp_conv_ring_head(const void*, long, int, int, const void*, long, int, int, int, int, int, const float*,
+                       const float*, const float*, const float*, float, void*, hipStream_t);
 int rdp_maxpool2_bwd(const void*, int, const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int rdp_bn_relu_apply_pool(const void*, int, void*, int, void*, int, const float*, int, int, int, int, hipStream_t);
 int rdp_maxpool2_bwd_bn_reduce(const void*, int, const void*, int, const void*, int, void*, int, const void*, int,
@@ -498,6 +500,26 @@ void head_bn_bwd_apply(torch::Tensor y, torch::Tensor w, torch::Tensor logits, t
               "head_bn_bwd_apply: pitches must be multiples of 8");
 }
 
+// eval conv (64 -> 64, BN fold + ReLU) + serving 1x1 head + (logit > thr) in one kernel (row ring);
+// returns false (nothing launched) where that kernel does not apply
+bool conv_head_mask(torch::Tensor x, torch::Tensor w, torch::Tensor coef, torch::Tensor hw, torch::Tensor hb,
+                    double thr, torch::Tensor mask) {
+  Act a = act(x, "x");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
+  check_f32(coef, "coef");
+  check_f32(hw, "head_w");
+  check_f32(hb, "head_b");
+  TORCH_CHECK(coef.numel() >= 4l * w.size(0) && hw.numel() == w.size(0) && hb.numel() >= 1, "coef / head sizes");
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == torch::kUInt8 && mask.is_contiguous() &&
+              mask.numel() >= (long)a.N * a.H * a.W, "mask: u8 [N*H*W]");
+  const int Co = (int)w.size(0);
+  const int r = rdp_conv_ring_head(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), Co, a.N, a.H,
+                                   a.W, coef.data_ptr<float>() + 2 * Co, coef.data_ptr<float>() + 3 * Co,
+                                   hw.data_ptr<float>(), hb.data_ptr<float>(), (float)thr, mask.data_ptr(),
+                                   cur_stream());
+  return r == 0;
+}
+
 void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_thr, torch::Tensor mask) {
   Act x = act(a, "a");
   TORCH_CHECK(mask.scalar_type() == torch::kUInt8 && mask.numel() == (long)x.N * x.H * x.W, "mask u8 numel");
@@ -782,6 +804,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale"), py::arg("coef") = py::none(), py::arg("bnpart") = py::none());
   m.def("head_bn_bwd_apply", &head_bn_bwd_apply);
   m.def("head_mask", &head_mask);
+  m.def("conv_head_mask", &conv_head_mask);
   m.def("adam", &adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
         py::arg("inc") = true);

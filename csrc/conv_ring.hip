@@ -45,6 +45,12 @@ struct RingArgs {
   const u16* bny;
   int bnypitch;
   const float* bncoef;
+  // serving head (HEAD variant): mask[m] = (sum_c a[m][c] * hw[c] + hb > hthr) for the eval output a
+  // (BN folded + ReLU, bf16-rounded); the 64-channel output itself is not stored
+  const float* hw;
+  const float* hb;
+  float hthr;
+  uint8_t* hmask;
   int H, W, WS;  // WS = W / 64 segments per image row
   int nrows;     // N * WS * H: input rows in column order (R = column * H + h)
   int npairs;    // nrows / 2: steps (two output rows each)
@@ -59,7 +65,12 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 // COUT = 64: 8 waves = 2 channel groups x 4 pixel groups (32 px); COUT = 128: 4 x 2 (64 px).
 // BNR: dgrad epilogue fused with the owner layer's BN-backward reduction (a separate instantiation:
 // its y registers would otherwise cost every other variant 12 VGPRs -- spills at COUT = 128)
-template <int COUT, int ABL = 0, bool BNR = false>
+// HEAD (COUT = 64, eval): the serving 1x1 head + threshold in the epilogue (SURVEY.md §7.3 "Conv1x1
+// head fused into the epilogue of up4.conv2"). A pixel's 64 channels live in two waves (cg = 0, 1):
+// each reduces its 32 over the lane groups, cg = 1 leaves its partial in LDS (double-buffered by step
+// parity), and cg = 0 finishes the pixel after the next step's barrier (the last step after a final
+// barrier) and stores the u8 mask.
+template <int COUT, int ABL = 0, bool BNR = false, bool HEAD = false>
 __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
   constexpr int PXW = 128 / NPG, NI = PXW / 16;  // pixels per wave (one output row half or whole)
@@ -67,8 +78,10 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NX = 8;           // ring slots: 4 rows in use + 2 steps x 2 rows in flight
   constexpr int PIECES = 18;      // 1-KiB DMA pieces per step (2 rows x 9)
   constexpr int MINPW = PIECES / 8;
-  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 4 * COUT * 4];  // + zero slot, BN fold / BN-bwd coefs
+  constexpr int HPART = HEAD ? 2 * NPG * PXW * 4 : 0;  // head partials [parity][pixel group][pixel]
+  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 4 * COUT * 4 + HPART];  // + zero slot, BN fold / BN-bwd coefs
   float* const efold = (float*)(ring + (NX + 1) * XREG);  // eval BN fold [scale | shift] (LDS, not VGPRs)
+  float* const hpart = (float*)(ring + (NX + 1) * XREG + 4 * COUT * 4);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -181,21 +194,50 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   const int gq = lane >> 4;
   const int coff = 16 * (gq & 1) + 8 * (gq >> 1);  // this lane's 8 channels after the pair swap
 
+  // head: this lane's 8 head weights (channels 32 cg + 16 j + 4 gq + r), the previous step's own
+  // partials (cg = 0) and output row
+  float hwl[2][4];
+  float hprev[NI];
+  int hm_prev = -1;
+  if constexpr (HEAD) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hwl[j][r] = a.hw[32 * cg + 16 * j + 4 * gq + r];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) hprev[i] = 0.f;
+  }
+  const float hbias = HEAD ? a.hb[0] : 0.f;
+  // cg = 0: finish the pixels of the step whose partials (parity par) are in LDS
+  auto head_finish = [&](int par) {
+    if (cg != 0 || hm_prev < 0) return;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int px = 16 * i + (lane & 15);
+      const float x = hprev[i] + hpart[(par * NPG + pg) * PXW + px] + hbias;
+      if (lane < 16) a.hmask[hm_prev + px0 + px] = x > a.hthr ? 1 : 0;
+    }
+  };
+
   for (int ks = 0; ks < nks; ++ks) {
     const int P = P0 + ks;
     // Stage P must have landed. vmcnt also counts the NI output stores every wave issues at the end
     // of a step, in issue order: younger than stage P are the stores of steps ks-2 and ks-1 and
     // (unless this is the last step) stage P+1 -- leave exactly those in flight.
+    // (HEAD: no activation stores; the mask stores of cg = 0 are not counted, which only makes the
+    // wait stricter)
+    constexpr int NS = HEAD ? 0 : NI;  // counted output stores per step
     if (ks + 1 < nks) {
-      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2 * NI) : "memory");
-      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + NI) : "memory");
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2 * NS) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + NS) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
     } else {
-      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NI) : "memory");
-      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NS) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     raw_barrier();
+    if constexpr (HEAD) head_finish((ks - 1) & 1);
     // BN-backward fusion: the owner layer's pre-BN activations at this step's outputs, loaded before
     // the stage P + 2 DMAs so their latency hides under the taps. (hipcc cannot see the DMAs, so its
     // vmcnt(0) before the first use also waits for stage P + 2; keeping the loads invisible to it with
@@ -284,6 +326,35 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     // ---- epilogue of the step: acc[j][i][r] = out[pixel px0 + 16 i + (lane & 15)][cout 32 cg + 16 j + 4 gq + r]
     int m0, w0;
     row_base(R0, m0, w0);
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        float p = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 o = acc[j][i];
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          const int c = 32 * cg + 16 * j + 4 * gq;
+          const float4 sc = *(const float4*)(efold + c), sh = *(const float4*)(efold + COUT + c);
+          o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+          o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float q = bf2f(f2bf(fmaxf(o[r], 0.f)));  // the bf16 activation the unfused head reads
+            p = fmaf(q, hwl[j][r], p);
+          }
+        }
+        p += __shfl_xor(p, 16, 64);
+        p += __shfl_xor(p, 32, 64);
+        if (cg == 1) {
+          if (lane < 16) hpart[((ks & 1) * NPG + pg) * PXW + 16 * i + lane] = p;
+        } else {
+          hprev[i] = p;
+        }
+      }
+      hm_prev = m0;
+      continue;  // no activation output in head mode
+    }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       uint2 v[2];
@@ -335,6 +406,11 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     }
   }
 
+  if constexpr (HEAD) {
+    __syncthreads();
+    head_finish((nks - 1) & 1);
+    return;
+  }
   if (a.stats) {  // one partial row per (block, pixel group); waves cg = 0 / 1 fill its two halves
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -371,6 +447,32 @@ extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const
                           stats, N, H, W, escale, eshift, erelu, max_blocks, nullptr, 0, nullptr, s);
 }
 
+// Eval conv (64 -> 64, BN folded + ReLU) fused with the serving 1x1 head: writes only the u8 mask
+// (logit > thr) of the 64-channel output. Returns 0, or -1 when the ring kernel does not apply.
+extern "C" int rdp_conv_ring_head(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                                  int Cout, int N, int H, int W, const float* escale, const float* eshift,
+                                  const float* hw, const float* hb, float hthr, void* mask, hipStream_t s) {
+  if (C != 64 || Cout != 64 || W % 64 || H % 2 || ldw < 576 || !escale || !eshift || !hw || !hb || !mask) return -1;
+  if (xbytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+  RingArgs a;
+  a.x = (const u16*)x; a.xbytes = (uint32_t)xbytes; a.pitch = pitch;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y = nullptr; a.ybytes = 0; a.ypitch = 64; a.y2 = nullptr; a.ybytes2 = 0; a.ypitch2 = 64; a.Cy1 = 64;
+  a.stats = nullptr; a.escale = escale; a.eshift = eshift; a.erelu = 1;
+  a.bny = nullptr; a.bnypitch = 0; a.bncoef = nullptr;
+  a.hw = hw; a.hb = hb; a.hthr = hthr; a.hmask = (uint8_t*)mask;
+  a.H = H; a.W = W; a.WS = W / 64;
+  a.nrows = N * a.WS * H;
+  a.npairs = a.nrows / 2;
+  const int blocks = std::max(1, std::min(256, a.npairs));
+  a.pairs_per_block = (a.npairs + blocks - 1) / blocks;
+  const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
+  const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
+  a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
+  hipLaunchKernelGGL((conv_ring_kernel<64, 0, false, true>), dim3(grid), dim3(512), 0, s, a);
+  return 0;
+}
+
 // Row-ring dgrad whose epilogue also produces the BN-backward partial rows of the layer that owns
 // the output (bn_y: its pre-BN activations, bn_coef: its [mean|invstd|scale|shift]; ReLU applied):
 // replaces a separate bn_relu_bwd_reduce pass over (da, y). Returns the partial rows, or -1.
@@ -392,6 +494,7 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   a.Cy1 = Cy1;
   a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
   a.bny = bn_y; a.bnypitch = bn_ypitch; a.bncoef = bn_coef;
+  a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;

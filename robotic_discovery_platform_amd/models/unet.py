@@ -273,6 +273,8 @@ class UNetNative(nn.Module):
 
 # eval-mode MaxPool2d fused into the split-K conv reduce (serving); "0" = separate maxpool launches
 _FUSE_POOL_EVAL = os.environ.get("RDP_FUSE_POOL_EVAL", "1") != "0"
+# serving 1x1 head + threshold fused into the last conv's epilogue; "0" = separate head_mask launch
+_FUSE_HEAD_EVAL = os.environ.get("RDP_FUSE_HEAD_EVAL", "1") != "0"
 
 
 def _native():
@@ -588,12 +590,16 @@ class UNetExecutor:
             C.bn_eval_coef(m.store.view(sp.bn + ".weight"), m.store.view(sp.bn + ".bias"),
                            m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"), 1e-5, L.coef)
 
-    def forward(self, head: bool = True, refresh_eval: bool = True):
+    def forward(self, head: bool = True, refresh_eval: bool = True, mask_head: Optional[tuple] = None):
         """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead).
 
         Eval mode folds BN into the conv epilogues with coefficients from the running statistics;
         ``refresh_eval=False`` reuses the coefficients from the last ``prepare_eval()`` (the serving
-        pipeline recomputes them only when the weights change, not per frame)."""
+        pipeline recomputes them only when the weights change, not per frame).
+        ``mask_head=(head_w, head_b, logit_thr, mask_u8)`` (eval, with ``head=False``): the serving mask
+        ``head(a_final) > logit_thr``; where the row-ring kernel runs the last conv, the head is fused
+        into its epilogue and ``final`` is not materialised (RDP_FUSE_HEAD_EVAL=0: the separate
+        ``head_mask`` launch)."""
         C = _native()
         D = self.m.depth
         if not self.training and refresh_eval:
@@ -627,9 +633,13 @@ class UNetExecutor:
             la, lb = self.up_layers[i - 1]
             self._conv_bn_relu(C, la)
             last = i == D
+            if last and mask_head is not None and not head and self._conv_head_mask(C, lb, mask_head):
+                return
             self._conv_bn_relu(C, lb, apply=not ((last and self.fuse_head and head) or (not last and self.fuse_up_bn)))
             low, low_layer = lb.a, lb
         if not head:
+            if mask_head is not None:
+                C.head_mask(self.final, *mask_head)
             return
         head_w = self.m.store.view("outc.conv.weight").reshape(-1)
         head_b = self.m.store.view("outc.conv.bias")
@@ -646,6 +656,14 @@ class UNetExecutor:
         else:
             C.head_fwd(self.final, head_w, head_b, self.target, self.logits, self.head_partial, self.loss_sums,
                        self.loss, self.dice_w, self.dice_eps)
+
+    def _conv_head_mask(self, C, L: _Layer, mask_head: tuple) -> bool:
+        """Eval: the last conv + BN fold + ReLU + 1x1 head + threshold in one row-ring launch."""
+        sp = L.spec
+        if self.training or not _FUSE_HEAD_EVAL or L.x2 is not None or sp.taps != 9 or sp.packed:
+            return False
+        hw, hb, thr, mask = mask_head
+        return bool(C.conv_head_mask(L.x1, self.m.fwd_weight(sp), L.coef, hw, hb, float(thr), mask))
 
     def logits_nchw(self) -> torch.Tensor:
         return self.logits.view(self.N, 1, self.H, self.W)

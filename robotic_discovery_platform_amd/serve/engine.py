@@ -6,8 +6,10 @@ resize -> numpy/scipy geometry -> coverage) with one device program per frame:
 
     pinned H2D (colour u8, depth u16)          side HIP stream, async
     preprocess      u8 BGR -> AA resize -> bf16 NHWC8          csrc/serve_kernels.hip
-    UNet forward    18 implicit-GEMM convs, BN folded in epilogues   csrc/conv_igemm.hip
-    head_mask       1x1 head + (logit > 0) -> u8 256x256        csrc/head_loss.hip
+    UNet forward    18 convs (implicit GEMM / row ring), BN folded in the epilogues, eval
+                    maxpools fused into the split-K reduces    csrc/conv_igemm.hip, conv_ring.hip
+    head mask       1x1 head + (logit > 0) -> u8 256x256, fused into the last conv's epilogue
+                    (csrc/conv_ring.hip HEAD; head_mask in csrc/head_loss.hip where it does not apply)
     geo_edges       nearest upsample -> HxW u8 mask + coverage, deproject + compaction + 50-bin
                     top-5 %                                     csrc/geometry.hip
     geo_spline      per-bin x-sort, FITPACK-equivalent spline fit, 100-sample splev + curvature
@@ -136,9 +138,10 @@ class FramePipeline:
         # pipelines no longer overlap: GPU p50 0.622 -> 0.648 ms, pipelined 2307 -> 1502 FPS.
         C, ex, m = self.C, self.ex, self.model
         C.preprocess(self.d_color, *self.tab, ex.x_in, rgb)
-        ex.forward(head=False, refresh_eval=False)  # BN-fold coefficients: see refresh_weights()
-        C.head_mask(ex.final, m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
-                    self.thr_logit, self.m256)
+        # BN-fold coefficients: see refresh_weights(); the head (+ threshold) is fused into the last conv
+        ex.forward(head=False, refresh_eval=False,
+                   mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
+                              self.thr_logit, self.m256))
         self.geo.launch_frame(self.m256.view(self.S, self.S), self.mask, self.d_depth, self.K, self.scale)
         self.geo.launch_spline()
 

@@ -520,6 +520,37 @@ def test_conv_eval_fused_pool(C, N, H, W, C1, C2, Cout):
     assert relerr(nchw(a), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(1, 256, 256), (2, 64, 128), (1, 128, 64)])
+def test_conv_head_mask_fused(C, N, H, W):
+    """Serving: last conv (64 -> 64, BN fold + ReLU) + 1x1 head + threshold in the row-ring epilogue ==
+    conv_fwd(eval) + head_mask, except pixels whose logit is within rounding of the threshold."""
+    torch.manual_seed(10)
+    dev = "cuda"
+    x = bf(torch.randn(N, H, W, 64, device=dev))
+    w = bf(torch.randn(64, 64, 3, 3, device=dev) / math.sqrt(9 * 64))
+    wk = ohwi(w).contiguous()
+    g, b = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.5
+    rm, rv = torch.randn(64, device=dev) * 0.1, torch.rand(64, device=dev) + 0.5
+    coef = torch.zeros(4 * 64, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    hw = torch.randn(64, device=dev) * 0.3
+    hb = torch.randn(1, device=dev) * 0.1
+    a = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x, None, wk, 9, 0, a, None, None, 0, coef, 1)
+    ref = torch.full((N * H * W,), 7, dtype=torch.uint8, device=dev)
+    C.head_mask(a, hw, hb, 0.0, ref)
+    got = torch.full((N * H * W,), 7, dtype=torch.uint8, device=dev)
+    assert C.conv_head_mask(x, wk, coef, hw, hb, 0.0, got)
+    logit = a.float().reshape(-1, 64) @ hw + hb
+    diff = got != ref
+    assert (got <= 1).all()
+    assert (logit[diff].abs() < 1e-3).all(), logit[diff].abs().max()
+    assert diff.float().mean() < 1e-3
+    # not applicable (W % 64 != 0): nothing launched, caller falls back
+    xs = bf(torch.randn(1, 16, 24, 64, device=dev))
+    assert not C.conv_head_mask(xs, wk, coef, hw, hb, 0.0, got)
+
+
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [(1, 64, 64, 256, 0, 256, 0), (1, 16, 16, 512, 0, 512, 0),
                                                    (4, 256, 256, 64, 0, 128, 0), (2, 33, 47, 64, 64, 64, 0),
                                                    (1, 64, 64, 128, 0, 128, 128), (1, 64, 64, 128, 0, 64, 256)])
