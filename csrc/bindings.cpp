@@ -22,7 +22,7 @@ int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
 int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
                   double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, const void*, int, int,
-                  int*, hipStream_t);
+                  int*, double*, int*, int, hipStream_t);
 int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*, int,
                    int, int, void*, hipStream_t);
 int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
@@ -79,7 +79,7 @@ int rdp_area_maxtap();
 int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
                        const double*, int, int, int, void*, hipStream_t);
 int rdp_geo_spline(const double*, int, int, const int*, const int*, double*, int*, double*, int, double, int, int,
-                   double, int, int, const int*, int, double*, double*, hipStream_t);
+                   double, int, int, const int*, int, double*, double*, int, hipStream_t);
 }
 
 namespace {
@@ -613,7 +613,8 @@ py::tuple fit_curvature(torch::Tensor pts, double s, int k, int nsamp, double ep
 void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, double cx, double cy, double scale,
                torch::Tensor work_i, torch::Tensor work_d, torch::Tensor pts, torch::Tensor npts, torch::Tensor out,
                torch::Tensor kout, int nbins, double top, int min_points, c10::optional<torch::Tensor> edges,
-               c10::optional<torch::Tensor> hdr, c10::optional<torch::Tensor> m256, c10::optional<torch::Tensor> cov) {
+               c10::optional<torch::Tensor> hdr, c10::optional<torch::Tensor> m256, c10::optional<torch::Tensor> cov,
+               c10::optional<torch::Tensor> sorted, c10::optional<torch::Tensor> gperm) {
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == torch::kUInt8 && mask.dim() == 2 && mask.is_contiguous(), "mask");
   TORCH_CHECK(depth.is_cuda() && depth.element_size() == 2 && depth.sizes() == mask.sizes() && depth.is_contiguous(),
               "depth u16");
@@ -642,11 +643,24 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
     mw = m256->size(1);
     covp = cov->data_ptr<int>();
   }
+  // sorted (+ gperm): the x-sorted edge points for geo_spline(presorted=True), fused into the select
+  double* sp = nullptr;
+  int* gp = nullptr;
+  int secap = 0;
+  if (sorted && sorted->defined()) {
+    TORCH_CHECK(sorted->is_cuda() && sorted->scalar_type() == torch::kFloat64 && sorted->dim() == 2 &&
+                sorted->size(1) == 3 && sorted->is_contiguous(), "sorted [ecap][3] f64");
+    secap = sorted->size(0);
+    TORCH_CHECK(gperm && gperm->defined() && gperm->scalar_type() == torch::kInt32 && gperm->numel() >= 2L * secap,
+                "gperm: 2*ecap int32");
+    sp = sorted->data_ptr<double>();
+    gp = gperm->data_ptr<int>();
+  }
   const int r = rdp_geo_edges(mask.data_ptr(), depth.data_ptr(), H, W, fx, fy, cx, cy, scale, work_i.data_ptr<int>(),
                               work_d.data_ptr<double>(), work_d.data_ptr<double>() + nblk, pts.data_ptr<double>(), H * W,
                               npts.data_ptr<int>(), out.data_ptr<double>(), out.size(1), kout.data_ptr<int>(), nbins,
                               top, min_points, pack ? edges->data_ptr<double>() : nullptr, pack ? edges->size(0) : 0,
-                              pack ? hdr->data_ptr<int>() : nullptr, mp, mh, mw, covp, cur_stream());
+                              pack ? hdr->data_ptr<int>() : nullptr, mp, mh, mw, covp, sp, gp, secap, cur_stream());
   TORCH_CHECK(r >= 0, "geo_edges: nbins must be in [1, 128]");
 }
 
@@ -657,7 +671,7 @@ long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 // fit + nsamp-point evaluation and curvature into res (rdp_geo_spline_res_len(nsamp) doubles)
 void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch::Tensor sorted, torch::Tensor gperm,
                 torch::Tensor u, torch::Tensor res, double s, int k, int nsamp, double eps, int min_points,
-                int min_edge, c10::optional<torch::Tensor> cov, c10::optional<torch::Tensor> dbg) {
+                int min_edge, c10::optional<torch::Tensor> cov, c10::optional<torch::Tensor> dbg, bool presorted) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(2) == 4 &&
               out.is_contiguous(), "out [nbins][kcap][4] f64");
   TORCH_CHECK(kout.scalar_type() == torch::kInt32 && kout.numel() >= out.size(0), "kout");
@@ -683,7 +697,7 @@ void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch
   const int r = rdp_geo_spline(out.data_ptr<double>(), out.size(0), out.size(1), kout.data_ptr<int>(),
                                npts.data_ptr<int>(), sorted.data_ptr<double>(), gperm.data_ptr<int>(),
                                u.data_ptr<double>(), ecap, s, k, nsamp, eps, min_points, min_edge, covp, ncov,
-                               res.data_ptr<double>(), dbgp, cur_stream());
+                               res.data_ptr<double>(), dbgp, presorted ? 1 : 0, cur_stream());
   TORCH_CHECK(r == 0, "geo_spline: k must be in [1, 5], nsamp in [1, 256]");
 }
 
@@ -817,11 +831,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cy"), py::arg("scale"), py::arg("work_i"), py::arg("work_d"), py::arg("pts"), py::arg("npts"),
         py::arg("out"), py::arg("kout"), py::arg("nbins"), py::arg("top"), py::arg("min_points"),
         py::arg("edges") = py::none(), py::arg("hdr") = py::none(), py::arg("m256") = py::none(),
-        py::arg("cov") = py::none());
+        py::arg("cov") = py::none(), py::arg("sorted") = py::none(), py::arg("gperm") = py::none());
   m.def("geo_nblocks", &geo_nblocks);
   m.def("geo_spline", &geo_spline, py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
-        py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none());
+        py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
+        py::arg("presorted") = false);
   m.def("png_decode", &png_decode);
   m.def("png_encode_gray8", &png_encode_gray8);
   m.def("resize_area_u8", &resize_area_u8);

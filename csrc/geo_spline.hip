@@ -35,13 +35,13 @@
 // [3] fp, [4] mean kappa, [5] max kappa, [6] E edge points, [7] valid points, [8..] nsamp x 3 points,
 // [8 + 3 nsamp] mask coverage count (serving form; -1 without coverage input).
 #include "common.h"
+#include "geo_sort.h"
 #include <stdint.h>
 
 #define SPL_THREADS 256
 #define SPL_NK 64                   // max spline coefficients per dimension on the device
 #define SPL_KMAX 5
 #define SPL_NMAX (SPL_NK + SPL_KMAX + 1)  // max knots
-#define SORT_LCAP 2048
 
 enum { SPL_OK = 0, SPL_TOO_FEW_POINTS = 1, SPL_TOO_FEW_EDGES = 2, SPL_FIT_FAILED = 3, SPL_NEEDS_HOST = 4 };
 
@@ -59,59 +59,7 @@ __global__ __launch_bounds__(256) void geo_sort_kernel(const double* __restrict_
     s_off = o;
   }
   __syncthreads();
-  const int off = s_off;
-  int k = min(kout[b], kcap);
-  if (k <= 0 || off >= ecap) return;
-  if (off + k > ecap) k = ecap - off;
-  const double* ob = out + (size_t)b * kcap * 4;
-  int P = 1;
-  while (P < k) P <<= 1;
-  const bool lds = P <= SORT_LCAP;
-  // global fallback: [2*off, 2*off + P) is private to this bin because P < 2k
-  int* perm = lds ? sperm : gperm + 2 * (size_t)off;
-  if (lds)
-    for (int i = tid; i < k; i += blockDim.x) {
-      sx[i] = ob[(size_t)i * 4];
-      sy[i] = ob[(size_t)i * 4 + 1];
-      sid[i] = (int)ob[(size_t)i * 4 + 3];
-    }
-  for (int i = tid; i < P; i += blockDim.x) perm[i] = i;
-  __syncthreads();
-  // a after c in the order (x asc, y desc, index asc); padding (>= k) sorts last
-  auto after = [&](int a, int c) -> bool {
-    if (a >= k) return c < k || a > c;
-    if (c >= k) return false;
-    double xa, xc, ya, yc;
-    int ia, ic;
-    if (lds) {
-      xa = sx[a]; xc = sx[c]; ya = sy[a]; yc = sy[c]; ia = sid[a]; ic = sid[c];
-    } else {
-      xa = ob[(size_t)a * 4]; xc = ob[(size_t)c * 4];
-      ya = ob[(size_t)a * 4 + 1]; yc = ob[(size_t)c * 4 + 1];
-      ia = (int)ob[(size_t)a * 4 + 3]; ic = (int)ob[(size_t)c * 4 + 3];
-    }
-    if (xa != xc) return xa > xc;
-    if (ya != yc) return ya < yc;
-    return ia > ic;
-  };
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = tid; t < P / 2; t += blockDim.x) {
-        const int i = 2 * stride * (t / stride) + (t % stride), j = i + stride;
-        const int a = perm[i], c = perm[j];
-        const bool up = (i & size) == 0;
-        if (up ? after(a, c) : after(c, a)) {
-          perm[i] = c;
-          perm[j] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = tid; i < k; i += blockDim.x) {
-    const int s = perm[i];
-    for (int c = 0; c < 3; ++c) sorted[(size_t)(off + i) * 3 + c] = ob[(size_t)s * 4 + c];
-  }
+  geo_sort_bin(out + (size_t)b * kcap * 4, min(kout[b], kcap), s_off, sorted, gperm, ecap, sx, sy, sid, sperm);
 }
 
 // ------------------------------------------------------------------------------------------ fit
@@ -906,9 +854,12 @@ int rdp_geo_spline_res_len(int nsamp) { return 9 + 3 * nsamp; }
 // sort the per-bin edge points (out [nbins][kcap][4], kout) into sorted [ecap][3] and fit/evaluate.
 int rdp_geo_spline(const double* out, int nbins, int kcap, const int* kout, const int* npts, double* sorted,
                    int* gperm, double* u, int ecap, double s, int k, int nsamp, double eps, int min_points,
-                   int min_edge, const int* cov, int ncov, double* res, double* dbg, hipStream_t st) {
+                   int min_edge, const int* cov, int ncov, double* res, double* dbg, int presorted,
+                   hipStream_t st) {
   if (k < 1 || k > SPL_KMAX || nsamp < 1 || nsamp > SPL_THREADS) return -1;
-  hipLaunchKernelGGL(geo_sort_kernel, dim3(nbins), dim3(256), 0, st, out, kcap, kout, sorted, gperm, ecap);
+  // presorted: rdp_geo_edges already wrote `sorted` (fused select + sort)
+  if (!presorted)
+    hipLaunchKernelGGL(geo_sort_kernel, dim3(nbins), dim3(256), 0, st, out, kcap, kout, sorted, gperm, ecap);
 #define RDP_FIT(KK)                                                                                                \
   hipLaunchKernelGGL(geo_fit_kernel<KK>, dim3(1), dim3(SPL_THREADS), 0, st, sorted, u, kout, nbins, kcap, npts, \
                      ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res, dbg)

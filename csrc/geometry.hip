@@ -12,9 +12,13 @@
 // Kernels (all fixed-size launches, graph-capturable):
 //   geo_count:   per row-block valid-pixel count + per-block x min/max (double)
 //   geo_write:   each block derives its exclusive offset from the counts and writes its points
-//   geo_edges:   one workgroup per bin: bin size, k, radix-select of the k-th largest y key,
-//                then writes the bin's k points (x, y, z, index) into a per-bin output slab
+//   geo_write:   also bins every point by x (per-bin counts)
+//   geo_bin_scatter: point indices grouped by bin
+//   geo_select:  one workgroup per bin: bin size, k, radix-select of the k-th largest y key,
+//                then writes the bin's k points (x, y, z, index) into a per-bin output slab, and
+//                (serving) x-sorts them into the packed edge array (geo_sort.h)
 #include "common.h"
+#include "geo_sort.h"
 #include <stdint.h>
 
 #define GEO_ROWS_PER_BLOCK 4
@@ -113,14 +117,35 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_count_kernel(const uint8_t* _
   }
 }
 
+RDP_DEV void geo_range(const double* bxmin, const double* bxmax, int nblk, double* s_lo, double* s_hi);
+
+// ---- binning: counting sort of point indices by x bin (bin computed once per point) ----
+// bin = clip(floor((x - lo) / w), 0, nbins-1) with the reference's division (not a reciprocal
+// multiply), so boundary points land in exactly the reference's bin.
+struct GeoBins {
+  int* bin_of;     // [cap]   bin of every point
+  int* bidx;       // [cap]   point indices grouped by bin (order within a bin is arbitrary)
+  int* cnt;        // [128]   points per bin
+  int* cursor;     // [128]   scatter cursors
+};
+
 // pts: [cap][4] doubles (x, y, z, index) ; npts[0] = total count (written by the last block's thread 0)
+// The x-bin of every written point and the per-bin counts are produced here too (the global x range
+// is reduced from geo_count's per-block partials by every block): no separate counting launch.
 __global__ __launch_bounds__(GEO_THREADS) void geo_write_kernel(const uint8_t* __restrict__ mask,
                                                                 const uint16_t* __restrict__ depth, int H, int W,
                                                                 GeoCam cam, const int* __restrict__ counts,
                                                                 int nblocks, double* __restrict__ pts, int cap,
-                                                                int* __restrict__ npts) {
+                                                                int* __restrict__ npts, const double* __restrict__ bxmin,
+                                                                const double* __restrict__ bxmax, int nbins,
+                                                                GeoBins gb) {
   __shared__ int sh[GEO_THREADS / 64];
   __shared__ int base_sh;
+  __shared__ unsigned lc[128];
+  double lo, hi;
+  geo_range(bxmin, bxmax, nblocks, &lo, &hi);
+  const double width = (hi - lo) / (double)nbins;
+  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS) lc[i] = 0;
   if (threadIdx.x == 0) {
     int b = 0;
     for (int i = 0; i < (int)blockIdx.x; ++i) b += counts[i];
@@ -141,14 +166,24 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_write_kernel(const uint8_t* _
       if (idx < cap) {
         const int u = p % W, row = p / W;
         const double z = (double)depth[p] * cam.scale;
-        pts[(size_t)idx * 4 + 0] = ((double)u - cam.cx) * z / cam.fx;
+        const double x = ((double)u - cam.cx) * z / cam.fx;
+        pts[(size_t)idx * 4 + 0] = x;
         pts[(size_t)idx * 4 + 1] = ((double)row - cam.cy) * z / cam.fy;
         pts[(size_t)idx * 4 + 2] = z;
         pts[(size_t)idx * 4 + 3] = (double)idx;
+        if (width > 0.0) {
+          const double f = floor((x - lo) / width);
+          const int b = (int)fmin(fmax(f, 0.0), (double)(nbins - 1));
+          gb.bin_of[idx] = b;
+          atomicAdd(&lc[b], 1u);
+        }
       }
     }
     base += total;
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS)
+    if (lc[i]) atomicAdd(&gb.cnt[i], (int)lc[i]);
 }
 
 // order-preserving key of a double (larger double -> larger key)
@@ -156,16 +191,6 @@ RDP_DEV uint64_t dkey(double d) {
   const uint64_t b = (uint64_t)__double_as_longlong(d);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
-
-// ---- binning: counting sort of point indices by x bin (bin computed once per point) ----
-// bin = clip(floor((x - lo) / w), 0, nbins-1) with the reference's division (not a reciprocal
-// multiply), so boundary points land in exactly the reference's bin.
-struct GeoBins {
-  int* bin_of;     // [cap]   bin of every point
-  int* bidx;       // [cap]   point indices grouped by bin (order within a bin is arbitrary)
-  int* cnt;        // [128]   points per bin
-  int* cursor;     // [128]   scatter cursors
-};
 
 RDP_DEV void geo_range(const double* bxmin, const double* bxmax, int nblk, double* s_lo, double* s_hi) {
   // every block reduces the per-row-block partials itself (nblk ~ H/4 doubles)
@@ -184,30 +209,6 @@ RDP_DEV void geo_range(const double* bxmin, const double* bxmax, int nblk, doubl
   }
   *s_lo = rlo[0];
   *s_hi = rhi[0];
-}
-
-__global__ __launch_bounds__(GEO_THREADS) void geo_bin_count_kernel(const double* __restrict__ pts,
-                                                                    const int* __restrict__ npts_p,
-                                                                    const double* __restrict__ bxmin,
-                                                                    const double* __restrict__ bxmax, int nblk,
-                                                                    int nbins, GeoBins gb) {
-  __shared__ unsigned lc[128];
-  double lo, hi;
-  geo_range(bxmin, bxmax, nblk, &lo, &hi);
-  const int n = npts_p[0];
-  const double width = (hi - lo) / (double)nbins;
-  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS) lc[i] = 0;
-  __syncthreads();
-  if (width > 0.0)
-    for (int i = blockIdx.x * GEO_THREADS + threadIdx.x; i < n; i += gridDim.x * GEO_THREADS) {
-      const double f = floor((pts[(size_t)i * 4] - lo) / width);
-      const int b = (int)fmin(fmax(f, 0.0), (double)(nbins - 1));
-      gb.bin_of[i] = b;
-      atomicAdd(&lc[b], 1u);
-    }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nbins; i += GEO_THREADS)
-    if (lc[i]) atomicAdd(&gb.cnt[i], (int)lc[i]);
 }
 
 __global__ __launch_bounds__(GEO_THREADS) void geo_bin_scatter_kernel(const int* __restrict__ npts_p, int nbins,
@@ -283,14 +284,20 @@ RDP_DEV void geo_pick_digit(const unsigned* hist, int need, int* s_digit, int* s
 // among the ties to keep. The bin's keys and ids are cached in LDS (up to GEO_LCAP points; larger
 // bins read the excess from global memory), so each pass is LDS traffic + one histogram.
 #define GEO_LCAP 4096
+// sorted != nullptr: the block also x-sorts its bin's k points into sorted[off ..] (geo_sort.h), off =
+// the k of the earlier bins, derived from the bin counts -- no separate sort launch.
 __global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* __restrict__ pts,
                                                                  const int* __restrict__ npts_p, int nbins,
                                                                  double top, GeoBins gb, double* __restrict__ out,
-                                                                 int kcap, int* __restrict__ kout, int min_points) {
+                                                                 int kcap, int* __restrict__ kout, int min_points,
+                                                                 double* __restrict__ sorted, int* __restrict__ gperm,
+                                                                 int ecap) {
   __shared__ unsigned hist[256];
   __shared__ uint64_t skey[GEO_LCAP];
   __shared__ int sid[GEO_LCAP];
   __shared__ int s_digit, s_need, s_eq, s_cnt;
+  __shared__ double srt_x[SORT_LCAP], srt_y[SORT_LCAP];
+  __shared__ int srt_id[SORT_LCAP], srt_perm[SORT_LCAP];
   const int bin = blockIdx.x;
   const int n = npts_p[0];
   const int nb = gb.cnt[bin];
@@ -367,6 +374,18 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* _
     }
   }
   if (threadIdx.x == 0) kout[bin] = k;
+  if (sorted) {
+    int off = 0;  // sum of the earlier bins' k (the select's own rule, from the bin counts)
+    for (int b = 0; b < bin; ++b) {
+      const int c = gb.cnt[b];
+      int kb = (int)((double)c * top);
+      if (kb < 1) kb = 1;
+      if (kb > kcap) kb = kcap;
+      off += c > 0 ? kb : 0;
+    }
+    __syncthreads();  // this block's `out` writes are visible to all its threads
+    geo_sort_bin(ob, k, off, sorted, gperm, ecap, srt_x, srt_y, srt_id, srt_perm);
+  }
 }
 
 // Pack the per-bin edge points contiguously (one block per bin): hdr[0] = E, edges[E][4].
@@ -403,11 +422,14 @@ long rdp_geo_work_ints(int H, int W) { return (long)rdp_geo_nblocks(H) + 2L * H 
 // pts [cap][4]; out [nbins][kcap][4]
 // m256 != nullptr (serving form): `mask` is an OUTPUT, derived from the mh x mw model mask by
 // nearest upsampling, and cov[nblk] receives per-row-block coverage counts. edges == nullptr: no
-// packed edge list (the on-device spline reads the per-bin slabs directly).
+// packed edge list (the on-device spline reads the per-bin slabs directly). sorted != nullptr: the
+// x-sorted edge points [secap][3] are written too (gperm: 2*secap ints of sort scratch), so the
+// spline stage runs with presorted = 1.
 int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, double fy, double cx, double cy,
                   double scale, int* counts, double* xmin, double* xmax, double* pts, int cap, int* npts,
                   double* out, int kcap, int* kout, int nbins, double top, int min_points, double* edges,
-                  int ecap, int* hdr, const void* m256, int mh, int mw, int* cov, hipStream_t s) {
+                  int ecap, int* hdr, const void* m256, int mh, int mw, int* cov, double* sorted, int* gperm,
+                  int secap, hipStream_t s) {
   if (nbins > 128 || nbins < 1) return -1;
   const int nblk = rdp_geo_nblocks(H);
   GeoCam cam{fx, fy, cx, cy, scale};
@@ -429,13 +451,11 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
   hipLaunchKernelGGL(geo_count_kernel, dim3(nblk), dim3(GEO_THREADS), 0, s, (const uint8_t*)mask,
                      (const uint16_t*)depth, H, W, cam, counts, xmin, xmax, gs);
   hipLaunchKernelGGL(geo_write_kernel, dim3(nblk), dim3(GEO_THREADS), 0, s, (const uint8_t*)mask,
-                     (const uint16_t*)depth, H, W, cam, counts, nblk, pts, cap, npts);
+                     (const uint16_t*)depth, H, W, cam, counts, nblk, pts, cap, npts, xmin, xmax, nbins, gb);
   const int pblocks = (cap + GEO_THREADS * 4 - 1) / (GEO_THREADS * 4);
-  hipLaunchKernelGGL(geo_bin_count_kernel, dim3(pblocks < 256 ? pblocks : 256), dim3(GEO_THREADS), 0, s, pts, npts,
-                     xmin, xmax, nblk, nbins, gb);
   hipLaunchKernelGGL(geo_bin_scatter_kernel, dim3(pblocks), dim3(GEO_THREADS), 0, s, npts, nbins, gb);
   hipLaunchKernelGGL(geo_select_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, nbins, top, gb, out, kcap,
-                     kout, min_points);
+                     kout, min_points, sorted, gperm, secap);
   if (edges) hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
   return nblk;
 }

@@ -159,15 +159,16 @@ class GeometryEngine:
         c = self.cfg
         self.C.geo_edges(mask_out, depth_dev, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]),
                          float(scale), self.work_i, self.work_d, self.pts, self.npts, self.out, self.kout, c.num_bins,
-                         c.top_k_percent, c.min_points, None, None, m256_dev, self.cov)
-        self._serving_form = True
+                         c.top_k_percent, c.min_points, None, None, m256_dev, self.cov, self.sorted, self.gperm)
+        self._serving_form = True  # the select kernel also wrote the x-sorted edge points
 
     def launch_spline(self):
         """Enqueue the on-device spline stage after ``launch`` (no host sync; graph-capturable)."""
         c = self.cfg
+        serving = getattr(self, "_serving_form", False)
         self.C.geo_spline(self.out, self.kout, self.npts, self.sorted, self.gperm, self.u, self.res, c.smoothing,
                           c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points,
-                          self.cov if getattr(self, "_serving_form", False) else None)
+                          self.cov if serving else None, presorted=serving)
 
     def finish_device(self, res_host: np.ndarray) -> CurvatureResult:
         """Result of ``launch_spline`` (``res`` read back); a fit beyond the device capacity is redone

@@ -120,6 +120,19 @@ def test_geometry_kernels_match_oracle(seed):
     eo = eo[np.argsort(eo[:, 0], kind="stable")]
     got = sort_edges(eng.edges[:E].cpu().numpy())
     assert E == eo.shape[0] and np.array_equal(got, eo)
+    # serving form: the select kernel also x-sorts the edge points (fused with the per-bin sort) ==
+    # the separate sort launch of the spline stage, bitwise
+    m256 = torch.from_numpy(sc.mask[::2, ::2].copy()).cuda()  # any model-resolution mask
+    mask_out = torch.empty(480, 640, dtype=torch.uint8, device="cuda")
+    eng.launch_frame(m256, mask_out, d, DEFAULT_K, 0.001)
+    E2 = int(eng.kout.clamp(max=eng.out.shape[1]).sum().item())
+    fused = eng.sorted[:E2].clone()
+    c = eng.cfg
+    eng.C.geo_spline(eng.out, eng.kout, eng.npts, eng.sorted, eng.gperm, eng.u, eng.res, c.smoothing,
+                     c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points, eng.cov,
+                     presorted=False)
+    torch.cuda.synchronize()
+    assert E2 > 0 and torch.equal(fused, eng.sorted[:E2])
     r = compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001, device="cuda")  # on-device spline
     h = compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001, device="cuda", spline="host")
     x = ref.compute_curvature_profile(sc.mask, sc.depth, DEFAULT_K, 0.001)
@@ -164,16 +177,20 @@ def test_frame_pipeline_matches_reference_semantics():
     rg = pg.process(sc.color, sc.depth)
     re_ = pe.process(sc.color, sc.depth)
     assert np.array_equal(rg.mask, re_.mask) and rg.coverage == re_.coverage
-    # mask == nearest-upsampled (native logits > 0) of the same preprocessed input
+    # mask == nearest-upsampled (native logits > 0) of the same preprocessed input. The pipeline's head
+    # is fused into the last conv (no activation stored): re-run the executor unfused for the logits.
     ex = pe.ex
-    logits = torch.empty(0)
+    fused256 = pe.m256.view(256, 256).clone()
+    ex.forward(head=False, refresh_eval=False)
     head_w = nat.store.view("outc.conv.weight").reshape(-1).float()
     head_b = nat.store.view("outc.conv.bias").float()
     lg = (ex.final.float().reshape(-1, 64) @ head_w + head_b).view(256, 256)
+    flip = fused256.bool() != (lg > 0)
+    assert (lg[flip].abs() < 1e-3).all()  # only |logit| ~ 0 pixels may differ (dot order)
     m256 = (lg > 0).cpu().numpy().astype(np.uint8)
     exp_full = resize_nearest(m256, (640, 480))
     agree = (exp_full == rg.mask).mean()
-    assert agree > 0.999, agree  # fp32 vs in-kernel dot order can flip |logit| ~ 0 pixels
+    assert agree > 0.999, agree
     assert rg.coverage == pytest.approx(100.0 * rg.mask.sum() / rg.mask.size)
     x = gref.compute_curvature_profile(rg.mask, sc.depth, DEFAULT_K, 0.001)
     assert rg.curvature.status == x.status
