@@ -438,6 +438,10 @@ extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const
                              void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                              int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                              int erelu, int max_blocks, hipStream_t s);
+extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                                  void* y, long ybytes, int ypitch, int Cout, int N, int H, int W,
+                                  const float* escale, const float* eshift, int erelu, void* pool, int ppitch,
+                                  hipStream_t s);
 extern "C" int rdp_conv_halo_tiles(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed);
 extern "C" int rdp_conv_halo(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
                              int pitch2, const void* w, long wbytes, int ldw, void* y1, void* y2, long ybytes1,
@@ -663,6 +667,14 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
     const int pref = bm_pref % 1000;
     // row-ring kernel (conv_ring.hip): 64 -> 64 channels, 3x3, one source, no output split
     if ((pref == 6 || (pref == 0 && ring_env)) && taps == 9 && !packed && C2 == 0 && x2 == nullptr) {
+      if (pool && pooled && !stats && !y2 && escale) {  // eval: MaxPool2d fused into the ring epilogue
+        const int r = rdp_conv_ring_pool(x1, xbytes1, C1, pitch1, w, wbytes, ldw, y1, ybytes1, ypitch1, Cout, N, H, W,
+                                         escale, eshift, erelu, pool, ppitch, s);
+        if (r == 0) {
+          *pooled = 1;
+          return 0;
+        }
+      }
       const int r = rdp_conv_ring(x1, xbytes1, C1, pitch1, w, wbytes, ldw, y1, ybytes1, ypitch1, y2, ybytes2,
                                   ypitch2, Cy1, Cout, stats, N, H, W, escale, eshift, erelu, 256, s);
       if (r >= 0 || pref == 6) return r;

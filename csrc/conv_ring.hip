@@ -51,6 +51,9 @@ struct RingArgs {
   const float* hb;
   float hthr;
   uint8_t* hmask;
+  // eval MaxPool2d(2) of the output (POOL variant): pool [N][H/2][W/2][64] with pixel pitch ppitch
+  u16* pool;
+  int ppitch;
   int H, W, WS;  // WS = W / 64 segments per image row
   int nrows;     // N * WS * H: input rows in column order (R = column * H + h)
   int npairs;    // nrows / 2: steps (two output rows each)
@@ -70,7 +73,11 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 // each reduces its 32 over the lane groups, cg = 1 leaves its partial in LDS (double-buffered by step
 // parity), and cg = 0 finishes the pixel after the next step's barrier (the last step after a final
 // barrier) and stores the u8 mask.
-template <int COUT, int ABL = 0, bool BNR = false, bool HEAD = false>
+// POOL (COUT = 64, eval): MaxPool2d(2) of the output in the epilogue. A step's two output rows are
+// one row of 2x2 windows (rows 2P, 2P + 1 with H even): horizontal pairs are neighbouring lanes (DPP
+// swap), vertical pairs are the orow = 0 / 1 waves of a pixel group, exchanged through LDS (step-parity
+// double buffer) and finished by the orow = 0 waves after the next barrier.
+template <int COUT, int ABL = 0, bool BNR = false, bool HEAD = false, bool POOL = false>
 __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
   constexpr int PXW = 128 / NPG, NI = PXW / 16;  // pixels per wave (one output row half or whole)
@@ -79,9 +86,12 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int PIECES = 18;      // 1-KiB DMA pieces per step (2 rows x 9)
   constexpr int MINPW = PIECES / 8;
   constexpr int HPART = HEAD ? 2 * NPG * PXW * 4 : 0;  // head partials [parity][pixel group][pixel]
-  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 4 * COUT * 4 + HPART];  // + zero slot, BN fold / BN-bwd coefs
+  // pool halves [parity][wave][i][pixel pair][lane group] x 16 B (4 packed bf16 pairs)
+  constexpr int PPART = POOL ? 2 * 8 * NI * 8 * 4 * 16 : 0;
+  __shared__ __attribute__((aligned(16))) char ring[(NX + 1) * XREG + 4 * COUT * 4 + HPART + PPART];  // + zero slot, BN fold / BN-bwd coefs
   float* const efold = (float*)(ring + (NX + 1) * XREG);  // eval BN fold [scale | shift] (LDS, not VGPRs)
   float* const hpart = (float*)(ring + (NX + 1) * XREG + 4 * COUT * 4);
+  uint4* const ppart = (uint4*)(ring + (NX + 1) * XREG + 4 * COUT * 4 + HPART);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -208,6 +218,29 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     for (int i = 0; i < NI; ++i) hprev[i] = 0.f;
   }
   const float hbias = HEAD ? a.hb[0] : 0.f;
+  // pool: pooled-row base of the previous step's windows; orow = 0 waves finish them
+  int pb_prev = -1;
+  auto pool_finish = [&](int par) {
+    if (orow != 0 || pb_prev < 0) return;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (lane & 1) continue;
+      const int q = (lane & 15) >> 1;
+      const uint4 u0 = ppart[(((par * 8 + wave) * NI + i) * 8 + q) * 4 + gq];
+      const uint4 u1 = ppart[(((par * 8 + wave + NPG / 2) * NI + i) * 8 + q) * 4 + gq];
+      const uint32_t w0[4] = {u0.x, u0.y, u0.z, u0.w}, w1[4] = {u1.x, u1.y, u1.z, u1.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = fmaxf(__uint_as_float(w0[k] << 16), __uint_as_float(w1[k] << 16));
+        const float hi = fmaxf(__uint_as_float(w0[k] & 0xffff0000u), __uint_as_float(w1[k] & 0xffff0000u));
+        o[k] = pack2bf(lo, hi);
+      }
+      u16* dst = a.pool + (size_t)(pb_prev + ((px0 + 16 * i + (lane & 15)) >> 1)) * a.ppitch + 32 * cg + 4 * gq;
+      *(uint2*)dst = make_uint2(o[0], o[1]);         // channels 32 cg + 4 gq .. + 3
+      *(uint2*)(dst + 16) = make_uint2(o[2], o[3]);  // channels 32 cg + 16 + 4 gq .. + 3
+    }
+  };
   // cg = 0: finish the pixels of the step whose partials (parity par) are in LDS
   auto head_finish = [&](int par) {
     if (cg != 0 || hm_prev < 0) return;
@@ -238,6 +271,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     }
     raw_barrier();
     if constexpr (HEAD) head_finish((ks - 1) & 1);
+    if constexpr (POOL) pool_finish((ks - 1) & 1);
     // BN-backward fusion: the owner layer's pre-BN activations at this step's outputs, loaded before
     // the stage P + 2 DMAs so their latency hides under the taps. (hipcc cannot see the DMAs, so its
     // vmcnt(0) before the first use also waits for stage P + 2; keeping the loads invisible to it with
@@ -326,6 +360,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     // ---- epilogue of the step: acc[j][i][r] = out[pixel px0 + 16 i + (lane & 15)][cout 32 cg + 16 j + 4 gq + r]
     int m0, w0;
     row_base(R0, m0, w0);
+    if constexpr (POOL) pb_prev = (((m0 - w0) / a.W) >> 1) * (a.W >> 1) + (w0 >> 1);
     if constexpr (HEAD) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -397,6 +432,19 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
           }
         }
       }
+      if constexpr (POOL) {  // horizontal max with the neighbouring pixel (lane ^ 1), half to LDS
+        uint32_t hw4[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hw4[k], 0xB1, 0xf, 0xf, false);
+          const float lo = fmaxf(__uint_as_float(hw4[k] << 16), __uint_as_float(nb << 16));
+          const float hi = fmaxf(__uint_as_float(hw4[k] & 0xffff0000u), __uint_as_float(nb & 0xffff0000u));
+          hw4[k] = pack2bf(lo, hi);
+        }
+        if (!(lane & 1))
+          ppart[((((ks & 1) * 8 + wave) * NI + i) * 8 + ((lane & 15) >> 1)) * 4 + gq] =
+              make_uint4(hw4[0], hw4[1], hw4[2], hw4[3]);
+      }
       const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
       const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
       const int m = m0 + px0 + 16 * i + (lane & 15);
@@ -410,6 +458,10 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     __syncthreads();
     head_finish((nks - 1) & 1);
     return;
+  }
+  if constexpr (POOL) {
+    __syncthreads();
+    pool_finish((nks - 1) & 1);
   }
   if (a.stats) {  // one partial row per (block, pixel group); waves cg = 0 / 1 fill its two halves
 #pragma unroll
@@ -461,6 +513,7 @@ extern "C" int rdp_conv_ring_head(const void* x, long xbytes, int C, int pitch, 
   a.stats = nullptr; a.escale = escale; a.eshift = eshift; a.erelu = 1;
   a.bny = nullptr; a.bnypitch = 0; a.bncoef = nullptr;
   a.hw = hw; a.hb = hb; a.hthr = hthr; a.hmask = (uint8_t*)mask;
+  a.pool = nullptr; a.ppitch = 0;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -470,6 +523,35 @@ extern "C" int rdp_conv_ring_head(const void* x, long xbytes, int C, int pitch, 
   const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
   a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
   hipLaunchKernelGGL((conv_ring_kernel<64, 0, false, true>), dim3(grid), dim3(512), 0, s, a);
+  return 0;
+}
+
+// Eval conv (64 -> 64, BN folded + ReLU) that also writes MaxPool2d(2) of its output into pool
+// [N][H/2][W/2][64] (pixel pitch ppitch). Returns 0, or -1 when the ring kernel does not apply.
+extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                                  void* y, long ybytes, int ypitch, int Cout, int N, int H, int W,
+                                  const float* escale, const float* eshift, int erelu, void* pool, int ppitch,
+                                  hipStream_t s) {
+  if (C != 64 || Cout != 64 || W % 64 || H % 2 || ldw < 576 || !escale || !eshift || !pool || ppitch % 4) return -1;
+  if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+  RingArgs a;
+  a.x = (const u16*)x; a.xbytes = (uint32_t)xbytes; a.pitch = pitch;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+  a.y2 = (u16*)y; a.ybytes2 = 0; a.ypitch2 = ypitch; a.Cy1 = 64;
+  a.stats = nullptr; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  a.bny = nullptr; a.bnypitch = 0; a.bncoef = nullptr;
+  a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
+  a.pool = (u16*)pool; a.ppitch = ppitch;
+  a.H = H; a.W = W; a.WS = W / 64;
+  a.nrows = N * a.WS * H;
+  a.npairs = a.nrows / 2;
+  const int blocks = std::max(1, std::min(256, a.npairs));
+  a.pairs_per_block = (a.npairs + blocks - 1) / blocks;
+  const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
+  const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
+  a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
+  hipLaunchKernelGGL((conv_ring_kernel<64, 0, false, false, true>), dim3(grid), dim3(512), 0, s, a);
   return 0;
 }
 
@@ -495,6 +577,7 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
   a.bny = bn_y; a.bnypitch = bn_ypitch; a.bncoef = bn_coef;
   a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
+  a.pool = nullptr; a.ppitch = 0;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;

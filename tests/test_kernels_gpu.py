@@ -492,10 +492,12 @@ def _splitk_case(C, N, H, W, C1, C2, Cout):
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(1, 64, 64, 256, 0, 256), (1, 32, 32, 512, 0, 512),
                                               (1, 128, 128, 128, 0, 128), (2, 16, 16, 256, 256, 512),
-                                              (1, 256, 256, 64, 0, 128)])
+                                              (1, 256, 256, 64, 0, 128), (1, 256, 256, 64, 0, 64),
+                                              (2, 64, 128, 64, 0, 64), (1, 24, 40, 64, 0, 64)])
 def test_conv_eval_fused_pool(C, N, H, W, C1, C2, Cout):
     """Eval conv (BN fold + ReLU) with ``pool=``: MaxPool2d(2) fused into the split-K reduce (deep
-    serving shapes) or launched after the conv (no split, last case) -- bitwise the pool of the output."""
+    serving shapes), into the row-ring epilogue (64 -> 64, W % 64 == 0) or launched after the conv
+    (the rest) -- bitwise the pool of the output."""
     torch.manual_seed(9)
     dev = "cuda"
     x1 = bf(torch.randn(N, H, W, C1, device=dev))
