@@ -11,7 +11,7 @@
 extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
-                   float*, long, void*, int, int*, hipStream_t);
+                   float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
                      hipStream_t);
@@ -139,7 +139,7 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
 int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, int taps, int packed,
              torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref,
              c10::optional<torch::Tensor> affine, int relu, c10::optional<torch::Tensor> ws,
-             c10::optional<torch::Tensor> pool) {
+             c10::optional<torch::Tensor> pool, c10::optional<torch::Tensor> up, int up_oy, int up_ox) {
   Act a1 = act(x1, "x1"), a2;
   if (x2) {
     a2 = act(*x2, "x2");
@@ -176,17 +176,30 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     TORCH_CHECK(!y2 && !stats && po.N == o1.N && po.H == o1.H / 2 && po.W == o1.W / 2 && po.C == o1.C,
                 "pool: eval conv with one destination, [N][H/2][W/2][Cout]");
   }
+  // up (eval): bilinear x2 upsample of y1 into up at (up_oy, up_ox); fused into the split-K reduce
+  // when that path runs, else an upsample2_fwd launch after the conv
+  Act uo;
+  if (up) {
+    uo = act(*up, "up");
+    TORCH_CHECK(!pool && !y2 && !stats && uo.N == o1.N && uo.C == o1.C && up_oy >= 0 && up_ox >= 0 &&
+                2 * o1.H + up_oy <= uo.H && 2 * o1.W + up_ox <= uo.W, "up: eval conv, [N][>=2H][>=2W][Cout]");
+  }
   int pooled = 0;
   const int r = rdp_conv_igemm(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
                                a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1), o1.ptr,
                                y2 ? o2.ptr : nullptr, o1.bytes, y2 ? o2.bytes : 0, o1.C, o1.pitch, y2 ? o2.pitch : 0,
                                sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu,
                                ws ? ws->data_ptr<float>() : nullptr, ws ? (long)ws->numel() : 0L,
-                               pool ? po.ptr : nullptr, pool ? po.pitch : 0, pool ? &pooled : nullptr, cur_stream());
+                               pool ? po.ptr : nullptr, pool ? po.pitch : 0, (pool || up) ? &pooled : nullptr,
+                               up ? uo.ptr : nullptr, up ? uo.pitch : 0, up ? uo.H : 0, up ? uo.W : 0, up_oy, up_ox,
+                               cur_stream());
   TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
   if (pool && !pooled)
     TORCH_CHECK(rdp_maxpool2_fwd(o1.ptr, o1.pitch, po.ptr, po.pitch, o1.N, o1.H, o1.W, o1.C, cur_stream()) == 0,
                 "conv_fwd: maxpool");
+  if (up && !pooled)
+    TORCH_CHECK(rdp_upsample2_fwd(o1.ptr, o1.pitch, uo.ptr, uo.pitch, o1.N, o1.H, o1.W, uo.H, uo.W, up_oy, up_ox, o1.C,
+                                  nullptr, cur_stream()) == 0, "conv_fwd: upsample");
   return r;
 }
 
@@ -779,7 +792,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "rdp MI355X (gfx950) HIP kernels";
   m.def("conv_fwd", &conv_fwd, py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
         py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
-        py::arg("ws") = py::none(), py::arg("pool") = py::none());
+        py::arg("ws") = py::none(), py::arg("pool") = py::none(), py::arg("up") = py::none(),
+        py::arg("up_oy") = 0, py::arg("up_ox") = 0);
   m.def("conv_set_fixup_kb", &rdp_conv_set_fixup_kb, "split-K in-kernel fixup bound in KB (0 = reduce kernel)");
   m.def("conv_set_stages", &rdp_conv_set_stages, "igemm K-pipeline depth: 0 = auto, 2-4 = forced");
   m.def("conv_ws_elems", [](int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {

@@ -55,6 +55,11 @@ struct ConvArgs {
   int fixup;       // split-K: 1 = the tile's last-arriving block reduces + runs the epilogue in-kernel
   u16* pool;       // split-K reduce only: also write MaxPool2d(2) of the output (eval), [M/4][ppitch]
   int ppitch;
+  // split-K reduce only: also write the bilinear x2 (align_corners) upsample of the output (eval), into
+  // up [N][uH][uW][upitch] at offset (uoy, uox) (F.pad of the decoder), zeros outside
+  u16* up;
+  int upitch, uH, uW, uoy, uox;
+  float urh, urw;
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
   int store_aware;  // 1: the per-step vmcnt leaves the previous epilogue's stores in flight
@@ -542,6 +547,100 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
   }
 }
 
+// Split-K reduce fused with the decoder's bilinear x2 upsample (eval; serving at N = 1): a block owns
+// UP_TY output rows of one image x UP_CG channels. Phase 1 reduces the slices of the (at most
+// UP_TY / 2 + 2) source rows those output rows read -- same summation and epilogue as
+// conv_splitk_reduce_kernel, so the low-resolution output y is written bitwise as there (rows shared by
+// two bands are written twice with equal values) -- into LDS as bf16; phase 2 interpolates the output
+// rows from LDS with the arithmetic of upsample2_fwd_kernel (csrc/pool_up.hip). The low-res tensor is
+// never re-read from memory and the upsample launch disappears.
+#define UP_TY 4
+#define UP_CG 16
+RDP_DEV void up_src_f(int u, int in, float r, int& i0, int& i1, float& l1) {  // = up_src (pool_up.hip)
+  const float sv = r * (float)u;
+  i0 = (int)sv;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = sv - (float)i0;
+}
+__global__ __launch_bounds__(256) void conv_splitk_reduce_up_kernel(const ConvArgs a) {
+  extern __shared__ uint32_t srcs[];  // [source row][W][UP_CG / 2] packed bf16 pairs
+  const int nb = (a.uH + UP_TY - 1) / UP_TY;
+  const int img = blockIdx.x / nb, band = blockIdx.x - img * nb;
+  const int c0 = blockIdx.y * UP_CG;
+  const int Y0 = band * UP_TY, Y1 = min(a.uH, Y0 + UP_TY);
+  int sy_lo = a.H, sy_hi = -1;
+  for (int Y = Y0; Y < Y1; ++Y) {
+    const int uy = Y - a.uoy;
+    if (uy < 0 || uy >= 2 * a.H) continue;
+    int y0, y1;
+    float ly;
+    up_src_f(uy, a.H, a.urh, y0, y1, ly);
+    sy_lo = min(sy_lo, y0);
+    sy_hi = max(sy_hi, y1);
+  }
+  const int nrows = sy_hi >= sy_lo ? sy_hi - sy_lo + 1 : 0;
+  const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
+  const uint32_t sstride = (uint32_t)a.M * (uint32_t)a.Cout * 4u;
+  constexpr int NQ = UP_CG / 4;  // 4-channel quads per block
+  for (int it = threadIdx.x; it < nrows * a.W * NQ; it += 256) {
+    const int q = it % NQ, px = it / NQ;
+    const int r = px / a.W, x = px - r * a.W;
+    const int m = (img * a.H + sy_lo + r) * a.W + x;
+    const int n = c0 + 4 * q;
+    f32x4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t base = ((uint32_t)m * (uint32_t)a.Cout + (uint32_t)n) * 4u;
+    for (int sp0 = 0; sp0 < a.ksplit; sp0 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t off = sp0 + u < a.ksplit ? base + (uint32_t)(sp0 + u) * sstride : RDP_OOB;
+        v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u & 3] += v[u];
+    }
+    f32x4 o = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    const float4 sc = *(const float4*)(a.escale + n), sh = *(const float4*)(a.eshift + n);
+    o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+    o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+    if (a.erelu) {
+      o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
+    }
+    const uint2 w = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+    *(uint2*)(a.y1 + (long)m * a.ypitch1 + n) = w;
+    srcs[(px * NQ + q) * 2] = w.x;
+    srcs[(px * NQ + q) * 2 + 1] = w.y;
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < (Y1 - Y0) * a.uW * NQ; it += 256) {
+    const int q = it % NQ, t = it / NQ;
+    const int X = t % a.uW, Y = Y0 + t / a.uW;
+    const int uy = Y - a.uoy, ux = X - a.uox;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!(uy < 0 || ux < 0 || uy >= 2 * a.H || ux >= 2 * a.W)) {
+      int y0, y1, x0, x1;
+      float ly, lx;
+      up_src_f(uy, a.H, a.urh, y0, y1, ly);
+      up_src_f(ux, a.W, a.urw, x0, x1, lx);
+      auto ld = [&](int yy, int xx, float* f) {
+        const int i = (((yy - sy_lo) * a.W + xx) * NQ + q) * 2;
+        const uint32_t lo = srcs[i], hi = srcs[i + 1];
+        f[0] = __uint_as_float(lo << 16); f[1] = __uint_as_float(lo & 0xffff0000u);
+        f[2] = __uint_as_float(hi << 16); f[3] = __uint_as_float(hi & 0xffff0000u);
+      };
+      float pa[4], pb[4], pc[4], pd[4];
+      ld(y0, x0, pa); ld(y0, x1, pb); ld(y1, x0, pc); ld(y1, x1, pd);
+      const float hy = 1.f - ly, hx = 1.f - lx;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = hy * (hx * pa[k] + lx * pb[k]) + ly * (hx * pc[k] + lx * pd[k]);
+    }
+    *(uint2*)(a.up + ((long)(img * a.uH + Y) * a.uW + X) * a.upitch + c0 + 4 * q) =
+        make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+  }
+}
+
 // split-K workspace layout: [KCNT_WORDS] u32 arrival counters (zero-initialised by the caller, left
 // zero by every launch) followed by the fp32 slab
 #define KCNT_WORDS 256
@@ -623,6 +722,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, 
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
     if (a.fixup) {
       a.pool = nullptr;
+      a.up = nullptr;
       launch_depth<BM, BN, NWV, true>(a, grid, s);
       return tilesM * (BM / 64);  // stats rows (tm, wave row), written by the reducers
     }
@@ -630,6 +730,13 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, 
     const int rpb = 256 / (a.Cout / 4);
     int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
+    if (a.up) {  // fused eval upsample: bands of UP_TY output rows x UP_CG channels
+      const int nb = (a.uH + UP_TY - 1) / UP_TY;
+      const size_t lds = (size_t)(UP_TY / 2 + 2) * a.W * UP_CG * 2;
+      hipLaunchKernelGGL(conv_splitk_reduce_up_kernel, dim3(a.N * nb, a.Cout / UP_CG), dim3(256), lds, s, a);
+      if (pooled) *pooled = 1;
+      return 0;
+    }
     if (a.pool) {  // fused eval MaxPool2d(2): one work row per 2x2 window, no stats rows
       nblk = (a.M / 4 + rpb - 1) / rpb;
       nblk = nblk < 2048 ? nblk : 2048;
@@ -639,7 +746,8 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, 
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
     return nblk;
   }
-  a.pool = nullptr;  // the non-split epilogue does not pool (the caller launches maxpool2_fwd)
+  a.pool = nullptr;  // the non-split epilogue does not pool / upsample (the caller launches them)
+  a.up = nullptr;
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
   // the per-block stats rows need every block to keep one channel tile (see the kernel)
   if (a.stats && grid % a.tilesN) return -1;
@@ -653,9 +761,12 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
                               long ybytes1, long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats,
                               int N, int H, int W, int Cout, int taps, int packed, int bm_pref,
                               const float* escale, const float* eshift, int erelu, float* ws, long ws_elems,
-                              void* pool, int ppitch, int* pooled, hipStream_t s) {
+                              void* pool, int ppitch, int* pooled, void* up, int upitch, int uH, int uW,
+                              int uoy, int uox, hipStream_t s) {
   // pool (eval, optional): MaxPool2d(2) of y1 fused into the split-K reduce when that path runs;
-  // *pooled = 1 if it was written (otherwise the caller pools)
+  // up (eval, optional, exclusive with pool): bilinear x2 upsample of y1 into up [N][uH][uW] at
+  // (uoy, uox), fused the same way; *pooled = 1 if the fused output was written (else the caller
+  // launches the pool / upsample)
   if (pooled) *pooled = 0;
   // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 6 = force the row-ring kernel,
   // 128 / 256 (2 / 3: 8-wave) = force this kernel's tile
@@ -702,6 +813,19 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   a.pool = (pool != nullptr && pooled != nullptr && stats == nullptr && y2 == nullptr && H % 2 == 0 && W % 2 == 0)
                ? (u16*)pool : nullptr;
   a.ppitch = ppitch;
+  // fused upsample needs the eval epilogue, 16-channel groups and the LDS band (<= 64 KB). Measured
+  // (serving frame, N = 1): it wins only at the 16^2 bottleneck (6.9 us vs 4.8 + 4.8 us); at 32^2 /
+  // 64^2 / 128^2 the banded two-phase kernel is slower than reduce + upsample (10.9 / 13.2 / 15.4 vs
+  // 9.8 / 10.3 / 10.6 us; 2-row bands x 8 channels were slower still), so larger maps take the
+  // separate upsample launch.
+  const bool up_ok = up != nullptr && pooled != nullptr && pool == nullptr && stats == nullptr && y2 == nullptr &&
+                     escale != nullptr && eshift != nullptr && Cout % UP_CG == 0 && upitch % 4 == 0 &&
+                     (long)(UP_TY / 2 + 2) * W * UP_CG * 2 <= 65536 && uH >= 2 * H && uW >= 2 * W &&
+                     (long)H * W <= 256;
+  a.up = up_ok ? (u16*)up : nullptr;
+  a.upitch = upitch; a.uH = uH; a.uW = uW; a.uoy = uoy; a.uox = uox;
+  a.urh = 2 * H > 1 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;  // = ac_scale (pool_up.hip)
+  a.urw = 2 * W > 1 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
   long wse = has_ws ? ws_elems - KCNT_WORDS : 0;
   wse = wse < (1L << 29) ? wse : (1L << 29);  // slab bytes < 2 GiB (buffer offsets)
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;

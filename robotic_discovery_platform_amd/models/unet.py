@@ -273,6 +273,8 @@ class UNetNative(nn.Module):
 
 # eval-mode MaxPool2d fused into the split-K conv reduce (serving); "0" = separate maxpool launches
 _FUSE_POOL_EVAL = os.environ.get("RDP_FUSE_POOL_EVAL", "1") != "0"
+# eval decoder upsample fused into the split-K reduce of the conv producing its input; "0" = separate
+_FUSE_UP_EVAL = os.environ.get("RDP_FUSE_UP_EVAL", "1") != "0"
 # serving 1x1 head + threshold fused into the last conv's epilogue; "0" = separate head_mask launch
 _FUSE_HEAD_EVAL = os.environ.get("RDP_FUSE_HEAD_EVAL", "1") != "0"
 
@@ -552,18 +554,30 @@ class UNetExecutor:
                 self.target.copy_(target.reshape(-1))
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn_relu(self, C, L: _Layer, pool: Optional[torch.Tensor] = None, apply: bool = True):
+    def _conv_bn_relu(self, C, L: _Layer, pool: Optional[torch.Tensor] = None, apply: bool = True,
+                      up: Optional[torch.Tensor] = None):
         """conv -> BN(train: batch stats) -> ReLU into ``L.a``; with ``pool`` also MaxPool2d(2) of
         ``L.a`` into ``pool`` (fused with the BN apply in training). Returns True if it pooled.
-        ``apply=False`` (training) stops after the BN statistics: the consumer applies BN+ReLU."""
+        ``apply=False`` (training) stops after the BN statistics: the consumer applies BN+ReLU.
+        ``up`` (eval): also the decoder's bilinear x2 upsample of ``L.a`` into ``up`` (centred, as the
+        F.pad of Up.forward); returns True when it was produced."""
         sp = L.spec
         m = self.m
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
-            # with ``pool``: MaxPool2d(2) too (fused into the split-K reduce where that path runs;
-            # RDP_FUSE_POOL_EVAL=0: the separate maxpool launch, for A/B)
+            # with ``pool`` / ``up``: MaxPool2d(2) / the upsample too (fused into the split-K reduce or
+            # the row-ring epilogue where those run; RDP_FUSE_POOL_EVAL=0 / RDP_FUSE_UP_EVAL=0: the
+            # separate launches, for A/B)
             if pool is not None and not _FUSE_POOL_EVAL:
                 pool = None
+            if up is not None and not _FUSE_UP_EVAL:
+                up = None
+            if up is not None:
+                oy = (up.shape[1] - 2 * L.a.shape[1]) // 2
+                ox = (up.shape[2] - 2 * L.a.shape[2]) // 2
+                C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, None, up,
+                           oy, ox)
+                return True
             C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool)
             return pool is not None
         rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
@@ -607,11 +621,17 @@ class UNetExecutor:
         l0, l1 = self.down_layers[0]
         self._conv_bn_relu(C, l0)
         pooled = self._conv_bn_relu(C, l1, self.pools[0] if D > 0 else None)
+        # eval, bilinear decoder: each decoder input upsample is produced by the conv that makes `low`
+        eval_up = not self.training and self.m.bilinear and not self.fuse_up_bn
+        upsampled = False
         for i in range(1, D + 1):
             if not pooled:
                 C.maxpool2_fwd(self.skips[i - 1], self.pools[i - 1])
             la, lb = self.down_layers[i]
             self._conv_bn_relu(C, la)
+            if i == D and eval_up:
+                upsampled = self._conv_bn_relu(C, lb, up=self.ups[0])
+                continue
             pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None,
                                         apply=not (i == D and self.fuse_up_bn))
         low = self.skips[D]
@@ -621,7 +641,9 @@ class UNetExecutor:
             u = self.ups[i - 1]
             oy = (u.shape[1] - 2 * low.shape[1]) // 2
             ox = (u.shape[2] - 2 * low.shape[2]) // 2
-            if self.m.bilinear and self.fuse_up_bn:
+            if upsampled:
+                upsampled = False
+            elif self.m.bilinear and self.fuse_up_bn:
                 C.upsample2_fwd(low_layer.y, u, oy, ox, low_layer.coef)  # BN + ReLU of low_layer on the fly
             elif self.m.bilinear:
                 C.upsample2_fwd(low, u, oy, ox)
@@ -635,7 +657,11 @@ class UNetExecutor:
             last = i == D
             if last and mask_head is not None and not head and self._conv_head_mask(C, lb, mask_head):
                 return
-            self._conv_bn_relu(C, lb, apply=not ((last and self.fuse_head and head) or (not last and self.fuse_up_bn)))
+            if not last and eval_up:
+                upsampled = self._conv_bn_relu(C, lb, up=self.ups[i])
+            else:
+                self._conv_bn_relu(C, lb, apply=not ((last and self.fuse_head and head) or
+                                                     (not last and self.fuse_up_bn)))
             low, low_layer = lb.a, lb
         if not head:
             if mask_head is not None:

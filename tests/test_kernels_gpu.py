@@ -522,6 +522,44 @@ def test_conv_eval_fused_pool(C, N, H, W, C1, C2, Cout):
     assert relerr(nchw(a), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pad", [(1, 16, 16, 512, 0, 512, 0), (1, 32, 32, 512, 512, 256, 0),
+                                                   (1, 64, 64, 256, 256, 128, 1), (2, 16, 16, 256, 0, 256, 1),
+                                                   (1, 128, 128, 128, 128, 64, 0)])
+def test_conv_eval_fused_upsample(C, N, H, W, C1, C2, Cout, pad):
+    """Eval conv (BN fold + ReLU) with ``up=``: the decoder's bilinear x2 upsample (align_corners,
+    centred pad) fused into the split-K reduce (maps of <= 16^2 pixels; larger ones take the separate
+    launch) == conv_fwd + upsample2_fwd (y bitwise; the upsample to within one bf16 rounding of the
+    interpolation: FMA contraction may differ between the kernels)."""
+    torch.manual_seed(11)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    n_ws = C.conv_ws_elems(N, H, W, C1, C2, Cout, 9, 0, 0)
+    assert n_ws > 0
+    ws = torch.zeros(n_ws, device=dev)
+    g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    Hu, Wu = 2 * H + 2 * pad, 2 * W + 2 * pad
+    a = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    u = torch.full((N, Hu, Wu, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, a, None, None, 0, coef, 1, ws, None, u, pad, pad)
+    a2 = torch.empty_like(a)
+    C.conv_fwd(x1, x2, wk, 9, 0, a2, None, None, 0, coef, 1, ws)
+    assert torch.equal(a, a2)
+    u2 = torch.full_like(u, float("nan"))
+    C.upsample2_fwd(a2, u2, pad, pad)
+    assert not torch.isnan(u.float()).any()
+    d = (u.float() - u2.float()).abs()
+    assert (d <= 2 ** -7 * u2.float().abs() + 1e-6).all(), d.max()
+    assert (u == u2).float().mean() > 0.99
+    ref = F.interpolate(nchw(a2).float(), scale_factor=2, mode="bilinear", align_corners=True)
+    assert relerr(nchw(u)[:, :, pad:pad + 2 * H, pad:pad + 2 * W], ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W", [(1, 256, 256), (2, 64, 128), (1, 128, 64)])
 def test_conv_head_mask_fused(C, N, H, W):
     """Serving: last conv (64 -> 64, BN fold + ReLU) + 1x1 head + threshold in the row-ring epilogue ==
