@@ -20,6 +20,7 @@
 #include "common.h"
 #include "geo_sort.h"
 #include <stdint.h>
+#include <stdlib.h>
 
 #define GEO_ROWS_PER_BLOCK 1  // 480 blocks at 480 rows (4 rows = 120 blocks left half the CUs idle: count + write 22 -> 11 us)
 #define GEO_THREADS 256
@@ -395,6 +396,234 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* _
   }
 }
 
+// Wave-per-bin variant of geo_select_kernel (the default): the same selection rule and tie-breaking,
+// with one wave owning one bin, so the 8 + 4 radix passes and the bitonic x-sort need no workgroup
+// barrier (a wave's LDS operations execute in issue order; the digit owner is found by ballot and
+// broadcast by a lane shuffle). The k selected points are compacted in point-index order (ballot +
+// popcount), so `out` is deterministic too. Bins beyond the LDS caches read / sort through global
+// memory (vmcnt-ordered within the wave).
+#define GEO_WLCAP 2048
+#define GEO_WSORT 256
+// cross-lane LDS hand-off inside one wave: drain this wave's LDS operations and keep the compiler
+// from moving LDS accesses across (no workgroup barrier: other waves own other bins)
+RDP_DEV void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+template <bool LARGEST>
+RDP_DEV void wave_pick_digit(const unsigned* hist, int need, int lane, int& digit, int& nneed, int& eq) {
+  int h[4], tot = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { h[j] = (int)hist[4 * lane + j]; tot += h[j]; }
+  int sc = tot;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = LARGEST ? __shfl_down(sc, off, 64) : __shfl_up(sc, off, 64);
+    if (LARGEST ? lane + off < 64 : lane >= off) sc += o;
+  }
+  const int before = sc - tot;
+  int d = 0, nn = 0, e = 0;
+  const bool own = before < need && need <= sc;
+  if (own) {
+    int acc = before;
+    if (LARGEST) {
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        if (acc + h[j] >= need) { d = 4 * lane + j; nn = need - acc; e = h[j]; break; }
+        acc += h[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (acc + h[j] >= need) { d = 4 * lane + j; nn = need - acc; e = h[j]; break; }
+        acc += h[j];
+      }
+    }
+  }
+  const int owner = __ffsll((unsigned long long)__ballot(own)) - 1;
+  digit = __shfl(d, owner, 64);
+  nneed = __shfl(nn, owner, 64);
+  eq = __shfl(e, owner, 64);
+}
+
+__global__ __launch_bounds__(256) void geo_select_wave_kernel(const double* __restrict__ pts,
+                                                              const int* __restrict__ npts_p, int nbins, double top,
+                                                              GeoBins gb, double* __restrict__ out, int kcap,
+                                                              int* __restrict__ kout, int min_points,
+                                                              double* __restrict__ sorted, int* __restrict__ gperm,
+                                                              int ecap) {
+  __shared__ unsigned whist[4][256];
+  __shared__ uint64_t wkey[4][GEO_WLCAP];
+  __shared__ int wid[4][GEO_WLCAP];
+  __shared__ double wsx[4][GEO_WSORT], wsy[4][GEO_WSORT], wsz[4][GEO_WSORT];
+  __shared__ int wsi[4][GEO_WSORT], wperm[4][GEO_WSORT];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int bin = blockIdx.x * 4 + w;
+  if (bin >= nbins) return;  // whole wave; no workgroup barriers below
+  unsigned* hist = whist[w];
+  uint64_t* skey = wkey[w];
+  int* sid = wid[w];
+  const int n = npts_p[0];
+  const int nb = gb.cnt[bin];
+  if (n < min_points || nb == 0) {
+    if (lane == 0) kout[bin] = 0;
+    return;
+  }
+  int start = 0, off = 0;  // first point of the bin in bidx; sum of the earlier bins' k
+  for (int b = lane; b < bin; b += 64) {
+    const int c = gb.cnt[b];
+    start += c;
+    int kb = (int)((double)c * top);
+    if (kb < 1) kb = 1;
+    if (kb > kcap) kb = kcap;
+    off += c > 0 ? kb : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    start += __shfl_xor(start, o, 64);
+    off += __shfl_xor(off, o, 64);
+  }
+  const int* ids = gb.bidx + start;
+  int k = (int)((double)nb * top);
+  if (k < 1) k = 1;
+  if (k > kcap) k = kcap;
+  for (int i = lane; i < nb && i < GEO_WLCAP; i += 64) {
+    const int id = ids[i];
+    sid[i] = id;
+    skey[i] = dkey(pts[(size_t)id * 4 + 1]);
+  }
+  wave_lds_sync();
+  auto key_at = [&](int i) -> uint64_t { return i < GEO_WLCAP ? skey[i] : dkey(pts[(size_t)ids[i] * 4 + 1]); };
+  auto id_at = [&](int i) -> int { return i < GEO_WLCAP ? sid[i] : ids[i]; };
+  // 1) k-th largest key (8 x 8-bit digits, MSB first)
+  uint64_t prefix = 0;
+  int need = k, eq = 0;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hist[4 * lane + j] = 0;
+    wave_lds_sync();
+    const uint64_t pmask = pass == 0 ? 0ull : (~0ull << (64 - 8 * pass));
+    for (int i = lane; i < nb; i += 64) {
+      const uint64_t key = key_at(i);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+    }
+    wave_lds_sync();
+    int d, nn;
+    wave_pick_digit<true>(hist, need, lane, d, nn, eq);
+    prefix |= (uint64_t)d << shift;
+    need = nn;
+  }
+  const uint64_t kth = prefix;
+  // 2) ties at kth: the `need` smallest indices
+  uint32_t last_id = 0xffffffffu;
+  if (need < eq) {
+    uint32_t ip = 0;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hist[4 * lane + j] = 0;
+      wave_lds_sync();
+      const uint32_t pmask = pass == 0 ? 0u : (~0u << (32 - 8 * pass));
+      for (int i = lane; i < nb; i += 64) {
+        const uint32_t id = (uint32_t)id_at(i);
+        if (key_at(i) == kth && (id & pmask) == ip) atomicAdd(&hist[(id >> shift) & 255], 1u);
+      }
+      wave_lds_sync();
+      int d, nn, e2;
+      wave_pick_digit<false>(hist, need, lane, d, nn, e2);
+      ip |= (uint32_t)d << shift;
+      need = nn;
+    }
+    last_id = ip;
+  }
+  // 3) compact the k points in bin order (ballot prefix): out slab + the sort caches
+  double* ob = out + (size_t)bin * kcap * 4;
+  const bool lsort = sorted != nullptr && k <= GEO_WSORT;
+  int base = 0;
+  for (int i0 = 0; i0 < nb; i0 += 64) {
+    const int i = i0 + lane;
+    bool sel = false;
+    int id = 0;
+    if (i < nb) {
+      const uint64_t key = key_at(i);
+      id = id_at(i);
+      sel = key > kth || (key == kth && (uint32_t)id <= last_id);
+    }
+    const unsigned long long msk = __ballot(sel);
+    const int pos = base + __popcll(msk & ((1ull << lane) - 1ull));
+    if (sel && pos < kcap) {
+      const double px = pts[(size_t)id * 4], py = pts[(size_t)id * 4 + 1], pz = pts[(size_t)id * 4 + 2];
+      ob[(size_t)pos * 4] = px;
+      ob[(size_t)pos * 4 + 1] = py;
+      ob[(size_t)pos * 4 + 2] = pz;
+      ob[(size_t)pos * 4 + 3] = pts[(size_t)id * 4 + 3];
+      if (lsort) {
+        wsx[w][pos] = px;
+        wsy[w][pos] = py;
+        wsz[w][pos] = pz;
+        wsi[w][pos] = (int)pts[(size_t)id * 4 + 3];
+      }
+    }
+    base += __popcll(msk);
+  }
+  wave_lds_sync();
+  if (lane == 0) kout[bin] = k;
+  if (!sorted) return;
+  // 4) x-sort (x asc, y desc, index asc) of the k points into sorted[off ..] (as geo_sort_bin)
+  if (off >= ecap) return;
+  int kk = k;
+  if (off + kk > ecap) kk = ecap - off;
+  int P = 1;
+  while (P < k) P <<= 1;
+  int* perm = lsort ? wperm[w] : gperm + 2 * (size_t)off;
+  if (!lsort) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's `out` stores, before re-reading
+  for (int i = lane; i < P; i += 64) perm[i] = i;
+  wave_lds_sync();
+  auto after = [&](int a, int c) -> bool {
+    if (a >= k) return c < k || a > c;
+    if (c >= k) return false;
+    double xa, xc, ya, yc;
+    int ia, ic;
+    if (lsort) {
+      xa = wsx[w][a]; xc = wsx[w][c]; ya = wsy[w][a]; yc = wsy[w][c]; ia = wsi[w][a]; ic = wsi[w][c];
+    } else {
+      xa = ob[(size_t)a * 4]; xc = ob[(size_t)c * 4];
+      ya = ob[(size_t)a * 4 + 1]; yc = ob[(size_t)c * 4 + 1];
+      ia = (int)ob[(size_t)a * 4 + 3]; ic = (int)ob[(size_t)c * 4 + 3];
+    }
+    if (xa != xc) return xa > xc;
+    if (ya != yc) return ya < yc;
+    return ia > ic;
+  };
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (!lsort) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // previous stage's perm stores
+      for (int t = lane; t < P / 2; t += 64) {
+        const int i = 2 * stride * (t / stride) + (t % stride), j = i + stride;
+        const int a = perm[i], c = perm[j];
+        const bool up = (i & size) == 0;
+        if (up ? after(a, c) : after(c, a)) {
+          perm[i] = c;
+          perm[j] = a;
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  if (!lsort) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int i = lane; i < kk; i += 64) {
+    const int sidx = perm[i];
+    if (lsort) {
+      sorted[(size_t)(off + i) * 3] = wsx[w][sidx];
+      sorted[(size_t)(off + i) * 3 + 1] = wsy[w][sidx];
+      sorted[(size_t)(off + i) * 3 + 2] = wsz[w][sidx];
+    } else {
+      for (int c = 0; c < 3; ++c) sorted[(size_t)(off + i) * 3 + c] = ob[(size_t)sidx * 4 + c];
+    }
+  }
+}
+
 // Pack the per-bin edge points contiguously (one block per bin): hdr[0] = E, edges[E][4].
 __global__ void geo_pack_kernel(const double* __restrict__ out, int kcap, const int* __restrict__ kout, int nbins,
                                 double* __restrict__ edges, int ecap, int* __restrict__ hdr) {
@@ -461,8 +690,16 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
                      (const uint16_t*)depth, H, W, cam, counts, nblk, pts, cap, npts, xmin, xmax, nbins, gb);
   const int pblocks = (cap + GEO_THREADS * 4 - 1) / (GEO_THREADS * 4);
   hipLaunchKernelGGL(geo_bin_scatter_kernel, dim3(pblocks), dim3(GEO_THREADS), 0, s, npts, nbins, gb);
-  hipLaunchKernelGGL(geo_select_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, nbins, top, gb, out, kcap,
-                     kout, min_points, sorted, gperm, secap);
+  static const int env_sel = [] {  // RDP_GEO_SELECT=block: the workgroup-per-bin kernel (A/B)
+    const char* e = getenv("RDP_GEO_SELECT");
+    return e && e[0] == 'b' ? 1 : 0;
+  }();
+  if (env_sel)
+    hipLaunchKernelGGL(geo_select_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, nbins, top, gb, out, kcap,
+                       kout, min_points, sorted, gperm, secap);
+  else
+    hipLaunchKernelGGL(geo_select_wave_kernel, dim3((nbins + 3) / 4), dim3(256), 0, s, pts, npts, nbins, top, gb, out,
+                       kcap, kout, min_points, sorted, gperm, secap);
   if (edges) hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
   return nblk;
 }

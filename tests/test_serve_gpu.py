@@ -147,6 +147,40 @@ def test_geometry_kernels_match_oracle(seed):
     assert r.n_edge_points == E and r.n_points == n
 
 
+def test_geometry_large_bins_match_oracle():
+    """Every pixel valid (307k points, ~6k per x bin, k ~ 300 > the wave kernel's LDS sort cache):
+    the select / sort paths through global memory == the numpy oracle, and the fused serving-form sort ==
+    the separate sort launch."""
+    from robotic_discovery_platform_amd.config import GeometryConfig
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
+    from robotic_discovery_platform_amd.geometry import reference as ref
+    from robotic_discovery_platform_amd.geometry.curvature import GeometryEngine, sort_edges
+    rng = np.random.default_rng(5)
+    mask = np.ones((480, 640), np.uint8)
+    depth = rng.integers(300, 900, (480, 640)).astype(np.uint16)
+    eng = GeometryEngine(480, 640, torch.device("cuda"), GeometryConfig())
+    d = torch.from_numpy(depth.view(np.int16)).cuda()
+    eng.launch(torch.from_numpy(mask).cuda(), d, DEFAULT_K, 0.001)
+    E = int(eng.hdr.item())
+    pcd = ref.point_cloud(mask, depth, DEFAULT_K, 0.001)
+    eo = ref.edge_points(pcd)
+    eo = eo[np.argsort(eo[:, 0], kind="stable")]
+    got = sort_edges(eng.edges[:E].cpu().numpy())
+    assert E == eo.shape[0] and np.array_equal(got, eo)
+    assert int(eng.kout.max().item()) > 256
+    mask_out = torch.empty(480, 640, dtype=torch.uint8, device="cuda")
+    eng.launch_frame(torch.ones(256, 256, dtype=torch.uint8, device="cuda"), mask_out, d, DEFAULT_K, 0.001)
+    E2 = int(eng.kout.clamp(max=eng.out.shape[1]).sum().item())
+    fused = eng.sorted[:E2].clone()
+    c = eng.cfg
+    eng.C.geo_spline(eng.out, eng.kout, eng.npts, eng.sorted, eng.gperm, eng.u, eng.res, c.smoothing,
+                     c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points, eng.cov,
+                     presorted=False)
+    torch.cuda.synchronize()
+    assert E2 == E and torch.equal(fused, eng.sorted[:E2])
+    assert np.array_equal(fused.cpu().numpy(), eo[:, :3])
+
+
 def test_geometry_early_exits():
     from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
     from robotic_discovery_platform_amd.geometry.curvature import compute_curvature_profile
