@@ -776,8 +776,12 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
       return e ? atoi(e) : 1;
     }();
     const int pref = bm_pref % 1000;
-    // row-ring kernel (conv_ring.hip): 64 -> 64 channels, 3x3, one source, no output split
-    if ((pref == 6 || (pref == 0 && ring_env)) && taps == 9 && !packed && C2 == 0 && x2 == nullptr) {
+    // row-ring kernel (conv_ring.hip): 64 -> 64 channels, 3x3, one source, no output split. Auto only
+    // when its grid (one block per pair of 64-pixel row segments, <= 256) fills the chip: at N = 1,
+    // 128^2 x 64 -> 128 the 128-block ring took 15.2 us vs 11.9 us for the implicit GEMM
+    const long ring_pairs = W % 64 == 0 ? (long)N * (W / 64) * H / 2 : 0;
+    if ((pref == 6 || (pref == 0 && ring_env && ring_pairs >= 256)) && taps == 9 && !packed && C2 == 0 &&
+        x2 == nullptr) {
       if (pool && pooled && !stats && !y2 && escale) {  // eval: MaxPool2d fused into the ring epilogue
         const int r = rdp_conv_ring_pool(x1, xbytes1, C1, pitch1, w, wbytes, ldw, y1, ybytes1, ypitch1, Cout, N, H, W,
                                          escale, eshift, erelu, pool, ppitch, s);
