@@ -439,6 +439,321 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong 256 x BN tile (BN = 256 or 128): 8 waves, ONE block per CU, 2-3 stage K ring.
+//
+// The 2-barrier structure above (2 blocks / CU, 128 x 128 tiles) tops out near 0.9-1.1 PF: every
+// K step waits for its own stage behind one barrier, with about one K step of MFMA work to hide
+// the DMA. Here the two wave groups of the block (wm = 0: waves 0-3, wm = 1: waves 4-7; one wave
+// of each group per SIMD) run staggered by one barrier (cdna_hip_programming.md "The 256^2 8-phase
+// template", T3+T4+T5): while one group issues its LDS fragment reads and DMA, its partner on the
+// same SIMD runs a 16-MFMA cluster. A K step (64 channels of one tap) is NPH phases; a phase is a
+// memory segment (fragment reads [+ the DMA of a later stage at phase 0] + lgkmcnt(0)) and a
+// compute segment (16 MFMAs), each ended by one raw s_barrier. Stage g+NST-1 is issued at phase 0
+// of K step g and waited for (counted vmcnt, never a drain of newer stages) in the memory segment
+// of the last phase of K step NST-2 later, i.e. 1.5 K steps (NST 2) to 2.5 K steps (NST 3) of
+// MFMA work hide each DMA -- and the 256-wide tile halves the LDS fill bytes per FLOP of the
+// 128 x 128 tile. Ordering (one barrier more than unstaggered, as the template requires):
+//   * RAW: each wave waits for its own DMA of stage g+1 in M(g, NPH-1); group 1 runs that segment
+//     one slot later than group 0, i.e. in the slot just before group 0's first read M(g+1, 0).
+//   * WAR: every memory segment ends with lgkmcnt(0), so the last reads of a buffer (M(g-1,
+//     NPH-1), group 1 one slot later) are complete before the barrier that precedes the first DMA
+//     into it (M(g, 0) of group 0).
+// Accumulation order per output element is the K-step order with the two K halves of a step in
+// order, exactly as conv_igemm_kernel: outputs are bitwise equal to it. Training BN statistics
+// accumulate per block in LDS words owned by one lane each (no registers held across tiles).
+// Generic (non-packed) im2col only, no split-K / fixup / fused pool or upsample.
+// RD_INFLIGHT: fragment reads of phases 0..NPH-2 stay in flight across the segment barrier;
+// HOLDB: both cout halves of the weight fragments stay in registers (no re-read in phase 3).
+template <int BN, int NST, bool RD_INFLIGHT, bool HOLDB>
+__global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
+  constexpr int BM = 256;
+  constexpr int WNT = BN / 4;           // couts per wave (64 / 32)
+  constexpr int NJ = WNT / 16;          // cout fragments per wave (4 / 2)
+  constexpr int NPH = NJ == 4 ? 4 : 2;  // phases per K step, 16 MFMAs each
+  constexpr int P_BYTES = BM * 128, W_BYTES = BN * 128, BUF = P_BYTES + W_BYTES;
+  constexpr int NROW = 4;            // 8-row pixel DMA pieces per wave per stage (256 / 8 / 8)
+  constexpr int WPIECES = BN / 64;   // weight DMA pieces per wave per stage
+  constexpr int DMA_OPS = NROW + WPIECES;
+  constexpr int ST_OFF = NST * BUF;  // BN statistics: [wm][2][BN] fp32
+  static_assert(NST * BUF + 2 * 2 * BN * 4 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NST * BUF + 2 * 2 * BN * 4];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int gch = (lane & 7) ^ (lane >> 3);
+
+  const uint32_t G = gridDim.x;
+  const uint32_t lid = xcd_remap(blockIdx.x, G);
+  const int my_tiles = lid < (uint32_t)a.ntiles ? (a.ntiles - 1 - (int)lid) / (int)G + 1 : 0;
+  const int total = my_tiles * a.nks;
+
+  const auto rx1 = make_rsrc(a.x1, a.xbytes1);
+  const auto rx2 = make_rsrc(a.x2 ? a.x2 : a.x1, a.x2 ? a.xbytes2 : 0u);
+  const auto rw = make_rsrc(a.w, a.wbytes);
+  const auto ry1 = make_rsrc(a.y1, a.ybytes1);
+  const auto ry2 = make_rsrc(a.y2 ? a.y2 : a.y1, a.y2 ? a.ybytes2 : 0u);
+
+  // DMA state of the tile being staged (see conv_igemm_kernel::set_tile)
+  uint32_t pb1[NROW], pb2[NROW], nmask[NROW], woff[WPIECES];
+  int itap = 0, icc = 0;
+  auto set_tile = [&](int t) {
+    const int tile = (int)lid + t * (int)G;
+    itap = 0;
+    icc = 0;
+    const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
+#pragma unroll
+    for (int r = 0; r < NROW; ++r) {
+      const int m = tm * BM + (wave * NROW + r) * 8 + (lane >> 3);
+      const bool valid = m < a.M;
+      const uint32_t mm = valid ? (uint32_t)m : 0u;
+      const uint32_t hw = mm - ((__umulhi(mm, a.fhw_m) + mm) >> a.fhw_s) * (uint32_t)(a.H * a.W);
+      const uint32_t h = (__umulhi(hw, a.fw_m) + hw) >> a.fw_s;
+      const uint32_t w = hw - h * (uint32_t)a.W;
+      const uint32_t rok = (h > 0 ? 1u : 0u) | 2u | (h + 1 < (uint32_t)a.H ? 4u : 0u);
+      const uint32_t cok = (w > 0 ? 1u : 0u) | 2u | (w + 1 < (uint32_t)a.W ? 4u : 0u);
+      uint32_t msk = 0;
+      msk |= (rok & 1u) ? cok : 0u;
+      msk |= (rok & 2u) ? (cok << 3) : 0u;
+      msk |= (rok & 4u) ? (cok << 6) : 0u;
+      if (a.taps == 1) msk = 1u;
+      nmask[r] = valid ? ~msk : ~0u;
+      pb1[r] = (mm * (uint32_t)a.pitch1 + (uint32_t)gch * 8u) * 2u;
+      pb2[r] = (mm * (uint32_t)a.pitch2 + (uint32_t)gch * 8u) * 2u;
+    }
+#pragma unroll
+    for (int f = 0; f < WPIECES; ++f) {
+      const int n = tn * BN + (wave * WPIECES + f) * 8 + (lane >> 3);
+      woff[f] = (uint32_t)(n * a.ldw + gch * 8) * 2u;
+    }
+  };
+  auto issue = [&](int ks, char* buf) {
+    const int c0 = icc * 64;
+    const bool s2 = c0 >= a.C1;
+    const int pitch = s2 ? a.pitch2 : a.pitch1;
+    const int tap_lin = a.taps == 9 ? tap_dr(itap) * a.W + tap_ds(itap) : 0;
+    const int soff = (tap_lin * pitch + (s2 ? c0 - a.C1 : c0)) * 2;
+    const int bit = a.taps == 9 ? itap : 0;
+#pragma unroll
+    for (int r = 0; r < NROW; ++r) {
+      const uint32_t bad = __builtin_amdgcn_ubfe(nmask[r], (uint32_t)bit, 1u);
+      const uint32_t off = (bad << 31) | (uint32_t)((int)(s2 ? pb2[r] : pb1[r]) + soff);
+      dma16(s2 ? rx2 : rx1, (lds_void*)(buf + (wave * NROW + r) * 1024), off);
+    }
+    if (++icc == a.cpt) { icc = 0; ++itap; if (itap == a.taps) itap = 0; }
+    char* wbuf = buf + P_BYTES;
+#pragma unroll
+    for (int f = 0; f < WPIECES; ++f)
+      dma16(rw, (lds_void*)(wbuf + (wave * WPIECES + f) * 1024), woff[f] + (uint32_t)ks * 128u);
+  };
+
+  int rdoff[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) rdoff[hf] = (lane & 15) * 128 + 16 * (((lane >> 4) + 4 * hf) ^ (lane & 7));
+
+  float* const sst = (float*)(smem + ST_OFF) + wm * 2 * BN;  // this wave row's statistics words
+  if (a.stats && (lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = wn * WNT + j * 16 + 4 * (lane >> 4);
+      *(float4*)(sst + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)(sst + BN + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  f32x4 acc[NJ][8];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // [cout half held][k half][cout frag of the phase] / [k half][pixel frag of the phase]
+  bf16x8 fa[HOLDB ? 2 : 1][2][2], fb[2][4];
+
+  int ks = 0, t = 0;              // compute position
+  int iks = 0, it = 0, ig = 0;    // newest issued stage: K step, tile, global index
+  int cbuf = 0, ibuf = 0;
+  if (total > 0) {
+    set_tile(0);
+    issue(0, smem);
+    if (NST > 2 && total > 1) {
+      if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
+      issue(iks, smem + BUF);
+      ig = 1;
+      ibuf = 1;
+    }
+    if (ig > 0) vm_wait<DMA_OPS>();
+    else vm_wait<0>();
+  }
+  raw_barrier();
+  if (wm == 1) raw_barrier();  // stagger the two wave groups by one segment
+
+  auto epilogue = [&]() {
+    const int item = (int)lid + t * (int)G;
+    const int tm = item / a.tilesN, tn = item - tm * a.tilesN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int gq = lane >> 4;
+    const int coff = 16 * (gq & 1) + 8 * (gq >> 1);
+    float s1[NJ][4], s2[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int jp = 0; jp < NJ; jp += 2) {
+      const int nb = n0 + wn * WNT + jp * 16;
+      const int n = nb + coff;
+      const bool d2 = nb >= a.Cy1;  // wave-uniform: Cy1 % 32 == 0 (host-checked), one SRD per store
+      const int nn = d2 ? n - a.Cy1 : n;
+      const int yp = d2 ? a.ypitch2 : a.ypitch1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+        uint2 v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = jp + h;
+          f32x4 o = acc[j][i];
+          if (a.escale) {
+            const int nc = nb + h * 16 + 4 * gq;
+            const float4 sc = *(const float4*)(a.escale + nc), sh = *(const float4*)(a.eshift + nc);
+            o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+            o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+            if (a.erelu) {
+              o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
+            }
+          }
+          v[h].x = pack2bf(o[0], o[1]);
+          v[h].y = pack2bf(o[2], o[3]);
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (a.stats && m < a.M) {
+            const float q0 = __uint_as_float(v[h].x << 16), q1 = __uint_as_float(v[h].x & 0xffff0000u);
+            const float q2 = __uint_as_float(v[h].y << 16), q3 = __uint_as_float(v[h].y & 0xffff0000u);
+            s1[j][0] += q0; s2[j][0] += q0 * q0;
+            s1[j][1] += q1; s2[j][1] += q1 * q1;
+            s1[j][2] += q2; s2[j][2] += q2 * q2;
+            s1[j][3] += q3; s2[j][3] += q3 * q3;
+          }
+        }
+        const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
+        const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
+        const uint32_t off = m < a.M ? (uint32_t)(m * yp + nn) * 2u : RDP_OOB;
+        bstore16(d2 ? ry2 : ry1, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s1[j][r] = row16_sum(s1[j][r]);
+          s2[j][r] = row16_sum(s2[j][r]);
+        }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = wn * WNT + j * 16 + 4 * gq;
+          float4 u = *(float4*)(sst + c), q = *(float4*)(sst + BN + c);
+          u.x += s1[j][0]; u.y += s1[j][1]; u.z += s1[j][2]; u.w += s1[j][3];
+          q.x += s2[j][0]; q.y += s2[j][1]; q.z += s2[j][2]; q.w += s2[j][3];
+          *(float4*)(sst + c) = u;
+          *(float4*)(sst + BN + c) = q;
+        }
+      }
+    }
+  };
+
+  for (int g = 0; g < total; ++g) {
+    const char* pb = smem + cbuf * BUF;
+    const char* wb = pb + P_BYTES;
+#pragma unroll
+    for (int p = 0; p < NPH; ++p) {
+      // phase -> (pixel half ih, cout half jh): NPH 4: (0,0) (0,1) (1,1) (1,0); NPH 2: (0,*) (1,*)
+      const int ih = NPH == 4 ? (p >> 1) : p;
+      const int jh = NPH == 4 ? (((p + 1) >> 1) & 1) : 0;
+      const bool new_b = NPH == 4 ? (p == 0 || p == 2) : true;
+      const bool new_a = NPH == 4 ? (HOLDB ? p < 2 : p != 2) : (p == 0);
+      const int fh = HOLDB ? jh : 0;  // register set of the phase's weight fragments
+      // ---- memory segment
+      if (p == 0 && ig + 1 < total) {
+        if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
+        ibuf = ibuf + 1 == NST ? 0 : ibuf + 1;
+        issue(iks, smem + ibuf * BUF);
+        ++ig;
+      }
+      if (new_a) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fa[fh][hf][j] = *(const bf16x8*)(wb + (wn * NJ + jh * 2 + j) * 2048 + rdoff[hf]);
+      }
+      if (new_b) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fb[hf][i] = *(const bf16x8*)(pb + (wm * 8 + ih * 4 + i) * 2048 + rdoff[hf]);
+      }
+      // The last memory segment of a K step drains its fragment reads (lgkmcnt(0)) before the barrier:
+      // the next DMA into this buffer follows that barrier (WAR). The other phases' reads stay in
+      // flight across the barrier and are waited for by the MFMAs that use them (the segment ends as
+      // soon as they are issued; their LDS latency overlaps the partner group's MFMA cluster).
+      if (p == NPH - 1 && g + 1 < total) {  // + this wave's DMA of stage g+1 has landed
+        if (ig > g + 1) vm_wait<DMA_OPS>();
+        else vm_wait<0>();
+      } else if (p == NPH - 1 || !RD_INFLIGHT) {
+        wait_lgkm0();
+      }
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- compute segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[jh * 2 + j][ih * 4 + i] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[fh][hf][j], fb[hf][i], acc[jh * 2 + j][ih * 4 + i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (p == NPH - 1 && ks + 1 == a.nks) epilogue();
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+    }
+    cbuf = cbuf + 1 == NST ? 0 : cbuf + 1;
+    if (++ks == a.nks) { ks = 0; ++t; }
+  }
+  if (wm == 0) raw_barrier();  // same barrier count for both groups
+  if (a.stats && total > 0 && (lane & 15) == 0) {
+    const int tn = (int)lid % a.tilesN;
+    float* row = a.stats + (size_t)(((int)lid / a.tilesN) * 2 + wm) * 2 * a.Cout;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cl = wn * WNT + j * 16 + 4 * (lane >> 4);
+      *(float4*)(row + tn * BN + cl) = *(const float4*)(sst + cl);
+      *(float4*)(row + a.Cout + tn * BN + cl) = *(const float4*)(sst + BN + cl);
+    }
+  }
+}
+
+template <int BN, bool RDF = false, bool HOLDB = false>
+static int launch_pp(ConvArgs a, hipStream_t s) {
+  constexpr int BM = 256;
+  constexpr int NST = BN == 256 ? 2 : 3;
+  if (a.packed || a.Cout % BN || a.Cy1 % 32) return -1;
+  const int tilesM = (a.M + BM - 1) / BM;
+  a.tilesN = a.Cout / BN;
+  a.ntiles = tilesM * a.tilesN;
+  a.ksplit = 1;
+  a.fixup = 0;
+  a.pool = nullptr;
+  a.up = nullptr;
+  const int grid = a.ntiles < 256 ? a.ntiles : 256;  // one block per CU, persistent
+  if (a.stats && grid % a.tilesN) return -1;
+  hipLaunchKernelGGL((conv_pp_kernel<BN, NST, RDF, HOLDB>), dim3(grid), dim3(512), 0, s, a);
+  return grid / a.tilesN * 2;
+}
+
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
                              void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                              int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
@@ -864,6 +1179,27 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
       return e ? atoi(e) : 0;
     }();
     per_cu = env_per_cu > 0 ? env_per_cu : 2;
+  }
+  // bm_pref 4 / 5: the ping-pong 256 x 256 / 256 x 128 kernel (conv_pp_kernel)
+  if (bm_pref == 4) return launch_pp<256>(a, s);
+  if (bm_pref == 5) return launch_pp<128>(a, s);
+  if (bm_pref == 7) return launch_pp<256, true>(a, s);
+  if (bm_pref == 8) return launch_pp<128, true>(a, s);
+  if (bm_pref == 9) return launch_pp<256, true, true>(a, s);
+  if (bm_pref == 10) return launch_pp<256, false, true>(a, s);
+  // auto: the ping-pong 256 x 256 kernel wherever its tile grid fills the chip (>= 256 tiles of 256
+  // pixels x 256 couts; fewer tiles leave CUs idle at one block per CU). RDP_CONV_PP=0 disables it
+  // (A/B knob). Measured (scripts/conv_microbench.py, bs 64, one MI355X): 64^2 256->256 903 -> 1082
+  // TF/s, 32^2 512->512 962 -> 1205, 32^2 512+512->256 927 -> 1120; its 256 x 128 form measured no
+  // faster than the 128 x 128 kernel and is not auto-selected.
+  if (bm_pref == 0 && !packed) {
+    static const int pp_env = [] {
+      const char* e = getenv("RDP_CONV_PP");
+      return e ? atoi(e) : 1;
+    }();
+    const long tiles256 = (long)(a.M + 255) / 256 * (Cout / 256);
+    if (pp_env && Cout % 256 == 0 && Cy1 % 32 == 0 && tiles256 >= 256 && escale == nullptr)
+      return launch_pp<256, true, true>(a, s);
   }
   const int max_blocks = 256 * per_cu;
   // bm_pref 2 / 3: 8-wave blocks (64 x 32 per wave; twice the waves per SIMD to hide the per-step

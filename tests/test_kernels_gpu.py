@@ -645,6 +645,51 @@ def test_conv_fwd_8wave_variant(C, N, H, W, C1, C2, Cout):
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [
+    (2, 32, 32, 256, 0, 256, 4), (3, 37, 29, 128, 0, 256, 4), (1, 24, 40, 128, 128, 256, 4),
+    (1, 24, 40, 128, 128, 256, 5), (20, 64, 64, 64, 0, 128, 5), (5, 64, 64, 256, 0, 512, 4),
+    (2, 16, 16, 512, 512, 1024, 4), (9, 32, 32, 64, 64, 128, 5)])
+def test_conv_pingpong_bitwise(C, N, H, W, C1, C2, Cout, pref):
+    """bm_pref 4 / 5: the ping-pong 256 x 256 / 256 x 128 kernel (one 8-wave block per CU, staggered
+    wave groups, 2-3 stage ring) accumulates in the same K order as the 128 x 128 kernel: outputs
+    bitwise equal, BN partial sums equal to rounding; covers persistent blocks walking several tiles
+    (320 / 640 tiles), a ragged last tile (M = 3219), the concat input and 1024 couts."""
+    torch.manual_seed(11)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    rows = C.conv_stats_rows(N * H * W, Cout, 0)
+    outs = []
+    prefs = (128,) + ((4, 7, 9, 10) if pref == 4 else (5, 8))  # schedule variants of the same kernel
+    for p in prefs:
+        y = torch.full((N, H, W, Cout), 7.0, dtype=torch.bfloat16, device=dev)
+        st = torch.zeros(rows * 2 * Cout, device=dev)
+        r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, st, p, None, 0)
+        assert 0 < r <= rows
+        outs.append((y, st[: r * 2 * Cout].view(r, 2, Cout).sum(0)))
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.conv2d(xin, w.float(), padding=1)
+    assert relerr(nchw(outs[1][0]), ref) < 1e-2
+    for y, s in outs[1:]:
+        assert torch.equal(outs[0][0], y)
+        assert torch.allclose(outs[0][1], s, rtol=1e-4, atol=1e-2)
+    # dgrad form: one input, output split at a concat boundary (y1 | y2)
+    if C2:
+        d1 = torch.zeros(N, H, W, C1, dtype=torch.bfloat16, device=dev)
+        d2 = torch.zeros(N, H, W, C2, dtype=torch.bfloat16, device=dev)
+        dy = bf(torch.randn(N, H, W, Cout, device=dev))
+        wt = bf(torch.randn(C1 + C2, Cout * 9, device=dev) / math.sqrt(9 * Cout))
+        e1, e2 = torch.empty_like(d1), torch.empty_like(d2)
+        C.conv_fwd(dy, None, wt, 9, 0, e1, e2, None, 128, None, 0)
+        for p in prefs[1:]:
+            d1.zero_()
+            d2.zero_()
+            C.conv_fwd(dy, None, wt, 9, 0, d1, d2, None, p, None, 0)
+            assert torch.equal(d1, e1) and torch.equal(d2, e2)
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 6, 64), (1, 4, 128), (3, 2, 192), (1, 10, 64)])
 def test_conv_ring_fwd_stats_eval_dgrad(C, N, H, W):
     """Row-ring kernel (64 -> 64, W % 64 == 0): forward + BN stats, eval BN fold + ReLU, and the
