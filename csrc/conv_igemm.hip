@@ -1188,18 +1188,24 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   if (bm_pref == 9) return launch_pp<256, true, true>(a, s);
   if (bm_pref == 10) return launch_pp<256, false, true>(a, s);
   // auto: the ping-pong 256 x 256 kernel wherever its tile grid fills the chip (>= 256 tiles of 256
-  // pixels x 256 couts; fewer tiles leave CUs idle at one block per CU). RDP_CONV_PP=0 disables it
-  // (A/B knob). Measured (scripts/conv_microbench.py, bs 64, one MI355X): 64^2 256->256 903 -> 1082
-  // TF/s, 32^2 512->512 962 -> 1205, 32^2 512+512->256 927 -> 1120; its 256 x 128 form measured no
-  // faster than the 128 x 128 kernel and is not auto-selected.
+  // pixels x 256 couts; fewer tiles leave CUs idle at one block per CU). Measured
+  // (scripts/conv_microbench.py, bs 64, one MI355X): 64^2 256->256 903 -> 1082 TF/s, 32^2 512->512
+  // 962 -> 1205, 32^2 512+512->256 927 -> 1120; bs 64 step 2973 -> 3150 img/s. The 256 x 128 form is
+  // 2-4 % faster than the 128 x 128 kernel where K >= 1152 (128^2 128->128 851 -> 889, 64^2
+  // 256+256->128 882 -> 907; slower at K = 576) and +1.0-1.4 % on the bs 64 step (3003 / 3042 ->
+  // 3045 / 3071 img/s, interleaved). RDP_CONV_PP = 0: off, 1: 256-wide only, 2 (default): both.
   if (bm_pref == 0 && !packed) {
     static const int pp_env = [] {
       const char* e = getenv("RDP_CONV_PP");
-      return e ? atoi(e) : 1;
+      return e ? atoi(e) : 2;
     }();
     const long tiles256 = (long)(a.M + 255) / 256 * (Cout / 256);
     if (pp_env && Cout % 256 == 0 && Cy1 % 32 == 0 && tiles256 >= 256 && escale == nullptr)
       return launch_pp<256, true, true>(a, s);
+    // 256 x 128 form (RDP_CONV_PP=2 A/B): only where K is long enough (>= 128 input channels)
+    const long tiles128 = (long)(a.M + 255) / 256 * (Cout / 128);
+    if (pp_env == 2 && Cout % 128 == 0 && Cy1 % 32 == 0 && tiles128 >= 256 && C1 + C2 >= 128 && escale == nullptr)
+      return launch_pp<128, true>(a, s);
   }
   const int max_blocks = 256 * per_cu;
   // bm_pref 2 / 3: 8-wave blocks (64 x 32 per wave; twice the waves per SIMD to hide the per-step

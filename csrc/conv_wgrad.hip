@@ -253,8 +253,25 @@ struct WgradHaloArgs {
 };
 
 // ABL (microbenchmark ablations only): 1 = no DMA after the prologue, 2 = no MFMA, 4 = no LDS reads
-template <int BN, int STAGES, bool MULTIROW, int ABL = 0>
+//
+// STAG (BN = 128, STAGES = 3): the two wave groups (waves 0-3 = couts 0..63, waves 4-7 = couts 64..127;
+// one wave of each per SIMD) run staggered by half a K step (one segment = one k half of the
+// step, 36 MFMAs, ended by a raw barrier), so one group's DMA wait and barrier overlap its SIMD
+// partner's MFMAs (cdna_hip_programming.md T3/T4 ping-pong). Ablations of the unstaggered kernel
+// (scripts/gpu_wg_abl.sh, 128^2 128->128 bs 64): 535 us full, 382 without the DMA, 381 without the
+// MFMAs, 344 with neither -- the DMA stream and the MFMA/LDS-read work each take ~70 % of the kernel
+// but barely overlap. Measured dead end: 11-13 % SLOWER than the unstaggered kernel (128^2 128->128
+// bs 64: 611 vs 539 us; 64^2 256->256: 582 vs 515) and -0.5..-0.7 % on the bs 64 step, so it is off
+// by default (RDP_WGRAD_STAG=1 / variant 7 for A/B; tests keep it bitwise equal). Schedule (segment (k, h) of group 0 runs in slot 2k + h, group 1 one slot later):
+//   * each wave's DMA segment is h = 1 (group 0) / h = 0 (group 1) -- both in slot 2k + 1: it issues
+//     step k + 2 into buffer (k + 2) % 3 (last read by group 1 in slot 2k) and, after its MFMAs, waits
+//     (counted vmcnt, step k + 2 left in flight) for its pieces of step k + 1, first read in slot
+//     2k + 2: 1.5 steps of lead instead of 1;
+//   * every segment's reads are consumed by its own MFMAs, so all LDS reads of a buffer are done
+//     before the barrier that precedes the next DMA into it.
+template <int BN, int STAGES, bool MULTIROW, int ABL = 0, bool STAG = false>
 __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradHaloArgs a) {
+  static_assert(!STAG || (BN == 128 && STAGES == 3), "staggered schedule: 8 waves, 3 stages");
   constexpr int NWV = BN / 16;
   constexpr int XREG = 72 * 128;                  // one staged input row region (72 pixel rows x 64 ch)
   constexpr int DSUB = 64 * 128;                  // one [64 px][64 cout] dY subtile
@@ -330,15 +347,32 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
 #pragma unroll
   for (int st = 0; st < STAGES - 1; ++st)
     if (st < nks) issue(st, smem + st * BUF);
-  for (int ks = 0; ks < nks; ++ks) {
-    if (STAGES == 3 && ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPIECES / NWV) : "memory");
+  // pieces this wave issues per stage (wave-uniform): PPW or PPW - 1
+  const bool full_w = wave < NPIECES - (PPW - 1) * NWV;
+  auto wait_one_stage_in_flight = [&]() {  // all but the newest stage's pieces of this wave landed
+    if (full_w) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW - 1) : "memory");
+  };
+  const int grp = STAG ? wave >> 2 : 0;
+  if constexpr (STAG) {
+    if (nks > 1) wait_one_stage_in_flight();
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (!(ABL & 1) && ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
+    if (grp == 1) raw_barrier();  // stagger by one segment
+  }
+  for (int ks = 0; ks < nks; ++ks) {
+    if constexpr (!STAG) {
+      if (STAGES == 3 && ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPIECES / NWV) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (!(ABL & 1) && ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
+    }
     const char* cur = smem + (ks % STAGES) * BUF;
     const char* db = cur + 3 * XREG + cg * DSUB;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
+      const bool dma_seg = STAG && hf == 1 - grp;
+      if (dma_seg && ks + 2 < nks) issue(ks + 2, smem + ((ks + 2) % 3) * BUF);
       const int p0 = 32 * hf + 8 * tg + tq;
       bf16x8 fb[4];
       {
@@ -393,7 +427,20 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
           }
         }
       }
+      if constexpr (STAG) {
+        if (dma_seg && ks + 1 < nks) {  // this wave's pieces of step ks + 1 have landed
+          if (ks + 2 < nks) wait_one_stage_in_flight();
+          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        } else {
+          wait_lgkm0();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        raw_barrier();
+      }
     }
+  }
+  if constexpr (STAG) {
+    if (grp == 0) raw_barrier();  // same barrier count for both groups
   }
 
   // acc[tap][i][r]: cin = cin0 + 16 cf + 4 (lane >> 4) + r, cout = cout0 + 64 cg + 16 i + (lane & 15)
@@ -686,8 +733,8 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   if (Cout % 64) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || dybytes >= (1l << 31)) return -1;
   // halo-reuse kernel: 3x3, whole 64-pixel row segments (variant 0 = auto, 5 = force)
-  const bool halo_ok = !packed && taps == 9 && (W % 64 == 0 || (W >= (variant == 5 ? 8 : 32) && 64 % W == 0 && (H * W) % 64 == 0));
-  if ((variant == 0 || variant == 5 || (variant >= 30 && variant < 40)) && halo_ok) {
+  const bool halo_ok = !packed && taps == 9 && (W % 64 == 0 || (W >= (variant == 5 || variant == 7 ? 8 : 32) && 64 % W == 0 && (H * W) % 64 == 0));
+  if ((variant == 0 || variant == 5 || variant == 7 || (variant >= 30 && variant < 40)) && halo_ok) {
     static const int env_blocks = [] {
       const char* e = getenv("RDP_WGRAD_HALO_BLOCKS");
       return e ? atoi(e) : 0;
@@ -755,7 +802,15 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
       const char* e = getenv("RDP_WGRAD_HALO_STAGES");  // 3 measured 3-8 % slower than 2
       return e ? atoi(e) : 2;
     }();
-    if (BN == 128 && mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, true>), dim3(nblk), dim3(512), 0, s, h);
+    static const int env_stag = [] {
+      const char* e = getenv("RDP_WGRAD_STAG");
+      return e ? atoi(e) : 0;
+    }();
+    const bool stag = variant == 7 || (variant == 0 && env_stag != 0);  // 7: force the staggered halo kernel
+    // (multi-row segments keep the unstaggered kernel: the staggered multi-row build spills)
+    if (BN == 128 && stag && !mr)
+      hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 3, false, 0, true>), dim3(nblk), dim3(512), 0, s, h);
+    else if (BN == 128 && mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, true>), dim3(nblk), dim3(512), 0, s, h);
     else if (BN == 128 && env_stages == 3)
       hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 3, false>), dim3(nblk), dim3(512), 0, s, h);
     else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, false>), dim3(nblk), dim3(512), 0, s, h);
@@ -765,7 +820,7 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     launch_wgrad_reduce(slab, out, h.splits, Cout, h.ncols, 9, a.Cin, a.Cin, accumulate, s);
     return h.splits;
   }
-  if (variant == 5) return -1;
+  if (variant == 5 || variant == 7) return -1;
   if (variant >= 10 && variant < 30 && halo_ok && W % 64 == 0) {  // ablation builds (microbenchmark)
     WgradHaloArgs h;
     h.x1 = a.x1; h.x2 = a.x2; h.xbytes1 = a.xbytes1; h.xbytes2 = a.xbytes2;

@@ -189,6 +189,32 @@ def test_conv_wgrad(C, N, H, W, C1, C2, Cout, splits):
     assert relerr(out, ref) < 2e-3
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [
+    (1, 6, 128, 64, 64, 128), (2, 9, 64, 256, 0, 256), (3, 16, 64, 128, 0, 128), (1, 2, 64, 64, 0, 128),
+    (8, 64, 64, 128, 128, 128)])
+def test_conv_wgrad_staggered_bitwise(C, N, H, W, C1, C2, Cout):
+    """variant 7: the halo wgrad with its two wave groups staggered by half a K step (3-stage ring) runs
+    the same MFMA sequence per accumulator as the unstaggered halo kernel (variant 5): the weight
+    gradient is bitwise equal; covers 1 and 2 K steps per block (prologue-only pipelines), long
+    split ranges and the concat input."""
+    torch.manual_seed(5)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    dy = bf(torch.randn(N, H, W, Cout, device=dev))
+    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, C1 + C2, Cout, 9, 0, 512), device=dev)
+    outs = []
+    for v in (5, 7):
+        out = torch.full((Cout * 9 * (C1 + C2),), 3.0, device=dev)
+        C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, 512, v)
+        outs.append(out)
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    w = torch.zeros(Cout, C1 + C2, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(xin, w, padding=1).backward(nchw(dy).float())
+    assert relerr(outs[1], w.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("N,H,W,splits", [(2, 18, 14, 5), (2, 64, 64, 300)])
 def test_conv_wgrad_packed(C, N, H, W, splits):
     torch.manual_seed(4)
