@@ -109,6 +109,18 @@ Act act(const torch::Tensor& t, const char* name) {
   return a;
 }
 
+// Images per launch so that every tensor of the launch stays below 2 GiB (the conv kernels' 32-bit
+// buffer offsets). RDP_CONV_CHUNK_BYTES (tests) lowers the bound to exercise the chunked path.
+int chunk_images(long bytes_per_image, int N) {
+  static const long lim = [] {
+    const char* e = getenv("RDP_CONV_CHUNK_BYTES");
+    const long v = e ? atol(e) : 0L;
+    return v > 0 ? v : (1L << 31) - 1;
+  }();
+  if (bytes_per_image <= 0 || bytes_per_image * N <= lim) return N > 0 ? N : 1;
+  return (int)std::max(1L, lim / bytes_per_image);
+}
+
 void check_f32(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), name,
               ": must be a contiguous fp32 GPU tensor");
@@ -132,7 +144,10 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
   // split-K reduce: up to 512 rows
   const long a = (M + 127) / 128 * 2, b = (M + 255) / 256 * 8;
   const long ab = a > b ? a : b;
-  return (int)(ab > 512 ? ab : 512);
+  // + room for batch-chunked launches (conv_fwd: tensors past 2 GiB run as image slices, each with
+  // its own 512-row floor and tile rounding): one chunk per 2 GiB of a 1024-channel bf16 tensor
+  const long chunks = 1 + M * 2048 / (1L << 31);
+  return (int)((ab > 512 ? ab : 512) + 520 * chunks);
 }
 
 // y = conv(cat(x1, x2), w); returns #M-tiles (stats rows)
@@ -184,23 +199,40 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     TORCH_CHECK(!pool && !y2 && !stats && uo.N == o1.N && uo.C == o1.C && up_oy >= 0 && up_ox >= 0 &&
                 2 * o1.H + up_oy <= uo.H && 2 * o1.W + up_ox <= uo.W, "up: eval conv, [N][>=2H][>=2W][Cout]");
   }
-  int pooled = 0;
-  const int r = rdp_conv_igemm(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
-                               a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1), o1.ptr,
-                               y2 ? o2.ptr : nullptr, o1.bytes, y2 ? o2.bytes : 0, o1.C, o1.pitch, y2 ? o2.pitch : 0,
-                               sp, a1.N, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu,
-                               ws ? ws->data_ptr<float>() : nullptr, ws ? (long)ws->numel() : 0L,
-                               pool ? po.ptr : nullptr, pool ? po.pitch : 0, (pool || up) ? &pooled : nullptr,
-                               up ? uo.ptr : nullptr, up ? uo.pitch : 0, up ? uo.H : 0, up ? uo.W : 0, up_oy, up_ox,
-                               cur_stream());
-  TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
-  if (pool && !pooled)
-    TORCH_CHECK(rdp_maxpool2_fwd(o1.ptr, o1.pitch, po.ptr, po.pitch, o1.N, o1.H, o1.W, o1.C, cur_stream()) == 0,
-                "conv_fwd: maxpool");
-  if (up && !pooled)
-    TORCH_CHECK(rdp_upsample2_fwd(o1.ptr, o1.pitch, uo.ptr, uo.pitch, o1.N, o1.H, o1.W, uo.H, uo.W, up_oy, up_ox, o1.C,
-                                  nullptr, cur_stream()) == 0, "conv_fwd: upsample");
-  return r;
+  // Batch chunks: the conv kernels address each tensor through ONE buffer descriptor with 32-bit
+  // offsets (< 2 GiB), so a batch whose largest tensor passes that (256^2 x 64 ch bf16 at N >= 256)
+  // runs as consecutive launches over image slices (convs never cross images); BN partial rows of
+  // the slices are appended, fused pool / upsample outputs sliced alike.
+  const long per_img = std::max(std::max((long)a1.H * a1.W * a1.pitch, x2 ? (long)a2.H * a2.W * a2.pitch : 0L),
+                                std::max((long)o1.H * o1.W * o1.pitch, y2 ? (long)o2.H * o2.W * o2.pitch : 0L)) * 2;
+  const int nc = chunk_images(per_img, a1.N);
+  const long avail_rows = stats ? stats->numel() / (2l * Cout) : 0;
+  int rows = 0;
+  for (int n0 = 0; n0 < a1.N; n0 += nc) {
+    const int nn = std::min(nc, a1.N - n0);
+    auto img = [&](const Act& t, int n) { return (void*)((char*)t.ptr + (long)n * t.H * t.W * t.pitch * 2); };
+    auto nbytes = [&](const Act& t) { return ((long)nn * t.H * t.W - 1) * t.pitch * 2 + (long)t.C * 2; };
+    float* spc = sp ? sp + (long)rows * 2 * Cout : nullptr;
+    if (sp) TORCH_CHECK(rows + conv_stats_rows((long)nn * a1.H * a1.W, Cout, bm_pref) <= avail_rows, "stats slab too small");
+    int pooled = 0;
+    const int r = rdp_conv_igemm(img(a1, n0), x2 ? img(a2, n0) : nullptr, nbytes(a1), x2 ? nbytes(a2) : 0, a1.C,
+                                 x2 ? a2.C : 0, a1.pitch, x2 ? a2.pitch : 0, w.data_ptr(), w.numel() * 2, w.size(1),
+                                 img(o1, n0), y2 ? img(o2, n0) : nullptr, nbytes(o1), y2 ? nbytes(o2) : 0, o1.C,
+                                 o1.pitch, y2 ? o2.pitch : 0, spc, nn, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh,
+                                 relu, ws ? ws->data_ptr<float>() : nullptr, ws ? (long)ws->numel() : 0L,
+                                 pool ? img(po, n0) : nullptr, pool ? po.pitch : 0, (pool || up) ? &pooled : nullptr,
+                                 up ? img(uo, n0) : nullptr, up ? uo.pitch : 0, up ? uo.H : 0, up ? uo.W : 0, up_oy,
+                                 up_ox, cur_stream());
+    TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", x2 ? a2.C : 0, ", Cout=", Cout, ")");
+    if (pool && !pooled)
+      TORCH_CHECK(rdp_maxpool2_fwd(img(o1, n0), o1.pitch, img(po, n0), po.pitch, nn, o1.H, o1.W, o1.C, cur_stream()) == 0,
+                  "conv_fwd: maxpool");
+    if (up && !pooled)
+      TORCH_CHECK(rdp_upsample2_fwd(img(o1, n0), o1.pitch, img(uo, n0), uo.pitch, nn, o1.H, o1.W, uo.H, uo.W, up_oy,
+                                    up_ox, o1.C, nullptr, cur_stream()) == 0, "conv_fwd: upsample");
+    rows += r;
+  }
+  return rows;
 }
 
 
@@ -214,11 +246,21 @@ int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor 
   check_f32(out, "out");
   const int Cin = packed ? cin_real : a1.C + (x2 ? a2.C : 0);
   TORCH_CHECK(out.numel() == (long)d.C * taps * Cin, "wgrad out numel mismatch");
-  const int r = rdp_conv_wgrad(a1.ptr, x2 ? a2.ptr : nullptr, a1.bytes, x2 ? a2.bytes : 0, a1.C, x2 ? a2.C : 0,
-                               a1.pitch, x2 ? a2.pitch : 0, d.ptr, d.bytes, d.pitch, slab.data_ptr<float>(),
-                               slab.numel(), out.data_ptr<float>(), accumulate, a1.N, a1.H, a1.W, d.C, taps, packed,
-                               cin_real, splits, variant, cur_stream());
-  TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
+  // batch chunks below the 2 GiB buffer-offset reach (see conv_fwd), accumulated into out
+  const long per_img = std::max(std::max((long)a1.H * a1.W * a1.pitch, x2 ? (long)a2.H * a2.W * a2.pitch : 0L),
+                                (long)d.H * d.W * d.pitch) * 2;
+  const int nc = chunk_images(per_img, a1.N);
+  int r = 0;
+  for (int n0 = 0; n0 < a1.N; n0 += nc) {
+    const int nn = std::min(nc, a1.N - n0);
+    auto img = [&](const Act& t) { return (void*)((char*)t.ptr + (long)n0 * t.H * t.W * t.pitch * 2); };
+    auto nbytes = [&](const Act& t) { return ((long)nn * t.H * t.W - 1) * t.pitch * 2 + (long)t.C * 2; };
+    r = rdp_conv_wgrad(img(a1), x2 ? img(a2) : nullptr, nbytes(a1), x2 ? nbytes(a2) : 0, a1.C, x2 ? a2.C : 0, a1.pitch,
+                       x2 ? a2.pitch : 0, img(d), nbytes(d), d.pitch, slab.data_ptr<float>(), slab.numel(),
+                       out.data_ptr<float>(), n0 > 0 ? 1 : accumulate, nn, a1.H, a1.W, d.C, taps, packed, cin_real,
+                       splits, variant, cur_stream());
+    TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
+  }
   return r;
 }
 
@@ -273,6 +315,9 @@ int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch:
   TORCH_CHECK(coef.numel() >= 4l * o.C, "coef must hold 4*C floats");
   // ring grid <= 256 blocks x 4 pixel groups (64 couts) or 2 (128): <= 1024 rows of 2*C
   TORCH_CHECK(partial.numel() >= 1024l * 2 * o.C, "partial too small");
+  // batches past the 2 GiB buffer-offset reach: the caller's chunked conv_fwd + bn_relu_bwd_reduce
+  const long per_img = std::max(std::max((long)a.H * a.W * a.pitch, (long)o.H * o.W * o.pitch), (long)b.H * b.W * b.pitch) * 2;
+  if (chunk_images(per_img, a.N) < a.N) return -1;
   return rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                           o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
                           0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), cur_stream());

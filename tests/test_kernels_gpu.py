@@ -671,6 +671,25 @@ def test_conv_fwd_8wave_variant(C, N, H, W, C1, C2, Cout):
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout,pref", [(4, 32, 32, 512, 1024, 4), (3, 20, 52, 256, 512, 5),
+                                                  (16, 64, 64, 64, 256, 0)])
+def test_conv_pingpong_1x1(C, N, H, W, Cin, Cout, pref):
+    """The ping-pong kernel on 1x1 GEMMs (the transposed decoder's ConvTranspose2d as taps=1, dgrad of
+    it too): bitwise equal to the 128 x 128 kernel; pref 0 = auto (>= 256 tiles of 256 x 256)."""
+    torch.manual_seed(12)
+    dev = "cuda"
+    x = bf(torch.randn(N, H, W, Cin, device=dev))
+    w = bf(torch.randn(Cout, Cin, device=dev) / math.sqrt(Cin))
+    ys = []
+    for p in (128, pref):
+        y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+        C.conv_fwd(x, None, w, 1, 0, y, None, None, p, None, 0)
+        ys.append(y)
+    ref = torch.einsum("nhwc,oc->nhwo", x.float(), w.float())
+    assert relerr(ys[1], ref) < 1e-2
+    assert torch.equal(ys[0], ys[1])
+
+
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [
     (2, 32, 32, 256, 0, 256, 4), (3, 37, 29, 128, 0, 256, 4), (1, 24, 40, 128, 128, 256, 4),
     (1, 24, 40, 128, 128, 256, 5), (20, 64, 64, 64, 0, 128, 5), (5, 64, 64, 256, 0, 512, 4),
@@ -925,3 +944,45 @@ def test_head_bn_fused(C, dice_w):
         got = bp2.view(nb, 2, Ch).double().sum(0)
         ref = bp.view(nb, 2, Ch).double().sum(0)
         assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_conv_batch_chunks_subprocess():
+    """Batches past the kernels' 2 GiB buffer-offset reach run as image slices (conv_fwd appends the BN
+    partial rows, conv_wgrad accumulates, conv_dgrad_bnred defers to the chunked fallback). The bound
+    is lowered with RDP_CONV_CHUNK_BYTES (read once per process) in a child process so the chunked
+    path runs on small tensors; results must match the unchunked launches of this process."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import math, sys, torch
+sys.path.insert(0, sys.argv[1])
+from robotic_discovery_platform_amd.ops import native
+C = native()
+torch.manual_seed(21)
+dev = "cuda"
+bf = lambda t: t.to(torch.bfloat16)
+N, H, W = 5, 64, 64
+x1 = bf(torch.randn(N, H, W, 64, device=dev)); x2 = bf(torch.randn(N, H, W, 64, device=dev))
+w = bf(torch.randn(128, 9 * 128, device=dev) / 34.0)
+y = torch.empty(N, H, W, 128, dtype=torch.bfloat16, device=dev)
+rows = 8 * C.conv_stats_rows(N * H * W, 128, 0)  # 5 chunked launches: 5 x the per-launch floor
+st = torch.zeros(rows * 2 * 128, device=dev)
+r = C.conv_fwd(x1, x2, w, 9, 0, y, None, st, 0, None, 0)
+dy = bf(torch.randn(N, H, W, 128, device=dev))
+slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 128, 128, 9, 0, 64), device=dev)
+out = torch.zeros(128 * 9 * 128, device=dev)
+C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, 64, 0)
+torch.save({"y": y.cpu(), "s": st[: r * 256].view(r, 2, 128).sum(0).cpu(), "g": out.cpu()}, sys.argv[2])
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for lim in ("0", str(2 * 64 * 64 * 128 * 2 - 1)):  # unchunked / 1 image per launch (5 launches)
+        path = os.path.join("/tmp", f"rdp_chunk_{lim}_{os.getpid()}.pt")
+        env = dict(os.environ, RDP_CONV_CHUNK_BYTES=lim, RDP_NO_BUILD="1")
+        subprocess.run([sys.executable, "-c", code, root, path], check=True, env=env, timeout=240)
+        outs.append(torch.load(path, weights_only=True))
+        os.unlink(path)
+    assert torch.equal(outs[0]["y"], outs[1]["y"])
+    assert torch.allclose(outs[0]["s"], outs[1]["s"], rtol=1e-4, atol=1e-2)
+    assert relerr(outs[1]["g"], outs[0]["g"]) < 1e-5
