@@ -467,22 +467,29 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
 // HOLDB: both cout halves of the weight fragments stay in registers (no re-read in phase 3).
 template <int BN, int NST, bool RD_INFLIGHT, bool HOLDB>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
-  constexpr int BM = 256;
-  constexpr int WNT = BN / 4;           // couts per wave (64 / 32)
-  constexpr int NJ = WNT / 16;          // cout fragments per wave (4 / 2)
-  constexpr int NPH = NJ == 4 ? 4 : 2;  // phases per K step, 16 MFMAs each
+  // BN = 256 / 128: 256-pixel tile, wave (wm, wn) = 128 pixels x BN/4 couts. BN = 64: 512-pixel tile,
+  // wave (wm, wn) = 64 pixels (rows wm * 256 + wn * 64) x all 64 couts.
+  constexpr bool C64 = BN == 64;
+  constexpr int BM = C64 ? 512 : 256;
+  constexpr int WNT = C64 ? 64 : BN / 4;  // couts per wave
+  constexpr int NJ = WNT / 16;            // cout fragments per wave (4 / 2 / 4)
+  constexpr int NI = C64 ? 4 : 8;         // pixel fragments per wave
+  constexpr int NPH = (NJ / 2) * (NI / 4);  // phases per K step, 16 MFMAs each (4 / 2 / 2)
   constexpr int P_BYTES = BM * 128, W_BYTES = BN * 128, BUF = P_BYTES + W_BYTES;
-  constexpr int NROW = 4;            // 8-row pixel DMA pieces per wave per stage (256 / 8 / 8)
+  constexpr int NROW = BM / 64;      // 8-row pixel DMA pieces per wave per stage
   constexpr int WPIECES = BN / 64;   // weight DMA pieces per wave per stage
   constexpr int DMA_OPS = NROW + WPIECES;
-  constexpr int ST_OFF = NST * BUF;  // BN statistics: [wm][2][BN] fp32
-  static_assert(NST * BUF + 2 * 2 * BN * 4 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NST * BUF + 2 * 2 * BN * 4];
+  constexpr int SROWS = C64 ? 8 : 2;  // statistics rows per block (one per wave / per wave row)
+  constexpr int ST_OFF = NST * BUF;   // BN statistics: [SROWS][2][BN] fp32
+  static_assert(NST * BUF + SROWS * 2 * BN * 4 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NST * BUF + SROWS * 2 * BN * 4];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int gch = (lane & 7) ^ (lane >> 3);
+  const int wpx = C64 ? wm * 256 + wn * 64 : wm * 128;  // first pixel row of this wave in the tile
+  const int wco = C64 ? 0 : wn * WNT;                   // first cout of this wave in the tile
 
   const uint32_t G = gridDim.x;
   const uint32_t lid = xcd_remap(blockIdx.x, G);
@@ -552,21 +559,22 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) rdoff[hf] = (lane & 15) * 128 + 16 * (((lane >> 4) + 4 * hf) ^ (lane & 7));
 
-  float* const sst = (float*)(smem + ST_OFF) + wm * 2 * BN;  // this wave row's statistics words
+  const int srow = C64 ? wave : wm;
+  float* const sst = (float*)(smem + ST_OFF) + srow * 2 * BN;  // this wave (row)'s statistics words
   if (a.stats && (lane & 15) == 0) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int c = wn * WNT + j * 16 + 4 * (lane >> 4);
+      const int c = wco + j * 16 + 4 * (lane >> 4);
       *(float4*)(sst + c) = make_float4(0.f, 0.f, 0.f, 0.f);
       *(float4*)(sst + BN + c) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 
-  f32x4 acc[NJ][8];
+  f32x4 acc[NJ][NI];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   // [cout half held][k half][cout frag of the phase] / [k half][pixel frag of the phase]
   bf16x8 fa[HOLDB ? 2 : 1][2][2], fb[2][4];
 
@@ -601,14 +609,14 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
       for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
 #pragma unroll
     for (int jp = 0; jp < NJ; jp += 2) {
-      const int nb = n0 + wn * WNT + jp * 16;
+      const int nb = n0 + wco + jp * 16;
       const int n = nb + coff;
       const bool d2 = nb >= a.Cy1;  // wave-uniform: Cy1 % 32 == 0 (host-checked), one SRD per store
       const int nn = d2 ? n - a.Cy1 : n;
       const int yp = d2 ? a.ypitch2 : a.ypitch1;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+      for (int i = 0; i < NI; ++i) {
+        const int m = m0 + wpx + i * 16 + (lane & 15);
         uint2 v[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -652,7 +660,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
       if ((lane & 15) == 0) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const int c = wn * WNT + j * 16 + 4 * gq;
+          const int c = wco + j * 16 + 4 * gq;
           float4 u = *(float4*)(sst + c), q = *(float4*)(sst + BN + c);
           u.x += s1[j][0]; u.y += s1[j][1]; u.z += s1[j][2]; u.w += s1[j][3];
           q.x += s2[j][0]; q.y += s2[j][1]; q.z += s2[j][2]; q.w += s2[j][3];
@@ -668,11 +676,12 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
     const char* wb = pb + P_BYTES;
 #pragma unroll
     for (int p = 0; p < NPH; ++p) {
-      // phase -> (pixel half ih, cout half jh): NPH 4: (0,0) (0,1) (1,1) (1,0); NPH 2: (0,*) (1,*)
-      const int ih = NPH == 4 ? (p >> 1) : p;
-      const int jh = NPH == 4 ? (((p + 1) >> 1) & 1) : 0;
-      const bool new_b = NPH == 4 ? (p == 0 || p == 2) : true;
-      const bool new_a = NPH == 4 ? (HOLDB ? p < 2 : p != 2) : (p == 0);
+      // phase -> (pixel half ih, cout half jh): BN 256: (0,0) (0,1) (1,1) (1,0); BN 128: (0,*) (1,*);
+      // BN 64 (4 pixel fragments per wave): (*,0) (*,1)
+      const int ih = C64 ? 0 : (NPH == 4 ? (p >> 1) : p);
+      const int jh = C64 ? p : (NPH == 4 ? (((p + 1) >> 1) & 1) : 0);
+      const bool new_b = C64 ? p == 0 : (NPH == 4 ? (p == 0 || p == 2) : true);
+      const bool new_a = C64 ? (HOLDB ? true : true) : (NPH == 4 ? (HOLDB ? p < 2 : p != 2) : (p == 0));
       const int fh = HOLDB ? jh : 0;  // register set of the phase's weight fragments
       // ---- memory segment
       if (p == 0 && ig + 1 < total) {
@@ -685,13 +694,13 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) fa[fh][hf][j] = *(const bf16x8*)(wb + (wn * NJ + jh * 2 + j) * 2048 + rdoff[hf]);
+          for (int j = 0; j < 2; ++j) fa[fh][hf][j] = *(const bf16x8*)(wb + (wco / 16 + jh * 2 + j) * 2048 + rdoff[hf]);
       }
       if (new_b) {
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) fb[hf][i] = *(const bf16x8*)(pb + (wm * 8 + ih * 4 + i) * 2048 + rdoff[hf]);
+          for (int i = 0; i < 4; ++i) fb[hf][i] = *(const bf16x8*)(pb + (wpx / 16 + ih * 4 + i) * 2048 + rdoff[hf]);
       }
       // The last memory segment of a K step drains its fragment reads (lgkmcnt(0)) before the barrier:
       // the next DMA into this buffer follows that barrier (WAR). The other phases' reads stay in
@@ -726,10 +735,10 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   if (wm == 0) raw_barrier();  // same barrier count for both groups
   if (a.stats && total > 0 && (lane & 15) == 0) {
     const int tn = (int)lid % a.tilesN;
-    float* row = a.stats + (size_t)(((int)lid / a.tilesN) * 2 + wm) * 2 * a.Cout;
+    float* row = a.stats + (size_t)(((int)lid / a.tilesN) * SROWS + srow) * 2 * a.Cout;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int cl = wn * WNT + j * 16 + 4 * (lane >> 4);
+      const int cl = wco + j * 16 + 4 * (lane >> 4);
       *(float4*)(row + tn * BN + cl) = *(const float4*)(sst + cl);
       *(float4*)(row + a.Cout + tn * BN + cl) = *(const float4*)(sst + BN + cl);
     }
@@ -738,8 +747,8 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 
 template <int BN, bool RDF = false, bool HOLDB = false>
 static int launch_pp(ConvArgs a, hipStream_t s) {
-  constexpr int BM = 256;
-  constexpr int NST = BN == 256 ? 2 : 3;
+  constexpr int BM = BN == 64 ? 512 : 256;
+  constexpr int NST = BN == 128 ? 3 : 2;
   if (a.packed || a.Cout % BN || a.Cy1 % 32) return -1;
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
@@ -751,7 +760,7 @@ static int launch_pp(ConvArgs a, hipStream_t s) {
   const int grid = a.ntiles < 256 ? a.ntiles : 256;  // one block per CU, persistent
   if (a.stats && grid % a.tilesN) return -1;
   hipLaunchKernelGGL((conv_pp_kernel<BN, NST, RDF, HOLDB>), dim3(grid), dim3(512), 0, s, a);
-  return grid / a.tilesN * 2;
+  return grid / a.tilesN * (BN == 64 ? 8 : 2);
 }
 
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
@@ -1187,6 +1196,11 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   if (bm_pref == 8) return launch_pp<128, true>(a, s);
   if (bm_pref == 9) return launch_pp<256, true, true>(a, s);
   if (bm_pref == 10) return launch_pp<256, false, true>(a, s);
+  // 512 x 64 form (11 / 12): measured dead end -- the 64-cout layers are LDS-fill bound (58 FLOP per
+  // staged byte vs 128 at 256 x 256): 256^2 64+64->64 bs 64 661-691 TF/s vs 721 for the 256 x 64
+  // kernel, 128^2 128->64 652-667 vs 723; those layers keep the ring / halo / 256 x 64 kernels.
+  if (bm_pref == 11) return launch_pp<64, true, true>(a, s);
+  if (bm_pref == 12) return launch_pp<64, true, false>(a, s);
   // auto: the ping-pong 256 x 256 kernel wherever its tile grid fills the chip (>= 256 tiles of 256
   // pixels x 256 couts; fewer tiles leave CUs idle at one block per CU). Measured
   // (scripts/conv_microbench.py, bs 64, one MI355X): 64^2 256->256 903 -> 1082 TF/s, 32^2 512->512

@@ -362,7 +362,9 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
   }
   for (int ks = 0; ks < nks; ++ks) {
     if constexpr (!STAG) {
-      if (STAGES == 3 && ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPIECES / NWV) : "memory");
+      // 3 stages: leave THIS wave's pieces of step ks + 1 in flight (waves issue PPW or PPW - 1 pieces;
+      // a uniform NPIECES / NWV count made the PPW-piece waves wait for one piece of the next stage)
+      if (STAGES == 3 && ks + 1 < nks) wait_one_stage_in_flight();
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       raw_barrier();
       if (!(ABL & 1) && ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);

@@ -693,9 +693,10 @@ def test_conv_pingpong_1x1(C, N, H, W, Cin, Cout, pref):
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [
     (2, 32, 32, 256, 0, 256, 4), (3, 37, 29, 128, 0, 256, 4), (1, 24, 40, 128, 128, 256, 4),
     (1, 24, 40, 128, 128, 256, 5), (20, 64, 64, 64, 0, 128, 5), (5, 64, 64, 256, 0, 512, 4),
-    (2, 16, 16, 512, 512, 1024, 4), (9, 32, 32, 64, 64, 128, 5)])
+    (2, 16, 16, 512, 512, 1024, 4), (9, 32, 32, 64, 64, 128, 5), (1, 24, 40, 64, 64, 64, 11),
+    (20, 64, 64, 128, 0, 64, 11), (3, 37, 29, 64, 0, 64, 11), (2, 32, 32, 128, 128, 128, 11)])
 def test_conv_pingpong_bitwise(C, N, H, W, C1, C2, Cout, pref):
-    """bm_pref 4 / 5: the ping-pong 256 x 256 / 256 x 128 kernel (one 8-wave block per CU, staggered
+    """bm_pref 4 / 5 / 11: the ping-pong 256 x 256 / 256 x 128 / 512 x 64 kernel (one 8-wave block per CU, staggered
     wave groups, 2-3 stage ring) accumulates in the same K order as the 128 x 128 kernel: outputs
     bitwise equal, BN partial sums equal to rounding; covers persistent blocks walking several tiles
     (320 / 640 tiles), a ragged last tile (M = 3219), the concat input and 1024 couts."""
@@ -707,7 +708,7 @@ def test_conv_pingpong_bitwise(C, N, H, W, C1, C2, Cout, pref):
     wk = ohwi(w).contiguous()
     rows = C.conv_stats_rows(N * H * W, Cout, 0)
     outs = []
-    prefs = (128,) + ((4, 7, 9, 10) if pref == 4 else (5, 8))  # schedule variants of the same kernel
+    prefs = (128,) + {4: (4, 7, 9, 10), 5: (5, 8), 11: (11, 12)}[pref]  # schedule variants of the same kernel
     for p in prefs:
         y = torch.full((N, H, W, Cout), 7.0, dtype=torch.bfloat16, device=dev)
         st = torch.zeros(rows * 2 * Cout, device=dev)
