@@ -12,6 +12,7 @@
 //   kind 1: packed first layer  Wp[cout][16][8] (taps 0..8, channels 0..cin-1, zeros elsewhere)
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, u16* __restrict__ shadow, long n, float lr, float b1, float b2,
@@ -129,7 +130,14 @@ int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* s
     if (step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
     return 0;
   }
-  hipLaunchKernelGGL(wprep_kernel, dim3(128, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, step);
+  // blocks per segment: the largest layer (512 x 1024 x 9) has 1152 64x64 tiles; at 128 blocks per
+  // segment every block of it walked 9 tiles back to back (latency-bound: 68 us per step, a fixed
+  // cost at every batch size). Blocks of smaller segments past their tile count exit at once.
+  static const int gx = [] {
+    const char* e = getenv("RDP_WPREP_GRID");
+    return e ? std::max(1, atoi(e)) : 1152;
+  }();
+  hipLaunchKernelGGL(wprep_kernel, dim3(gx, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, step);
   return 0;
 }
 int rdp_wseg_size() { return (int)sizeof(WSeg); }
