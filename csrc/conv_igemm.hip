@@ -772,6 +772,9 @@ extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, 
                                   const float* escale, const float* eshift, int erelu, void* pool, int ppitch,
                                   hipStream_t s);
 extern "C" int rdp_conv_halo_tiles(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed);
+extern "C" int rdp_conv_first(const void* x, long xbytes, int pitch, const void* w, long wbytes, void* y, long ybytes,
+                              int ypitch, float* stats, int N, int H, int W, const float* escale, const float* eshift,
+                              int erelu, hipStream_t s);
 extern "C" int rdp_conv_halo(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
                              int pitch2, const void* w, long wbytes, int ldw, void* y1, void* y2, long ybytes1,
                              long ybytes2, int Cy1, int ypitch1, int ypitch2, float* stats, int N, int H, int W,
@@ -1092,6 +1095,21 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // (uoy, uox), fused the same way; *pooled = 1 if the fused output was written (else the caller
   // launches the pool / upsample)
   if (pooled) *pooled = 0;
+  // first layer (3-channel input, packed K): conv_first.hip (auto, or bm_pref 13 = force;
+  // RDP_CONV_FIRST=0: this file's packed implicit GEMM, for A/B)
+  {
+    static const int first_env = [] {
+      const char* e = getenv("RDP_CONV_FIRST");
+      return e ? atoi(e) : 1;
+    }();
+    const int pref = bm_pref % 1000;
+    if (packed && (pref == 13 || (pref == 0 && first_env)) && C1 == 8 && C2 == 0 && x2 == nullptr && taps == 9 &&
+        Cout == 64 && y2 == nullptr) {
+      const int r = rdp_conv_first(x1, xbytes1, pitch1, w, wbytes, y1, ybytes1, ypitch1, stats, N, H, W, escale, eshift,
+                                   erelu, s);
+      if (r >= 0 || pref == 13) return r;
+    }
+  }
   // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 6 = force the row-ring kernel,
   // 128 / 256 (2 / 3: 8-wave) = force this kernel's tile
   {

@@ -147,6 +147,43 @@ def test_conv_packed_first_layer(C):
     assert relerr(nchw(y), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 20, 12), (3, 256, 256), (1, 7, 9), (5, 64, 96)])
+def test_conv_first_layer_kernel(C, N, H, W):
+    """conv_first.hip (bm_pref 13; auto for the packed 3-channel layer) vs the packed implicit GEMM
+    (bm_pref 256) and fp32 torch: training output + BN partial sums, eval BN fold + ReLU; ragged last
+    segment (M % 64 != 0) and image borders."""
+    torch.manual_seed(13)
+    dev = "cuda"
+    Cout = 64
+    x = torch.rand(N, 3, H, W, device=dev)
+    x8 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device=dev)
+    x8[..., :3] = bf(nhwc(x))
+    w = bf(torch.randn(Cout, 3, 3, 3, device=dev) * 0.3)
+    wp = torch.zeros(Cout, 16, 8, dtype=torch.bfloat16, device=dev)
+    wp[:, :9, :3] = w.permute(0, 2, 3, 1).reshape(Cout, 9, 3)
+    wk = wp.view(Cout, 128)
+    rows = C.conv_stats_rows(N * H * W, Cout, 0)
+    ys, ss = [], []
+    for pref in (256, 13):
+        y = torch.full((N, H, W, Cout), 5.0, dtype=torch.bfloat16, device=dev)
+        st = torch.zeros(rows * 2 * Cout, device=dev)
+        r = C.conv_fwd(x8, None, wk, 9, 1, y, None, st, pref, None, 0)
+        assert 0 < r <= rows
+        ys.append(y)
+        ss.append(st[: r * 2 * Cout].view(r, 2, Cout).sum(0))
+    ref = F.conv2d(nchw(x8[..., :3]).float(), w.float(), padding=1)
+    assert relerr(nchw(ys[1]), ref) < 1e-2
+    assert relerr(ys[1], ys[0]) < 1e-2
+    yq = nchw(ys[1]).float()
+    assert torch.allclose(ss[1][0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(ss[1][1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    coef = torch.randn(4 * Cout, device=dev)
+    a = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x8, None, wk, 9, 1, a, None, None, 13, coef, 1)
+    sc, sh = coef[2 * Cout:3 * Cout].view(1, -1, 1, 1), coef[3 * Cout:].view(1, -1, 1, 1)
+    assert relerr(nchw(a), torch.relu(ref * sc + sh)) < 1e-2
+
+
 def test_conv_dgrad_split_output(C):
     """dgrad = conv(dy, flip(W)^T) written into two destinations (the Up-block concat split)."""
     torch.manual_seed(2)
