@@ -302,6 +302,12 @@ class _Layer:
     bwd_rows: int = 0  # BN-backward partial rows already produced by a fused producer of da
 
 
+def _stream_wait(waiter: "torch.cuda.Stream", waitee: "torch.cuda.Stream"):
+    """``waiter.wait_stream(waitee)`` through the native runtime, so that a launch plan being recorded
+    (NativeTrainer plan mode, csrc/bindings.cpp) also holds the cross-stream dependency."""
+    _native().stream_wait(waiter.cuda_stream, waitee.cuda_stream)
+
+
 class UNetExecutor:
     """Static-shape forward/backward/step program for one (batch, H, W)."""
 
@@ -771,7 +777,7 @@ class UNetExecutor:
         """Make the first side stream wait for the others (before a DDP bucket hook: the bucket's
         all-reduce must see every wgrad issued so far, whichever side stream ran it)."""
         for st in self.sides[1:]:
-            self.side.wait_stream(st)
+            _stream_wait(self.side, st)
 
     def _on_wgrad_stream(self, fn):
         """Run ``fn(slab)`` (a weight gradient) on the next side stream with that stream's slab."""
@@ -780,7 +786,7 @@ class UNetExecutor:
         k = self._side_rr % len(self.sides)
         self._side_rr += 1
         st = self.sides[k]
-        st.wait_stream(torch.cuda.current_stream())
+        _stream_wait(st, torch.cuda.current_stream())
         with torch.cuda.stream(st):
             return fn(self.slabs[k])
 
@@ -789,7 +795,7 @@ class UNetExecutor:
         (fork); without a side stream it runs inline."""
         if self.side is None:
             return fn()
-        self.side.wait_stream(torch.cuda.current_stream())
+        _stream_wait(self.side, torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
             return fn()
 
@@ -831,7 +837,7 @@ class UNetExecutor:
         finally:
             if main is not None:
                 for side in self.sides:
-                    main.wait_stream(side)  # join
+                    _stream_wait(main, side)  # join
 
     def _backward(self, C, D, st, grad_hook, gscale):
         head_w = st.view("outc.conv.weight").reshape(-1)

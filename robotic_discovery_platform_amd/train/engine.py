@@ -18,6 +18,20 @@ With world > 1 the bucketed all-reduces overlap backward on RCCL's stream.
 ``RDP_MAIN_PRIO=1`` runs the step on a high-priority stream (side stream at normal priority);
 measured neutral at bs 64 (2710 vs 2715 img/s), so off by default.
 
+Plan mode (``plan=True``; "auto" = on for single-process training without a graph): the third step
+is recorded by the native runtime (``csrc/bindings.cpp``: every kernel launch and cross-stream wait of
+the step, with its validated raw arguments and stream) and every later step is ONE ``plan_replay``
+call that re-issues the same launches on the same two streams from C++. The executor's Python
+(~8 us of host time per launch) then runs once instead of every step; at small batch the host no
+longer falls behind the GPU. Requirements, all true of the training step: static buffers, no
+host-side decisions that change between steps, a constant learning rate and the same current stream
+at every call. ``RDP_PLAN=0`` disables it. Measured (one MI355X, interleaved): host enqueue per bs-4
+step 1.55 -> 1.37 ms, step time unchanged (bs 4 2.53 ms, bs 64 20.1 ms either way) -- the remaining
+host cost is HIP's own ~7 us per kernel launch, which the GPU still outruns only in runs of
+sub-10-us kernels. ``RDP_PLAN_GRAPH=1`` additionally compiles each single-stream run of the plan into
+a hipGraph (``plan_compile``; bitwise equal, tests/test_unet_native_gpu.py): measured SLOWER (bs 4
+2.53 -> 2.68 ms, bs 64 20.3 -> 20.5 ms), so off by default.
+
 ``EagerTrainer`` is the reference execution model (torch autograd + MIOpen) used for the CPU path,
 CPU/gloo DDP tests and as the measured comparison baseline.
 """
@@ -43,7 +57,7 @@ class NativeTrainer:
 
     def __init__(self, model: UNetNative, batch: int, h: int, w: int, lr: float = 1e-4, loss: str = "bce",
                  dice_weight: float = 1.0, graph="auto", bucket_mb: float = 16.0, sync_bn: bool = False,
-                 grad_comm: Optional[str] = None, ddp_force: Optional[bool] = None):
+                 grad_comm: Optional[str] = None, ddp_force: Optional[bool] = None, plan="auto"):
         self.model = model
         self.ex = model.executor(batch, h, w, training=True, loss=loss, dice_weight=dice_weight)
         self.opt = NativeAdam(model, lr=lr)
@@ -79,7 +93,23 @@ class NativeTrainer:
             lo, hi = torch.cuda.Stream.priority_range()
             if hi != lo:
                 self.stream = torch.cuda.Stream(device=model.store.device, priority=hi)
+        if plan == "auto":
+            plan = os.environ.get("RDP_PLAN", "1") != "0"
+        self.use_plan = (bool(plan) and not self.ddp and not self.use_graph and self.stream is None
+                         and torch.cuda.is_available() and model.store.device.type == "cuda")
+        self.plan_id: Optional[int] = None
+        # RDP_PLAN_GRAPH=1: replay each single-stream run of launches of the plan as one hipGraph
+        self._plan_stream = (torch.cuda.Stream(device=model.store.device)
+                             if self.use_plan and os.environ.get("RDP_PLAN_GRAPH", "0") != "0" else None)
         self.steps = 0
+
+    def __del__(self):
+        if getattr(self, "plan_id", None) is not None:
+            try:
+                from ..ops import native
+                native(build_if_missing=False).plan_free(self.plan_id)
+            except Exception:  # interpreter teardown
+                pass
 
     def _hook(self, spec):
         self.bucketer.mark_ready(self._layer_params[spec.name])
@@ -107,6 +137,35 @@ class NativeTrainer:
 
     def step(self) -> torch.Tensor:
         """One training step on the current input buffers; returns the (device) loss tensor."""
+        if self.use_plan:
+            from ..ops import native
+            C = native(build_if_missing=False)
+            cur = torch.cuda.current_stream()
+            ps = self._plan_stream
+            if ps is not None:  # graph-compiled plans run on an owned stream (the null stream cannot be captured)
+                C.stream_wait(ps.cuda_stream, cur.cuda_stream)
+                ctx = torch.cuda.stream(ps)
+            else:
+                ctx = contextlib.nullcontext()
+            with ctx:
+                if self.plan_id is not None:
+                    C.plan_replay(self.plan_id)
+                elif self.steps < 2:  # first steps eagerly (first-launch costs, flags that settle)
+                    self._step_body()
+                else:
+                    C.plan_begin()
+                    try:
+                        self._step_body()
+                    except BaseException:
+                        C.plan_abort()
+                        raise
+                    self.plan_id = C.plan_end()
+                    if ps is not None:
+                        C.plan_compile(self.plan_id)
+            if ps is not None:
+                C.stream_wait(cur.cuda_stream, ps.cuda_stream)
+            self.steps += 1
+            return self.ex.loss
         if self.use_graph:
             if self.graph is None:
                 if self.steps < 2:  # warm up eagerly (allocator, first-launch costs) before capture

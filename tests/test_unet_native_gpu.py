@@ -108,3 +108,43 @@ def test_native_training_reduces_loss_and_graph_replay_matches():
         assert ls[-1] < ls[0] * 0.8, ls
     # eager and graph-replayed training are the same program
     assert max(abs(a - b) for a, b in zip(losses[False], losses[True])) < 1e-3
+
+
+@pytest.mark.parametrize("bilinear,loss", [(True, "bce"), (False, "bce_dice")])
+def test_plan_replay_bitwise_equals_eager(bilinear, loss, monkeypatch):
+    """NativeTrainer plan mode (the step recorded once by the native runtime, then replayed from C++)
+    is the eager program: losses and every parameter / Adam state bitwise equal to eager steps over 7
+    steps with a new batch each step (eager warm-up, the recorded step, 4 replays), both decoders."""
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.train.engine import NativeTrainer
+    torch.manual_seed(3)
+    dev = torch.device("cuda")
+    ref = UNetRef(3, 1, bilinear=bilinear)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    batches = [(torch.rand(2, 3, 64, 96, generator=g), (torch.rand(2, 1, 64, 96, generator=g) > 0.5).float())
+               for _ in range(7)]
+    runs = {}
+    for mode in ("eager", "plan", "plan_graph"):  # plan_graph: replay as per-stream hipGraphs (plan_compile)
+        plan = mode != "eager"
+        monkeypatch.setenv("RDP_PLAN_GRAPH", "1" if mode == "plan_graph" else "0")
+        nat = UNetNative(3, 1, bilinear=bilinear, device=dev, init_from=ref)
+        tr = NativeTrainer(nat, 2, 64, 96, lr=1e-3, loss=loss, plan=plan)
+        assert tr.use_plan == plan
+        ls = []
+        for x, y in batches:
+            tr.set_batch(x.to(dev), y.to(dev))
+            ls.append(tr.step().clone())
+        torch.cuda.synchronize()
+        if plan:
+            assert tr.plan_id is not None
+        st = nat.store
+        runs[mode] = (torch.stack(ls), st.flat.clone(), st.exp_avg.clone(), st.exp_avg_sq.clone(),
+                      nat.derived.clone(), [b.clone() for _, b in nat.named_buffers()])
+    a = runs["eager"]
+    for mode in ("plan", "plan_graph"):
+        b = runs[mode]
+        for u, v in zip(a[:5], b[:5]):
+            assert torch.equal(u, v), mode
+        for u, v in zip(a[5], b[5]):
+            assert torch.equal(u, v), mode
