@@ -531,13 +531,17 @@ void maxpool2_bwd(torch::Tensor dp, torch::Tensor x, c10::optional<torch::Tensor
 }
 
 // training forward at a Down boundary: a = relu(bn(y)) (skip activation) and its 2x2 max pool, one pass
-void bn_relu_apply_pool(torch::Tensor y, torch::Tensor out, torch::Tensor pool, torch::Tensor coef) {
-  Act a = act(y, "y"), o = act(out, "out"), p = act(pool, "pool");
-  TORCH_CHECK(a.N == o.N && a.H == o.H && a.W == o.W && a.C == o.C, "bn_relu_apply_pool shape");
+// out = None: only the pool is written (bf16-exact activation, as if a had been stored and re-read)
+void bn_relu_apply_pool(torch::Tensor y, c10::optional<torch::Tensor> out, torch::Tensor pool, torch::Tensor coef) {
+  Act a = act(y, "y"), o, p = act(pool, "pool");
+  if (out) {
+    o = act(*out, "out");
+    TORCH_CHECK(a.N == o.N && a.H == o.H && a.W == o.W && a.C == o.C, "bn_relu_apply_pool shape");
+  }
   TORCH_CHECK(p.N == a.N && p.H == a.H / 2 && p.W == a.W / 2 && p.C == a.C, "bn_relu_apply_pool pool shape");
   check_f32(coef, "coef");
   TORCH_CHECK(coef.numel() >= 4 * a.C, "coef");
-  TORCH_CHECK(RDP_PLAN(rdp_bn_relu_apply_pool(a.ptr, a.pitch, o.ptr, o.pitch, p.ptr, p.pitch, coef.data_ptr<float>(), a.N, a.H,
+  TORCH_CHECK(RDP_PLAN(rdp_bn_relu_apply_pool(a.ptr, a.pitch, out ? o.ptr : nullptr, out ? o.pitch : 0, p.ptr, p.pitch, coef.data_ptr<float>(), a.N, a.H,
                                      a.W, a.C, st)) == 0, "bn_relu_apply_pool: channels must be 2^k in [8, 2048]");
 }
 

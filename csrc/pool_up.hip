@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_pool_kernel(const u16* __re
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], ss[k], hh[k]), 0.f);
       const uint4 o = pack8f(f);
-      *(uint4*)(a + px[q] * apitch + c) = o;
+      if (a) *(uint4*)(a + px[q] * apitch + c) = o;  // a == nullptr: pool only (the caller writes a elsewhere)
       unpack8f(o, av[q]);  // the pool sees exactly the stored (bf16) activation
     }
     if (hc < Ho && wc < Wo) {

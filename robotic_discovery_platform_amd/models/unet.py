@@ -333,6 +333,12 @@ class UNetExecutor:
         # vs 2981 / 2973 img/s, same box, interleaved) -- the upsample re-applies BN to each of the 4
         # taps of every output (4x the input elements) and these tensors are small. RDP_FUSE_UP_BN=1 on.
         self.fuse_up_bn = training and model.bilinear and os.environ.get("RDP_FUSE_UP_BN", "0") != "0"
+        # training, RDP_SKIP_SIDE=1: at each Down boundary the pool-only BN+ReLU+maxpool runs on the main
+        # stream and the skip activation on the wgrad side stream (idle during forward). Measured dead
+        # end (same box, interleaved): bs 64 3096 / 3097 -> 3072 / 3077 img/s, bs 4 neutral -- the
+        # side-stream pass competes for HBM with the forward; default: one fused kernel on the main stream
+        self.skip_side = False
+        self._skip_pending = False
         C = _native()
         D = model.depth
         bf = torch.bfloat16
@@ -444,6 +450,7 @@ class UNetExecutor:
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
         self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
+        self.skip_side = self.side is not None and self.fuse_pool and os.environ.get("RDP_SKIP_SIDE", "0") != "0"
         # RDP_WGRAD_STREAMS > 1: weight gradients round-robin over that many side streams, each with
         # its own slab (consecutive layers' wgrads run concurrently, not queued behind each other).
         # Measured dead end (same box, 2 rounds): bs4 1499 / 1451 / 1444 img/s and bs64 2994-2998 /
@@ -596,7 +603,14 @@ class UNetExecutor:
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
                           m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
         if pool is not None and self.fuse_pool:
-            C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
+            if self.skip_side:
+                # the pool (next conv's input) on the critical path; the skip activation (read only by the
+                # decoder and the backward) written on the side stream, overlapping the next convs
+                C.bn_relu_apply_pool(L.y, None, pool, L.coef)
+                self._on_side(lambda: C.bn_relu_apply(L.y, L.a, L.coef, 1))
+                self._skip_pending = True
+            else:
+                C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
             return True
         if apply:
             C.bn_relu_apply(L.y, L.a, L.coef, 1)
@@ -642,6 +656,9 @@ class UNetExecutor:
                                         apply=not (i == D and self.fuse_up_bn))
         low = self.skips[D]
         low_layer = self.down_layers[D][1]
+        if self._skip_pending:  # the decoder reads the skip activations written on the side stream
+            _stream_wait(torch.cuda.current_stream(), self.side)
+            self._skip_pending = False
         for i in range(1, D + 1):
             lv = D - i
             u = self.ups[i - 1]
