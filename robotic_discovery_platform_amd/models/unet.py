@@ -222,6 +222,9 @@ class UNetNative(nn.Module):
             self._dw[us.name] = (off, n)
             off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.derived = torch.zeros(max(off, 1), dtype=torch.bfloat16, device=st.device)
+        # launch plans recorded against the previous derived buffers are stale from here (NativeTrainer
+        # re-records when this changes)
+        self.__dict__["_layout_version"] = self.__dict__.get("_layout_version", 0) + 1
         seg_size = C.wseg_size()
         raw = bytearray()
         import struct

@@ -98,6 +98,7 @@ class NativeTrainer:
         self.use_plan = (bool(plan) and not self.ddp and not self.use_graph and self.stream is None
                          and torch.cuda.is_available() and model.store.device.type == "cuda")
         self.plan_id: Optional[int] = None
+        self._plan_version = None
         # RDP_PLAN_GRAPH=1: replay each single-stream run of launches of the plan as one hipGraph
         self._plan_stream = (torch.cuda.Stream(device=model.store.device)
                              if self.use_plan and os.environ.get("RDP_PLAN_GRAPH", "0") != "0" else None)
@@ -147,6 +148,9 @@ class NativeTrainer:
                 ctx = torch.cuda.stream(ps)
             else:
                 ctx = contextlib.nullcontext()
+            if self.plan_id is not None and self._plan_version != self.model.__dict__.get("_layout_version"):
+                C.plan_free(self.plan_id)  # weights re-laid out (load_state_dict): record again
+                self.plan_id = None
             with ctx:
                 if self.plan_id is not None:
                     C.plan_replay(self.plan_id)
@@ -160,6 +164,7 @@ class NativeTrainer:
                         C.plan_abort()
                         raise
                     self.plan_id = C.plan_end()
+                    self._plan_version = self.model.__dict__.get("_layout_version")
                     if ps is not None:
                         C.plan_compile(self.plan_id)
             if ps is not None:
