@@ -32,6 +32,8 @@ int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStre
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
                    float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
+int rdp_wgrad_first_bn(const void*, long, int, const void*, long, int, const void*, long, int, const float*, const float*,
+                       float*, long, float*, int, int, int, int, int, int, hipStream_t);
 void rdp_conv_set_debug_flags(int);
 int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
                     float*, float*, hipStream_t);
@@ -425,6 +427,29 @@ int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor 
                                 a1.H, a1.W, d.C, taps, packed, cin_real, splits, variant, st));
     TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
   }
+  return r;
+}
+
+// First layer: BN-backward apply (+ ReLU mask) fused into the packed weight gradient (conv_wgrad.hip).
+// x: the 8-channel packed input, da: dL/d(post-ReLU activation), y: pre-BN conv output, coef / coef2:
+// the layer's BN coefficients (bn_finalize / bn_bwd_finalize). Returns the splits, or -1 when the
+// shape does not fit the kernel (nothing launched: the caller runs bn_relu_bwd_apply + conv_wgrad).
+int wgrad_first_bn(torch::Tensor x, torch::Tensor da, torch::Tensor y, torch::Tensor coef, torch::Tensor coef2,
+                   torch::Tensor slab, torch::Tensor out, int cin_real, int accumulate, int splits) {
+  Act a = act(x, "x"), d = act(da, "da"), b = act(y, "y");
+  TORCH_CHECK(a.C == 8 && d.C == 64 && b.C == 64, "wgrad_first_bn: x must have 8 (packed) and da / y 64 channels");
+  TORCH_CHECK(d.N == a.N && d.H == a.H && d.W == a.W && b.N == a.N && b.H == a.H && b.W == a.W,
+              "wgrad_first_bn: spatial mismatch");
+  check_f32(coef, "coef"); check_f32(coef2, "coef2"); check_f32(slab, "slab"); check_f32(out, "out");
+  TORCH_CHECK(coef.numel() >= 4 * 64 && coef2.numel() >= 3 * 64, "wgrad_first_bn: coef / coef2 too small");
+  TORCH_CHECK(out.numel() == 64l * 9 * cin_real, "wgrad_first_bn: out numel mismatch");
+  if (a.bytes >= (1l << 31) || d.bytes >= (1l << 31) || b.bytes >= (1l << 31)) return -1;
+  if (((long)a.N * a.H * a.W) % 64) return -1;
+  const int r = RDP_PLAN(rdp_wgrad_first_bn(a.ptr, a.bytes, a.pitch, d.ptr, d.bytes, d.pitch, b.ptr, b.bytes, b.pitch,
+                                            coef.data_ptr<float>(), coef2.data_ptr<float>(), slab.data_ptr<float>(),
+                                            slab.numel(), out.data_ptr<float>(), accumulate, a.N, a.H, a.W, cin_real,
+                                            splits, st));
+  TORCH_CHECK(r > 0, "wgrad_first_bn: slab too small (code ", r, ")");
   return r;
 }
 
@@ -1023,6 +1048,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_stats_rows", &conv_stats_rows);
   m.def("conv_set_debug_flags", [](int f) { rdp_conv_set_debug_flags(f); }, "A/B flags for microbenchmarks");
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("wgrad_first_bn", &wgrad_first_bn);
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coef", &bn_eval_coef);

@@ -752,8 +752,16 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     h.nseg = a.M / 64;
     // one resident wave of blocks (2/CU at BN = 64, 1/CU at BN = 128), within the slab
     const int target = env_blocks > 0 ? env_blocks : (BN == 64 ? 512 : 256);
+    // RDP_WGRAD_MINSEG: at least this many 64-pixel segments per split (fewer splits, a smaller slab
+    // at small batch). Measured neutral (same box, 2 rounds, img/s): bs4 1595 / 1591 / 1589 / 1160
+    // and bs64 3105-3127 / 3127 / 3102-3156 / 3113-3174 for 1 / 4 / 16 / 64 -- the side-stream slab
+    // traffic is hidden under the main stream; 64 starves the bs4 grid. Default 1.
+    static const int env_minseg = [] {
+      const char* e = getenv("RDP_WGRAD_MINSEG");
+      return e ? std::max(1, atoi(e)) : 1;
+    }();
     int sp = std::max(1, (target + tiles - 1) / tiles);
-    sp = std::min(sp, h.nseg);
+    sp = std::min(sp, std::max(1, h.nseg / env_minseg));
     const long per_split = (long)Cout * h.ncols;
     sp = (int)std::min<long>(sp, slab_elems / per_split);
     if (sp < 1) return -2;
@@ -877,6 +885,207 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   launch_wgrad_reduce(slab, out, a.splits, Cout, a.ncols_pad, taps, packed ? 8 : a.Cin, packed ? cin_real : a.Cin,
                       accumulate, s);
   return a.splits;
+}
+
+// ---------------------------------------------------------------------------------------------
+// First layer (inc.double_conv.0, 3 -> 64, reference /root/reference/pkg/segmentation_model.py:31):
+// BN-backward apply + ReLU mask fused into the weight gradient. The first conv has no input
+// gradient, so its pre-BN gradient dz = A * relu_mask(y) * da + B * y + K (the bn_relu_bwd_apply
+// formula, norm_act.hip) is consumed ONLY by this wgrad: computing it here, in registers, and staging
+// it straight into the LDS dY tile drops the 537 MB dz write + re-read of a bs-64 step (the separate
+// apply pass plus the packed wgrad's dY stream) at the end of backward, where it sits on the
+// critical path.
+//
+// Per 64-pixel K step a block stages: x taps 0..7 (8 channels each, channel 3..7 the stored zero pad)
+// and tap 8 by LDS-DMA (the packed layout of conv_wgrad_kernel<PACKED>), and dz [64 px][64 couts]
+// computed from da / y by every thread (channel group tc = tid & 7 fixed per thread, so the 40
+// BN coefficients stay in registers; swizzle applied on the LDS write address). Only the 80 valid
+// (tap, channel) columns are multiplied (5 MFMA column fragments instead of the packed kernel's 16).
+// Wave w owns couts 16w .. 16w + 15. The dz loads of step k + 1 are issued before step k's MFMAs and
+// written to the other LDS buffer after them (one barrier per step). Slab [splits][64][80] fp32,
+// reduced by the shared two-level wgrad reduction.
+struct FirstWgradArgs {
+  const u16* x;
+  uint32_t xbytes;
+  int xpitch;
+  const u16* da;
+  uint32_t dabytes;
+  int dapitch;
+  const u16* y;
+  uint32_t ybytes;
+  int ypitch;
+  const float* coef;   // [mean | invstd | scale | shift] x 64
+  const float* coef2;  // [A | B | K] x 64 (bn_bwd_finalize)
+  float* slab;
+  uint32_t slab_bytes;
+  int H, W, M, pix_per_split;
+  uint32_t fw_m, fw_s, fh_m, fh_s;
+};
+constexpr int FWG_NCOLS = 80;
+
+RDP_DEV void fw_unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad_first_bn_kernel(const FirstWgradArgs a) {
+  constexpr int SUB = 64 * 128;  // [64 px][64 bf16]
+  constexpr int BUF = 3 * SUB;   // x taps 0..7 | x tap 8 | dz
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int split = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int pbeg = split * a.pix_per_split;
+  const int nks = max(0, min(a.M, pbeg + a.pix_per_split) - pbeg) / 64;  // host: multiples of 64
+  const auto rx = make_rsrc(a.x, a.xbytes);
+  const auto rda = make_rsrc(a.da, a.dabytes);
+  const auto ry = make_rsrc(a.y, a.ybytes);
+
+  // dz producer role: channel group tc (fixed), pixel rows tr0 and tr0 + 32 of each K step
+  const int tc = threadIdx.x & 7, tr0 = threadIdx.x >> 3;
+  float ss[8], hh[8], cA[8], cB[8], cK[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = 8 * tc + k;
+    ss[k] = a.coef[128 + c]; hh[k] = a.coef[192 + c];
+    cA[k] = a.coef2[c]; cB[k] = a.coef2[64 + c]; cK[k] = a.coef2[128 + c];
+  }
+  uint4 vd[2], vy[2];
+  auto load_dz = [&](int ks) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = pbeg + ks * 64 + tr0 + 32 * u;
+      vd[u] = bload16(rda, (uint32_t)(m * a.dapitch + 8 * tc) * 2u);
+      vy[u] = bload16(ry, (uint32_t)(m * a.ypitch + 8 * tc) * 2u);
+    }
+  };
+  auto store_dz = [&](char* buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tr0 + 32 * u;
+      float fd[8], fy[8];
+      fw_unpack8(vd[u], fd);
+      fw_unpack8(vy[u], fy);
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) {
+        const float g0 = fmaf(fy[k], ss[k], hh[k]) > 0.f ? fd[k] : 0.f;
+        const float g1 = fmaf(fy[k + 1], ss[k + 1], hh[k + 1]) > 0.f ? fd[k + 1] : 0.f;
+        o[k / 2] = pack2bf(fmaf(cA[k], g0, fmaf(cB[k], fy[k], cK[k])),
+                           fmaf(cA[k + 1], g1, fmaf(cB[k + 1], fy[k + 1], cK[k + 1])));
+      }
+      *(uint4*)(buf + 2 * SUB + p * 128 + 16 * (tc ^ swz(p))) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  };
+  const int rowl = lane >> 3, cpos = lane & 7;
+  // x: 16 DMA pieces (2 subtiles x 8 pieces of 8 pixel rows), 4 per wave
+  auto issue_x = [&](int ks, char* buf) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int s = wave * 4 + t, sub = s >> 3, pj = s & 7;
+      const int p = pj * 8 + rowl;
+      const int g = cpos ^ swz(p);
+      const int m = pbeg + ks * 64 + p;
+      const uint32_t q = fdiv2((uint32_t)m, a.fw_m, a.fw_s);
+      const int w = m - (int)q * a.W;
+      const int h = (int)q - (int)fdiv2(q, a.fh_m, a.fh_s) * a.H;
+      const int tap = sub * 8 + g;
+      const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+      const bool ok = (tap < 9) & inb(h + dr, a.H) & inb(w + ds, a.W);
+      const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * a.xpitch) * 2u : RDP_OOB;
+      dma16_async(rx, (lds_void*)(buf + sub * SUB + pj * 1024), off);
+    }
+  };
+
+  f32x4 acc[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tpp = lane & 3;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+
+  if (nks > 0) {
+    load_dz(0);
+    issue_x(0, smem);
+    store_dz(smem);
+  }
+  for (int ks = 0; ks < nks; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    const char* cur = smem + (ks & 1) * BUF;
+    char* nxt = smem + ((ks + 1) & 1) * BUF;
+    const bool more = ks + 1 < nks;
+    if (more) {
+      load_dz(ks + 1);
+      issue_x(ks + 1, nxt);
+    }
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int p0 = 32 * hf + 8 * tg + tq;
+      const int sw0 = swz(p0), sw1 = swz(p0 + 4);
+      const int ro0 = p0 * 128 + 8 * (tpp & 1), ro1 = ro0 + 4 * 128;
+      auto frag = [&](const char* base, int i) {
+        const int c = 2 * i + (tpp >> 1);
+        const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(base + ro0 + 16 * (c ^ sw0)));
+        const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(base + ro1 + 16 * (c ^ sw1)));
+        return __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      const bf16x8 fb = frag(cur + 2 * SUB, wave);
+      bf16x8 fa[5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag(cur, i);
+      fa[4] = frag(cur + SUB, 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i], 0, 0, 0);
+    }
+    if (more) store_dz(nxt);
+  }
+
+  // acc[i][r]: col = 16 i + 4 (lane >> 4) + r, cout = 16 wave + (lane & 15)
+  const auto rs = make_rsrc(a.slab, a.slab_bytes);
+  const int co = 16 * wave + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int col = 16 * i + 4 * (lane >> 4);
+    const uint32_t off = (uint32_t)(((long)split * 64 + co) * FWG_NCOLS + col) * 4u;
+    uint4 v;
+    v.x = __float_as_uint(acc[i][0]); v.y = __float_as_uint(acc[i][1]);
+    v.z = __float_as_uint(acc[i][2]); v.w = __float_as_uint(acc[i][3]);
+    bstore16(rs, off, v);
+  }
+}
+
+// Returns the number of splits, or < 0 (nothing launched) when the shape does not fit this kernel.
+extern "C" int rdp_wgrad_first_bn(const void* x, long xbytes, int xpitch, const void* da, long dabytes, int dapitch,
+                                  const void* y, long ybytes, int ypitch, const float* coef, const float* coef2,
+                                  float* slab, long slab_elems, float* out, int accumulate, int N, int H, int W,
+                                  int cin_real, int splits, hipStream_t s) {
+  const long M = (long)N * H * W;
+  if (M % 64 || cin_real > 8 || cin_real < 1) return -1;
+  if (xbytes >= (1l << 31) || dabytes >= (1l << 31) || ybytes >= (1l << 31)) return -1;
+  if (xpitch % 8 || dapitch % 8 || ypitch % 8) return -1;
+  splits = (int)std::max(1L, std::min<long>(splits, M / 64));
+  long pps = (M + splits - 1) / splits;
+  pps = (pps + 63) / 64 * 64;
+  splits = (int)((M + pps - 1) / pps);
+  const long per_split = 64l * FWG_NCOLS;
+  if ((long)splits * per_split > slab_elems) return -2;
+  if ((long)splits * per_split * 4l >= (1l << 31)) return -3;
+  FirstWgradArgs a;
+  a.x = (const u16*)x; a.xbytes = (uint32_t)xbytes; a.xpitch = xpitch;
+  a.da = (const u16*)da; a.dabytes = (uint32_t)dabytes; a.dapitch = dapitch;
+  a.y = (const u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+  a.coef = coef; a.coef2 = coef2;
+  a.slab = slab; a.slab_bytes = (uint32_t)(splits * per_split * 4l);
+  a.H = H; a.W = W; a.M = (int)M; a.pix_per_split = (int)pps;
+  FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
+  a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
+  hipLaunchKernelGGL(wgrad_first_bn_kernel, dim3(splits), dim3(256), 0, s, a);
+  launch_wgrad_reduce(slab, out, splits, 64, FWG_NCOLS, 9, 8, cin_real, accumulate, s);
+  return splits;
 }
 
 // Slab size needed (elements) for a given configuration.

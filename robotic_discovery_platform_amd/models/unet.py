@@ -479,6 +479,8 @@ class UNetExecutor:
         # dgrad into the da of a BN layer: where the row-ring kernel runs it (64 -> 64 channels), its
         # epilogue also produces that layer's BN-backward partial sums (no bn_relu_bwd_reduce pass)
         self.dgrad_bnred = os.environ.get("RDP_DGRAD_BNRED", "1") != "0"
+        # first layer: BN-backward apply fused into its weight gradient (no dz tensor pass)
+        self.fuse_first_wgrad = dev.type == "cuda" and os.environ.get("RDP_FUSE_FIRST_WGRAD", "1") != "0"
         N = self.N
         D = self.m.depth
 
@@ -721,7 +723,7 @@ class UNetExecutor:
         return self.logits.view(self.N, 1, self.H, self.W)
 
     # ------------------------------------------------------------------ backward
-    def _bn_bwd(self, C, L: _Layer, head_gscale: Optional[float] = None):
+    def _bn_bwd(self, C, L: _Layer, head_gscale: Optional[float] = None, apply: bool = True):
         sp = L.spec
         st = self.m.store
         M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
@@ -741,6 +743,8 @@ class UNetExecutor:
             C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
                               st.view(sp.bn + ".weight", st.grad), st.view(sp.bn + ".bias", st.grad), L.coef2,
                               self.red_ws)
+        if not apply:  # the consumer (the first layer's fused wgrad) applies it on the fly
+            return
         if head_gscale is not None:  # fused head: g recomputed from the logits, no da
             C.head_bn_bwd_apply(L.y, st.view("outc.conv.weight").reshape(-1), self.logits, self.target,
                                 self.loss_sums, L.coef, L.coef2, L.dy, self.dice_w, self.dice_eps, head_gscale)
@@ -822,8 +826,28 @@ class UNetExecutor:
     def _conv_bwd(self, C, L: _Layer, hooks=None, head_gscale: Optional[float] = None):
         sp = L.spec
         st = self.m.store
-        self._bn_bwd(C, L, head_gscale)
         gw = st.flat_slice(sp.name + ".weight", st.grad)
+        if (self.fuse_first_wgrad and L is self.down_layers[0][0] and sp.packed and L.dx1 is None
+                and head_gscale is None and sp.cout == 64):
+            # first layer: its pre-BN gradient feeds only the weight gradient, so the BN-backward apply
+            # runs inside that wgrad (wgrad_first_bn) and dz is never stored
+            self._bn_bwd(C, L, None, apply=False)
+
+            def fused(slab):
+                r = C.wgrad_first_bn(L.x1, L.da, L.y, L.coef, L.coef2, slab, gw, sp.cin_real, 0, L.splits)
+                if r < 0:  # shape outside the kernel (e.g. tensors past 2 GiB): separate passes
+                    C.bn_relu_bwd_apply(L.da, L.y, L.coef, L.coef2, L.dy, 1)
+                    C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, slab, gw, 0, L.splits, 0)
+
+            if self.slab_main is not None:
+                fused(self.slab_main)
+            else:
+                self._on_wgrad_stream(fused)
+            if hooks is not None:
+                self._join_sides_into_side()
+                self._on_side(lambda: hooks(sp))
+            return
+        self._bn_bwd(C, L, head_gscale)
         # wgrad (latency-bound on x / dY streams) overlaps the main stream's dgrad + next BN backward;
         # all wgrads share the slab, so they stay serialized on the one side stream
         if self.slab_main is not None and L is self.down_layers[0][0]:

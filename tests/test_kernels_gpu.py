@@ -269,6 +269,51 @@ def test_conv_wgrad_packed(C, N, H, W, splits):
     assert relerr(out, w.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
 
 
+@pytest.mark.parametrize("N,H,W,splits", [(2, 16, 12, 5), (2, 64, 64, 300), (3, 32, 96, 1)])
+def test_wgrad_first_bn_fused(C, N, H, W, splits):
+    """First layer: BN-backward apply fused into the packed wgrad (wgrad_first_bn) vs the separate
+    bn_relu_bwd_apply + conv_wgrad passes (same bf16 dz, fp32 sums in another split order) and vs an
+    fp32 torch reference of the whole BN-backward + weight gradient."""
+    torch.manual_seed(6)
+    dev = "cuda"
+    Cout, M = 64, N * H * W
+    x = bf(torch.rand(N, H, W, 3, device=dev))
+    x8 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device=dev)
+    x8[..., :3] = x
+    y = bf(torch.randn(N, H, W, Cout, device=dev) * 1.5 + 0.2)
+    da = bf(torch.randn(N, H, W, Cout, device=dev))
+    gamma = torch.rand(Cout, device=dev) + 0.5
+    beta = torch.randn(Cout, device=dev) * 0.1
+    stats = torch.stack([y.float().sum((0, 1, 2)), (y.float() ** 2).sum((0, 1, 2))]).reshape(-1).contiguous()
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_finalize(stats, 1, M, gamma, beta, None, None, None, 0.1, 1e-5, coef, None)
+    part = torch.zeros(1024 * 2 * Cout, device=dev)
+    T = C.bn_relu_bwd_reduce(da, y, coef, 1, part)
+    coef2 = torch.zeros(3 * Cout, device=dev)
+    C.bn_bwd_finalize(part, T, M, gamma, coef, None, None, coef2, torch.zeros(64 * 2 * Cout, device=dev))
+    # separate passes
+    dz = torch.empty_like(y)
+    C.bn_relu_bwd_apply(da, y, coef, coef2, dz, 1)
+    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 8, Cout, 9, 1, splits), device=dev)
+    ref_sep = torch.zeros(Cout * 27, device=dev)
+    C.conv_wgrad(x8, None, dz, 9, 1, 3, slab, ref_sep, 0, splits, 0)
+    out = torch.full((Cout * 27,), 7.0, device=dev)
+    r = C.wgrad_first_bn(x8, da, y, coef, coef2, slab, out, 3, 0, splits)
+    assert r >= 1
+    assert relerr(out, ref_sep) < 1e-5
+    # fp32 torch: BN(train) + ReLU backward, then the conv weight gradient
+    yf = nchw(y).float().requires_grad_(True)
+    bn = torch.nn.functional.batch_norm(yf, None, None, gamma, beta, training=True, eps=1e-5)
+    torch.relu(bn).backward(nchw(da).float())
+    w = torch.zeros(Cout, 3, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(nchw(x).float(), w, padding=1).backward(yf.grad)
+    assert relerr(out, w.grad.permute(0, 2, 3, 1).reshape(-1)) < 1e-2
+    # accumulate mode adds onto out
+    out2 = out.clone()
+    C.wgrad_first_bn(x8, da, y, coef, coef2, slab, out2, 3, 1, splits)
+    assert torch.allclose(out2, 2 * out, rtol=1e-6, atol=1e-6)
+
+
 def test_bn_relu_train_fwd_bwd(C):
     torch.manual_seed(5)
     dev = "cuda"
