@@ -32,6 +32,8 @@ int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStre
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
                    float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
+int rdp_conv_dgrad_pp_bnred(const void*, long, int, int, const void*, long, int, void*, long, int, int, float*, long, int,
+                            int, int, int, const void*, long, int, const float*, hipStream_t);
 int rdp_wgrad_first_bn(const void*, long, int, const void*, long, int, const void*, long, int, const float*, const float*,
                        float*, long, float*, int, int, int, int, int, int, hipStream_t);
 void rdp_conv_set_debug_flags(int);
@@ -510,6 +512,25 @@ int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch:
   return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                           o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
                           0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), st));
+}
+
+// dgrad on the ping-pong kernel with the BN-backward reduction of the layer owning dx (y_bn: its
+// pre-BN output, coef: its [mean|invstd|scale|shift]) in the epilogue. Returns the partial rows for
+// bn_bwd_finalize, or -1 when the auto dispatch would not run the ping-pong kernel on this shape
+// (nothing launched: the caller runs conv_fwd + bn_relu_bwd_reduce).
+int conv_dgrad_pp_bnred(torch::Tensor dy, torch::Tensor w, int taps, torch::Tensor dx, torch::Tensor y_bn,
+                        torch::Tensor coef, torch::Tensor partial) {
+  Act a = act(dy, "dy"), o = act(dx, "dx"), b = act(y_bn, "y_bn");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && b.N == a.N && b.H == a.H && b.W == a.W && b.C == o.C,
+              "conv_dgrad_pp_bnred: shape mismatch");
+  TORCH_CHECK(w.size(0) == o.C, "w rows != Cout");
+  check_f32(coef, "coef");
+  check_f32(partial, "partial");
+  TORCH_CHECK(coef.numel() >= 4l * o.C, "coef must hold 4*C floats");
+  return RDP_PLAN(rdp_conv_dgrad_pp_bnred(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr,
+                                          o.bytes, o.pitch, o.C, partial.data_ptr<float>(), partial.numel(), a.N, a.H,
+                                          a.W, taps, b.ptr, b.bytes, b.pitch, coef.data_ptr<float>(), st));
 }
 
 int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, int relu, torch::Tensor partial) {
@@ -1049,6 +1070,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_debug_flags", [](int f) { rdp_conv_set_debug_flags(f); }, "A/B flags for microbenchmarks");
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_first_bn", &wgrad_first_bn);
+  m.def("conv_dgrad_pp_bnred", &conv_dgrad_pp_bnred);
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coef", &bn_eval_coef);

@@ -63,6 +63,12 @@ struct ConvArgs {
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
   int store_aware;  // 1: the per-step vmcnt leaves the previous epilogue's stores in flight
+  // dgrad + BN-backward reduction (conv_pp_kernel<..., BNR = true>): the output is dL/da of the layer
+  // that owns it; bny = that layer's pre-BN output [M][bnypitch], bncoef its [mean|invstd|scale|shift]
+  const u16* bny;
+  uint32_t bnybytes;
+  int bnypitch;
+  const float* bncoef;
 };
 
 // debug / A-B flags for the microbenchmark (rdp_conv_set_debug_flags): bit 0 = plain vmcnt(0)
@@ -465,7 +471,11 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
 // Generic (non-packed) im2col only, no split-K / fixup / fused pool or upsample.
 // RD_INFLIGHT: fragment reads of phases 0..NPH-2 stay in flight across the segment barrier;
 // HOLDB: both cout halves of the weight fragments stay in registers (no re-read in phase 3).
-template <int BN, int NST, bool RD_INFLIGHT, bool HOLDB>
+// BNR: dgrad whose output da belongs to a BN+ReLU layer; the statistics rows hold that layer's
+// BN-backward partial sums (sum g, sum g * xhat, g = da masked by ReLU(BN(y))) instead of the
+// output moments, from the bf16-rounded da as stored and the owner's pre-BN y read in the epilogue:
+// the separate bn_relu_bwd_reduce pass (which re-reads da and y) is dropped.
+template <int BN, int NST, bool RD_INFLIGHT, bool HOLDB, bool BNR = false>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   // BN = 256 / 128: 256-pixel tile, wave (wm, wn) = 128 pixels x BN/4 couts. BN = 64: 512-pixel tile,
   // wave (wm, wn) = 64 pixels (rows wm * 256 + wn * 64) x all 64 couts.
@@ -603,6 +613,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
     const int gq = lane >> 4;
     const int coff = 16 * (gq & 1) + 8 * (gq >> 1);
     float s1[NJ][4], s2[NJ][4];
+    const auto rbny = make_rsrc(BNR ? a.bny : a.y1, BNR ? a.bnybytes : 0u);
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -614,10 +625,26 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
       const bool d2 = nb >= a.Cy1;  // wave-uniform: Cy1 % 32 == 0 (host-checked), one SRD per store
       const int nn = d2 ? n - a.Cy1 : n;
       const int yp = d2 ? a.ypitch2 : a.ypitch1;
+      float4 bmu[2], binv[2], bss[2], bhh[2];  // BNR: owner coefficients of this lane's 2 x 4 channels
+      if constexpr (BNR) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int nc = nb + h * 16 + 4 * gq;
+          bmu[h] = *(const float4*)(a.bncoef + nc);
+          binv[h] = *(const float4*)(a.bncoef + a.Cout + nc);
+          bss[h] = *(const float4*)(a.bncoef + 2 * a.Cout + nc);
+          bhh[h] = *(const float4*)(a.bncoef + 3 * a.Cout + nc);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int m = m0 + wpx + i * 16 + (lane & 15);
-        uint2 v[2];
+        uint2 v[2], yb[2];
+        if constexpr (BNR) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            yb[h] = bload8(rbny, m < a.M ? (uint32_t)(m * a.bnypitch + nb + h * 16 + 4 * gq) * 2u : RDP_OOB);
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int j = jp + h;
@@ -637,10 +664,23 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
           if (a.stats && m < a.M) {
             const float q0 = __uint_as_float(v[h].x << 16), q1 = __uint_as_float(v[h].x & 0xffff0000u);
             const float q2 = __uint_as_float(v[h].y << 16), q3 = __uint_as_float(v[h].y & 0xffff0000u);
-            s1[j][0] += q0; s2[j][0] += q0 * q0;
-            s1[j][1] += q1; s2[j][1] += q1 * q1;
-            s1[j][2] += q2; s2[j][2] += q2 * q2;
-            s1[j][3] += q3; s2[j][3] += q3 * q3;
+            if constexpr (BNR) {
+              const float y0 = __uint_as_float(yb[h].x << 16), y1 = __uint_as_float(yb[h].x & 0xffff0000u);
+              const float y2 = __uint_as_float(yb[h].y << 16), y3 = __uint_as_float(yb[h].y & 0xffff0000u);
+              const float g0 = fmaf(y0, bss[h].x, bhh[h].x) > 0.f ? q0 : 0.f;
+              const float g1 = fmaf(y1, bss[h].y, bhh[h].y) > 0.f ? q1 : 0.f;
+              const float g2 = fmaf(y2, bss[h].z, bhh[h].z) > 0.f ? q2 : 0.f;
+              const float g3 = fmaf(y3, bss[h].w, bhh[h].w) > 0.f ? q3 : 0.f;
+              s1[j][0] += g0; s2[j][0] += g0 * (y0 - bmu[h].x) * binv[h].x;
+              s1[j][1] += g1; s2[j][1] += g1 * (y1 - bmu[h].y) * binv[h].y;
+              s1[j][2] += g2; s2[j][2] += g2 * (y2 - bmu[h].z) * binv[h].z;
+              s1[j][3] += g3; s2[j][3] += g3 * (y3 - bmu[h].w) * binv[h].w;
+            } else {
+              s1[j][0] += q0; s2[j][0] += q0 * q0;
+              s1[j][1] += q1; s2[j][1] += q1 * q1;
+              s1[j][2] += q2; s2[j][2] += q2 * q2;
+              s1[j][3] += q3; s2[j][3] += q3 * q3;
+            }
           }
         }
         const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
@@ -745,7 +785,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   }
 }
 
-template <int BN, bool RDF = false, bool HOLDB = false>
+template <int BN, bool RDF = false, bool HOLDB = false, bool BNR = false>
 static int launch_pp(ConvArgs a, hipStream_t s) {
   constexpr int BM = BN == 64 ? 512 : 256;
   constexpr int NST = BN == 128 ? 3 : 2;
@@ -759,7 +799,7 @@ static int launch_pp(ConvArgs a, hipStream_t s) {
   a.up = nullptr;
   const int grid = a.ntiles < 256 ? a.ntiles : 256;  // one block per CU, persistent
   if (a.stats && grid % a.tilesN) return -1;
-  hipLaunchKernelGGL((conv_pp_kernel<BN, NST, RDF, HOLDB>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((conv_pp_kernel<BN, NST, RDF, HOLDB, BNR>), dim3(grid), dim3(512), 0, s, a);
   return grid / a.tilesN * (BN == 64 ? 8 : 2);
 }
 
@@ -1250,6 +1290,49 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   if (bm_pref == 0 && Cout % 128 == 0) return launch_cfg<128, 128, 8>(a, max_blocks, wse, s, pooled);
   if (bm_pref == 256) return launch_cfg<256, 64>(a, max_blocks, wse, s, pooled);
   return launch_cfg<256, 64, 8>(a, max_blocks, wse, s, pooled);
+}
+
+// dgrad (3x3 or 1x1, one source, one destination) on the ping-pong kernel with the BN-backward
+// reduction of the layer owning dx in its epilogue (BNR). Only where the auto dispatch of
+// rdp_conv_igemm would pick the ping-pong kernel for this shape (same kernel, same K order: dx is
+// bitwise equal to the plain dgrad); returns the partial rows written to `partial` ([rows][2][C]), or
+// -1 with nothing launched (the caller runs the plain dgrad + bn_relu_bwd_reduce).
+extern "C" int rdp_conv_dgrad_pp_bnred(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
+                                       void* y, long ybytes, int ypitch, int Cout, float* partial, long partial_elems,
+                                       int N, int H, int W, int taps, const void* bny, long bnybytes, int bnypitch,
+                                       const float* bncoef, hipStream_t s) {
+  static const int pp_env = [] {
+    const char* e = getenv("RDP_CONV_PP");
+    return e ? atoi(e) : 2;
+  }();
+  if (!pp_env || C % 64 || (taps != 9 && taps != 1) || ldw < taps * C || bnypitch % 4) return -1;
+  if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || bnybytes >= (1l << 31)) return -1;
+  const long M = (long)N * H * W;
+  const long tiles256 = (M + 255) / 256 * (Cout / 256);
+  const long tiles128 = (M + 255) / 256 * (Cout / 128);
+  const bool use256 = Cout % 256 == 0 && tiles256 >= 256;
+  const bool use128 = !use256 && pp_env == 2 && Cout % 128 == 0 && tiles128 >= 256 && C >= 128;
+  if (!use256 && !use128) return -1;
+  const int BN = use256 ? 256 : 128;
+  const long grid = std::min<long>((M + 255) / 256 * (Cout / BN), 256);
+  const long rows = grid / (Cout / BN) * 2;
+  if (rows * 2 * Cout > partial_elems) return -1;
+  ConvArgs a{};
+  a.x1 = (const u16*)x; a.x2 = nullptr; a.xbytes1 = (uint32_t)xbytes; a.xbytes2 = 0;
+  a.C1 = C; a.C2 = 0; a.pitch1 = pitch; a.pitch2 = 0;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y1 = (u16*)y; a.y2 = nullptr; a.ybytes1 = (uint32_t)ybytes; a.ybytes2 = 0;
+  a.Cy1 = Cout; a.ypitch1 = ypitch; a.ypitch2 = 0; a.stats = partial;
+  a.escale = nullptr; a.eshift = nullptr; a.erelu = 0;
+  a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.M = (int)M;
+  a.taps = taps; a.packed = 0; a.cpt = C / 64; a.nks = taps * a.cpt;
+  a.kcnt = nullptr; a.kslab = nullptr;
+  a.store_aware = (g_conv_debug_flags & 1) ? 0 : 1;
+  const FastDiv fhw = make_fastdiv((uint32_t)(H * W)), fw = make_fastdiv((uint32_t)W);
+  a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;
+  a.bny = (const u16*)bny; a.bnybytes = (uint32_t)bnybytes; a.bnypitch = bnypitch; a.bncoef = bncoef;
+  // the same template arguments as the auto dispatch (+ BNR)
+  return use256 ? launch_pp<256, true, true, true>(a, s) : launch_pp<128, true, false, true>(a, s);
 }
 
 // fp32 workspace elements the auto dispatch would use for split-K on this shape (0 = no split)

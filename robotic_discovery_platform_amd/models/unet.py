@@ -479,6 +479,12 @@ class UNetExecutor:
         # dgrad into the da of a BN layer: where the row-ring kernel runs it (64 -> 64 channels), its
         # epilogue also produces that layer's BN-backward partial sums (no bn_relu_bwd_reduce pass)
         self.dgrad_bnred = os.environ.get("RDP_DGRAD_BNRED", "1") != "0"
+        # ping-pong dgrad with the owner's BN-backward reduction in its epilogue (conv_dgrad_pp_bnred, the
+        # 7 remaining bn_relu_bwd_reduce passes at bs64). Measured dead end, off by default: bs64 1.2 %
+        # SLOWER (3084-3095 vs 3119-3137 img/s, 3 interleaved rounds, same box; bs4 neutral) -- the owner's
+        # y loads sit latency-exposed in the persistent kernel's per-tile epilogue, stalling both wave
+        # groups, which costs more than the separate 376 us (serialised) reduce pass it removes.
+        self.dgrad_pp_bnred = self.dgrad_bnred and os.environ.get("RDP_DGRAD_PP_BNRED", "0") != "0"
         # first layer: BN-backward apply fused into its weight gradient (no dz tensor pass)
         self.fuse_first_wgrad = dev.type == "cuda" and os.environ.get("RDP_FUSE_FIRST_WGRAD", "1") != "0"
         N = self.N
@@ -858,6 +864,14 @@ class UNetExecutor:
         owner = L.dx1_owner if self.dgrad_bnred else None
         if owner is not None and L.dx2 is None and sp.taps == 9 and not owner.bwd_rows:
             rows = C.conv_dgrad_bnred(L.dy, self.m.dgrad_weight(sp), L.dx1, owner.y, owner.coef, self.bn_partial)
+            if rows > 0:
+                owner.bwd_rows = rows
+                owner = True
+        if (owner is not None and owner is not True and L.dx2 is None and self.dgrad_pp_bnred
+                and not owner.bwd_rows):
+            # wider layers: the ping-pong dgrad's epilogue produces the owner's BN-backward partials
+            rows = C.conv_dgrad_pp_bnred(L.dy, self.m.dgrad_weight(sp), sp.taps, L.dx1, owner.y, owner.coef,
+                                         self.bn_partial)
             if rows > 0:
                 owner.bwd_rows = rows
                 owner = True

@@ -1069,3 +1069,50 @@ torch.save({"y": y.cpu(), "s": st[: r * 256].view(r, 2, 128).sum(0).cpu(), "g": 
     assert torch.equal(outs[0]["y"], outs[1]["y"])
     assert torch.allclose(outs[0]["s"], outs[1]["s"], rtol=1e-4, atol=1e-2)
     assert relerr(outs[1]["g"], outs[0]["g"]) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,taps", [(16, 64, 64, 256, 256, 9), (16, 64, 64, 128, 128, 9),
+                                                 (4, 128, 128, 256, 256, 1), (18, 62, 61, 128, 128, 9)])
+def test_conv_dgrad_pp_bnred(C, N, H, W, Cin, Cout, taps):
+    """Ping-pong dgrad with the owner layer's BN-backward reduction in its epilogue (conv_dgrad_pp_bnred):
+    dx bitwise equal to the plain dgrad (same kernel and K order); the partial sums fold to the same
+    BN-backward coefficients as bn_relu_bwd_reduce over (dx, y). Covers both tile widths, 1x1 and a
+    ragged last tile."""
+    torch.manual_seed(13)
+    dev = "cuda"
+    M = N * H * W
+    dy = bf(torch.randn(N, H, W, Cin, device=dev))
+    w = bf(torch.randn(Cout, taps * Cin, device=dev) / math.sqrt(taps * Cin))
+    y = bf(torch.randn(N, H, W, Cout, device=dev) * 1.5 + 0.2)
+    mean, inv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    gamma, beta = torch.randn(Cout, device=dev), torch.randn(Cout, device=dev) * 0.2
+    ss = gamma * inv
+    coef = torch.cat([mean, inv, ss, beta - mean * ss]).contiguous()
+    dx_r = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(dy, None, w, taps, 0, dx_r, None, None, 0, None, 0, None)
+    bp_r = torch.zeros(1024 * 2 * Cout, device=dev)
+    T_r = C.bn_relu_bwd_reduce(dx_r, y, coef, 1, bp_r)
+    dx = torch.empty_like(dx_r)
+    bp = torch.zeros(1024 * 2 * Cout, device=dev)
+    T = C.conv_dgrad_pp_bnred(dy, w, taps, dx, y, coef, bp)
+    assert T > 0, "shape should run on the ping-pong kernel"
+    assert torch.equal(dx, dx_r)
+    s_r = bp_r.view(-1, 2, Cout)[:T_r].double().sum(0)
+    s = bp.view(-1, 2, Cout)[:T].double().sum(0)
+    assert relerr(s, s_r) < 1e-5
+    # fp32 reference of the sums
+    g = torch.where(y.float() * ss + (beta - mean * ss) > 0, dx_r.float(), torch.zeros((), device=dev))
+    ref = torch.stack([g.sum((0, 1, 2)), (g * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
+    assert relerr(s, ref) < 1e-4
+
+
+def test_conv_dgrad_pp_bnred_declines_small(C):
+    """Shapes the auto dispatch would not run on the ping-pong kernel: nothing launched, -1."""
+    dev = "cuda"
+    dy = bf(torch.randn(1, 16, 16, 128, device=dev))
+    w = bf(torch.randn(128, 9 * 128, device=dev))
+    y = bf(torch.randn(1, 16, 16, 128, device=dev))
+    dx = torch.full_like(y, 3.0)
+    coef = torch.ones(4 * 128, device=dev)
+    assert C.conv_dgrad_pp_bnred(dy, w, 9, dx, y, coef, torch.zeros(1024 * 256, device=dev)) == -1
+    assert torch.all(dx == 3.0)
