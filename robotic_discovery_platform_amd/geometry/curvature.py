@@ -17,6 +17,7 @@ dataclasses, same early-exit and failure semantics), executed MI355X-first:
 from __future__ import annotations
 
 from dataclasses import dataclass, field
+import itertools
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -25,7 +26,7 @@ import torch
 from ..config import GeometryConfig
 
 
-@dataclass
+@dataclass(slots=True)  # one per spline sample, built on every served frame
 class Point:
     x: float = 0.0
     y: float = 0.0
@@ -83,9 +84,8 @@ def result_from_device(res: np.ndarray, cfg: GeometryConfig) -> Optional[Curvatu
     if st != 0:
         return CurvatureResult(status=_DEV_STATUS.get(st, "fit_failed"), n_points=npts,
                                n_edge_points=E if st != 1 else 0)
-    p = res[8:8 + 3 * cfg.num_samples].reshape(-1, 3)
-    return CurvatureResult(float(res[4]), float(res[5]), [Point(float(a), float(b), float(c)) for a, b, c in p],
-                           "ok", npts, E)
+    p = res[8:8 + 3 * cfg.num_samples].reshape(-1, 3).tolist()  # Python floats in one C pass
+    return CurvatureResult(float(res[4]), float(res[5]), list(itertools.starmap(Point, p)), "ok", npts, E)
 
 
 def edges_numpy(mask, depth, K, scale, cfg: GeometryConfig) -> Tuple[np.ndarray, int]:

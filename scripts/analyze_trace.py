@@ -12,7 +12,7 @@ specs = unet_conv_specs(4, 64, 3, True)
 # spatial size per spec in forward order
 D = 4; sizes = []
 lv = [0, 0] + sum([[i, i] for i in range(1, D + 1)], []) + sum([[D - i, D - i] for i in range(1, D + 1)], [])
-MAIN = ('conv_igemm_kernel', 'conv_pp_kernel', 'conv_halo_kernel', 'conv_ring_kernel', 'conv_wgrad_kernel', 'conv_wgrad_halo_kernel', 'conv_wgrad_ring_kernel')
+MAIN = ('conv_first_kernel', 'wgrad_first_bn_kernel', 'conv_igemm_kernel', 'conv_pp_kernel', 'conv_halo_kernel', 'conv_ring_kernel', 'conv_wgrad_kernel', 'conv_wgrad_halo_kernel', 'conv_wgrad_ring_kernel')
 REDUCE = ('conv_splitk_reduce_kernel', 'wgrad_reduce_kernel')
 conv = []  # main conv dispatches; a following split-K / slab reduce is folded into its time
 for r in rows:
