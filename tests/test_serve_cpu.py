@@ -264,3 +264,35 @@ def test_metrics_log_threadsafe(tmp_path):
     rows = list(csv.reader(open(tmp_path / "m.csv")))
     assert rows[0] == ["timestamp", "mean_curvature", "max_curvature", "mask_coverage_percent"]
     assert len(rows) == 1601 and all(len(r) == 4 for r in rows)
+
+
+def test_stage_copies_every_frame_layout():
+    """engine._stage (pinned staging of a host frame): torch's threaded copy for plain arrays, numpy
+    assignment for read-only decodes and negative-stride views; the staged bytes equal the frame."""
+    from robotic_discovery_platform_amd.serve.engine import _stage
+    rng = np.random.default_rng(0)
+    c = rng.integers(0, 256, (48, 64, 3), dtype=np.uint8)
+    d = rng.integers(0, 60000, (48, 64), dtype=np.uint16)
+    hc = torch.empty(48, 64, 3, dtype=torch.uint8)
+    hd = torch.empty(48, 64, dtype=torch.int16)
+    for src in (c, np.frombuffer(c.tobytes(), np.uint8).reshape(c.shape), c[:, ::-1], c[::-1]):
+        hc.zero_()
+        _stage(hc, src)
+        assert np.array_equal(hc.numpy(), src)
+    _stage(hd, d.view(np.int16))
+    assert np.array_equal(hd.numpy().view(np.uint16), d)
+
+
+def test_result_from_device_points():
+    """Device result vector -> CurvatureResult: status, curvatures and the 100 spline samples."""
+    from robotic_discovery_platform_amd.config import GeometryConfig
+    from robotic_discovery_platform_amd.geometry.curvature import Point, result_from_device
+    cfg = GeometryConfig()
+    res = np.zeros(8 + 3 * cfg.num_samples + 1)
+    res[4], res[5], res[6], res[7] = 0.5, 2.0, 123, 4567
+    pts = np.arange(3 * cfg.num_samples, dtype=np.float64) * 0.25
+    res[8:8 + 3 * cfg.num_samples] = pts
+    r = result_from_device(res, cfg)
+    assert r.status == "ok" and r.mean_curvature == 0.5 and r.max_curvature == 2.0
+    assert r.n_points == 4567 and len(r.spline_points) == cfg.num_samples
+    assert r.spline_points[1] == Point(0.75, 1.0, 1.25) and type(r.spline_points[0].x) is float
