@@ -150,16 +150,6 @@ class FramePipeline:
         self.ev1 = torch.cuda.Event(enable_timing=True)
         self.graphs = {}  # channel order of the staged colour frame (0 BGR, 1 RGB) -> hipGraph
         self.use_graph = graph
-        # split frame (graph mode, RDP_SERVE_SPLIT=1): the network part (preprocess + U-Net) and the
-        # geometry part are two graphs, and the depth frame (only the geometry reads it) is staged on
-        # the host and copied on a copy stream while the network runs: the depth staging and its H2D
-        # leave the frame's critical path. Measured (same box, 2 rounds): engine p50 0.604 / 0.588 ->
-        # 0.584 / 0.582 ms, p99 0.704 / 0.675 -> 0.619 / 0.597 ms, FPS 1617 / 1662 -> 1692 / 1677
-        self.split = graph and os.environ.get("RDP_SERVE_SPLIT", "1") != "0"
-        self.copy_stream = torch.cuda.Stream(dev) if self.split else None
-        self.ev_depth = torch.cuda.Event()
-        self.ev_geo = torch.cuda.Event()  # the geometry graph's reads of d_depth are done
-        self.graphs_geo = None
         self.lock = threading.Lock()
         self._rgb = 0
         if graph:
@@ -207,16 +197,8 @@ class FramePipeline:
         self.stream.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
-            if self.split:
-                self._net_program(rgb)
-            else:
-                self._device_program(rgb)
+            self._device_program(rgb)
         self.graphs[rgb] = g
-        if self.split and self.graphs_geo is None:
-            gg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gg, stream=self.stream):
-                self._geo_program()
-            self.graphs_geo = gg
 
     # ---------------------------------------------------------------- per frame
     def submit(self, color_bgr: np.ndarray, depth: np.ndarray, rgb: bool = False):
@@ -224,36 +206,17 @@ class FramePipeline:
         ``rgb``: the colour frame is RGB (as the server decodes it), not OpenCV's BGR."""
         if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
+        # colour staged and its H2D enqueued first; the depth frame is staged on the host while that
+        # copy runs. (Measured alternative: the network and the geometry as two graphs with the depth
+        # H2D on a copy stream under the network -- the cross-queue wait left a ~14 us gap between the
+        # graphs, about what it hid.)
         _stage(self.h_color, color_bgr)
-        depth16 = depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16)
         s = self.stream
-        if self.split:
-            with trace.range("serve.frame.enqueue"), torch.cuda.stream(s):
-                self.ev0.record(s)
-                self.d_color.copy_(self.h_color, non_blocking=True)
-                g = self.graphs.get(int(rgb))
-                if g is None:  # first frame in this channel order: capture its graph (stream-ordered)
-                    self._capture(int(rgb))
-                    g = self.graphs[int(rgb)]
-                g.replay()
-            _stage(self.h_depth, depth16)  # host copy while the network runs
-            cs = self.copy_stream
-            with torch.cuda.stream(cs):
-                cs.wait_event(self.ev_geo)  # the previous frame's geometry has read d_depth
-                self.d_depth.copy_(self.h_depth, non_blocking=True)
-                self.ev_depth.record(cs)
-            with torch.cuda.stream(s):
-                s.wait_event(self.ev_depth)
-                self.graphs_geo.replay()
-                self.ev_geo.record(s)
-                self.h_mask.copy_(self.mask, non_blocking=True)
-                self.h_res.copy_(self.geo.res, non_blocking=True)
-                self.ev1.record(s)
-            return
-        _stage(self.h_depth, depth16)
-        with trace.range("serve.frame.enqueue"), torch.cuda.stream(s):
+        with torch.cuda.stream(s):
             self.ev0.record(s)
             self.d_color.copy_(self.h_color, non_blocking=True)
+        _stage(self.h_depth, depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16))
+        with trace.range("serve.frame.enqueue"), torch.cuda.stream(s):
             self.d_depth.copy_(self.h_depth, non_blocking=True)
             if self.use_graph:
                 g = self.graphs.get(int(rgb))
