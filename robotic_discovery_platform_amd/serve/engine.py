@@ -79,13 +79,19 @@ class FrameResult:
 
 
 def _stage(dst: torch.Tensor, src: np.ndarray) -> None:
-    """Copy a host frame into its pinned staging tensor with torch's multi-threaded copy (a 640x480
-    RGB + depth frame: ~30 us vs ~130 us for numpy's single-threaded assignment, measured; the copy
-    sits on every frame's latency path). Negative-stride views take numpy's path. Read-only arrays
-    (PIL / np.frombuffer decodes) are only read here; torch's one-time "not writable" warning is
-    silenced."""
+    """Copy a host frame into its pinned staging tensor (on every frame's latency path).
+
+    RDP_STAGE_TORCH: 0 (default) = numpy assignment; 1 = torch's OpenMP-threaded copy (640x480 RGB +
+    depth: ~26 us p50 vs ~140 us, but its spinning workers compete with the codec / gRPC threads).
+    Measured with the colour H2D enqueued before the depth is staged (same box, 4 interleaved rounds):
+    engine p50 0.591-0.594 vs 0.575-0.595 ms (a wash), engine 1681-1693 vs 1535-1660 FPS, pipelined
+    2942-2966 vs 2529-3003 FPS, e2e 814-1021 vs 529-1005 FPS -- the numpy copy is steadier and
+    faster under load. (A worker pool of numpy band copies took ~375 us: GIL hand-offs.) Negative-
+    stride views always take numpy's path; read-only arrays are only read (torch's one-time "not
+    writable" warning is silenced)."""
     global _stage_warned
-    if _STAGE_TORCH and all(st >= 0 for st in src.strides) and src.dtype == np.dtype(str(dst.dtype).replace("torch.", "")):
+    if _STAGE_MODE == 1 and all(st >= 0 for st in src.strides) and \
+            src.dtype == np.dtype(str(dst.dtype).replace("torch.", "")):
         if src.flags.writeable or _stage_warned:
             dst.copy_(torch.from_numpy(src))
         else:
@@ -99,9 +105,7 @@ def _stage(dst: torch.Tensor, src: np.ndarray) -> None:
 
 
 _stage_warned = False
-# A/B knob (0 = numpy assignment). Measured (same box, 2 rounds): engine p50 0.691 / 0.680 -> 0.654 /
-# 0.649 ms, pipelined 2616 / 2514 -> 2772 / 2721 FPS, e2e streamed 899 / 741 -> 944 / 916 FPS
-_STAGE_TORCH = os.environ.get("RDP_STAGE_TORCH", "1") != "0"
+_STAGE_MODE = int(os.environ.get("RDP_STAGE_TORCH", "0"))
 
 
 def _logit(p: float) -> float:

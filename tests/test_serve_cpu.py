@@ -266,10 +266,13 @@ def test_metrics_log_threadsafe(tmp_path):
     assert len(rows) == 1601 and all(len(r) == 4 for r in rows)
 
 
-def test_stage_copies_every_frame_layout():
-    """engine._stage (pinned staging of a host frame): torch's threaded copy for plain arrays, numpy
-    assignment for read-only decodes and negative-stride views; the staged bytes equal the frame."""
-    from robotic_discovery_platform_amd.serve.engine import _stage
+@pytest.mark.parametrize("mode", [0, 1])
+def test_stage_copies_every_frame_layout(monkeypatch, mode):
+    """engine._stage (pinned staging of a host frame), numpy (0) and torch-threaded (1) modes, for plain,
+    read-only and negative-stride frames: the staged bytes equal the frame."""
+    from robotic_discovery_platform_amd.serve import engine
+    monkeypatch.setattr(engine, "_STAGE_MODE", mode)
+    _stage = engine._stage
     rng = np.random.default_rng(0)
     c = rng.integers(0, 256, (48, 64, 3), dtype=np.uint8)
     d = rng.integers(0, 60000, (48, 64), dtype=np.uint16)
