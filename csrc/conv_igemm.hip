@@ -1313,6 +1313,13 @@ extern "C" int rdp_conv_dgrad_pp_bnred(const void* x, long xbytes, int C, int pi
   const bool use256 = Cout % 256 == 0 && tiles256 >= 256;
   const bool use128 = !use256 && pp_env == 2 && Cout % 128 == 0 && tiles128 >= 256 && C >= 128;
   if (!use256 && !use128) return -1;
+  // RDP_PP_BNRED_WIDTH: 128 = only the 256 x 128 form takes the fused reduction (A/B: the 256-wide
+  // kernel has no VGPR headroom for the owner's y loads); 0 (default) = both
+  static const int width_env = [] {
+    const char* e = getenv("RDP_PP_BNRED_WIDTH");
+    return e ? atoi(e) : 0;
+  }();
+  if (width_env == 128 && use256) return -1;
   const int BN = use256 ? 256 : 128;
   const long grid = std::min<long>((M + 255) / 256 * (Cout / BN), 256);
   const long rows = grid / (Cout / BN) * 2;
