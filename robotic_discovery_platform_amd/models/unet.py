@@ -483,7 +483,9 @@ class UNetExecutor:
         # 7 remaining bn_relu_bwd_reduce passes at bs64). Measured dead end, off by default: bs64 1.2 %
         # SLOWER (3084-3095 vs 3119-3137 img/s, 3 interleaved rounds, same box; bs4 neutral) -- the owner's
         # y loads sit latency-exposed in the persistent kernel's per-tile epilogue, stalling both wave
-        # groups, which costs more than the separate 376 us (serialised) reduce pass it removes.
+        # groups, which costs more than the separate 376 us (serialised) reduce pass it removes. Restricted
+        # to the 256 x 128 form (RDP_PP_BNRED_WIDTH=128, which has VGPR headroom): neutral (3036-3044 vs
+        # 3032-3051 img/s, 3 rounds; both widths 3010-3023).
         self.dgrad_pp_bnred = self.dgrad_bnred and os.environ.get("RDP_DGRAD_PP_BNRED", "0") != "0"
         # first layer: BN-backward apply fused into its weight gradient (no dz tensor pass)
         self.fuse_first_wgrad = dev.type == "cuda" and os.environ.get("RDP_FUSE_FIRST_WGRAD", "1") != "0"
