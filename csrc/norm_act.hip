@@ -10,6 +10,7 @@
 // reduce (sum g, sum g*xhat) -> finalize (dgamma, dbeta, 3 apply coefficients) -> apply.
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 // Stage-1 column reduction: in[T][K] -> out[S][K], S row-chunks reduced by S x ceil(K/64) blocks
 // (many CUs, 4 independent accumulators per thread) so the finalize kernels read <= 64 rows.
@@ -40,20 +41,21 @@ __global__ void colsum_kernel(const float* __restrict__ in, int T, int K, int rp
 // sum over rows t = ty, ty + FIN_RG, ... of p[t][c] and p[t][C + c] (row stride 2C), fp64
 // (Measured dead end: 16 rows = 32 loads in flight per thread, tail rows clamped to row T - 1 and
 // dropped by a select -- bs 4 step 2.54 -> 2.65 ms, bs 64 20.43 -> 20.59 ms, same box interleaved.)
+template <int RG = FIN_RG>
 RDP_DEV void fin_rows(const float* __restrict__ p, int T, int C, int c, int ty, double& s, double& q) {
   double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
   int t = ty;
-  for (; t + 3 * FIN_RG < T; t += 4 * FIN_RG) {
+  for (; t + 3 * RG < T; t += 4 * RG) {
     const float a0 = p[(size_t)t * 2 * C + c], b0 = p[(size_t)t * 2 * C + C + c];
-    const float a1 = p[(size_t)(t + FIN_RG) * 2 * C + c], b1 = p[(size_t)(t + FIN_RG) * 2 * C + C + c];
-    const float a2 = p[(size_t)(t + 2 * FIN_RG) * 2 * C + c], b2 = p[(size_t)(t + 2 * FIN_RG) * 2 * C + C + c];
-    const float a3 = p[(size_t)(t + 3 * FIN_RG) * 2 * C + c], b3 = p[(size_t)(t + 3 * FIN_RG) * 2 * C + C + c];
+    const float a1 = p[(size_t)(t + RG) * 2 * C + c], b1 = p[(size_t)(t + RG) * 2 * C + C + c];
+    const float a2 = p[(size_t)(t + 2 * RG) * 2 * C + c], b2 = p[(size_t)(t + 2 * RG) * 2 * C + C + c];
+    const float a3 = p[(size_t)(t + 3 * RG) * 2 * C + c], b3 = p[(size_t)(t + 3 * RG) * 2 * C + C + c];
     s0 += (double)a0 + (double)a2;
     s1 += (double)a1 + (double)a3;
     q0 += (double)b0 + (double)b2;
     q1 += (double)b1 + (double)b3;
   }
-  for (; t < T; t += FIN_RG) {
+  for (; t < T; t += RG) {
     s0 += (double)p[(size_t)t * 2 * C + c];
     q0 += (double)p[(size_t)t * 2 * C + C + c];
   }
@@ -78,23 +80,37 @@ static const float* shrink_rows(const float* in, int T, int K, float* ws, int& r
   return ws;
 }
 
+static int fin_cpb() {  // channels per finalize block (RDP_FIN_CPB: 64 or 16)
+  static const int v = [] {
+    const char* e = getenv("RDP_FIN_CPB");
+    return e && atoi(e) == 16 ? 16 : 64;
+  }();
+  return v;
+}
+
 // coef layout: [0:C) mean, [C:2C) invstd, [2C:3C) scale = gamma*invstd, [3C:4C) shift = beta - mean*scale
+// CPB channels per block, 1024 / CPB row groups (CPB 16: four times the row groups, a quarter of the
+// dependent load rounds per thread, four times the blocks; RDP_FIN_CPB A/B). Measured neutral (same
+// box, 2 rounds: bs4 1587 / 1584 vs 1576 / 1590 img/s, bs64 3173 / 3154 vs 3157 / 3119): the ~7 us per
+// finalize is the kernel boundary, not the row walk. Default 64.
+template <int CPB>
 __global__ __launch_bounds__(64 * FIN_RG) void bn_finalize_kernel(const float* __restrict__ stats, int T, int C, double count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ rmean, float* __restrict__ rvar, long long* nbt,
                                    float momentum, float eps, float* __restrict__ coef) {
-  __shared__ double red[2][FIN_RG][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  constexpr int RG = 64 * FIN_RG / CPB;
+  __shared__ double red[2][RG][CPB];
+  const int tx = threadIdx.x % CPB, ty = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + tx;
   double s = 0.0, q = 0.0;
-  if (c < C) fin_rows(stats, T, C, c, ty, s, q);
+  if (c < C) fin_rows<RG>(stats, T, C, c, ty, s, q);
   red[0][ty][tx] = s;
   red[1][ty][tx] = q;
   __syncthreads();
   if (ty == 0 && c < C) {
     s = 0.0;
     q = 0.0;
-    for (int g = 0; g < FIN_RG; ++g) { s += red[0][g][tx]; q += red[1][g][tx]; }
+    for (int g = 0; g < RG; ++g) { s += red[0][g][tx]; q += red[1][g][tx]; }
     const double mean = s / count;
     double var = q / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -241,22 +257,24 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_kernel(const u16* __re
 
 // Backward finalize: dgamma, dbeta (written or accumulated into fp32 grads) and the apply
 // coefficients coef2 = [A | B | Cc]: dy = A*g + B*y + Cc.
+template <int CPB>
 __global__ __launch_bounds__(64 * FIN_RG) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int T, int C, double count,
                                        const float* __restrict__ gamma, const float* __restrict__ coef,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
                                        float* __restrict__ coef2) {
-  __shared__ double red[2][FIN_RG][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  constexpr int RG = 64 * FIN_RG / CPB;
+  __shared__ double red[2][RG][CPB];
+  const int tx = threadIdx.x % CPB, ty = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + tx;
   double s = 0.0, q = 0.0;
-  if (c < C) fin_rows(partial, T, C, c, ty, s, q);
+  if (c < C) fin_rows<RG>(partial, T, C, c, ty, s, q);
   red[0][ty][tx] = s;
   red[1][ty][tx] = q;
   __syncthreads();
   if (ty == 0 && c < C) {
     s = 0.0;
     q = 0.0;
-    for (int g = 0; g < FIN_RG; ++g) { s += red[0][g][tx]; q += red[1][g][tx]; }
+    for (int g = 0; g < RG; ++g) { s += red[0][g][tx]; q += red[1][g][tx]; }
     if (dbeta) dbeta[c] = (float)s;
     if (dgamma) dgamma[c] = (float)q;
     const double mean = coef[c], inv = coef[C + c], gm = gamma[c];
@@ -323,7 +341,9 @@ int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* g
                     float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef, float* ws,
                     hipStream_t s) {
   stats = shrink_rows(stats, T, 2 * C, ws, T, s);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
+  if (fin_cpb() == 16) hipLaunchKernelGGL(bn_finalize_kernel<16>, dim3((C + 15) / 16), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
+                     beta, rmean, rvar, nbt, momentum, eps, coef);
+  else hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
                      beta, rmean, rvar, nbt, momentum, eps, coef);
   return 0;
 }
@@ -358,7 +378,9 @@ int rdp_bn_relu_bwd_reduce(const void* da, int dapitch, const void* y, int ypitc
 int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const float* gamma, const float* coef,
                         float* dgamma, float* dbeta, float* coef2, float* ws, hipStream_t s) {
   partial = shrink_rows(partial, T, 2 * C, ws, T, s);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
+  if (fin_cpb() == 16) hipLaunchKernelGGL(bn_bwd_finalize_kernel<16>, dim3((C + 15) / 16), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
+                     coef, dgamma, dbeta, coef2);
+  else hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
                      coef, dgamma, dbeta, coef2);
   return 0;
 }
