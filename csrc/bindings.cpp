@@ -5,6 +5,7 @@
 // kernel never sees an inconsistent view; the kernels themselves use buffer descriptors sized from
 // these views (out-of-range = zero / dropped, never a fault).
 #include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <functional>
@@ -93,6 +94,34 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// ---- device placement: every binding runs on the GPU that holds its tensors -------------------------
+// `on_device(fn)` wraps a binding: it checks that every GPU tensor argument (plain or optional) lives
+// on ONE device and makes that device current for the call (HIPGuard), so the launches below go to
+// that device's current stream -- a per-GPU serving replica (serve/engine.py EnginePool) launches on
+// its own GPU whatever device the calling thread had current. Mixed devices raise.
+void note_device(int& dev, const torch::Tensor& t) {
+  if (!t.defined() || !t.is_cuda()) return;
+  const int d = t.get_device();
+  TORCH_CHECK(dev < 0 || d == dev, "tensor arguments on different GPUs (cuda:", dev, " and cuda:", d, ")");
+  dev = d;
+}
+void note_device(int& dev, const c10::optional<torch::Tensor>& t) {
+  if (t) note_device(dev, *t);
+}
+template <class T>
+void note_device(int&, const T&) {}
+
+template <class R, class... A>
+auto on_device(R (*fn)(A...)) {
+  return [fn](A... args) -> R {
+    int dev = -1;
+    (note_device(dev, args), ...);
+    c10::hip::OptionalHIPGuard guard;
+    if (dev >= 0) guard.set_index((c10::DeviceIndex)dev);
+    return fn(std::move(args)...);
+  };
+}
+
 // ---- launch plans: the training step recorded once and replayed from C++ --------------------------
 // A plan is the step's launch sequence: every kernel launch of the bindings below (RDP_PLAN) and every
 // cross-stream dependency (stream_wait), in issue order, each with the HIP stream it was issued on.
@@ -137,13 +166,34 @@ hipStream_t unplanned_stream() {
   return cur_stream();
 }
 
+// One reusable timing-free event per device and host thread for the eager path: hipStreamWaitEvent
+// captures the event's most recent record at the time of the call, so re-recording it for the next
+// wait is safe (no create / destroy per call). A plan being recorded owns one event per wait.
+hipEvent_t wait_event(hipStream_t s) {
+  int dev = 0;
+  TORCH_CHECK(hipStreamGetDevice(s, &dev) == hipSuccess, "stream_wait: stream device");
+  thread_local std::vector<hipEvent_t> evs;
+  if ((int)evs.size() <= dev) evs.resize(dev + 1, nullptr);
+  if (!evs[dev]) {
+    c10::hip::HIPGuard g((c10::DeviceIndex)dev);
+    TORCH_CHECK(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming) == hipSuccess, "stream_wait: event");
+  }
+  return evs[dev];
+}
+
 void stream_wait(long waiter, long waitee) {
   const hipStream_t w = (hipStream_t)waiter, e = (hipStream_t)waitee;
   hipEvent_t ev;
-  TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "stream_wait: event");
+  if (g_rec) {
+    int dev = 0;
+    TORCH_CHECK(hipStreamGetDevice(e, &dev) == hipSuccess, "stream_wait: stream device");
+    c10::hip::HIPGuard g((c10::DeviceIndex)dev);
+    TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "stream_wait: event");
+  } else {
+    ev = wait_event(e);
+  }
   TORCH_CHECK(hipEventRecord(ev, e) == hipSuccess && hipStreamWaitEvent(w, ev, 0) == hipSuccess, "stream_wait");
   if (g_rec) g_rec->ops.push_back(PlanOp{1, w, e, ev, nullptr});
-  else hipEventDestroy(ev);
 }
 
 void plan_begin() {
@@ -1057,7 +1107,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_compile", &plan_compile);
   m.def("plan_size", &plan_size);
   m.def("plan_free", &plan_free);
-  m.def("conv_fwd", &conv_fwd, py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
+  m.def("conv_fwd", on_device(&conv_fwd), py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
         py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
         py::arg("ws") = py::none(), py::arg("pool") = py::none(), py::arg("up") = py::none(),
         py::arg("up_oy") = 0, py::arg("up_ox") = 0);
@@ -1068,67 +1118,67 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("conv_stats_rows", &conv_stats_rows);
   m.def("conv_set_debug_flags", [](int f) { rdp_conv_set_debug_flags(f); }, "A/B flags for microbenchmarks");
-  m.def("conv_wgrad", &conv_wgrad);
-  m.def("wgrad_first_bn", &wgrad_first_bn);
-  m.def("conv_dgrad_pp_bnred", &conv_dgrad_pp_bnred);
+  m.def("conv_wgrad", on_device(&conv_wgrad));
+  m.def("wgrad_first_bn", on_device(&wgrad_first_bn));
+  m.def("conv_dgrad_pp_bnred", on_device(&conv_dgrad_pp_bnred));
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
-  m.def("bn_finalize", &bn_finalize);
-  m.def("bn_eval_coef", &bn_eval_coef);
-  m.def("bn_relu_apply", &bn_relu_apply);
-  m.def("bn_relu_bwd_reduce", &bn_relu_bwd_reduce);
-  m.def("conv_dgrad_bnred", &conv_dgrad_bnred);
-  m.def("bn_bwd_finalize", &bn_bwd_finalize);
-  m.def("bn_relu_bwd_apply", &bn_relu_bwd_apply);
-  m.def("maxpool2_fwd", &maxpool2_fwd);
-  m.def("maxpool2_bwd", &maxpool2_bwd);
-  m.def("bn_relu_apply_pool", &bn_relu_apply_pool);
-  m.def("maxpool2_bwd_bn_reduce", &maxpool2_bwd_bn_reduce);
-  m.def("upsample2_fwd", &upsample2_fwd, py::arg("x"), py::arg("out"), py::arg("oy"), py::arg("ox"),
+  m.def("bn_finalize", on_device(&bn_finalize));
+  m.def("bn_eval_coef", on_device(&bn_eval_coef));
+  m.def("bn_relu_apply", on_device(&bn_relu_apply));
+  m.def("bn_relu_bwd_reduce", on_device(&bn_relu_bwd_reduce));
+  m.def("conv_dgrad_bnred", on_device(&conv_dgrad_bnred));
+  m.def("bn_bwd_finalize", on_device(&bn_bwd_finalize));
+  m.def("bn_relu_bwd_apply", on_device(&bn_relu_bwd_apply));
+  m.def("maxpool2_fwd", on_device(&maxpool2_fwd));
+  m.def("maxpool2_bwd", on_device(&maxpool2_bwd));
+  m.def("bn_relu_apply_pool", on_device(&bn_relu_apply_pool));
+  m.def("maxpool2_bwd_bn_reduce", on_device(&maxpool2_bwd_bn_reduce));
+  m.def("upsample2_fwd", on_device(&upsample2_fwd), py::arg("x"), py::arg("out"), py::arg("oy"), py::arg("ox"),
         py::arg("coef") = py::none());
-  m.def("upT_shuffle", &upT_shuffle);
-  m.def("upT_unshuffle", &upT_unshuffle);
-  m.def("colsum_bf16", &colsum_bf16);
-  m.def("upsample2_bwd", &upsample2_bwd, py::arg("dout"), py::arg("dx"), py::arg("oy"), py::arg("ox"),
+  m.def("upT_shuffle", on_device(&upT_shuffle));
+  m.def("upT_unshuffle", on_device(&upT_unshuffle));
+  m.def("colsum_bf16", on_device(&colsum_bf16));
+  m.def("upsample2_bwd", on_device(&upsample2_bwd), py::arg("dout"), py::arg("dx"), py::arg("oy"), py::arg("ox"),
         py::arg("y") = py::none(), py::arg("coef") = py::none(), py::arg("partial") = py::none());
   m.def("head_partial_blocks", &head_partial_blocks);
-  m.def("head_fwd", &head_fwd, py::arg("a"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("logits"),
+  m.def("head_fwd", on_device(&head_fwd), py::arg("a"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("logits"),
         py::arg("partial"), py::arg("sums"), py::arg("loss"), py::arg("dice_w"), py::arg("dice_eps"),
         py::arg("coef") = py::none(), py::arg("gpart") = py::none(), py::arg("bnpart") = py::none(),
         py::arg("gscale") = 1.0);
-  m.def("head_grad_finalize", &head_grad_finalize);
-  m.def("head_bwd", &head_bwd, py::arg("a"), py::arg("w"), py::arg("logits"), py::arg("target"), py::arg("sums"),
+  m.def("head_grad_finalize", on_device(&head_grad_finalize));
+  m.def("head_bwd", on_device(&head_bwd), py::arg("a"), py::arg("w"), py::arg("logits"), py::arg("target"), py::arg("sums"),
         py::arg("da"), py::arg("partial"), py::arg("gw"), py::arg("gb"), py::arg("dice_w"), py::arg("dice_eps"),
         py::arg("gscale"), py::arg("coef") = py::none(), py::arg("bnpart") = py::none());
-  m.def("head_bn_bwd_apply", &head_bn_bwd_apply);
-  m.def("head_mask", &head_mask);
-  m.def("conv_head_mask", &conv_head_mask);
-  m.def("adam", &adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
+  m.def("head_bn_bwd_apply", on_device(&head_bn_bwd_apply));
+  m.def("head_mask", on_device(&head_mask));
+  m.def("conv_head_mask", on_device(&conv_head_mask));
+  m.def("adam", on_device(&adam), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
         py::arg("inc") = true);
-  m.def("cast_bf16", &cast_bf16);
-  m.def("wprep", &wprep, py::arg("master"), py::arg("out"), py::arg("segs"), py::arg("nseg"),
+  m.def("cast_bf16", on_device(&cast_bf16));
+  m.def("wprep", on_device(&wprep), py::arg("master"), py::arg("out"), py::arg("segs"), py::arg("nseg"),
         py::arg("step") = py::none());
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
-  m.def("geo_edges", &geo_edges, py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),
+  m.def("geo_edges", on_device(&geo_edges), py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),
         py::arg("cy"), py::arg("scale"), py::arg("work_i"), py::arg("work_d"), py::arg("pts"), py::arg("npts"),
         py::arg("out"), py::arg("kout"), py::arg("nbins"), py::arg("top"), py::arg("min_points"),
         py::arg("edges") = py::none(), py::arg("hdr") = py::none(), py::arg("m256") = py::none(),
         py::arg("cov") = py::none(), py::arg("sorted") = py::none(), py::arg("gperm") = py::none());
   m.def("geo_nblocks", &geo_nblocks);
-  m.def("geo_spline", &geo_spline, py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
+  m.def("geo_spline", on_device(&geo_spline), py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
         py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
         py::arg("presorted") = false);
   m.def("png_decode", &png_decode);
   m.def("png_encode_gray8", &png_encode_gray8);
-  m.def("resize_area_u8", &resize_area_u8);
+  m.def("resize_area_u8", on_device(&resize_area_u8));
   m.def("area_maxtap", &rdp_area_maxtap);
   m.def("geo_spline_res_len", &rdp_geo_spline_res_len);
   m.def("geo_work_ints", &geo_work_ints);
-  m.def("preprocess", &preprocess, py::arg("bgr"), py::arg("ystart"), py::arg("ysize"), py::arg("yw"),
+  m.def("preprocess", on_device(&preprocess), py::arg("bgr"), py::arg("ystart"), py::arg("ysize"), py::arg("yw"),
         py::arg("xstart"), py::arg("xsize"), py::arg("xw"), py::arg("out"), py::arg("rgb") = 0);
-  m.def("mask_upsample", &mask_upsample);
+  m.def("mask_upsample", on_device(&mask_upsample));
   m.def("splev", &splev);
   m.def("fit_curvature", &fit_curvature);
 }

@@ -23,6 +23,7 @@ inline void put32(std::vector<uint8_t>& v, uint32_t x) {
   v.push_back(x >> 24); v.push_back(x >> 16); v.push_back(x >> 8); v.push_back(x);
 }
 const uint8_t kSig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+const uint64_t kMaxPixels = 89478485;  // PIL Image.MAX_IMAGE_PIXELS
 
 struct Hdr {
   uint32_t w = 0, h = 0;
@@ -40,6 +41,13 @@ int parse_header(const uint8_t* d, long n, Hdr& hd) {
   hd.interlace = d[28];
   if (hd.w == 0 || hd.h == 0 || hd.w > (1u << 16) || hd.h > (1u << 16)) return -1;
   if (hd.ct != 0 || (hd.bd != 8 && hd.bd != 16) || hd.interlace != 0 || d[26] != 0 || d[27] != 0) return -2;
+  // The size comes from an untrusted request: refuse it before anything is allocated from it.
+  // (a) PIL's decompression-bomb limit (Image.MAX_IMAGE_PIXELS), the bound of the reader this replaces;
+  // (b) the filtered scanlines cannot be larger than deflate can expand the whole file to (at most
+  //     1032:1), so a header-only "image" of a few dozen bytes cannot claim gigabytes.
+  const uint64_t px = (uint64_t)hd.w * hd.h;
+  const uint64_t raw = ((uint64_t)hd.w * (hd.bd / 8) + 1) * hd.h;
+  if (px > kMaxPixels || raw > (uint64_t)n * 1032u) return -1;
   return 0;
 }
 

@@ -43,6 +43,19 @@ class UpTSpec:
 
 
 @dataclass
+class HeadSpec:
+    """The 1x1 head ``outc`` (conv + bias): its gradients are final as soon as backward starts, so its
+    DDP hook fires first (before any conv layer's)."""
+    name: str = "outc"
+
+    def param_names(self) -> List[str]:
+        return [self.name + ".conv.weight", self.name + ".conv.bias"]
+
+
+HEAD_SPEC = HeadSpec()
+
+
+@dataclass
 class ConvSpec:
     name: str  # reference module path of the conv, e.g. "down1.maxpool_conv.1.double_conv.0"
     bn: str  # reference module path of its BatchNorm
@@ -53,7 +66,22 @@ class ConvSpec:
     cin_real: int = 0
 
     def param_names(self) -> List[str]:
-        return [self.name + ".weight", self.bn + ".weight", self.bn + ".bias"]
+        """The conv weight (its BN's gamma / beta are final earlier: :class:`BNHook`)."""
+        return [self.name + ".weight"]
+
+
+@dataclass
+class BNHook:
+    """Gradient hook of a conv layer's BatchNorm: gamma / beta gradients are final right after the BN
+    backward (main stream), before that layer's weight gradient (side stream) is."""
+    conv: ConvSpec
+
+    @property
+    def name(self) -> str:
+        return self.conv.bn
+
+    def param_names(self) -> List[str]:
+        return [self.conv.bn + ".weight", self.conv.bn + ".bias"]
 
 
 class ParamStore:
@@ -194,7 +222,9 @@ class UNetNative(nn.Module):
                     own[k].copy_(v.to(own[k].device))
                 elif k in ownb:
                     ownb[k].copy_(v.to(ownb[k].device))
-        self._build_derived()
+        # the derived layouts are rebuilt IN PLACE: launch plans and serving graphs captured against
+        # these buffers stay valid and see the new weights
+        self.refresh_weights()
         return missing, unexpected
 
     # ---- derived bf16 weight layouts ----
@@ -840,6 +870,8 @@ class UNetExecutor:
             # first layer: its pre-BN gradient feeds only the weight gradient, so the BN-backward apply
             # runs inside that wgrad (wgrad_first_bn) and dz is never stored
             self._bn_bwd(C, L, None, apply=False)
+            if hooks is not None:
+                hooks(BNHook(sp))
 
             def fused(slab):
                 r = C.wgrad_first_bn(L.x1, L.da, L.y, L.coef, L.coef2, slab, gw, sp.cin_real, 0, L.splits)
@@ -856,6 +888,8 @@ class UNetExecutor:
                 self._on_side(lambda: hooks(sp))
             return
         self._bn_bwd(C, L, head_gscale)
+        if hooks is not None:  # gamma / beta gradients are final (main stream)
+            hooks(BNHook(sp))
         # wgrad (latency-bound on x / dY streams) overlaps the main stream's dgrad + next BN backward;
         # all wgrads share the slab, so they stay serialized on the one side stream
         if self.slab_main is not None and L is self.down_layers[0][0]:
@@ -917,6 +951,8 @@ class UNetExecutor:
             C.head_bwd(self.final, head_w, self.logits, self.target, self.loss_sums, last.da, self.head_partial, hgw,
                        hgb, self.dice_w, self.dice_eps, gscale)
         self._head_fwd_grads = False
+        if grad_hook is not None:  # the head's gradients are final now: its bucket may go first
+            grad_hook(HEAD_SPEC)
         for i in range(D, 0, -1):
             la, lb = self.up_layers[i - 1]
             self._conv_bwd(C, lb, grad_hook, head_gscale if i == D else None)
@@ -960,19 +996,32 @@ class UNetExecutor:
         self._conv_bwd(C, l0, grad_hook)
 
     def backward_order(self) -> List:
-        """Conv layers in the order their gradients become final during backward()."""
-        D = self.m.depth
-        out = []
-        for i in range(D, 0, -1):
-            la, lb = self.up_layers[i - 1]
-            out += [lb.spec, la.spec]
-            if not self.m.bilinear:
-                out.append(self.m.up_specs[i - 1])
-        for i in range(D, 0, -1):
-            la, lb = self.down_layers[i]
-            out += [lb.spec, la.spec]
-        l0, l1 = self.down_layers[0]
-        return out + [l1.spec, l0.spec]
+        """Gradient hooks in the order backward() fires them (see :func:`backward_hook_order`)."""
+        return backward_hook_order(self.m.specs, self.m.up_specs, self.m.depth)
+
+
+def backward_hook_order(specs: List[ConvSpec], up_specs: List[UpTSpec], depth: int) -> List:
+    """The gradient hooks of ``UNetExecutor.backward`` in firing order: the head first (its gradients
+    come with the loss), then per conv layer from the output back to the input its BN's gamma / beta
+    (:class:`BNHook`) and its weight; a transposed decoder's ConvTranspose2d after its Up block's
+    first conv. ``specs`` is the forward order of :func:`unet_conv_specs`."""
+    D = depth
+    enc = specs[: 2 * (D + 1)]
+    dec = specs[2 * (D + 1):]
+    out: List = [HEAD_SPEC]
+
+    def conv(sp):
+        out.extend([BNHook(sp), sp])
+
+    for i in range(D, 0, -1):
+        conv(dec[2 * (i - 1) + 1])
+        conv(dec[2 * (i - 1)])
+        if up_specs:
+            out.append(up_specs[i - 1])
+    for i in range(D, -1, -1):
+        conv(enc[2 * i + 1])
+        conv(enc[2 * i])
+    return out
 
 
 class NativeAdam:
@@ -992,6 +1041,10 @@ class NativeAdam:
         C.adam(st.flat, st.grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr, self.betas[0], self.betas[1], self.eps,
                self.wd, gscale, st.step, False)
         C.wprep(st.flat, self.m.derived, self.m._segs, self.m._nseg, st.step)  # + the step counter advance
+
+    def hyper_key(self) -> tuple:
+        """The hyper-parameters a recorded launch plan bakes in (NativeTrainer re-records on change)."""
+        return (float(self.lr), tuple(float(b) for b in self.betas), float(self.eps), float(self.wd))
 
     def state_dict(self):
         st = self.m.store

@@ -11,6 +11,9 @@ Design (MI355X-first):
   * A bucket is launched (``all_reduce(SUM, async_op=True)``) as soon as the last parameter in it is
     final; RCCL's internal stream waits on the compute stream at issue time and runs concurrently
     with the remaining backward kernels. ``finish()`` makes the compute stream wait for all buckets.
+  * A parameter of at least half a bucket that would overflow the open bucket starts a new one, so
+    the small decoder layers whose gradients are final first (outc, up4 .. up1.conv.3, 12.5 MB) go
+    out before the 18.9 MB up1.conv.0 gradient exists.
   * Bucket size: 17.3 M params = 69 MB fp32. On xGMI each GPU has 7 links (~153 GB/s each), and a
     ring all-reduce moves 2(n-1)/n of the bucket per GPU, so ~16 MB buckets (≈4-5 per step) keep
     every bucket well above the latency-bound regime while still giving backward-overlap.
@@ -59,6 +62,11 @@ class FlatBucketer:
             end_of[n] = ordered[i + 1][1] if i + 1 < len(ordered) else grad_flat.numel()
         for name, lo, hi in reversed(ordered):
             hi = end_of[name]
+            if cur_hi is not None and (cur_hi - lo) > cap and hi - lo >= cap // 2:
+                # a parameter of at least half a bucket that would overflow the open bucket closes it
+                # first: the gradients already final go out now instead of waiting for the big one
+                self._close(cur_lo, cur_hi, names)
+                cur_hi, names = None, []
             if cur_hi is None:
                 cur_hi, cur_lo, names = hi, lo, [name]
             else:

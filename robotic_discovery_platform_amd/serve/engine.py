@@ -118,20 +118,29 @@ class FramePipeline:
 
     def __init__(self, model, K: np.ndarray, depth_scale: float, H: int = 480, W: int = 640, size: int = 256,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 device: Optional[torch.device] = None):
-        from ..models.unet import UNetExecutor, UNetNative
-        from ..ops import native
+                 device: Optional[torch.device] = None, rgb: bool = False):
+        from ..models.unet import UNetNative
         if not isinstance(model, UNetNative):
             raise TypeError("FramePipeline needs the native UNet (UNetNative); use CpuFramePipeline otherwise")
+        dev = _norm_device(device if device is not None else model.store.device)
+        if dev != _norm_device(model.store.device):
+            raise ValueError(f"FramePipeline on {dev} for a model on {model.store.device}: replicate it first")
+        # everything below (buffers, stream, graph capture) belongs to the model's GPU, whatever device
+        # the calling thread has current
+        with torch.cuda.device(dev):
+            self._init(model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb)
+
+    def _init(self, model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb):
+        from ..models.unet import UNetExecutor
+        from ..ops import native
         self.C = native()
         self.model = model
-        self.dev = device or model.store.device
+        self.dev = dev
         self.H, self.W, self.S = H, W, size
         self.K = np.asarray(K, np.float64)
         self.scale = float(depth_scale)
         self.thr_logit = _logit(threshold)
         self.cfg = geo_cfg or GeometryConfig()
-        dev = self.dev
         self.stream = torch.cuda.Stream(dev)
         self.ex = UNetExecutor(model, 1, size, size, False, "bce", 1.0)
         # AA resize tables (device)
@@ -155,9 +164,10 @@ class FramePipeline:
         self.graphs = {}  # channel order of the staged colour frame (0 BGR, 1 RGB) -> hipGraph
         self.use_graph = graph
         self.lock = threading.Lock()
-        self._rgb = 0
+        # the graph for the channel order this pipeline will be fed (the gRPC server decodes to RGB) is
+        # captured here, at build time, never on a live request
         if graph:
-            self._capture(0)
+            self._capture(int(rgb))
         else:
             self.refresh_weights()
 
@@ -184,10 +194,15 @@ class FramePipeline:
 
     def refresh_weights(self):
         """Recompute the BN-fold coefficients from the current weights / running stats (after a
-        hot reload). The captured graph reads them from fixed buffers, so it stays valid."""
-        with torch.cuda.stream(self.stream):
+        hot reload). The captured graph reads them -- and every weight layout -- from buffers that a
+        reload rewrites in place (``UNetNative.load_state_dict``), so it stays valid."""
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
             self.ex.prepare_eval()
         self.stream.synchronize()
+
+    def wait_idle(self):
+        """Block until this pipeline's last submitted frame has left the GPU (its result is dropped)."""
+        self.ev1.synchronize()
 
     @property
     def graph(self):
@@ -196,12 +211,15 @@ class FramePipeline:
     def _capture(self, rgb: int):
         if not self.graphs:
             self.refresh_weights()
-        with torch.cuda.stream(self.stream):
-            self._device_program(rgb)  # warm-up (lazy allocations, kernel loading)
-        self.stream.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=self.stream):
-            self._device_program(rgb)
+        with torch.cuda.device(self.dev):
+            with torch.cuda.stream(self.stream):
+                self._device_program(rgb)  # warm-up (lazy allocations, kernel loading)
+            self.stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            # thread-local capture: other server threads may use the GPU meanwhile (a late capture of
+            # the other channel order happens on a live server)
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+                self._device_program(rgb)
         self.graphs[rgb] = g
 
     # ---------------------------------------------------------------- per frame
@@ -216,11 +234,11 @@ class FramePipeline:
         # graphs, about what it hid.)
         _stage(self.h_color, color_bgr)
         s = self.stream
-        with torch.cuda.stream(s):
+        with torch.cuda.device(self.dev), torch.cuda.stream(s):
             self.ev0.record(s)
             self.d_color.copy_(self.h_color, non_blocking=True)
         _stage(self.h_depth, depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16))
-        with trace.range("serve.frame.enqueue"), torch.cuda.stream(s):
+        with trace.range("serve.frame.enqueue"), torch.cuda.device(self.dev), torch.cuda.stream(s):
             self.d_depth.copy_(self.h_depth, non_blocking=True)
             if self.use_graph:
                 g = self.graphs.get(int(rgb))
@@ -269,6 +287,9 @@ class CpuFramePipeline:
     def refresh_weights(self):
         pass  # the torch module reads its parameters directly
 
+    def wait_idle(self):
+        self._pending = None
+
     def submit(self, color_bgr: np.ndarray, depth: np.ndarray, rgb: bool = False):
         if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
@@ -296,13 +317,30 @@ class CpuFramePipeline:
                                              "fit_ms": (time.perf_counter() - t1) * 1e3})
 
 
+def _norm_device(device) -> torch.device:
+    """``cuda`` without an index -> ``cuda:<current>`` (so equal devices compare equal)."""
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
+def _on(device):
+    """``torch.cuda.device(device)`` for a GPU device, else a no-op context."""
+    device = torch.device(device)
+    return torch.cuda.device(device) if device.type == "cuda" else contextlib.nullcontext()
+
+
 def replicate_model(model, device: torch.device):
-    """A copy of ``model`` on ``device`` (same architecture, weights and BN statistics)."""
+    """A copy of ``model`` on ``device`` (same architecture, weights and BN statistics); built with
+    ``device`` current, so every launch of its construction (bf16 shadow, weight re-layouts) runs on
+    that GPU."""
     if _is_native(model):
         from ..models.unet import UNetNative
-        rep = UNetNative(model.n_channels, model.n_classes, bilinear=model.bilinear, base_width=model.base_width,
-                         depth=model.depth, device=device)
-        rep.load_state_dict({k: v.detach() for k, v in model.state_dict().items()})
+        with _on(device):
+            rep = UNetNative(model.n_channels, model.n_classes, bilinear=model.bilinear, base_width=model.base_width,
+                             depth=model.depth, device=torch.device(device))
+            rep.load_state_dict({k: v.detach() for k, v in model.state_dict().items()})
         return rep.eval()
     import copy
     return copy.deepcopy(model).to(device).eval()
@@ -322,8 +360,9 @@ class EnginePool:
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 devices=None):
+                 devices=None, rgb: bool = False):
         self.model = model
+        self.rgb = rgb  # channel order of the frames this pool will be fed (graphs captured for it)
         self.args = dict(K=K, depth_scale=depth_scale, size=size, threshold=threshold, geo_cfg=geo_cfg)
         self.graph = graph
         self.n = max(1, n)
@@ -343,7 +382,7 @@ class EnginePool:
     def _new(self, r: int, H, W):
         m = self.replicas[r]
         if self.gpu:
-            return FramePipeline(m, H=H, W=W, graph=self.graph, device=self.devices[r], **self.args)
+            return FramePipeline(m, H=H, W=W, graph=self.graph, device=self.devices[r], rgb=self.rgb, **self.args)
         return CpuFramePipeline(m, H=H, W=W, **self.args)
 
     def _get(self, r: int, H, W) -> "queue.Queue":
@@ -377,11 +416,13 @@ class EnginePool:
                     q.put(p)
 
     def load_state_dict(self, sd):
-        """Hot reload: copy new weights into every replica (call inside ``exclusive()``)."""
-        for m in self.replicas:
-            m.load_state_dict(sd)
-            if hasattr(m, "refresh_weights"):
-                m.refresh_weights()
+        """Hot reload: copy new weights into every replica, each with its own GPU current (call inside
+        ``exclusive()``)."""
+        for m, d in zip(self.replicas, self.devices):
+            with _on(d):
+                m.load_state_dict(sd)
+                if hasattr(m, "refresh_weights"):
+                    m.refresh_weights()
 
     @staticmethod
     def refresh_weights(pipelines):
@@ -450,6 +491,18 @@ class EngineSession:
         while self.inflight:
             out.append(self._collect_one())
         return out
+
+    def close(self) -> None:
+        """Give every pipeline this session holds back to its pool without building results (a stream
+        that ended early: client cancel, transport error, abort). Idempotent."""
+        while self.inflight:
+            _, p, q = self.inflight.popleft()
+            try:
+                p.wait_idle()
+            except Exception:  # the pipeline goes back either way
+                pass
+            finally:
+                q.put(p)
 
 
 def _model_device(model) -> torch.device:

@@ -139,6 +139,16 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         ``more()`` tells whether the client has already sent the next frame."""
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         END = object()
+        stop = threading.Event()  # the handler is gone (stream ended early): the reader must not block
+
+        def put(item) -> bool:
+            while not stop.is_set():
+                try:
+                    q.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    continue
+            return False
 
         def reader():
             try:
@@ -149,27 +159,31 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                         cb, db = self.faults.corrupt_request(i, cb, db)
                     fc = self._pool.submit(decode_image, cb, True, "RGB")  # no BGR flip: the engine takes RGB
                     fd = self._pool.submit(decode_image, db, False)
-                    q.put((t, fc, fd, None))
+                    if not put((t, fc, fd, None)):
+                        return
             except Exception as e:  # surface transport errors in the handler thread
-                q.put((None, None, None, e))
-            q.put(END)
+                put((None, None, None, e))
+            put(END)
 
         th = threading.Thread(target=reader, daemon=True)
         th.start()
-        while True:
-            item = q.get()
-            if item is END:
-                return
-            if item[3] is not None:
-                raise item[3]
-            t, fc, fd, _ = item
-            try:
-                color, depth = fc.result(), fd.result()
-                err = None
-            except Exception as e:
-                color = depth = None
-                err = e
-            yield t, color, depth, err, lambda: q.qsize() > 0
+        try:
+            while True:
+                item = q.get()
+                if item is END:
+                    return
+                if item[3] is not None:
+                    raise item[3]
+                t, fc, fd, _ = item
+                try:
+                    color, depth = fc.result(), fd.result()
+                    err = None
+                except Exception as e:
+                    color = depth = None
+                    err = e
+                yield t, color, depth, err, lambda: q.qsize() > 0
+        finally:
+            stop.set()
 
     def close(self) -> None:
         """Stop the codec pool (its threads must not outlive the gRPC server at interpreter exit)."""
@@ -246,8 +260,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                 self._log(resp, r)
                 yield resp
 
+        frames = self._decoded(request_iterator)
         try:
-            for i, (t_read, color, depth, err, more) in enumerate(self._decoded(request_iterator)):
+            for i, (t_read, color, depth, err, more) in enumerate(frames):
                 t_start = time.perf_counter()
                 times[i] = (t_read, t_start)
                 if err is not None:
@@ -266,6 +281,11 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             context.set_code(grpc.StatusCode.INTERNAL)
             context.set_details(f"Internal error during analysis: {e}")
             yield pb.AnalysisResponse()
+        finally:
+            # however the stream ends (normal end, client cancel -> GeneratorExit at a yield, transport
+            # error, abort), the session's in-flight pipelines go back to the pool and the reader stops
+            sess.close()
+            frames.close()
 
 
 class ModelWatcher(threading.Thread):
@@ -329,7 +349,7 @@ def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_s
         return None
     metrics = MetricsLog(cfg.metrics_log)
     engine = EnginePool(model, K, ds, n=pool_size or cfg.replicas_per_device, threshold=cfg.mask_threshold,
-                        graph=cfg.graph, size=cfg.model_img_size, devices=devices)
+                        graph=cfg.graph, size=cfg.model_img_size, devices=devices, rgb=True)
     service = VisionAnalysisService(engine, metrics, frame_errors=cfg.frame_errors, faults=faults)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.max_workers))
     pb.add_VisionAnalysisServiceServicer_to_server(service, server)

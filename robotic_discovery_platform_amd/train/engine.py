@@ -81,7 +81,6 @@ class NativeTrainer:
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
             self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb,
                                          comm_dtype=torch.bfloat16 if grad_comm == "bf16" else None)
-            self._layer_params = {sp.name: sp.param_names() for sp in list(model.specs) + list(model.up_specs)}
             self.ex.set_sync_bn(enabled=sync_bn)
         if graph == "auto":
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
@@ -113,7 +112,8 @@ class NativeTrainer:
                 pass
 
     def _hook(self, spec):
-        self.bucketer.mark_ready(self._layer_params[spec.name])
+        """Gradient hook of one layer (head, BN, conv or ConvTranspose2d: ``spec.param_names()``)."""
+        self.bucketer.mark_ready(spec.param_names())
 
     def _step_body(self):
         ex = self.ex
@@ -122,8 +122,7 @@ class NativeTrainer:
         if self.bucketer is not None:
             self.bucketer.reset()
             with trace.range("train.backward+allreduce"):
-                ex.backward(grad_hook=self._hook)
-                self.bucketer.mark_ready(["outc.conv.weight", "outc.conv.bias"])
+                ex.backward(grad_hook=self._hook)  # every layer's hook fires inside, the head's first
                 self.bucketer.finish()
             with trace.range("train.adam"):
                 self.opt.step(gscale=1.0 / self.world)
@@ -148,8 +147,11 @@ class NativeTrainer:
                 ctx = torch.cuda.stream(ps)
             else:
                 ctx = contextlib.nullcontext()
-            if self.plan_id is not None and self._plan_version != self.model.__dict__.get("_layout_version"):
-                C.plan_free(self.plan_id)  # weights re-laid out (load_state_dict): record again
+            version = (self.model.__dict__.get("_layout_version"), self.opt.hyper_key())
+            if self.plan_id is not None and self._plan_version != version:
+                # buffers re-laid out or optimizer hyper-parameters changed (lr schedule, Adam
+                # load_state_dict): the recorded launches bake those in, so record again
+                C.plan_free(self.plan_id)
                 self.plan_id = None
             with ctx:
                 if self.plan_id is not None:
@@ -164,7 +166,7 @@ class NativeTrainer:
                         C.plan_abort()
                         raise
                     self.plan_id = C.plan_end()
-                    self._plan_version = self.model.__dict__.get("_layout_version")
+                    self._plan_version = version
                     if ps is not None:
                         C.plan_compile(self.plan_id)
             if ps is not None:

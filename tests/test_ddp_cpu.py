@@ -210,3 +210,56 @@ def test_train_model_two_ranks_rank0_writes(tmp_path):
     exp = st.get_experiment_by_name("Actuator Segmentation")
     runs = st.search_runs(exp["experiment_id"])
     assert len(runs) == 1 and runs[0].data["params"]["world_size"] == "2"
+
+
+# ----------------------------------------------------------------------------- bucket launch order
+def _hook_sequence_launches(bilinear: bool, bucket_mb: float):
+    """Drive a FlatBucketer over the native ParamStore layout of UNet(3, 1) with the executor's hook
+    order (no process group: launches are recorded, not reduced). Returns (hooks, launches) where
+    launches[k] = (bucket, number of hooks fired when it was issued)."""
+    from robotic_discovery_platform_amd.models.unet import (ALIGN, UpTSpec, backward_hook_order,
+                                                             unet_conv_specs)
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer
+    ref = UNetRef(3, 1, bilinear=bilinear)
+    ranges, off = [], 0
+    for n, p in ref.named_parameters():
+        ranges.append((n, off, off + p.numel()))
+        off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+    b = FlatBucketer(torch.zeros(off), ranges, bucket_mb)
+    launches, hooks = [], []
+    b._launch = lambda k: launches.append((k, len(hooks)))
+    specs = unet_conv_specs(4, 64, 3, bilinear)
+    ups = [] if bilinear else [UpTSpec(f"up{i}.up", 64 * 2 ** (5 - i), 64 * 2 ** (4 - i)) for i in range(1, 5)]
+    b.reset()
+    for sp in backward_hook_order(specs, ups, 4):
+        hooks.append(sp.name)
+        b.mark_ready(sp.param_names())
+    assert sorted(n for ns in b.bucket_params for n in ns) == sorted(n for n, _, _ in ranges)
+    return b, hooks, launches
+
+
+@pytest.mark.parametrize("bilinear", [True, False])
+def test_bucket_launch_order_follows_backward_hooks(bilinear):
+    """Every bucket is issued at the hook that completes it, in backward order; the decoder bucket
+    (head + up4 .. up1.conv.3) goes out before the first encoder hook -- not after backward, as when
+    the head's gradients were marked ready only once backward had returned."""
+    b, hooks, launches = _hook_sequence_launches(bilinear, 16.0)
+    assert [k for k, _ in launches] == list(range(len(b.buckets)))  # all launched inside backward, in order
+    assert hooks[0] == "outc"
+    first_enc = next(i for i, h in enumerate(hooks) if h.startswith(("down", "inc")))
+    assert launches[0][1] <= first_enc
+    # each bucket launches at the FIRST hook after which all its params are final
+    for k, n_fired in launches:
+        names = set(b.bucket_params[k])
+        done_at = max(i for i, h in enumerate(hooks) if any(p.startswith(h + ".") for p in names)) + 1
+        assert n_fired == done_at, (k, n_fired, done_at)
+    if bilinear:  # bucket 0 leaves before the 18 MB up1.conv.0 weight gradient exists
+        assert launches[0][1] <= hooks.index("up1.conv.double_conv.0")
+
+
+def test_bucket_big_param_starts_new_bucket():
+    from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer
+    ranges = [("a", 0, 1000), ("b", 1000, 1100), ("c", 1100, 1200)]  # reverse order: c, b, a
+    b = FlatBucketer(torch.zeros(1200), ranges, bucket_mb=400 * 4 / 2 ** 20)
+    assert b.bucket_params == [["c", "b"], ["a"]]

@@ -117,3 +117,51 @@ def test_bench_ddp_force_reports_rccl_path(tmp_path):
     line = [ln for ln in txt.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
     assert res["config"]["grad_comm"] == "bf16" and res["n_gpus"] == 1 and res["value"] > 0
+
+
+def _order_worker(rank, port, out):
+    """The real executor's hooks under nccl (world 1): record which hook had fired when each bucket
+    was issued."""
+    import json
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from robotic_discovery_platform_amd.models.unet import UNetNative
+        from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+        from robotic_discovery_platform_amd.train.engine import NativeTrainer
+        torch.manual_seed(7)
+        nat = UNetNative(3, 1, device=dev, init_from=UNetRef(3, 1))
+        tr = NativeTrainer(nat, 2, 64, 64, lr=1e-3, graph=False, bucket_mb=16.0, ddp_force=True)
+        hooks, launches = [], []
+        hook0, launch0 = tr._hook, tr.bucketer._launch
+        tr._hook = lambda sp: (hooks.append(sp.name), hook0(sp))
+        tr.bucketer._launch = lambda b: (launches.append((b, len(hooks))), launch0(b))
+        x, t = _data(2)
+        tr.set_batch(x.to(dev), t.to(dev))
+        tr.step()
+        torch.cuda.synchronize()
+        json.dump({"hooks": hooks, "launches": launches, "expected": [s.name for s in tr.ex.backward_order()],
+                   "buckets": tr.bucketer.bucket_params}, open(out, "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_bucket_launch_order(tmp_path):
+    """DDP overlap: the decoder bucket (head .. up1.conv.3) is issued inside backward, before any
+    encoder layer's hook, and every bucket is issued at the hook that completes it."""
+    import json
+    out = str(tmp_path / "order.json")
+    mp.spawn(_order_worker, args=(_free_port(), out), nprocs=1, join=True)
+    r = json.load(open(out))
+    hooks, launches = r["hooks"], r["launches"]
+    assert hooks == r["expected"] and hooks[0] == "outc"
+    assert [b for b, _ in launches] == list(range(len(r["buckets"])))
+    first_enc = next(i for i, h in enumerate(hooks) if h.startswith(("down", "inc")))
+    assert launches[0][1] <= first_enc
+    for b, n_fired in launches:
+        names = r["buckets"][b]
+        done_at = max(i for i, h in enumerate(hooks) if any(p.startswith(h + ".") for p in names)) + 1
+        assert n_fired == done_at

@@ -63,7 +63,6 @@ def _worker(rank, world, port, out, sync):
         tr.ex.forward()
         tr.bucketer.reset()
         tr.ex.backward(grad_hook=tr._hook)
-        tr.bucketer.mark_ready(["outc.conv.weight", "outc.conv.bias"])
         tr.bucketer.finish()
         torch.cuda.synchronize()
         if rank == 0:
