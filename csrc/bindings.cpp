@@ -19,8 +19,6 @@ int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, con
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
                      hipStream_t);
-void rdp_conv_set_fixup_kb(long);
-void rdp_conv_set_stages(int);
 long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
@@ -33,11 +31,8 @@ int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStre
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
                    float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
-int rdp_conv_dgrad_pp_bnred(const void*, long, int, int, const void*, long, int, void*, long, int, int, float*, long, int,
-                            int, int, int, const void*, long, int, const float*, hipStream_t);
 int rdp_wgrad_first_bn(const void*, long, int, const void*, long, int, const void*, long, int, const float*, const float*,
                        float*, long, float*, int, int, int, int, int, int, hipStream_t);
-void rdp_conv_set_debug_flags(int);
 int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
                     float*, float*, hipStream_t);
 int rdp_bn_eval_coef(int, const float*, const float*, const float*, const float*, float, float*, hipStream_t);
@@ -80,6 +75,11 @@ double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
 int rdp_geo_spline_res_len(int);
 int rdp_png_info(const uint8_t*, long, int*, int*, int*);
+long rdp_jpeg_info(const uint8_t*, long, int*);
+int rdp_jpeg_decode(const uint8_t*, long, int16_t*, long, uint16_t*, int);
+int rdp_jpeg_gpu(const void*, const int*, const int*, void*, int, int, int, void*, hipStream_t);
+long rdp_jpeg_plane_bytes(int, int);
+long rdp_jpeg_max_coefs(int, int);
 int rdp_png_decode(const uint8_t*, long, uint8_t*, long);
 long rdp_png_encode_gray8(const uint8_t*, int, int, int, uint8_t*, long);
 long rdp_png_encode_bound(int, int);
@@ -139,15 +139,8 @@ struct PlanOp {
   hipEvent_t ev;
   std::function<long(hipStream_t)> fn;
 };
-struct PlanSeg {    // compiled form: a run of launches on one stream as one instantiated graph, or a wait
-  hipStream_t s, s2;
-  hipEvent_t ev;     // wait (exec == nullptr)
-  hipGraphExec_t exec;
-  hipGraph_t graph;
-};
 struct Plan {
   std::vector<PlanOp> ops;
-  std::vector<PlanSeg> segs;  // empty until plan_compile
 };
 std::vector<std::unique_ptr<Plan>> g_plans;
 Plan* g_rec = nullptr;
@@ -216,51 +209,9 @@ void plan_abort() {
   }
 }
 
-// Compile a recorded plan: every maximal run of launches on one stream (between cross-stream waits)
-// is captured into a hipGraph and instantiated, so replay issues one graph launch per run instead of
-// one kernel launch per op (~7 us of HIP host time per kernel launch even from C++; measured: host
-// enqueue 1.37 ms per bs-4 step with per-op replay). The waits stay event record / stream wait
-// between the graph launches, so the two-stream schedule (one hardware queue each) is unchanged.
-int plan_compile(int id) {
-  TORCH_CHECK(id >= 0 && id < (int)g_plans.size() && g_plans[id], "plan_compile: bad plan id");
-  Plan& p = *g_plans[id];
-  if (!p.segs.empty()) return (int)p.segs.size();
-  size_t i = 0;
-  while (i < p.ops.size()) {
-    if (p.ops[i].kind == 1) {
-      p.segs.push_back(PlanSeg{p.ops[i].s, p.ops[i].s2, p.ops[i].ev, nullptr, nullptr});
-      ++i;
-      continue;
-    }
-    const hipStream_t s = p.ops[i].s;
-    size_t j = i;
-    while (j < p.ops.size() && p.ops[j].kind == 0 && p.ops[j].s == s) ++j;
-    TORCH_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess, "plan_compile: capture");
-    for (size_t k = i; k < j; ++k) p.ops[k].fn(s);
-    hipGraph_t g = nullptr;
-    TORCH_CHECK(hipStreamEndCapture(s, &g) == hipSuccess && g, "plan_compile: end capture");
-    hipGraphExec_t ex = nullptr;
-    TORCH_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess, "plan_compile: instantiate");
-    p.segs.push_back(PlanSeg{s, nullptr, nullptr, ex, g});
-    i = j;
-  }
-  return (int)p.segs.size();
-}
-
 void plan_replay(int id) {
   TORCH_CHECK(id >= 0 && id < (int)g_plans.size() && g_plans[id], "plan_replay: bad plan id");
   TORCH_CHECK(g_rec == nullptr, "plan_replay while recording");
-  if (!g_plans[id]->segs.empty()) {
-    for (auto& sg : g_plans[id]->segs) {
-      if (sg.exec) {
-        hipGraphLaunch(sg.exec, sg.s);
-      } else {
-        hipEventRecord(sg.ev, sg.s2);
-        hipStreamWaitEvent(sg.s, sg.ev, 0);
-      }
-    }
-    return;
-  }
   for (auto& op : g_plans[id]->ops) {
     if (op.kind == 0) {
       op.fn(op.s);
@@ -278,10 +229,6 @@ int plan_size(int id) {
 
 void plan_free(int id) {
   if (id < 0 || id >= (int)g_plans.size() || !g_plans[id]) return;
-  for (auto& sg : g_plans[id]->segs) {
-    if (sg.exec) hipGraphExecDestroy(sg.exec);
-    if (sg.graph) hipGraphDestroy(sg.graph);
-  }
   for (auto& op : g_plans[id]->ops) if (op.ev) hipEventDestroy(op.ev);
   g_plans[id].reset();
 }
@@ -562,25 +509,6 @@ int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch:
   return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                           o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
                           0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), st));
-}
-
-// dgrad on the ping-pong kernel with the BN-backward reduction of the layer owning dx (y_bn: its
-// pre-BN output, coef: its [mean|invstd|scale|shift]) in the epilogue. Returns the partial rows for
-// bn_bwd_finalize, or -1 when the auto dispatch would not run the ping-pong kernel on this shape
-// (nothing launched: the caller runs conv_fwd + bn_relu_bwd_reduce).
-int conv_dgrad_pp_bnred(torch::Tensor dy, torch::Tensor w, int taps, torch::Tensor dx, torch::Tensor y_bn,
-                        torch::Tensor coef, torch::Tensor partial) {
-  Act a = act(dy, "dy"), o = act(dx, "dx"), b = act(y_bn, "y_bn");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
-  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && b.N == a.N && b.H == a.H && b.W == a.W && b.C == o.C,
-              "conv_dgrad_pp_bnred: shape mismatch");
-  TORCH_CHECK(w.size(0) == o.C, "w rows != Cout");
-  check_f32(coef, "coef");
-  check_f32(partial, "partial");
-  TORCH_CHECK(coef.numel() >= 4l * o.C, "coef must hold 4*C floats");
-  return RDP_PLAN(rdp_conv_dgrad_pp_bnred(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr,
-                                          o.bytes, o.pitch, o.C, partial.data_ptr<float>(), partial.numel(), a.N, a.H,
-                                          a.W, taps, b.ptr, b.bytes, b.pitch, coef.data_ptr<float>(), st));
 }
 
 int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, int relu, torch::Tensor partial) {
@@ -1057,6 +985,65 @@ py::object png_decode(py::bytes data) {
   return py::cast(t);
 }
 
+// Baseline JPEG -> (geometry int32[32], quantized coefficient planes int16, quant tables int32[3*64]) on
+// the CPU, entropy-decoded without the GIL (restart segments in parallel); None when the stream is not
+// one this decoder handles (progressive, arithmetic, 12-bit, ...): the caller falls back to PIL.
+// geometry: [0] W, [1] H, [2] ncomp, [3] hmax, [4] vmax, [5] total blocks; per component c at 8 + 8c:
+// h, v, blocks per line, block rows, first block, plane byte offset, downsampled width, height.
+py::object jpeg_decode(py::bytes data, bool parallel) {
+  char* buf = nullptr;
+  Py_ssize_t n = 0;
+  if (PyBytes_AsStringAndSize(data.ptr(), &buf, &n) != 0) throw py::error_already_set();
+  int hi[24];
+  const long nco = rdp_jpeg_info((const uint8_t*)buf, n, hi);
+  if (nco <= 0) return py::none();
+  auto geo = torch::zeros({32}, torch::kInt32);
+  int* g = geo.data_ptr<int>();
+  const int W = hi[0], H = hi[1], nc = hi[2], hmax = hi[3], vmax = hi[4];
+  g[0] = W; g[1] = H; g[2] = nc; g[3] = hmax; g[4] = vmax;
+  long blk = 0, pb = 0;
+  for (int c = 0; c < nc; ++c) {
+    const int h = hi[9 + 5 * c], v = hi[10 + 5 * c], bw = hi[11 + 5 * c], bh = hi[12 + 5 * c];
+    int* q = g + 8 + 8 * c;
+    q[0] = h; q[1] = v; q[2] = bw; q[3] = bh; q[4] = (int)blk; q[5] = (int)pb;
+    q[6] = (W * h + hmax - 1) / hmax;
+    q[7] = (H * v + vmax - 1) / vmax;
+    blk += (long)bw * bh;
+    pb += (long)bw * 8 * bh * 8;
+  }
+  g[5] = (int)blk;
+  auto coefs = torch::empty({nco}, torch::kInt16);
+  auto qt16 = torch::empty({3 * 64}, torch::kInt16);
+  int r;
+  {
+    py::gil_scoped_release nogil;
+    r = rdp_jpeg_decode((const uint8_t*)buf, n, coefs.data_ptr<int16_t>(), nco, (uint16_t*)qt16.data_ptr(),
+                        parallel ? 1 : 0);
+  }
+  if (r != 0) return py::none();
+  auto qt = qt16.to(torch::kInt32).bitwise_and(0xFFFF);
+  return py::make_tuple(geo, coefs, qt);
+}
+
+// Dequantisation + ISLOW 8x8 IDCT of every block into the component planes (`planes`, u8 scratch of
+// jpeg_plane_bytes(H, W)), then fancy chroma upsampling + YCbCr -> RGB into rgb [H][W][3] u8 (GPU).
+// geo / coefs / qt: jpeg_decode's outputs, on the device. Launch sizes come from the pipeline's
+// frame size (H, W) so one captured graph serves every JPEG of that size; the kernels read the
+// actual geometry from `geo`.
+void jpeg_to_rgb(torch::Tensor coefs, torch::Tensor geo, torch::Tensor qt, torch::Tensor planes, torch::Tensor rgb) {
+  TORCH_CHECK(coefs.is_cuda() && coefs.scalar_type() == torch::kInt16 && coefs.is_contiguous(), "coefs int16");
+  TORCH_CHECK(geo.is_cuda() && geo.scalar_type() == torch::kInt32 && geo.numel() >= 32, "geo int32[32]");
+  TORCH_CHECK(qt.is_cuda() && qt.scalar_type() == torch::kInt32 && qt.numel() >= 192, "qt int32[192]");
+  TORCH_CHECK(rgb.is_cuda() && rgb.scalar_type() == torch::kUInt8 && rgb.dim() == 3 && rgb.size(2) == 3 &&
+              rgb.is_contiguous(), "rgb u8 HxWx3");
+  const int H = rgb.size(0), W = rgb.size(1);
+  TORCH_CHECK(planes.is_cuda() && planes.scalar_type() == torch::kUInt8 && planes.numel() >= rdp_jpeg_plane_bytes(H, W),
+              "planes: jpeg_plane_bytes(H, W) u8");
+  TORCH_CHECK(coefs.numel() >= rdp_jpeg_max_coefs(H, W), "coefs: jpeg_max_coefs(H, W) int16");
+  rdp_jpeg_gpu(coefs.data_ptr(), geo.data_ptr<int>(), qt.data_ptr<int>(), planes.data_ptr(), H, W,
+               (int)(coefs.numel() / 64), rgb.data_ptr(), unplanned_stream());
+}
+
 // u8 [H, W] CPU tensor -> 8-bit grayscale PNG bytes (deflate level), encoded without the GIL
 py::bytes png_encode_gray8(torch::Tensor img, int level) {
   TORCH_CHECK(!img.is_cuda() && img.scalar_type() == torch::kUInt8 && img.dim() == 2 && img.is_contiguous(),
@@ -1104,23 +1091,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_end", &plan_end);
   m.def("plan_abort", &plan_abort);
   m.def("plan_replay", &plan_replay);
-  m.def("plan_compile", &plan_compile);
   m.def("plan_size", &plan_size);
   m.def("plan_free", &plan_free);
   m.def("conv_fwd", on_device(&conv_fwd), py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
         py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
         py::arg("ws") = py::none(), py::arg("pool") = py::none(), py::arg("up") = py::none(),
         py::arg("up_oy") = 0, py::arg("up_ox") = 0);
-  m.def("conv_set_fixup_kb", &rdp_conv_set_fixup_kb, "split-K in-kernel fixup bound in KB (0 = reduce kernel)");
-  m.def("conv_set_stages", &rdp_conv_set_stages, "igemm K-pipeline depth: 0 = auto, 2-4 = forced");
   m.def("conv_ws_elems", [](int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
     return rdp_conv_ws_elems(N, H, W, C1, C2, Cout, taps, packed, bm_pref);
   });
   m.def("conv_stats_rows", &conv_stats_rows);
-  m.def("conv_set_debug_flags", [](int f) { rdp_conv_set_debug_flags(f); }, "A/B flags for microbenchmarks");
   m.def("conv_wgrad", on_device(&conv_wgrad));
   m.def("wgrad_first_bn", on_device(&wgrad_first_bn));
-  m.def("conv_dgrad_pp_bnred", on_device(&conv_dgrad_pp_bnred));
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
   m.def("bn_finalize", on_device(&bn_finalize));
   m.def("bn_eval_coef", on_device(&bn_eval_coef));
@@ -1171,6 +1153,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
         py::arg("presorted") = false);
   m.def("png_decode", &png_decode);
+  m.def("jpeg_decode", &jpeg_decode, py::arg("data"), py::arg("parallel") = true);
+  m.def("jpeg_to_rgb", on_device(&jpeg_to_rgb));
+  m.def("jpeg_plane_bytes", &rdp_jpeg_plane_bytes);
+  m.def("jpeg_max_coefs", &rdp_jpeg_max_coefs);
   m.def("png_encode_gray8", &png_encode_gray8);
   m.def("resize_area_u8", on_device(&resize_area_u8));
   m.def("area_maxtap", &rdp_area_maxtap);

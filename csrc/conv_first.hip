@@ -36,7 +36,6 @@ struct FirstArgs {
   int erelu;
   int H, W, M, nseg;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;
-  int abl;  // microbenchmark ablations (RDP_FIRST_ABL): 1 = no output stores, 2 = no input loads
 };
 
 RDP_DEV int ftap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
@@ -75,7 +74,7 @@ __global__ __launch_bounds__(256) void conv_first_kernel(const FirstArgs a) {
   const int gq = lane >> 4;
   const int coff = 16 * (gq & 1) + 8 * (gq >> 1);
   // pixel fragments: [i][K step] for pixels seg*64 + 16i + pr.
-  // Measured (scripts/first_layer_bench.py, bs 64, RDP_FIRST_ABL): 221 us, 111 us without the output
+  // Measured (scripts/first_layer_bench.py, bs 64, ablation builds): 221 us, 111 us without the output
   // stores, 111 us without the input gathers, 101 us with neither -- the 16 gather loads (8 B per
   // lane, 64 addresses) and 8 stores per segment share the vector-memory path and do not overlap;
   // issuing segment k+1's loads ahead of segment k's stores changed nothing at bs 64 and was slower at
@@ -99,7 +98,7 @@ __global__ __launch_bounds__(256) void conv_first_kernel(const FirstArgs a) {
         const int dr = ftap_dr(tap), ds = ftap_ds(tap);
         const bool ok = valid && tap < 9 && inb(h + dr, a.H) && inb(w + ds, a.W);
         const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * a.pitch) * 2u : RDP_OOB;
-        v[q] = (a.abl & 2) ? make_uint2(off, off + 1u) : bload8(rx, off);
+        v[q] = bload8(rx, off);
       }
       pf[i][0] = __builtin_bit_cast(bf16x8, make_uint4(v[0].x, v[0].y, v[1].x, v[1].y));
       pf[i][1] = __builtin_bit_cast(bf16x8, make_uint4(v[2].x, v[2].y, v[3].x, v[3].y));
@@ -152,8 +151,7 @@ __global__ __launch_bounds__(256) void conv_first_kernel(const FirstArgs a) {
         const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
         const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
         const uint32_t off = m < a.M ? (uint32_t)(m * a.ypitch + n) * 2u : RDP_OOB;
-        if (a.abl & 1) asm volatile("" ::"v"(rxs[0]), "v"(rxs[1]), "v"(rys[0]), "v"(rys[1]));
-        else bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
+        bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
       }
     }
   }
@@ -199,16 +197,7 @@ extern "C" int rdp_conv_first(const void* x, long xbytes, int pitch, const void*
   const FastDiv fhw = make_fastdiv((uint32_t)(H * W)), fw = make_fastdiv((uint32_t)W);
   a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;
   // grid <= nseg / 4 keeps the stats rows within conv_stats_rows() (>= M / 32 rows)
-  static const int cap = [] {
-    const char* e = getenv("RDP_FIRST_GRID");
-    return e ? std::max(1, atoi(e)) : 512;
-  }();
-  const int grid = std::max(1, std::min((a.nseg + 3) / 4, cap));
-  static const int abl = [] {
-    const char* e = getenv("RDP_FIRST_ABL");
-    return e ? atoi(e) : 0;
-  }();
-  a.abl = abl;
+  const int grid = std::max(1, std::min((a.nseg + 3) / 4, 512));
   hipLaunchKernelGGL(conv_first_kernel, dim3(grid), dim3(256), 0, s, a);
   return stats ? grid : 0;
 }

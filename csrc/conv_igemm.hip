@@ -51,8 +51,6 @@ struct ConvArgs {
   int cpt;  // 64-channel chunks per tap (generic mode)
   int ksplit;    // > 1: split-K, work item = (tile, split), fp32 partial tiles go to kslab
   float* kslab;  // [ksplit][M][Cout] fp32
-  uint32_t* kcnt;  // split-K arrival counter per output tile (zero between launches)
-  int fixup;       // split-K: 1 = the tile's last-arriving block reduces + runs the epilogue in-kernel
   u16* pool;       // split-K reduce only: also write MaxPool2d(2) of the output (eval), [M/4][ppitch]
   int ppitch;
   // split-K reduce only: also write the bilinear x2 (align_corners) upsample of the output (eval), into
@@ -62,18 +60,7 @@ struct ConvArgs {
   float urh, urw;
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
-  int store_aware;  // 1: the per-step vmcnt leaves the previous epilogue's stores in flight
-  // dgrad + BN-backward reduction (conv_pp_kernel<..., BNR = true>): the output is dL/da of the layer
-  // that owns it; bny = that layer's pre-BN output [M][bnypitch], bncoef its [mean|invstd|scale|shift]
-  const u16* bny;
-  uint32_t bnybytes;
-  int bnypitch;
-  const float* bncoef;
 };
-
-// debug / A-B flags for the microbenchmark (rdp_conv_set_debug_flags): bit 0 = plain vmcnt(0)
-static int g_conv_debug_flags = 0;
-extern "C" void rdp_conv_set_debug_flags(int f) { g_conv_debug_flags = f; }
 
 // tap (0..8) -> (dr, ds) without division: dr + 1 = (tap * 11) >> 5
 RDP_DEV int tap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
@@ -91,11 +78,11 @@ RDP_DEV void vm_wait_p(int pend) {
   else vm_wait<B + P2>();
 }
 
-// NST: K-pipeline stages (LDS buffers). 2 = double buffering at 2 blocks / CU (default: the
-// co-resident block hides the DMA latency); 3-4 = a deeper ring at 1 block / CU (A/B option for
-// grids that put at most one block on each CU; measured no faster, see conv_stages()).
-template <int BM, int BN, int NWV = 4, bool FIX = false, int NST = 2>
-__global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(const ConvArgs a) {
+// Double-buffered K pipeline at 2 blocks / CU: the co-resident block hides the DMA latency. (A 3-4
+// stage ring at 1 block / CU and an in-kernel split-K fixup were measured slower: profiles/dead_ends.md.)
+template <int BM, int BN, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs a) {
+  constexpr int NST = 2;
   constexpr int WAVES_M = BM / 64;
   constexpr int WAVES_N = NWV / WAVES_M;
   constexpr int WNT = BN / WAVES_N;  // couts per wave (64, or 32 with 8-wave blocks)
@@ -104,11 +91,7 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
   constexpr int NROW = BM / 8 / NWV;     // pixel-row DMA pieces per wave per K step
   constexpr int WPIECES = BN / 8 / NWV;  // weight-row DMA pieces per wave per K step
   constexpr int DMA_OPS = NROW + WPIECES;  // vector-memory ops per wave per stage
-  static_assert(NST >= 2 && NST <= 4, "pipeline depth");
-  // + 16 B: the split-K "last arriver" word (kept in the one LDS array: a second __shared__ object
-  // can make hipcc wait vmcnt(0) before every fragment read, cdna_hip_programming.md §5 item 4a)
-  // (only in the fixup variant: 2 x 40 KB + 16 B would drop the 256 x 64 tile to 1 block / CU)
-  __shared__ __attribute__((aligned(16))) char smem[NST * BUF + (FIX ? 16 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[NST * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -222,15 +205,6 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
   if (total > 0) {
     set_tile(0);
     issue(0, smem);
-#pragma unroll
-    for (int p = 1; p < NST - 1; ++p) {  // deeper pipelines: fill stages 1 .. NST-2 up front
-      if (p < total) {
-        if (++iks == a.nks) { iks = 0; ++it; set_tile(it); }
-        issue(iks, smem + p * BUF);
-        ig = p;
-        ibuf = p;
-      }
-    }
   }
   // vector-memory stores the previous step's epilogue issued after stage g's DMA: vmcnt counts
   // them in issue order, so stage g has landed once at most that many ops are outstanding (a plain
@@ -246,16 +220,9 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
   for (int g = 0; g < total; ++g) {
-    // stage g has landed once at most (stages issued after it) x DMA_OPS + (epilogue stores issued
-    // after it) ops are outstanding (in-order completion); older stores are not counted, which only
-    // makes the wait stricter
-    {
-      const int ahead = ig - g;  // 0 .. NST-2
-      const int pd = a.store_aware ? pend : 0;
-      if (NST <= 2 || ahead == 0) vm_wait_p<0, 2 * NJ, 4 * NJ>(pd);
-      else if (NST <= 3 || ahead == 1) vm_wait_p<(NST > 2 ? DMA_OPS : 0), 2 * NJ, 4 * NJ>(pd);
-      else vm_wait_p<(NST > 3 ? 2 * DMA_OPS : 0), 2 * NJ, 4 * NJ>(pd);
-    }
+    // stage g has landed once at most (epilogue stores issued after it) ops are outstanding
+    // (in-order completion); older stores are not counted, which only makes the wait stricter
+    vm_wait_p<0, 2 * NJ, 4 * NJ>(pend);
     pend = 0;
     raw_barrier();
     if (ig + 1 < total) {  // the buffer computed at step g-1: every wave is past it (barrier above)
@@ -292,7 +259,6 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
       const int split = item / tiles1;
       const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
       const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
-      // in-kernel fixup: slabs stored write-through (sc1), so no release fence is needed
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
@@ -302,49 +268,11 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
           const f32x4 o = acc[j][i];
           acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
           const uint32_t off = m < a.M ? (uint32_t)(((long)split * a.M + m) * a.Cout + n) * 4u : RDP_OOB;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rk, off, 0, FIX ? 16 : 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rk, off, 0, 0);
         }
       }
-      if constexpr (!FIX) {  // the epilogue runs in conv_splitk_reduce_kernel
-        pend = 4 * NJ;  // NJ x 4 slab stores
-        continue;
-      }
-      // Publish / consume (cdna_hip_programming.md §6 Guideline 16, R1 counter form): every storing
-      // wave drains its write-through stores, the block barrier joins them, ONE lane takes a ticket on
-      // the tile's counter (agent scope); the block that draws ksplit-1 resets the counter, acquires
-      // (agent: drops this CU's stale L1 lines), drains, and after a barrier every wave reads the
-      // ksplit slabs with plain loads -- correct for any placement of the slices over XCDs / CUs.
-      wait_vm0();
-      __syncthreads();
-      volatile uint32_t* last_w = (volatile uint32_t*)(smem + NST * BUF);
-      if (threadIdx.x == 0) {
-        auto* c = (__attribute__((address_space(1))) uint32_t*)(a.kcnt + tile);
-        const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t last = old == (uint32_t)(a.ksplit - 1) ? 1u : 0u;
-        if (last) {
-          __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          wait_vm0();
-        }
-        *last_w = last;
-      }
-      __syncthreads();
-      pend = 0;
-      if (*last_w == 0u) continue;
-      // sum the slabs in split order (bitwise independent of which slice arrived last)
-      for (int sp = 0; sp < a.ksplit; ++sp) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int n = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int m = tm * BM + wm * 64 + i * 16 + (lane & 15);
-            const uint32_t off = m < a.M ? (uint32_t)(((long)sp * a.M + m) * a.Cout + n) * 4u : RDP_OOB;
-            acc[j][i] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 0));
-          }
-        }
-      }
-      // fall through: the epilogue of the reduced tile
+      pend = 4 * NJ;  // NJ x 4 slab stores; the epilogue runs in conv_splitk_reduce_kernel
+      continue;
     }
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -397,31 +325,6 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
       }
     }
     pend = 2 * NJ;  // 2 NJ output stores
-    if (FIX && a.stats) {
-      // fixup: this block reduced tile (tm, tn) -- its BN partial sums go to stats row (tm, wm)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float q1 = row16_sum(s1[j][r]), q2 = row16_sum(s2[j][r]);
-          s1[j][r] = q1;
-          s2[j][r] = q2;
-        }
-      if ((lane & 15) == 0) {
-        float* row = a.stats + (size_t)(tm * WAVES_M + wm) * 2 * a.Cout;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int c = tn * BN + wn * WNT + j * 16 + 4 * (lane >> 4);
-          *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
-          *(float4*)(row + a.Cout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
-      pend += NJ * 2;  // stats stores (lanes 0/16/32/48)
-    }
   }
   if (a.stats && a.ksplit == 1 && total > 0) {
     // reduce over the 16 pixel lanes (lane & 15) sharing a channel group; one slab row per (block group, wm)
@@ -468,28 +371,26 @@ __global__ __launch_bounds__(64 * NWV, NST > 2 ? 1 : 2) void conv_igemm_kernel(c
 // Accumulation order per output element is the K-step order with the two K halves of a step in
 // order, exactly as conv_igemm_kernel: outputs are bitwise equal to it. Training BN statistics
 // accumulate per block in LDS words owned by one lane each (no registers held across tiles).
-// Generic (non-packed) im2col only, no split-K / fixup / fused pool or upsample.
-// RD_INFLIGHT: fragment reads of phases 0..NPH-2 stay in flight across the segment barrier;
-// HOLDB: both cout halves of the weight fragments stay in registers (no re-read in phase 3).
-// BNR: dgrad whose output da belongs to a BN+ReLU layer; the statistics rows hold that layer's
-// BN-backward partial sums (sum g, sum g * xhat, g = da masked by ReLU(BN(y))) instead of the
-// output moments, from the bf16-rounded da as stored and the owner's pre-BN y read in the epilogue:
-// the separate bn_relu_bwd_reduce pass (which re-reads da and y) is dropped.
-template <int BN, int NST, bool RD_INFLIGHT, bool HOLDB, bool BNR = false>
+// Generic (non-packed) im2col only, no split-K / fused pool or upsample.
+// Fragment reads of phases 0..NPH-2 stay in flight across the segment barrier; at BN = 256 both
+// cout halves of the weight fragments stay in registers (HOLDB: no re-read in phase 3); BN = 128
+// runs a 3-stage K ring (NST). (A 512 x 64 form and a BN-backward reduction in the dgrad epilogue
+// were measured slower: profiles/dead_ends.md.)
+template <int BN>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
-  // BN = 256 / 128: 256-pixel tile, wave (wm, wn) = 128 pixels x BN/4 couts. BN = 64: 512-pixel tile,
-  // wave (wm, wn) = 64 pixels (rows wm * 256 + wn * 64) x all 64 couts.
-  constexpr bool C64 = BN == 64;
-  constexpr int BM = C64 ? 512 : 256;
-  constexpr int WNT = C64 ? 64 : BN / 4;  // couts per wave
-  constexpr int NJ = WNT / 16;            // cout fragments per wave (4 / 2 / 4)
-  constexpr int NI = C64 ? 4 : 8;         // pixel fragments per wave
-  constexpr int NPH = (NJ / 2) * (NI / 4);  // phases per K step, 16 MFMAs each (4 / 2 / 2)
+  // 256-pixel tile, wave (wm, wn) = 128 pixels x BN/4 couts
+  constexpr int NST = BN == 128 ? 3 : 2;
+  constexpr bool RD_INFLIGHT = true, HOLDB = BN == 256;
+  constexpr int BM = 256;
+  constexpr int WNT = BN / 4;        // couts per wave
+  constexpr int NJ = WNT / 16;       // cout fragments per wave (4 / 2)
+  constexpr int NI = 8;              // pixel fragments per wave
+  constexpr int NPH = (NJ / 2) * (NI / 4);  // phases per K step, 16 MFMAs each (4 / 2)
   constexpr int P_BYTES = BM * 128, W_BYTES = BN * 128, BUF = P_BYTES + W_BYTES;
   constexpr int NROW = BM / 64;      // 8-row pixel DMA pieces per wave per stage
   constexpr int WPIECES = BN / 64;   // weight DMA pieces per wave per stage
   constexpr int DMA_OPS = NROW + WPIECES;
-  constexpr int SROWS = C64 ? 8 : 2;  // statistics rows per block (one per wave / per wave row)
+  constexpr int SROWS = 2;           // statistics rows per block (one per wave row)
   constexpr int ST_OFF = NST * BUF;   // BN statistics: [SROWS][2][BN] fp32
   static_assert(NST * BUF + SROWS * 2 * BN * 4 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[NST * BUF + SROWS * 2 * BN * 4];
@@ -498,8 +399,8 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int gch = (lane & 7) ^ (lane >> 3);
-  const int wpx = C64 ? wm * 256 + wn * 64 : wm * 128;  // first pixel row of this wave in the tile
-  const int wco = C64 ? 0 : wn * WNT;                   // first cout of this wave in the tile
+  const int wpx = wm * 128;   // first pixel row of this wave in the tile
+  const int wco = wn * WNT;   // first cout of this wave in the tile
 
   const uint32_t G = gridDim.x;
   const uint32_t lid = xcd_remap(blockIdx.x, G);
@@ -569,7 +470,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) rdoff[hf] = (lane & 15) * 128 + 16 * (((lane >> 4) + 4 * hf) ^ (lane & 7));
 
-  const int srow = C64 ? wave : wm;
+  const int srow = wm;
   float* const sst = (float*)(smem + ST_OFF) + srow * 2 * BN;  // this wave (row)'s statistics words
   if (a.stats && (lane & 15) == 0) {
 #pragma unroll
@@ -613,7 +514,6 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
     const int gq = lane >> 4;
     const int coff = 16 * (gq & 1) + 8 * (gq >> 1);
     float s1[NJ][4], s2[NJ][4];
-    const auto rbny = make_rsrc(BNR ? a.bny : a.y1, BNR ? a.bnybytes : 0u);
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -625,26 +525,10 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
       const bool d2 = nb >= a.Cy1;  // wave-uniform: Cy1 % 32 == 0 (host-checked), one SRD per store
       const int nn = d2 ? n - a.Cy1 : n;
       const int yp = d2 ? a.ypitch2 : a.ypitch1;
-      float4 bmu[2], binv[2], bss[2], bhh[2];  // BNR: owner coefficients of this lane's 2 x 4 channels
-      if constexpr (BNR) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int nc = nb + h * 16 + 4 * gq;
-          bmu[h] = *(const float4*)(a.bncoef + nc);
-          binv[h] = *(const float4*)(a.bncoef + a.Cout + nc);
-          bss[h] = *(const float4*)(a.bncoef + 2 * a.Cout + nc);
-          bhh[h] = *(const float4*)(a.bncoef + 3 * a.Cout + nc);
-        }
-      }
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int m = m0 + wpx + i * 16 + (lane & 15);
-        uint2 v[2], yb[2];
-        if constexpr (BNR) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            yb[h] = bload8(rbny, m < a.M ? (uint32_t)(m * a.bnypitch + nb + h * 16 + 4 * gq) * 2u : RDP_OOB);
-        }
+        uint2 v[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int j = jp + h;
@@ -664,23 +548,10 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
           if (a.stats && m < a.M) {
             const float q0 = __uint_as_float(v[h].x << 16), q1 = __uint_as_float(v[h].x & 0xffff0000u);
             const float q2 = __uint_as_float(v[h].y << 16), q3 = __uint_as_float(v[h].y & 0xffff0000u);
-            if constexpr (BNR) {
-              const float y0 = __uint_as_float(yb[h].x << 16), y1 = __uint_as_float(yb[h].x & 0xffff0000u);
-              const float y2 = __uint_as_float(yb[h].y << 16), y3 = __uint_as_float(yb[h].y & 0xffff0000u);
-              const float g0 = fmaf(y0, bss[h].x, bhh[h].x) > 0.f ? q0 : 0.f;
-              const float g1 = fmaf(y1, bss[h].y, bhh[h].y) > 0.f ? q1 : 0.f;
-              const float g2 = fmaf(y2, bss[h].z, bhh[h].z) > 0.f ? q2 : 0.f;
-              const float g3 = fmaf(y3, bss[h].w, bhh[h].w) > 0.f ? q3 : 0.f;
-              s1[j][0] += g0; s2[j][0] += g0 * (y0 - bmu[h].x) * binv[h].x;
-              s1[j][1] += g1; s2[j][1] += g1 * (y1 - bmu[h].y) * binv[h].y;
-              s1[j][2] += g2; s2[j][2] += g2 * (y2 - bmu[h].z) * binv[h].z;
-              s1[j][3] += g3; s2[j][3] += g3 * (y3 - bmu[h].w) * binv[h].w;
-            } else {
-              s1[j][0] += q0; s2[j][0] += q0 * q0;
-              s1[j][1] += q1; s2[j][1] += q1 * q1;
-              s1[j][2] += q2; s2[j][2] += q2 * q2;
-              s1[j][3] += q3; s2[j][3] += q3 * q3;
-            }
+            s1[j][0] += q0; s2[j][0] += q0 * q0;
+            s1[j][1] += q1; s2[j][1] += q1 * q1;
+            s1[j][2] += q2; s2[j][2] += q2 * q2;
+            s1[j][3] += q3; s2[j][3] += q3 * q3;
           }
         }
         const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
@@ -716,12 +587,11 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
     const char* wb = pb + P_BYTES;
 #pragma unroll
     for (int p = 0; p < NPH; ++p) {
-      // phase -> (pixel half ih, cout half jh): BN 256: (0,0) (0,1) (1,1) (1,0); BN 128: (0,*) (1,*);
-      // BN 64 (4 pixel fragments per wave): (*,0) (*,1)
-      const int ih = C64 ? 0 : (NPH == 4 ? (p >> 1) : p);
-      const int jh = C64 ? p : (NPH == 4 ? (((p + 1) >> 1) & 1) : 0);
-      const bool new_b = C64 ? p == 0 : (NPH == 4 ? (p == 0 || p == 2) : true);
-      const bool new_a = C64 ? (HOLDB ? true : true) : (NPH == 4 ? (HOLDB ? p < 2 : p != 2) : (p == 0));
+      // phase -> (pixel half ih, cout half jh): BN 256: (0,0) (0,1) (1,1) (1,0); BN 128: (0,*) (1,*)
+      const int ih = NPH == 4 ? (p >> 1) : p;
+      const int jh = NPH == 4 ? (((p + 1) >> 1) & 1) : 0;
+      const bool new_b = NPH == 4 ? (p == 0 || p == 2) : true;
+      const bool new_a = NPH == 4 ? (HOLDB ? p < 2 : p != 2) : (p == 0);
       const int fh = HOLDB ? jh : 0;  // register set of the phase's weight fragments
       // ---- memory segment
       if (p == 0 && ig + 1 < total) {
@@ -785,22 +655,20 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   }
 }
 
-template <int BN, bool RDF = false, bool HOLDB = false, bool BNR = false>
+template <int BN>
 static int launch_pp(ConvArgs a, hipStream_t s) {
-  constexpr int BM = BN == 64 ? 512 : 256;
-  constexpr int NST = BN == 128 ? 3 : 2;
+  constexpr int BM = 256;
   if (a.packed || a.Cout % BN || a.Cy1 % 32) return -1;
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
   a.ntiles = tilesM * a.tilesN;
   a.ksplit = 1;
-  a.fixup = 0;
   a.pool = nullptr;
   a.up = nullptr;
   const int grid = a.ntiles < 256 ? a.ntiles : 256;  // one block per CU, persistent
   if (a.stats && grid % a.tilesN) return -1;
-  hipLaunchKernelGGL((conv_pp_kernel<BN, NST, RDF, HOLDB, BNR>), dim3(grid), dim3(512), 0, s, a);
-  return grid / a.tilesN * (BN == 64 ? 8 : 2);
+  hipLaunchKernelGGL((conv_pp_kernel<BN>), dim3(grid), dim3(512), 0, s, a);
+  return grid / a.tilesN * 2;
 }
 
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
@@ -1008,26 +876,6 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_up_kernel(const ConvAr
   }
 }
 
-// split-K workspace layout: [KCNT_WORDS] u32 arrival counters (zero-initialised by the caller, left
-// zero by every launch) followed by the fp32 slab
-#define KCNT_WORDS 256
-
-// In-kernel split-K fixup (the tile's last-arriving block reduces) vs the separate reduce launch.
-// Measured dead end (serving frame, N = 1, one MI355X): each fixed-up conv took 9-11 us longer
-// (drain of the write-through slab stores + ticket + agent acquire + the reducer's serial slab reads
-// from HBM) than the 6-7 us reduce launch it replaced, so the default bound is 0 (always the reduce
-// kernel). RDP_SPLITK_FIXUP_KB (or rdp_conv_set_fixup_kb) enables it for ksplit x BM x BN x 4 bytes
-// up to that size; kept tested (tests/test_kernels_gpu.py) for the A/B.
-static long g_fixup_kb = -1;
-extern "C" void rdp_conv_set_fixup_kb(long kb) { g_fixup_kb = kb; }
-static long fixup_max_bytes() {
-  if (g_fixup_kb < 0) {
-    const char* e = getenv("RDP_SPLITK_FIXUP_KB");
-    g_fixup_kb = e ? atol(e) : 0L;
-  }
-  return g_fixup_kb * 1024L;
-}
-
 // Split-K when the tile grid leaves most CUs idle: the smallest divisor of the K steps that gives
 // >= 256 work items with >= 4 K steps each, as long as the fp32 slab fits `ws_elems`.
 static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long ws_elems) {
@@ -1043,39 +891,6 @@ static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long 
   return ks;
 }
 
-// K-pipeline depth. Measured dead end (serving frame at N = 1, one MI355X, same box A/B): the 4-stage
-// ring at 1 block / CU for grids of <= 256 blocks made every such conv 0.3-1 us SLOWER (e.g. 128^2
-// 128->128 13.4 -> 14.4 us, 64^2 256->256 17.5 -> 18.3 us; GPU p50 0.600 -> 0.614 ms): those convs
-// are bound by their fixed launch / prologue / epilogue cost, not by the per-step DMA round trip.
-// Default 2; RDP_CONV_STAGES (or rdp_conv_set_stages) = 3 / 4 forces the deep ring (1 block / CU) for
-// A/B runs (tests/test_kernels_gpu.py keeps all depths bitwise equal).
-static int g_conv_stages = -1;
-extern "C" void rdp_conv_set_stages(int n) { g_conv_stages = n; }
-static int conv_stages(int grid, int buf_bytes) {
-  if (g_conv_stages < 0) {
-    const char* e = getenv("RDP_CONV_STAGES");
-    g_conv_stages = e ? atoi(e) : 0;
-  }
-  (void)grid;
-  int nst = g_conv_stages > 2 ? g_conv_stages : 2;
-  while (nst > 2 && nst * buf_bytes + 16 > 160 * 1024) --nst;  // LDS per workgroup (+ fixup word)
-  return nst < 2 ? 2 : (nst > 4 ? 4 : nst);
-}
-
-template <int BM, int BN, int NWV, bool FIX>
-static void launch_depth(const ConvArgs& a, int grid, hipStream_t s) {
-  constexpr int BUF = (BM + BN) * 128;
-  const int nst = conv_stages(grid, BUF);
-  if constexpr (4 * BUF + 16 <= 160 * 1024) {
-    if (nst == 4) {
-      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV, FIX, 4>), dim3(grid), dim3(64 * NWV), 0, s, a);
-      return;
-    }
-  }
-  if (nst >= 3) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV, FIX, 3>), dim3(grid), dim3(64 * NWV), 0, s, a);
-  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV, FIX, 2>), dim3(grid), dim3(64 * NWV), 0, s, a);
-}
-
 template <int BM, int BN, int NWV = 4>
 static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, int* pooled = nullptr) {
   const int tilesM = (a.M + BM - 1) / BM;
@@ -1083,17 +898,10 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, 
   a.ntiles = tilesM * a.tilesN;
   a.ksplit = a.kslab ? choose_ksplit(a.ntiles, a.nks, a.M, a.Cout, a.packed, ws_elems) : 1;
   if (a.ksplit > 1) {
-    a.fixup = (long)a.ksplit * BM * BN * 4 <= fixup_max_bytes() && a.ntiles <= KCNT_WORDS;
     a.nks /= a.ksplit;
     a.ntiles *= a.ksplit;
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
-    if (a.fixup) {
-      a.pool = nullptr;
-      a.up = nullptr;
-      launch_depth<BM, BN, NWV, true>(a, grid, s);
-      return tilesM * (BM / 64);  // stats rows (tm, wave row), written by the reducers
-    }
-    launch_depth<BM, BN, NWV, false>(a, grid, s);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
     const int rpb = 256 / (a.Cout / 4);
     int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
     nblk = nblk < 512 ? nblk : 512;
@@ -1118,7 +926,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, 
   const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
   // the per-block stats rows need every block to keep one channel tile (see the kernel)
   if (a.stats && grid % a.tilesN) return -1;
-  launch_depth<BM, BN, NWV, false>(a, grid, s);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
   return grid / a.tilesN * (BM / 64);
 }
 
@@ -1135,15 +943,11 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // (uoy, uox), fused the same way; *pooled = 1 if the fused output was written (else the caller
   // launches the pool / upsample)
   if (pooled) *pooled = 0;
-  // first layer (3-channel input, packed K): conv_first.hip (auto, or bm_pref 13 = force;
-  // RDP_CONV_FIRST=0: this file's packed implicit GEMM, for A/B)
+  // first layer (3-channel input, packed K): conv_first.hip (auto, or bm_pref 13 = force; bm_pref 256
+  // runs this file's packed implicit GEMM, the tests' second opinion)
   {
-    static const int first_env = [] {
-      const char* e = getenv("RDP_CONV_FIRST");
-      return e ? atoi(e) : 1;
-    }();
     const int pref = bm_pref % 1000;
-    if (packed && (pref == 13 || (pref == 0 && first_env)) && C1 == 8 && C2 == 0 && x2 == nullptr && taps == 9 &&
+    if (packed && (pref == 13 || pref == 0) && C1 == 8 && C2 == 0 && x2 == nullptr && taps == 9 &&
         Cout == 64 && y2 == nullptr) {
       const int r = rdp_conv_first(x1, xbytes1, pitch1, w, wbytes, y1, ybytes1, ypitch1, stats, N, H, W, escale, eshift,
                                    erelu, s);
@@ -1153,16 +957,12 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 6 = force the row-ring kernel,
   // 128 / 256 (2 / 3: 8-wave) = force this kernel's tile
   {
-    static const int ring_env = [] {
-      const char* e = getenv("RDP_CONV_RING");
-      return e ? atoi(e) : 1;
-    }();
     const int pref = bm_pref % 1000;
     // row-ring kernel (conv_ring.hip): 64 -> 64 channels, 3x3, one source, no output split. Auto only
     // when its grid (one block per pair of 64-pixel row segments, <= 256) fills the chip: at N = 1,
     // 128^2 x 64 -> 128 the 128-block ring took 15.2 us vs 11.9 us for the implicit GEMM
     const long ring_pairs = W % 64 == 0 ? (long)N * (W / 64) * H / 2 : 0;
-    if ((pref == 6 || (pref == 0 && ring_env && ring_pairs >= 256)) && taps == 9 && !packed && C2 == 0 &&
+    if ((pref == 6 || (pref == 0 && ring_pairs >= 256)) && taps == 9 && !packed && C2 == 0 &&
         x2 == nullptr) {
       if (pool && pooled && !stats && !y2 && escale) {  // eval: MaxPool2d fused into the ring epilogue
         const int r = rdp_conv_ring_pool(x1, xbytes1, C1, pitch1, w, wbytes, ldw, y1, ybytes1, ypitch1, Cout, N, H, W,
@@ -1190,12 +990,10 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   }
   ConvArgs a;
   a.escale = escale; a.eshift = eshift; a.erelu = erelu;
-  // ws = [KCNT_WORDS counters | slab] (rdp_conv_ws_elems)
-  const bool has_ws = ws != nullptr && ws_elems > KCNT_WORDS;
-  a.kcnt = has_ws ? (uint32_t*)ws : nullptr;
-  a.kslab = has_ws ? ws + KCNT_WORDS : nullptr;
+  // ws = the split-K fp32 slab (rdp_conv_ws_elems)
+  const bool has_ws = ws != nullptr && ws_elems > 0;
+  a.kslab = has_ws ? ws : nullptr;
   a.ksplit = 1;
-  a.fixup = 0;
   a.pool = (pool != nullptr && pooled != nullptr && stats == nullptr && y2 == nullptr && H % 2 == 0 && W % 2 == 0)
                ? (u16*)pool : nullptr;
   a.ppitch = ppitch;
@@ -1212,7 +1010,7 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   a.upitch = upitch; a.uH = uH; a.uW = uW; a.uoy = uoy; a.uox = uox;
   a.urh = 2 * H > 1 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;  // = ac_scale (pool_up.hip)
   a.urw = 2 * W > 1 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
-  long wse = has_ws ? ws_elems - KCNT_WORDS : 0;
+  long wse = has_ws ? ws_elems : 0;
   wse = wse < (1L << 29) ? wse : (1L << 29);  // slab bytes < 2 GiB (buffer offsets)
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
   a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
@@ -1222,7 +1020,6 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   a.Cy1 = Cy1; a.ypitch1 = ypitch1; a.ypitch2 = ypitch2; a.stats = stats;
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.M = N * H * W;
   a.taps = taps; a.packed = packed;
-  a.store_aware = (g_conv_debug_flags & 1) ? 0 : 1;
   if (packed) {
     if (C1 != 8 || C2 != 0 || taps != 9 || ldw != 128) return -1;
     a.nks = 2; a.cpt = 1;
@@ -1240,44 +1037,23 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // grid (k = 0 => 2 per CU, every block resident; large k ~ one tile per block)
   int per_cu = bm_pref / 1000;
   bm_pref %= 1000;
-  if (per_cu == 0) {  // tuning knob for sweeps (RDP_CONV_PERCU), default 2 = every block resident
-    static const int env_per_cu = [] {
-      const char* e = getenv("RDP_CONV_PERCU");
-      return e ? atoi(e) : 0;
-    }();
-    per_cu = env_per_cu > 0 ? env_per_cu : 2;
-  }
-  // bm_pref 4 / 5: the ping-pong 256 x 256 / 256 x 128 kernel (conv_pp_kernel)
+  if (per_cu == 0) per_cu = 2;  // default: 2 blocks per CU, every block resident
+  // bm_pref 4 / 5: force the ping-pong 256 x 256 / 256 x 128 kernel (conv_pp_kernel)
   if (bm_pref == 4) return launch_pp<256>(a, s);
   if (bm_pref == 5) return launch_pp<128>(a, s);
-  if (bm_pref == 7) return launch_pp<256, true>(a, s);
-  if (bm_pref == 8) return launch_pp<128, true>(a, s);
-  if (bm_pref == 9) return launch_pp<256, true, true>(a, s);
-  if (bm_pref == 10) return launch_pp<256, false, true>(a, s);
-  // 512 x 64 form (11 / 12): measured dead end -- the 64-cout layers are LDS-fill bound (58 FLOP per
-  // staged byte vs 128 at 256 x 256): 256^2 64+64->64 bs 64 661-691 TF/s vs 721 for the 256 x 64
-  // kernel, 128^2 128->64 652-667 vs 723; those layers keep the ring / halo / 256 x 64 kernels.
-  if (bm_pref == 11) return launch_pp<64, true, true>(a, s);
-  if (bm_pref == 12) return launch_pp<64, true, false>(a, s);
   // auto: the ping-pong 256 x 256 kernel wherever its tile grid fills the chip (>= 256 tiles of 256
   // pixels x 256 couts; fewer tiles leave CUs idle at one block per CU). Measured
   // (scripts/conv_microbench.py, bs 64, one MI355X): 64^2 256->256 903 -> 1082 TF/s, 32^2 512->512
   // 962 -> 1205, 32^2 512+512->256 927 -> 1120; bs 64 step 2973 -> 3150 img/s. The 256 x 128 form is
   // 2-4 % faster than the 128 x 128 kernel where K >= 1152 (128^2 128->128 851 -> 889, 64^2
-  // 256+256->128 882 -> 907; slower at K = 576) and +1.0-1.4 % on the bs 64 step (3003 / 3042 ->
-  // 3045 / 3071 img/s, interleaved). RDP_CONV_PP = 0: off, 1: 256-wide only, 2 (default): both.
+  // 256+256->128 882 -> 907; slower at K = 576) and +1.0-1.4 % on the bs 64 step.
   if (bm_pref == 0 && !packed) {
-    static const int pp_env = [] {
-      const char* e = getenv("RDP_CONV_PP");
-      return e ? atoi(e) : 2;
-    }();
     const long tiles256 = (long)(a.M + 255) / 256 * (Cout / 256);
-    if (pp_env && Cout % 256 == 0 && Cy1 % 32 == 0 && tiles256 >= 256 && escale == nullptr)
-      return launch_pp<256, true, true>(a, s);
-    // 256 x 128 form (RDP_CONV_PP=2 A/B): only where K is long enough (>= 128 input channels)
+    if (Cout % 256 == 0 && Cy1 % 32 == 0 && tiles256 >= 256 && escale == nullptr) return launch_pp<256>(a, s);
+    // 256 x 128 form: only where K is long enough (>= 128 input channels)
     const long tiles128 = (long)(a.M + 255) / 256 * (Cout / 128);
-    if (pp_env == 2 && Cout % 128 == 0 && Cy1 % 32 == 0 && tiles128 >= 256 && C1 + C2 >= 128 && escale == nullptr)
-      return launch_pp<128, true>(a, s);
+    if (Cout % 128 == 0 && Cy1 % 32 == 0 && tiles128 >= 256 && C1 + C2 >= 128 && escale == nullptr)
+      return launch_pp<128>(a, s);
   }
   const int max_blocks = 256 * per_cu;
   // bm_pref 2 / 3: 8-wave blocks (64 x 32 per wave; twice the waves per SIMD to hide the per-step
@@ -1292,56 +1068,6 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   return launch_cfg<256, 64, 8>(a, max_blocks, wse, s, pooled);
 }
 
-// dgrad (3x3 or 1x1, one source, one destination) on the ping-pong kernel with the BN-backward
-// reduction of the layer owning dx in its epilogue (BNR). Only where the auto dispatch of
-// rdp_conv_igemm would pick the ping-pong kernel for this shape (same kernel, same K order: dx is
-// bitwise equal to the plain dgrad); returns the partial rows written to `partial` ([rows][2][C]), or
-// -1 with nothing launched (the caller runs the plain dgrad + bn_relu_bwd_reduce).
-extern "C" int rdp_conv_dgrad_pp_bnred(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
-                                       void* y, long ybytes, int ypitch, int Cout, float* partial, long partial_elems,
-                                       int N, int H, int W, int taps, const void* bny, long bnybytes, int bnypitch,
-                                       const float* bncoef, hipStream_t s) {
-  static const int pp_env = [] {
-    const char* e = getenv("RDP_CONV_PP");
-    return e ? atoi(e) : 2;
-  }();
-  if (!pp_env || C % 64 || (taps != 9 && taps != 1) || ldw < taps * C || bnypitch % 4) return -1;
-  if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || bnybytes >= (1l << 31)) return -1;
-  const long M = (long)N * H * W;
-  const long tiles256 = (M + 255) / 256 * (Cout / 256);
-  const long tiles128 = (M + 255) / 256 * (Cout / 128);
-  const bool use256 = Cout % 256 == 0 && tiles256 >= 256;
-  const bool use128 = !use256 && pp_env == 2 && Cout % 128 == 0 && tiles128 >= 256 && C >= 128;
-  if (!use256 && !use128) return -1;
-  // RDP_PP_BNRED_WIDTH: 128 = only the 256 x 128 form takes the fused reduction (A/B: the 256-wide
-  // kernel has no VGPR headroom for the owner's y loads); 0 (default) = both
-  static const int width_env = [] {
-    const char* e = getenv("RDP_PP_BNRED_WIDTH");
-    return e ? atoi(e) : 0;
-  }();
-  if (width_env == 128 && use256) return -1;
-  const int BN = use256 ? 256 : 128;
-  const long grid = std::min<long>((M + 255) / 256 * (Cout / BN), 256);
-  const long rows = grid / (Cout / BN) * 2;
-  if (rows * 2 * Cout > partial_elems) return -1;
-  ConvArgs a{};
-  a.x1 = (const u16*)x; a.x2 = nullptr; a.xbytes1 = (uint32_t)xbytes; a.xbytes2 = 0;
-  a.C1 = C; a.C2 = 0; a.pitch1 = pitch; a.pitch2 = 0;
-  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
-  a.y1 = (u16*)y; a.y2 = nullptr; a.ybytes1 = (uint32_t)ybytes; a.ybytes2 = 0;
-  a.Cy1 = Cout; a.ypitch1 = ypitch; a.ypitch2 = 0; a.stats = partial;
-  a.escale = nullptr; a.eshift = nullptr; a.erelu = 0;
-  a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.M = (int)M;
-  a.taps = taps; a.packed = 0; a.cpt = C / 64; a.nks = taps * a.cpt;
-  a.kcnt = nullptr; a.kslab = nullptr;
-  a.store_aware = (g_conv_debug_flags & 1) ? 0 : 1;
-  const FastDiv fhw = make_fastdiv((uint32_t)(H * W)), fw = make_fastdiv((uint32_t)W);
-  a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;
-  a.bny = (const u16*)bny; a.bnybytes = (uint32_t)bnybytes; a.bnypitch = bnypitch; a.bncoef = bncoef;
-  // the same template arguments as the auto dispatch (+ BNR)
-  return use256 ? launch_pp<256, true, true, true>(a, s) : launch_pp<128, true, false, true>(a, s);
-}
-
 // fp32 workspace elements the auto dispatch would use for split-K on this shape (0 = no split)
 extern "C" long rdp_conv_ws_elems(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
   const int pref = bm_pref % 1000;
@@ -1353,5 +1079,5 @@ extern "C" long rdp_conv_ws_elems(int N, int H, int W, int C1, int C2, int Cout,
   const int BM = ((pref == 128 || pref == 0) && Cout % 128 == 0) ? 128 : 256, BN = BM == 128 ? 128 : 64;
   const int ntiles = (M + BM - 1) / BM * (Cout / BN);
   const int d = choose_ksplit(ntiles, nks, M, Cout, packed, 1L << 29);
-  return d > 1 ? (long)d * M * Cout + KCNT_WORDS : 0;
+  return d > 1 ? (long)d * M * Cout : 0;
 }

@@ -63,8 +63,6 @@ struct RingArgs {
 
 RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
-// ABL (ablation builds for the microbenchmark, RDP_RING_ABL): 1 = no ring DMA after the prologue,
-// 2 = no MFMA, 4 = no epilogue stores
 // COUT = 64: 8 waves = 2 channel groups x 4 pixel groups (32 px); COUT = 128: 4 x 2 (64 px).
 // BNR: dgrad epilogue fused with the owner layer's BN-backward reduction (a separate instantiation:
 // its y registers would otherwise cost every other variant 12 VGPRs -- spills at COUT = 128)
@@ -77,7 +75,7 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 // one row of 2x2 windows (rows 2P, 2P + 1 with H even): horizontal pairs are neighbouring lanes (DPP
 // swap), vertical pairs are the orow = 0 / 1 waves of a pixel group, exchanged through LDS (step-parity
 // double buffer) and finished by the orow = 0 waves after the next barrier.
-template <int COUT, int ABL = 0, bool BNR = false, bool HEAD = false, bool POOL = false>
+template <int COUT, bool BNR = false, bool HEAD = false, bool POOL = false>
 __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
   constexpr int PXW = 128 / NPG, NI = PXW / 16;  // pixels per wave (one output row half or whole)
@@ -288,7 +286,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
           yb[i][j] = *(const uint2*)pa;
         }
     }
-    const bool dma_next = !(ABL & 1) && ks + 2 < nks;
+    const bool dma_next = ks + 2 < nks;
     if (dma_next) issue(P + 2);
 
     const int R0 = 2 * P + orow;  // this wave's output row (column order)
@@ -347,8 +345,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int i = 0; i < NI; ++i)
-            if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(wa[2 * tap + kh][j]), "v"(fcur[kh][i]));
-            else acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fcur[kh][i], acc[j][i], 0, 0, 0);
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2 * tap + kh][j], fcur[kh][i], acc[j][i], 0, 0, 0);
       if (PIPE && tap + 1 < 9) {
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
@@ -449,8 +446,7 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
       const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
       const int m = m0 + px0 + 16 * i + (lane & 15);
       const uint32_t off = (uint32_t)(m * ypitch + cbase + coff) * 2u;
-      if constexpr ((ABL & 4) != 0) asm volatile("" ::"v"(rxs[0]), "v"(rys[0]), "v"(rxs[1]), "v"(rys[1]), "v"(off));
-      else bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
+      bstore16(ry, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
     }
   }
 
@@ -522,7 +518,7 @@ extern "C" int rdp_conv_ring_head(const void* x, long xbytes, int C, int pitch, 
   const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
   const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
   a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
-  hipLaunchKernelGGL((conv_ring_kernel<64, 0, false, true>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((conv_ring_kernel<64, false, true>), dim3(grid), dim3(512), 0, s, a);
   return 0;
 }
 
@@ -551,7 +547,7 @@ extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, 
   const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
   const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
   a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
-  hipLaunchKernelGGL((conv_ring_kernel<64, 0, false, false, true>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((conv_ring_kernel<64, false, false, true>), dim3(grid), dim3(512), 0, s, a);
   return 0;
 }
 
@@ -586,23 +582,14 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
   const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
   a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
-  static const int abl = [] {
-    const char* e = getenv("RDP_RING_ABL");
-    return e ? atoi(e) : 0;
-  }();
   if (Cout == 128) {
     hipLaunchKernelGGL((conv_ring_kernel<128>), dim3(grid), dim3(512), 0, s, a);
     return grid * 2;
   }
   if (bn_y) {
-    hipLaunchKernelGGL((conv_ring_kernel<64, 0, true>), dim3(grid), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_ring_kernel<64, true>), dim3(grid), dim3(512), 0, s, a);
     return grid * 4;
   }
-  switch (abl) {
-    case 1: hipLaunchKernelGGL((conv_ring_kernel<64, 1>), dim3(grid), dim3(512), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((conv_ring_kernel<64, 2>), dim3(grid), dim3(512), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((conv_ring_kernel<64, 4>), dim3(grid), dim3(512), 0, s, a); break;
-    default: hipLaunchKernelGGL((conv_ring_kernel<64>), dim3(grid), dim3(512), 0, s, a);
-  }
+  hipLaunchKernelGGL((conv_ring_kernel<64>), dim3(grid), dim3(512), 0, s, a);
   return grid * 4;
 }

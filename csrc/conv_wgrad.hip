@@ -48,11 +48,12 @@ RDP_DEV int swz(int p) { return (((p >> 1) & 1) << 1) | (((p >> 3) & 1) << 2); }
 
 RDP_DEV uint32_t fdiv2(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
-// BKP pixels per K step (64 or 32), STAGES LDS buffers (STAGES-1 steps in flight under the MFMAs).
-// NWV = 4: wave w owns x-subtile w (64 columns) x 64 couts; NWV = 8: waves 2s, 2s+1 split
-// x-subtile s into two 32-column halves (twice the waves per SIMD, same LDS footprint).
-template <bool PACKED, bool TILE_FAST, int BKP, int STAGES, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV, 2) void conv_wgrad_kernel(const WgradArgs a) {
+// BKP = 64 pixels per K step, double-buffered; 8 waves: waves 2s, 2s+1 split x-subtile s into two
+// 32-column halves (twice the waves per SIMD of a 4-wave block, same LDS footprint).
+template <bool PACKED>
+__global__ __launch_bounds__(512, 2) void conv_wgrad_kernel(const WgradArgs a) {
+  constexpr bool TILE_FAST = true;
+  constexpr int BKP = 64, STAGES = 2, NWV = 8;
   constexpr int SUB = BKP * 128;        // one [BKP pixels][64 ch] bf16 tile
   constexpr int BUF = 5 * SUB;          // 4 x-subtiles + 1 dy tile
   constexpr int PIECES = BKP / 8;       // 8-row DMA pieces per subtile
@@ -252,26 +253,12 @@ struct WgradHaloArgs {
   uint32_t fw_m, fw_s, fh_m, fh_s;
 };
 
-// ABL (microbenchmark ablations only): 1 = no DMA after the prologue, 2 = no MFMA, 4 = no LDS reads
-//
-// STAG (BN = 128, STAGES = 3): the two wave groups (waves 0-3 = couts 0..63, waves 4-7 = couts 64..127;
-// one wave of each per SIMD) run staggered by half a K step (one segment = one k half of the
-// step, 36 MFMAs, ended by a raw barrier), so one group's DMA wait and barrier overlap its SIMD
-// partner's MFMAs (cdna_hip_programming.md T3/T4 ping-pong). Ablations of the unstaggered kernel
-// (scripts/gpu_wg_abl.sh, 128^2 128->128 bs 64): 535 us full, 382 without the DMA, 381 without the
-// MFMAs, 344 with neither -- the DMA stream and the MFMA/LDS-read work each take ~70 % of the kernel
-// but barely overlap. Measured dead end: 11-13 % SLOWER than the unstaggered kernel (128^2 128->128
-// bs 64: 611 vs 539 us; 64^2 256->256: 582 vs 515) and -0.5..-0.7 % on the bs 64 step, so it is off
-// by default (RDP_WGRAD_STAG=1 / variant 7 for A/B; tests keep it bitwise equal). Schedule (segment (k, h) of group 0 runs in slot 2k + h, group 1 one slot later):
-//   * each wave's DMA segment is h = 1 (group 0) / h = 0 (group 1) -- both in slot 2k + 1: it issues
-//     step k + 2 into buffer (k + 2) % 3 (last read by group 1 in slot 2k) and, after its MFMAs, waits
-//     (counted vmcnt, step k + 2 left in flight) for its pieces of step k + 1, first read in slot
-//     2k + 2: 1.5 steps of lead instead of 1;
-//   * every segment's reads are consumed by its own MFMAs, so all LDS reads of a buffer are done
-//     before the barrier that precedes the next DMA into it.
-template <int BN, int STAGES, bool MULTIROW, int ABL = 0, bool STAG = false>
+// (Measured dead ends, numbers in profiles/dead_ends.md: a staggered two-group schedule and a 3-stage
+// ring of this kernel; ablations: the DMA stream and the MFMA / LDS-read work each take ~70 % of the
+// kernel but barely overlap -- the reason conv_wgrad_pp.hip exists.)
+template <int BN, bool MULTIROW>
 __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradHaloArgs a) {
-  static_assert(!STAG || (BN == 128 && STAGES == 3), "staggered schedule: 8 waves, 3 stages");
+  constexpr int STAGES = 2;
   constexpr int NWV = BN / 16;
   constexpr int XREG = 72 * 128;                  // one staged input row region (72 pixel rows x 64 ch)
   constexpr int DSUB = 64 * 128;                  // one [64 px][64 cout] dY subtile
@@ -348,33 +335,14 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
   for (int st = 0; st < STAGES - 1; ++st)
     if (st < nks) issue(st, smem + st * BUF);
   // pieces this wave issues per stage (wave-uniform): PPW or PPW - 1
-  const bool full_w = wave < NPIECES - (PPW - 1) * NWV;
-  auto wait_one_stage_in_flight = [&]() {  // all but the newest stage's pieces of this wave landed
-    if (full_w) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PPW - 1) : "memory");
-  };
-  const int grp = STAG ? wave >> 2 : 0;
-  if constexpr (STAG) {
-    if (nks > 1) wait_one_stage_in_flight();
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    raw_barrier();
-    if (grp == 1) raw_barrier();  // stagger by one segment
-  }
   for (int ks = 0; ks < nks; ++ks) {
-    if constexpr (!STAG) {
-      // 3 stages: leave THIS wave's pieces of step ks + 1 in flight (waves issue PPW or PPW - 1 pieces;
-      // a uniform NPIECES / NWV count made the PPW-piece waves wait for one piece of the next stage)
-      if (STAGES == 3 && ks + 1 < nks) wait_one_stage_in_flight();
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-      if (!(ABL & 1) && ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
-    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, smem + ((ks + STAGES - 1) % STAGES) * BUF);
     const char* cur = smem + (ks % STAGES) * BUF;
     const char* db = cur + 3 * XREG + cg * DSUB;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      const bool dma_seg = STAG && hf == 1 - grp;
-      if (dma_seg && ks + 2 < nks) issue(ks + 2, smem + ((ks + 2) % 3) * BUF);
       const int p0 = 32 * hf + 8 * tg + tq;
       bf16x8 fb[4];
       {
@@ -383,13 +351,9 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = 2 * i + (tpp >> 1);
-          if constexpr ((ABL & 4) != 0) {
-            fb[i] = bf16x8{(short)(lane + i), (short)ks, 1, 2, 3, 4, 5, (short)hf};
-          } else {
-            const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro0 + 16 * (c ^ sw0)));
-            const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro1 + 16 * (c ^ sw1)));
-            fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
-          }
+          const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro0 + 16 * (c ^ sw0)));
+          const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro1 + 16 * (c ^ sw1)));
+          fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
         }
       }
       // multi-row segments (W < 64): window pixel p + ds of tap ds = -1 / +1 crosses into the
@@ -413,36 +377,15 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
 #pragma unroll
         for (int r = 0; r < 3; ++r) {  // dr + 1: input row region
           const char* xb = cur + r * XREG;
-          bf16x8 fa;
-          if constexpr ((ABL & 4) != 0) {
-            fa = bf16x8{(short)(oa + r), (short)ob, (short)sh, 2, 3, 4, 5, (short)ks};
-          } else {
-            const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + oa));
-            const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + ob));
-            fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-          }
+          const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + oa));
+          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + ob));
+          const bf16x8 fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
           const int tap = r * 3 + sh;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(fa), "v"(fbs[i]));
-            else acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbs[i], acc[tap][i], 0, 0, 0);
-          }
+          for (int i = 0; i < 4; ++i) acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbs[i], acc[tap][i], 0, 0, 0);
         }
-      }
-      if constexpr (STAG) {
-        if (dma_seg && ks + 1 < nks) {  // this wave's pieces of step ks + 1 have landed
-          if (ks + 2 < nks) wait_one_stage_in_flight();
-          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        } else {
-          wait_lgkm0();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        raw_barrier();
       }
     }
-  }
-  if constexpr (STAG) {
-    if (grp == 0) raw_barrier();  // same barrier count for both groups
   }
 
   // acc[tap][i][r]: cin = cin0 + 16 cf + 4 (lane >> 4) + r, cout = cout0 + 64 cg + 16 i + (lane & 15)
@@ -489,7 +432,7 @@ struct WgradRingArgs {
   uint32_t fh_m, fh_s, fs_m, fs_s;  // fast div by H and by WS
 };
 
-template <int BN, int ABL = 0>
+template <int BN>
 __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradRingArgs a) {
   constexpr int NWV = BN / 16;
   constexpr int XREG = 72 * 128;   // one staged input row region: pixels w0-1 .. w0+70 (66 used)
@@ -582,7 +525,7 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradR
     if (ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (!(ABL & 1) && ks + 2 < nks) { issue(P + 3, true, false); issue(P + 2, false, true); }
+    if (ks + 2 < nks) { issue(P + 3, true, false); issue(P + 2, false, true); }
     int m0, h, w0;
     locate(P, m0, h, w0);
     const bool top = h == 0, bottom = h == a.H - 1;
@@ -616,10 +559,7 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradR
           const bf16x8 fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
           const int tap = r * 3 + sh;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if constexpr ((ABL & 2) != 0) asm volatile("" ::"v"(fa), "v"(fb[i]));
-            else acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[i], acc[tap][i], 0, 0, 0);
-          }
+          for (int i = 0; i < 4; ++i) acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[i], acc[tap][i], 0, 0, 0);
         }
       }
     }
@@ -700,8 +640,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
   }
 }
 
-static void launch_wgrad_reduce(float* slab, float* out, int splits, int Cout, int ncols_pad, int taps, int cin_pad,
-                                int cin_real, int accumulate, hipStream_t s) {
+extern "C" void rdp_wgrad_reduce(float* slab, float* out, int splits, int Cout, int ncols_pad, int taps, int cin_pad,
+                                 int cin_real, int accumulate, hipStream_t s) {
   const long E = (long)Cout * ncols_pad;  // multiple of 4 (Cout % 64 == 0)
   const long chunks = (E / 4 + 255) / 256;
   // ~1000 level-1 blocks, at most 32 group rows for level 2; few splits (deep layers) need no level 1
@@ -713,6 +653,11 @@ static void launch_wgrad_reduce(float* slab, float* out, int splits, int Cout, i
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rb), dim3(256), 0, s, slab, out, splits, G, Cout, ncols_pad, taps, cin_pad,
                      cin_real, accumulate);
 }
+
+// Which weight-gradient kernel the auto dispatch (variant 0) runs for a 3x3 layer: halo / row-ring where
+// whole 64-pixel row segments exist, the generic implicit GEMM for the rest (16^2 maps, packed first
+// layer). variant: 0 = auto, 4 = force the generic kernel, 5 = force the halo kernel. (A ping-pong
+// 256 x 256 implicit-GEMM wgrad was built and measured 2x slower than the halo kernel: profiles/dead_ends.md.)
 
 extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
                               int pitch2, const void* dy, long dybytes, int dypitch, float* slab, long slab_elems,
@@ -734,13 +679,12 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   }
   if (Cout % 64) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || dybytes >= (1l << 31)) return -1;
-  // halo-reuse kernel: 3x3, whole 64-pixel row segments (variant 0 = auto, 5 = force)
-  const bool halo_ok = !packed && taps == 9 && (W % 64 == 0 || (W >= (variant == 5 || variant == 7 ? 8 : 32) && 64 % W == 0 && (H * W) % 64 == 0));
-  if ((variant == 0 || variant == 5 || variant == 7 || (variant >= 30 && variant < 40)) && halo_ok) {
-    static const int env_blocks = [] {
-      const char* e = getenv("RDP_WGRAD_HALO_BLOCKS");
-      return e ? atoi(e) : 0;
-    }();
+  // halo-reuse kernel: 3x3, whole 64-pixel row segments
+  const bool halo_ok = !packed && taps == 9 && (W % 64 == 0 || (W >= 32 && 64 % W == 0 && (H * W) % 64 == 0)) &&
+                       variant != 4;
+  if (variant == 5 && !(!packed && taps == 9 && (W % 64 == 0 || (W >= 8 && 64 % W == 0 && (H * W) % 64 == 0))))
+    return -1;
+  if (halo_ok || variant == 5) {
     WgradHaloArgs h;
     h.x1 = a.x1; h.x2 = a.x2; h.xbytes1 = a.xbytes1; h.xbytes2 = a.xbytes2;
     h.C1 = C1; h.C2 = C2; h.pitch1 = pitch1; h.pitch2 = pitch2;
@@ -750,18 +694,11 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     h.cinTiles = a.Cin / 64; h.coutTiles = Cout / BN;
     const int tiles = h.cinTiles * h.coutTiles;
     h.nseg = a.M / 64;
-    // one resident wave of blocks (2/CU at BN = 64, 1/CU at BN = 128), within the slab
-    const int target = env_blocks > 0 ? env_blocks : (BN == 64 ? 512 : 256);
-    // RDP_WGRAD_MINSEG: at least this many 64-pixel segments per split (fewer splits, a smaller slab
-    // at small batch). Measured neutral (same box, 2 rounds, img/s): bs4 1595 / 1591 / 1589 / 1160
-    // and bs64 3105-3127 / 3127 / 3102-3156 / 3113-3174 for 1 / 4 / 16 / 64 -- the side-stream slab
-    // traffic is hidden under the main stream; 64 starves the bs4 grid. Default 1.
-    static const int env_minseg = [] {
-      const char* e = getenv("RDP_WGRAD_MINSEG");
-      return e ? std::max(1, atoi(e)) : 1;
-    }();
+    // one resident wave of blocks (2/CU at BN = 64, 1/CU at BN = 128), within the slab. (Other grid
+    // targets, a minimum segment count per split and the row ring at BN = 128 measured neutral.)
+    const int target = BN == 64 ? 512 : 256;
     int sp = std::max(1, (target + tiles - 1) / tiles);
-    sp = std::min(sp, std::max(1, h.nseg / env_minseg));
+    sp = std::min(sp, std::max(1, h.nseg));
     const long per_split = (long)Cout * h.ncols;
     sp = (int)std::min<long>(sp, slab_elems / per_split);
     if (sp < 1) return -2;
@@ -772,14 +709,7 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
     h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
     const int nblk = tiles * h.splits;
-    // A/B: the row-ring variant also at BN = 128. Measured neutral in the overlapped step (bs 64
-    // 2892 / 2915 vs 2897 / 2916 img/s; bs 4 1539 / 1544 vs 1535 / 1538), as is the halo grid
-    // target (RDP_WGRAD_HALO_BLOCKS 256 / 512 / 1024: 2891 / 2881 / 2881, 2880 / 2890 / 2879).
-    static const int env_ring128 = [] {
-      const char* e = getenv("RDP_WGRAD_RING128");
-      return e ? atoi(e) : 0;
-    }();
-    if (variant == 0 && W % 64 == 0 && (BN == 64 || env_ring128)) {  // row-ring variant: same split of the positions
+    if (variant == 0 && W % 64 == 0 && BN == 64) {  // row-ring variant: same split of the positions
       WgradRingArgs g;
       g.x1 = h.x1; g.x2 = h.x2; g.xbytes1 = h.xbytes1; g.xbytes2 = h.xbytes2;
       g.C1 = C1; g.C2 = C2; g.pitch1 = pitch1; g.pitch2 = pitch2;
@@ -789,73 +719,15 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
       g.pos_per_split = h.segs_per_split; g.npos = h.nseg; g.WS = W / 64;
       FastDiv fs = make_fastdiv(W / 64);
       g.fh_m = fh.m; g.fh_s = fh.s; g.fs_m = fs.m; g.fs_s = fs.s;
-      if (BN == 128) hipLaunchKernelGGL((conv_wgrad_ring_kernel<128>), dim3(nblk), dim3(512), 0, s, g);
-      else hipLaunchKernelGGL((conv_wgrad_ring_kernel<64>), dim3(nblk), dim3(256), 0, s, g);
-    } else if (variant >= 30 && variant < 40 && W % 64 == 0) {  // ring ablations (microbenchmark)
-      WgradRingArgs g;
-      g.x1 = h.x1; g.x2 = h.x2; g.xbytes1 = h.xbytes1; g.xbytes2 = h.xbytes2;
-      g.C1 = C1; g.C2 = C2; g.pitch1 = pitch1; g.pitch2 = pitch2;
-      g.dy = h.dy; g.dybytes = h.dybytes; g.dypitch = dypitch;
-      g.slab = slab; g.slab_bytes = h.slab_bytes; g.H = H; g.W = W; g.Cout = Cout; g.ncols = h.ncols;
-      g.cinTiles = h.cinTiles; g.coutTiles = h.coutTiles; g.splits = h.splits;
-      g.pos_per_split = h.segs_per_split; g.npos = h.nseg; g.WS = W / 64;
-      FastDiv fs = make_fastdiv(W / 64);
-      g.fh_m = fh.m; g.fh_s = fh.s; g.fs_m = fs.m; g.fs_s = fs.s;
-      const int abl = variant % 10;
-      if (BN == 128 && abl == 1) hipLaunchKernelGGL((conv_wgrad_ring_kernel<128, 1>), dim3(nblk), dim3(512), 0, s, g);
-      if (BN == 128 && abl == 2) hipLaunchKernelGGL((conv_wgrad_ring_kernel<128, 2>), dim3(nblk), dim3(512), 0, s, g);
-      if (BN == 64 && abl == 1) hipLaunchKernelGGL((conv_wgrad_ring_kernel<64, 1>), dim3(nblk), dim3(256), 0, s, g);
-      if (BN == 64 && abl == 2) hipLaunchKernelGGL((conv_wgrad_ring_kernel<64, 2>), dim3(nblk), dim3(256), 0, s, g);
+      hipLaunchKernelGGL((conv_wgrad_ring_kernel<64>), dim3(nblk), dim3(256), 0, s, g);
     } else {
-    const bool mr = W < 64;
-    static const int env_stages = [] {
-      const char* e = getenv("RDP_WGRAD_HALO_STAGES");  // 3 measured 3-8 % slower than 2
-      return e ? atoi(e) : 2;
-    }();
-    static const int env_stag = [] {
-      const char* e = getenv("RDP_WGRAD_STAG");
-      return e ? atoi(e) : 0;
-    }();
-    const bool stag = variant == 7 || (variant == 0 && env_stag != 0);  // 7: force the staggered halo kernel
-    // (multi-row segments keep the unstaggered kernel: the staggered multi-row build spills)
-    if (BN == 128 && stag && !mr)
-      hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 3, false, 0, true>), dim3(nblk), dim3(512), 0, s, h);
-    else if (BN == 128 && mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, true>), dim3(nblk), dim3(512), 0, s, h);
-    else if (BN == 128 && env_stages == 3)
-      hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 3, false>), dim3(nblk), dim3(512), 0, s, h);
-    else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, 2, false>), dim3(nblk), dim3(512), 0, s, h);
-    else if (mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2, true>), dim3(nblk), dim3(256), 0, s, h);
-    else hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, 2, false>), dim3(nblk), dim3(256), 0, s, h);
+      const bool mr = W < 64;
+      if (BN == 128 && mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, true>), dim3(nblk), dim3(512), 0, s, h);
+      else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, false>), dim3(nblk), dim3(512), 0, s, h);
+      else if (mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, true>), dim3(nblk), dim3(256), 0, s, h);
+      else hipLaunchKernelGGL((conv_wgrad_halo_kernel<64, false>), dim3(nblk), dim3(256), 0, s, h);
     }
-    launch_wgrad_reduce(slab, out, h.splits, Cout, h.ncols, 9, a.Cin, a.Cin, accumulate, s);
-    return h.splits;
-  }
-  if (variant == 5 || variant == 7) return -1;
-  if (variant >= 10 && variant < 30 && halo_ok && W % 64 == 0) {  // ablation builds (microbenchmark)
-    WgradHaloArgs h;
-    h.x1 = a.x1; h.x2 = a.x2; h.xbytes1 = a.xbytes1; h.xbytes2 = a.xbytes2;
-    h.C1 = C1; h.C2 = C2; h.pitch1 = pitch1; h.pitch2 = pitch2;
-    h.dy = a.dy; h.dybytes = a.dybytes; h.dypitch = dypitch;
-    h.slab = slab; h.H = H; h.W = W; h.Cout = Cout; h.ncols = 9 * a.Cin;
-    const int BN = variant >= 20 ? 128 : 64;
-    if (Cout % BN) return -1;
-    h.cinTiles = a.Cin / 64; h.coutTiles = Cout / BN;
-    const int tiles = h.cinTiles * h.coutTiles;
-    h.nseg = a.M / 64;
-    int sp = std::min(std::max(1, ((BN == 64 ? 512 : 256) + tiles - 1) / tiles), h.nseg);
-    sp = (int)std::min<long>(sp, slab_elems / ((long)Cout * h.ncols));
-    h.segs_per_split = (h.nseg + sp - 1) / sp;
-    h.splits = (h.nseg + h.segs_per_split - 1) / h.segs_per_split;
-    h.slab_bytes = (uint32_t)(h.splits * (long)Cout * h.ncols * 4l);
-    FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
-    h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
-    const int nblk = tiles * h.splits;
-    const int abl = variant % 10;
-#define RDP_ABL(B, A) \
-    if (BN == B && abl == A) hipLaunchKernelGGL((conv_wgrad_halo_kernel<B, 2, false, A>), dim3(nblk), dim3(B * 4), 0, s, h);
-    RDP_ABL(64, 0) RDP_ABL(64, 1) RDP_ABL(64, 2) RDP_ABL(64, 4) RDP_ABL(64, 6)
-    RDP_ABL(128, 0) RDP_ABL(128, 1) RDP_ABL(128, 2) RDP_ABL(128, 4) RDP_ABL(128, 6)
-#undef RDP_ABL
+    rdp_wgrad_reduce(slab, out, h.splits, Cout, h.ncols, 9, a.Cin, a.Cin, accumulate, s);
     return h.splits;
   }
   a.colTiles = (a.ncols + 255) / 256;
@@ -871,19 +743,10 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
   a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
   const int nblk = a.colTiles * a.coutTiles * a.splits;
-  if (packed) {
-    hipLaunchKernelGGL((conv_wgrad_kernel<true, true, 64, 2, 8>), dim3(nblk), dim3(512), 0, s, a);
-  } else if (variant == 1) {  // alternatives kept for the microbenchmark (measured slower on gfx950)
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 32, 3>), dim3(nblk), dim3(256), 0, s, a);
-  } else if (variant == 2) {
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 3>), dim3(nblk), dim3(256), 0, s, a);
-  } else if (variant == 3) {  // 4-wave blocks (previous default)
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2, 4>), dim3(nblk), dim3(256), 0, s, a);
-  } else {  // default: BK=64 pixels per stage, double-buffered, 8 waves (64 couts x 32 columns each)
-    hipLaunchKernelGGL((conv_wgrad_kernel<false, true, 64, 2, 8>), dim3(nblk), dim3(512), 0, s, a);
-  }
-  launch_wgrad_reduce(slab, out, a.splits, Cout, a.ncols_pad, taps, packed ? 8 : a.Cin, packed ? cin_real : a.Cin,
-                      accumulate, s);
+  if (packed) hipLaunchKernelGGL((conv_wgrad_kernel<true>), dim3(nblk), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<false>), dim3(nblk), dim3(512), 0, s, a);
+  rdp_wgrad_reduce(slab, out, a.splits, Cout, a.ncols_pad, taps, packed ? 8 : a.Cin, packed ? cin_real : a.Cin,
+                   accumulate, s);
   return a.splits;
 }
 
@@ -1084,10 +947,11 @@ extern "C" int rdp_wgrad_first_bn(const void* x, long xbytes, int xpitch, const 
   FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
   a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
   hipLaunchKernelGGL(wgrad_first_bn_kernel, dim3(splits), dim3(256), 0, s, a);
-  launch_wgrad_reduce(slab, out, splits, 64, FWG_NCOLS, 9, 8, cin_real, accumulate, s);
+  rdp_wgrad_reduce(slab, out, splits, 64, FWG_NCOLS, 9, 8, cin_real, accumulate, s);
   return splits;
 }
 
+// Slab size needed (elements) for a given configuration.
 // Slab size needed (elements) for a given configuration.
 extern "C" long rdp_conv_wgrad_slab_elems(int N, int H, int W, int Cin, int Cout, int taps, int packed, int splits) {
   const int ncols = packed ? 72 : taps * Cin;

@@ -285,119 +285,10 @@ RDP_DEV void geo_pick_digit(const unsigned* hist, int need, int* s_digit, int* s
   }
 }
 
-// One workgroup per bin, over that bin's points only. out: [nbins][kcap][4]; kout[b] = k written.
 // Per-bin top-k by y (k = max(1, int(n_bin * top)), capped); ties at the k-th value go to the
-// smallest point indices (= the reference's stable descending sort): radix select (8 x 8 bits, MSB first) of the k-th largest y key, then -- only
-// when the ties at that key are not all taken -- radix select (4 x 8 bits) of the largest index
-// among the ties to keep. The bin's keys and ids are cached in LDS (up to GEO_LCAP points; larger
-// bins read the excess from global memory), so each pass is LDS traffic + one histogram.
-#define GEO_LCAP 4096
-// sorted != nullptr: the block also x-sorts its bin's k points into sorted[off ..] (geo_sort.h), off =
-// the k of the earlier bins, derived from the bin counts -- no separate sort launch.
-__global__ __launch_bounds__(GEO_THREADS) void geo_select_kernel(const double* __restrict__ pts,
-                                                                 const int* __restrict__ npts_p, int nbins,
-                                                                 double top, GeoBins gb, double* __restrict__ out,
-                                                                 int kcap, int* __restrict__ kout, int min_points,
-                                                                 double* __restrict__ sorted, int* __restrict__ gperm,
-                                                                 int ecap) {
-  __shared__ unsigned hist[256];
-  __shared__ uint64_t skey[GEO_LCAP];
-  __shared__ int sid[GEO_LCAP];
-  __shared__ int s_digit, s_need, s_eq, s_cnt;
-  __shared__ double srt_x[SORT_LCAP], srt_y[SORT_LCAP];
-  __shared__ int srt_id[SORT_LCAP], srt_perm[SORT_LCAP];
-  const int bin = blockIdx.x;
-  const int n = npts_p[0];
-  const int nb = gb.cnt[bin];
-  if (n < min_points || nb == 0) {
-    if (threadIdx.x == 0) kout[bin] = 0;
-    return;
-  }
-  int start = 0;
-  for (int b = 0; b < bin; ++b) start += gb.cnt[b];
-  const int* ids = gb.bidx + start;
-  int k = (int)((double)nb * top);
-  if (k < 1) k = 1;
-  if (k > kcap) k = kcap;
-  for (int i = threadIdx.x; i < nb && i < GEO_LCAP; i += GEO_THREADS) {
-    const int id = ids[i];
-    sid[i] = id;
-    skey[i] = dkey(pts[(size_t)id * 4 + 1]);
-  }
-  auto key_at = [&](int i) -> uint64_t { return i < GEO_LCAP ? skey[i] : dkey(pts[(size_t)ids[i] * 4 + 1]); };
-  auto id_at = [&](int i) -> int { return i < GEO_LCAP ? sid[i] : ids[i]; };
-  // 1) k-th largest key
-  uint64_t prefix = 0;
-  int need = k, eq = 0;
-  for (int pass = 0; pass < 8; ++pass) {
-    const int shift = 56 - 8 * pass;
-    hist[threadIdx.x] = 0;  // GEO_THREADS == 256
-    __syncthreads();
-    const uint64_t pmask = pass == 0 ? 0ull : (~0ull << (64 - 8 * pass));
-    for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
-      const uint64_t key = key_at(i);
-      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) geo_pick_digit<true>(hist, need, &s_digit, &s_need, &s_eq);
-    __syncthreads();
-    prefix |= (uint64_t)s_digit << shift;
-    need = s_need;
-    eq = s_eq;
-  }
-  const uint64_t kth = prefix;
-  // 2) ties at kth: take the `need` smallest indices (all of them when need == #ties)
-  uint32_t last_id = 0xffffffffu;
-  if (need < eq) {
-    uint32_t ip = 0;
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      __syncthreads();
-      hist[threadIdx.x] = 0;
-      __syncthreads();
-      const uint32_t pmask = pass == 0 ? 0u : (~0u << (32 - 8 * pass));
-      for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
-        const uint32_t id = (uint32_t)id_at(i);
-        if (key_at(i) == kth && (id & pmask) == ip) atomicAdd(&hist[(id >> shift) & 255], 1u);
-      }
-      __syncthreads();
-      if (threadIdx.x < 64) geo_pick_digit<false>(hist, need, &s_digit, &s_need, &s_eq);
-      __syncthreads();
-      ip |= (uint32_t)s_digit << shift;
-      need = s_need;
-    }
-    last_id = ip;
-  }
-  // 3) write: key > kth, or == kth with index <= last_id (exactly k points)
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-  double* ob = out + (size_t)bin * kcap * 4;
-  for (int i = threadIdx.x; i < nb; i += GEO_THREADS) {
-    const uint64_t key = key_at(i);
-    const int id = id_at(i);
-    if (key > kth || (key == kth && (uint32_t)id <= last_id)) {
-      const int o = atomicAdd(&s_cnt, 1);
-      if (o < kcap)
-        for (int j = 0; j < 4; ++j) ob[(size_t)o * 4 + j] = pts[(size_t)id * 4 + j];
-    }
-  }
-  if (threadIdx.x == 0) kout[bin] = k;
-  if (sorted) {
-    int off = 0;  // sum of the earlier bins' k (the select's own rule, from the bin counts)
-    for (int b = 0; b < bin; ++b) {
-      const int c = gb.cnt[b];
-      int kb = (int)((double)c * top);
-      if (kb < 1) kb = 1;
-      if (kb > kcap) kb = kcap;
-      off += c > 0 ? kb : 0;
-    }
-    __syncthreads();  // this block's `out` writes are visible to all its threads
-    geo_sort_bin(ob, k, off, sorted, gperm, ecap, srt_x, srt_y, srt_id, srt_perm);
-  }
-}
-
-// Wave-per-bin variant of geo_select_kernel (the default): the same selection rule and tie-breaking,
-// with one wave owning one bin, so the 8 + 4 radix passes and the bitonic x-sort need no workgroup
+// smallest point indices (= the reference's stable descending sort), by radix select (8 x 8 bits,
+// MSB first) of the k-th largest y key, then -- only when the ties at that key are not all taken --
+// radix select (4 x 8 bits) of the largest index among the ties to keep. One wave owns one bin, so the 8 + 4 radix passes and the bitonic x-sort need no workgroup
 // barrier (a wave's LDS operations execute in issue order; the digit owner is found by ballot and
 // broadcast by a lane shuffle). The k selected points are compacted in point-index order (ballot +
 // popcount), so `out` is deterministic too. Bins beyond the LDS caches read / sort through global
@@ -690,15 +581,7 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
                      (const uint16_t*)depth, H, W, cam, counts, nblk, pts, cap, npts, xmin, xmax, nbins, gb);
   const int pblocks = (cap + GEO_THREADS * 4 - 1) / (GEO_THREADS * 4);
   hipLaunchKernelGGL(geo_bin_scatter_kernel, dim3(pblocks), dim3(GEO_THREADS), 0, s, npts, nbins, gb);
-  static const int env_sel = [] {  // RDP_GEO_SELECT=block: the workgroup-per-bin kernel (A/B)
-    const char* e = getenv("RDP_GEO_SELECT");
-    return e && e[0] == 'b' ? 1 : 0;
-  }();
-  if (env_sel)
-    hipLaunchKernelGGL(geo_select_kernel, dim3(nbins), dim3(GEO_THREADS), 0, s, pts, npts, nbins, top, gb, out, kcap,
-                       kout, min_points, sorted, gperm, secap);
-  else
-    hipLaunchKernelGGL(geo_select_wave_kernel, dim3((nbins + 3) / 4), dim3(256), 0, s, pts, npts, nbins, top, gb, out,
+  hipLaunchKernelGGL(geo_select_wave_kernel, dim3((nbins + 3) / 4), dim3(256), 0, s, pts, npts, nbins, top, gb, out,
                        kcap, kout, min_points, sorted, gperm, secap);
   if (edges) hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
   return nblk;

@@ -80,19 +80,9 @@ static const float* shrink_rows(const float* in, int T, int K, float* ws, int& r
   return ws;
 }
 
-static int fin_cpb() {  // channels per finalize block (RDP_FIN_CPB: 64 or 16)
-  static const int v = [] {
-    const char* e = getenv("RDP_FIN_CPB");
-    return e && atoi(e) == 16 ? 16 : 64;
-  }();
-  return v;
-}
-
 // coef layout: [0:C) mean, [C:2C) invstd, [2C:3C) scale = gamma*invstd, [3C:4C) shift = beta - mean*scale
-// CPB channels per block, 1024 / CPB row groups (CPB 16: four times the row groups, a quarter of the
-// dependent load rounds per thread, four times the blocks; RDP_FIN_CPB A/B). Measured neutral (same
-// box, 2 rounds: bs4 1587 / 1584 vs 1576 / 1590 img/s, bs64 3173 / 3154 vs 3157 / 3119): the ~7 us per
-// finalize is the kernel boundary, not the row walk. Default 64.
+// CPB channels per block, 1024 / CPB row groups. (16 channels per block -- four times the row groups --
+// measured neutral: the ~7 us per finalize is the kernel boundary, not the row walk.)
 template <int CPB>
 __global__ __launch_bounds__(64 * FIN_RG) void bn_finalize_kernel(const float* __restrict__ stats, int T, int C, double count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -341,9 +331,7 @@ int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* g
                     float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef, float* ws,
                     hipStream_t s) {
   stats = shrink_rows(stats, T, 2 * C, ws, T, s);
-  if (fin_cpb() == 16) hipLaunchKernelGGL(bn_finalize_kernel<16>, dim3((C + 15) / 16), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
-                     beta, rmean, rvar, nbt, momentum, eps, coef);
-  else hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
                      beta, rmean, rvar, nbt, momentum, eps, coef);
   return 0;
 }
@@ -378,9 +366,7 @@ int rdp_bn_relu_bwd_reduce(const void* da, int dapitch, const void* y, int ypitc
 int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const float* gamma, const float* coef,
                         float* dgamma, float* dbeta, float* coef2, float* ws, hipStream_t s) {
   partial = shrink_rows(partial, T, 2 * C, ws, T, s);
-  if (fin_cpb() == 16) hipLaunchKernelGGL(bn_bwd_finalize_kernel<16>, dim3((C + 15) / 16), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
-                     coef, dgamma, dbeta, coef2);
-  else hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, partial, T, C, (double)count, gamma,
                      coef, dgamma, dbeta, coef2);
   return 0;
 }

@@ -133,10 +133,7 @@ int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* s
   // blocks per segment: the largest layer (512 x 1024 x 9) has 1152 64x64 tiles; at 128 blocks per
   // segment every block of it walked 9 tiles back to back (latency-bound: 68 us per step, a fixed
   // cost at every batch size). Blocks of smaller segments past their tile count exit at once.
-  static const int gx = [] {
-    const char* e = getenv("RDP_WPREP_GRID");
-    return e ? std::max(1, atoi(e)) : 1152;
-  }();
+  constexpr int gx = 1152;
   hipLaunchKernelGGL(wprep_kernel, dim3(gx, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, step);
   return 0;
 }

@@ -100,3 +100,163 @@ int rdp_mask_upsample(const void* m, int mh, int mw, void* out, int H, int W, un
   return 0;
 }
 }
+
+// ---------------------------------------------------------------------------------------------
+// JPEG pixel stage on the GPU (the entropy decode is csrc/jpeg.cpp on the host). Follows libjpeg's
+// default decode of the reference server's cv2.imdecode (server.py:117): dequantisation + the ISLOW
+// integer IDCT (13-bit constants, 2 extra bits in pass 1, +128 and clamp), "fancy" (triangle) chroma
+// upsampling for 2x2 / 2x1 subsampling with edge replication, and the fixed-point YCbCr -> RGB of
+// jdcolor.c (16-bit scale). geo: see bindings.cpp jpeg_decode.
+#define JF_0_298631336 2446
+#define JF_0_390180644 3196
+#define JF_0_541196100 4433
+#define JF_0_765366865 6270
+#define JF_0_899976223 7373
+#define JF_1_175875602 9633
+#define JF_1_501321110 12299
+#define JF_1_847759065 15137
+#define JF_1_961570560 16069
+#define JF_2_053119869 16819
+#define JF_2_562915447 20995
+#define JF_3_072711026 25172
+
+// one 1-D ISLOW pass over v[0..7] (stride 1); results before the final descale: out[i] = value << shift
+RDP_DEV void jidct_1d(const int* v, int& e0, int& e1, int& e2, int& e3, int& o0, int& o1, int& o2, int& o3) {
+  int z2 = v[2], z3 = v[6];
+  int z1 = (z2 + z3) * JF_0_541196100;
+  const int t2 = z1 + z3 * (-JF_1_847759065);
+  const int t3 = z1 + z2 * JF_0_765366865;
+  z2 = v[0];
+  z3 = v[4];
+  const int t0 = (z2 + z3) << 13;
+  const int t1 = (z2 - z3) << 13;
+  e0 = t0 + t3;  // tmp10
+  e3 = t0 - t3;  // tmp13
+  e1 = t1 + t2;  // tmp11
+  e2 = t1 - t2;  // tmp12
+  int a0 = v[7], a1 = v[5], a2 = v[3], a3 = v[1];
+  z1 = a0 + a3;
+  z2 = a1 + a2;
+  z3 = a0 + a2;
+  int z4 = a1 + a3;
+  const int z5 = (z3 + z4) * JF_1_175875602;
+  a0 *= JF_0_298631336;
+  a1 *= JF_2_053119869;
+  a2 *= JF_3_072711026;
+  a3 *= JF_1_501321110;
+  z1 *= -JF_0_899976223;
+  z2 *= -JF_2_562915447;
+  z3 *= -JF_1_961570560;
+  z4 *= -JF_0_390180644;
+  z3 += z5;
+  z4 += z5;
+  o0 = a0 + z1 + z3;  // tmp0
+  o1 = a1 + z2 + z4;  // tmp1
+  o2 = a2 + z2 + z3;  // tmp2
+  o3 = a3 + z1 + z4;  // tmp3
+}
+
+__global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restrict__ coefs, const int* __restrict__ geo,
+                                                        const int* __restrict__ qt, uint8_t* __restrict__ planes) {
+  __shared__ int ws[32][64];
+  const int lb = threadIdx.x >> 3, k = threadIdx.x & 7;
+  const int jb = blockIdx.x * 32 + lb;
+  const int nc = geo[2];
+  const bool act = jb < geo[5];
+  int c = 0;
+  if (nc > 1 && jb >= geo[8 + 8 + 4]) c = 1;
+  if (nc > 2 && jb >= geo[8 + 16 + 4]) c = 2;
+  const int* g = geo + 8 + 8 * c;
+  if (act) {  // pass 1: column k, dequantised, results scaled by 2^2 (PASS1_BITS)
+    const int16_t* in = coefs + (long)jb * 64;
+    const int* q = qt + 64 * c;
+    int v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = (int)in[r * 8 + k] * q[r * 8 + k];
+    int e0, e1, e2, e3, o0, o1, o2, o3;
+    jidct_1d(v, e0, e1, e2, e3, o0, o1, o2, o3);
+    constexpr int S = 13 - 2, R = 1 << (S - 1);
+    ws[lb][0 * 8 + k] = (e0 + o3 + R) >> S;
+    ws[lb][7 * 8 + k] = (e0 - o3 + R) >> S;
+    ws[lb][1 * 8 + k] = (e1 + o2 + R) >> S;
+    ws[lb][6 * 8 + k] = (e1 - o2 + R) >> S;
+    ws[lb][2 * 8 + k] = (e2 + o1 + R) >> S;
+    ws[lb][5 * 8 + k] = (e2 - o1 + R) >> S;
+    ws[lb][3 * 8 + k] = (e3 + o0 + R) >> S;
+    ws[lb][4 * 8 + k] = (e3 - o0 + R) >> S;
+  }
+  __syncthreads();
+  if (!act) return;
+  int v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = ws[lb][k * 8 + i];
+  int e0, e1, e2, e3, o0, o1, o2, o3;
+  jidct_1d(v, e0, e1, e2, e3, o0, o1, o2, o3);
+  constexpr int S = 13 + 2 + 3, R = 1 << (S - 1);
+  auto px = [](int x) -> uint32_t { return (uint32_t)min(max(((x + R) >> S) + 128, 0), 255); };
+  const uint32_t p0 = px(e0 + o3), p7 = px(e0 - o3), p1 = px(e1 + o2), p6 = px(e1 - o2);
+  const uint32_t p2 = px(e2 + o1), p5 = px(e2 - o1), p3 = px(e3 + o0), p4 = px(e3 - o0);
+  const int lbi = jb - g[4], bw = g[2];
+  const int by = lbi / bw, bx = lbi - by * bw;
+  uint8_t* dst = planes + g[5] + (long)(by * 8 + k) * (bw * 8) + bx * 8;
+  *(uint2*)dst = make_uint2(p0 | p1 << 8 | p2 << 16 | p3 << 24, p4 | p5 << 8 | p6 << 16 | p7 << 24);
+}
+
+RDP_DEV int jpeg_chroma(const uint8_t* __restrict__ planes, const int* g, int hmax, int vmax, int y, int x) {
+  const uint8_t* base = planes + g[5];
+  const int stride = g[2] * 8, dsw = g[6], dsh = g[7];
+  const int hr = hmax / g[0], vr = vmax / g[1];
+  if (hr == 1 && vr == 1) return base[y * stride + x];
+  if (hr == 2 && vr == 1) {  // h2v1 fancy
+    const int cx = x >> 1;
+    const int v0 = base[y * stride + cx];
+    if ((x & 1) == 0) return (3 * v0 + base[y * stride + max(cx - 1, 0)] + 1) >> 2;
+    return (3 * v0 + base[y * stride + min(cx + 1, dsw - 1)] + 2) >> 2;
+  }
+  if (hr == 2 && vr == 2) {  // h2v2 fancy: vertical 3:1 column sums, then horizontal 3:1
+    const int cy = y >> 1, ny = (y & 1) ? min(cy + 1, dsh - 1) : max(cy - 1, 0);
+    const int cx = x >> 1;
+    auto colsum = [&](int cc) { return 3 * base[cy * stride + cc] + base[ny * stride + cc]; };
+    const int t = colsum(cx);
+    if ((x & 1) == 0) return (3 * t + colsum(max(cx - 1, 0)) + 8) >> 4;
+    return (3 * t + colsum(min(cx + 1, dsw - 1)) + 7) >> 4;
+  }
+  return base[(y / vr) * stride + x / hr];
+}
+
+__global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restrict__ planes, const int* __restrict__ geo,
+                                                         int H, int W, uint8_t* __restrict__ rgb) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= H * W) return;
+  const int y = p / W, x = p - y * W;
+  const int* g0 = geo + 8;
+  const int yy = planes[g0[5] + (long)y * (g0[2] * 8) + x];
+  int r = yy, gg = yy, b = yy;
+  if (geo[2] == 3) {
+    const int cb = jpeg_chroma(planes, geo + 16, geo[3], geo[4], y, x) - 128;
+    const int cr = jpeg_chroma(planes, geo + 24, geo[3], geo[4], y, x) - 128;
+    r = yy + ((91881 * cr + 32768) >> 16);
+    gg = yy + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
+    b = yy + ((116130 * cb + 32768) >> 16);
+  }
+  uint8_t* o = rgb + (long)p * 3;
+  o[0] = (uint8_t)min(max(r, 0), 255);
+  o[1] = (uint8_t)min(max(gg, 0), 255);
+  o[2] = (uint8_t)min(max(b, 0), 255);
+}
+
+extern "C" {
+// coefficient / plane capacity for frames of H x W (any supported sampling: Y and chroma planes at most
+// MCU-padded to 16 x 16)
+long rdp_jpeg_max_coefs(int H, int W) { return 3L * ((W + 15) / 16 * 16) * ((H + 15) / 16 * 16); }
+long rdp_jpeg_plane_bytes(int H, int W) { return rdp_jpeg_max_coefs(H, W); }
+
+int rdp_jpeg_gpu(const void* coefs, const int* geo, const int* qt, void* planes, int H, int W, int max_blocks, void* rgb,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(jpeg_idct_kernel, dim3((max_blocks + 31) / 32), dim3(256), 0, s, (const int16_t*)coefs, geo, qt,
+                     (uint8_t*)planes);
+  hipLaunchKernelGGL(jpeg_color_kernel, dim3((H * W + 255) / 256), dim3(256), 0, s, (const uint8_t*)planes, geo, H, W,
+                     (uint8_t*)rgb);
+  return 0;
+}
+}

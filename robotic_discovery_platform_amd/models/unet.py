@@ -304,14 +304,6 @@ class UNetNative(nn.Module):
         return cache[key]
 
 
-# eval-mode MaxPool2d fused into the split-K conv reduce (serving); "0" = separate maxpool launches
-_FUSE_POOL_EVAL = os.environ.get("RDP_FUSE_POOL_EVAL", "1") != "0"
-# eval decoder upsample fused into the split-K reduce of the conv producing its input; "0" = separate
-_FUSE_UP_EVAL = os.environ.get("RDP_FUSE_UP_EVAL", "1") != "0"
-# serving 1x1 head + threshold fused into the last conv's epilogue; "0" = separate head_mask launch
-_FUSE_HEAD_EVAL = os.environ.get("RDP_FUSE_HEAD_EVAL", "1") != "0"
-
-
 def _native():
     from ..ops import native
     return native()
@@ -351,27 +343,12 @@ class UNetExecutor:
         self.dice_eps = 1.0
         dev = model.store.device
         self.dev = dev
-        # BN apply + maxpool (forward) and maxpool backward + BN reduce (backward) in one pass each at
-        # the Down boundaries, upsample backward + BN reduce at the Up boundaries (RDP_FUSE_POOL=0:
-        # separate kernels, for A/B measurements)
-        self.fuse_pool = os.environ.get("RDP_FUSE_POOL", "1") != "0"
-        # training: the 1x1 head applies the last conv's BN+ReLU itself (forward) and produces that BN's
-        # backward partials and dy from the logits (backward), so the 64-ch activation and its gradient
-        # are never materialised (RDP_FUSE_HEAD=0: separate kernels, for A/B measurements)
-        self.fuse_head = training and os.environ.get("RDP_FUSE_HEAD", "1") != "0"
-        # training, bilinear decoder: the BN+ReLU of the layer under each Up block (down4.conv2,
-        # up1..3.conv2) is applied by the upsample kernel as it reads the pre-BN tensor, so those
-        # post-activation tensors are never written (their only reader is the upsample; backward
-        # works from the pre-BN tensor). Off by default: measured 0.3-0.5 % SLOWER at bs 64 (2966 / 2965
-        # vs 2981 / 2973 img/s, same box, interleaved) -- the upsample re-applies BN to each of the 4
-        # taps of every output (4x the input elements) and these tensors are small. RDP_FUSE_UP_BN=1 on.
-        self.fuse_up_bn = training and model.bilinear and os.environ.get("RDP_FUSE_UP_BN", "0") != "0"
-        # training, RDP_SKIP_SIDE=1: at each Down boundary the pool-only BN+ReLU+maxpool runs on the main
-        # stream and the skip activation on the wgrad side stream (idle during forward). Measured dead
-        # end (same box, interleaved): bs 64 3096 / 3097 -> 3072 / 3077 img/s, bs 4 neutral -- the
-        # side-stream pass competes for HBM with the forward; default: one fused kernel on the main stream
-        self.skip_side = False
-        self._skip_pending = False
+        # Fusions (each measured against its separate-kernel form, profiles/dead_ends.md): BN apply +
+        # maxpool (forward) and maxpool backward + BN reduce (backward) in one pass each at the Down
+        # boundaries, upsample backward + BN reduce at the Up boundaries; in training the 1x1 head
+        # applies the last conv's BN+ReLU itself (forward) and produces that BN's backward partials and
+        # dy from the logits (backward), so the 64-ch activation and its gradient are never stored.
+        self.fuse_head = training
         C = _native()
         D = model.depth
         bf = torch.bfloat16
@@ -469,8 +446,6 @@ class UNetExecutor:
             ws = max(ws, C.conv_ws_elems(n, h, w, us.cin, 0, 4 * us.cout, 1, 0, 0))
             if training:
                 ws = max(ws, C.conv_ws_elems(n, h, w, 4 * us.cout, 0, us.cin, 1, 0, 0))
-        if os.environ.get("RDP_SPLITK", "1") == "0":  # A/B knob: no split-K (every conv one pass)
-            ws = 0
         self.kws = torch.zeros(ws, dtype=torch.float32, device=dev) if ws else None
         if training:
             self._alloc_backward(C)
@@ -483,43 +458,14 @@ class UNetExecutor:
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
         self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
-        self.skip_side = self.side is not None and self.fuse_pool and os.environ.get("RDP_SKIP_SIDE", "0") != "0"
-        # RDP_WGRAD_STREAMS > 1: weight gradients round-robin over that many side streams, each with
-        # its own slab (consecutive layers' wgrads run concurrently, not queued behind each other).
-        # Measured dead end (same box, 2 rounds): bs4 1499 / 1451 / 1444 img/s and bs64 2994-2998 /
-        # 2949-2964 / 2944-2962 for 1 / 2 / 3 streams -- every extra stream lands on another hardware
-        # queue and the contention costs more than the added concurrency (cf. graph replay, engine.py)
-        nside = max(1, int(os.environ.get("RDP_WGRAD_STREAMS", "1"))) if self.side is not None else 1
-        self.sides = [self.side] + [torch.cuda.Stream(dev) for _ in range(nside - 1)] if self.side is not None else []
-        self._side_rr = 0
-        # Measured dead ends on this side stream (bs64, one MI355X): (a) the skip half of each Up conv's
-        # input gradient moved here off the main stream's critical path: 1% slower with the old
-        # 2048-block wgrad grid (2717 vs 2740 img/s), 5% slower with the 512-block grid (2790 vs 2940;
-        # 4% at bs4); (b) a CU-masked side stream (hipExtStreamCreateWithCUMask, 25-87.5% of the CUs):
-        # 8% slower; (c) a high-priority main stream: neutral.
-        # split-K grid target of the weight-gradient kernels (tuning knob, RDP_WGRAD_BLOCKS). Fewer
-        # splits = less fp32 slab traffic (written by the wgrad, re-read by the reduction), more =
-        # more parallelism. Re-measured after the epilogue/fusion work (img/s): bs64 256 -> 2334,
-        # 512 -> 2926 / 2890, 768 -> 2912, 1024 -> 2879, 2048 -> 2880 / 2864, 4096 -> 2882;
-        # bs32 512 -> 2809 vs 2048 -> 2738; bs4 512 -> 1477 vs 2048 -> 1462 (the cliff is below 512);
-        # same-box repeat at bs64: 512 -> 2882 / 2902, 768 -> 2872 / 2872, 1024 -> 2845 / 2842,
-        # 2048 -> 2841 / 2839. (Serialised, the wgrads alone prefer more splits: the side stream's
-        # wgrads overlap the main stream, so a lighter slab wins.)
-        self.wgrad_blocks = int(os.environ.get("RDP_WGRAD_BLOCKS", "512"))
-        # dgrad into the da of a BN layer: where the row-ring kernel runs it (64 -> 64 channels), its
-        # epilogue also produces that layer's BN-backward partial sums (no bn_relu_bwd_reduce pass)
-        self.dgrad_bnred = os.environ.get("RDP_DGRAD_BNRED", "1") != "0"
-        # ping-pong dgrad with the owner's BN-backward reduction in its epilogue (conv_dgrad_pp_bnred, the
-        # 7 remaining bn_relu_bwd_reduce passes at bs64). Measured dead end, off by default: bs64 1.2 %
-        # SLOWER (3084-3095 vs 3119-3137 img/s, 3 interleaved rounds, same box; bs4 neutral) -- the owner's
-        # y loads sit latency-exposed in the persistent kernel's per-tile epilogue, stalling both wave
-        # groups, which costs more than the separate 376 us (serialised) reduce pass it removes. Restricted
-        # to the 256 x 128 form (RDP_PP_BNRED_WIDTH=128, which has VGPR headroom): neutral (3036-3044 vs
-        # 3032-3051 img/s, 3 rounds; both widths 3010-3023).
-        self.dgrad_pp_bnred = self.dgrad_bnred and os.environ.get("RDP_DGRAD_PP_BNRED", "0") != "0"
-        # first layer: BN-backward apply fused into its weight gradient (no dz tensor pass)
-        self.fuse_first_wgrad = dev.type == "cuda" and os.environ.get("RDP_FUSE_FIRST_WGRAD", "1") != "0"
+        # split-K grid target of the generic / packed weight-gradient kernels. Fewer splits = less fp32
+        # slab traffic, more = more parallelism; 512 measured best at bs 4 .. 64 (the side stream's wgrads
+        # overlap the main stream, so a lighter slab wins over the serialised optimum).
+        self.wgrad_blocks = 512
         N = self.N
+        D = self.m.depth
+
+        def like(x):        N = self.N
         D = self.m.depth
 
         def like(x):
@@ -576,15 +522,11 @@ class UNetExecutor:
             # roles swapped in conv_wgrad: "x" = dyT (4*cout ch), "dy" = the ConvT input (cin ch)
             slab = max(slab, C.wgrad_slab_elems(n, h, w, 4 * us.cout, us.cin, 1, 0, sp_))
         self.slab = torch.zeros(slab, dtype=torch.float32, device=dev)
-        self.slabs = [self.slab] + [torch.zeros(slab, dtype=torch.float32, device=dev)
-                                    for _ in range(max(0, len(self.sides) - 1))]
         # The first layer's wgrad is the step's last gradient; the side stream is still working off
         # its backlog then while the main stream idles, so it runs on the main stream with its own slab
-        # (RDP_LAST_WGRAD_MAIN=0: on the side stream like the others; also moving the second-to-last
-        # layer's wgrad to the main stream measured 1.3% slower, 2913 / 2869 vs 2947 / 2912 img/s)
-        self.last_wgrad_main = self.side is not None and os.environ.get("RDP_LAST_WGRAD_MAIN", "1") != "0"
+        # (moving the second-to-last layer's wgrad there too measured 1.3 % slower)
         self.slab_main = None
-        if self.last_wgrad_main:
+        if self.side is not None:
             L0 = self.down_layers[0][0]
             n, h, w, _ = L0.x1.shape
             cin = L0.spec.cin if not L0.spec.packed else 8
@@ -622,12 +564,7 @@ class UNetExecutor:
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
             # with ``pool`` / ``up``: MaxPool2d(2) / the upsample too (fused into the split-K reduce or
-            # the row-ring epilogue where those run; RDP_FUSE_POOL_EVAL=0 / RDP_FUSE_UP_EVAL=0: the
-            # separate launches, for A/B)
-            if pool is not None and not _FUSE_POOL_EVAL:
-                pool = None
-            if up is not None and not _FUSE_UP_EVAL:
-                up = None
+            # the row-ring epilogue where those run, else separate launches)
             if up is not None:
                 oy = (up.shape[1] - 2 * L.a.shape[1]) // 2
                 ox = (up.shape[2] - 2 * L.a.shape[2]) // 2
@@ -645,15 +582,8 @@ class UNetExecutor:
                 rows, M = self._sync_rows(self.stats, rows, sp.cout, (L.y.shape[1], L.y.shape[2]))
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
                           m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
-        if pool is not None and self.fuse_pool:
-            if self.skip_side:
-                # the pool (next conv's input) on the critical path; the skip activation (read only by the
-                # decoder and the backward) written on the side stream, overlapping the next convs
-                C.bn_relu_apply_pool(L.y, None, pool, L.coef)
-                self._on_side(lambda: C.bn_relu_apply(L.y, L.a, L.coef, 1))
-                self._skip_pending = True
-            else:
-                C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
+        if pool is not None:
+            C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
             return True
         if apply:
             C.bn_relu_apply(L.y, L.a, L.coef, 1)
@@ -675,8 +605,7 @@ class UNetExecutor:
         pipeline recomputes them only when the weights change, not per frame).
         ``mask_head=(head_w, head_b, logit_thr, mask_u8)`` (eval, with ``head=False``): the serving mask
         ``head(a_final) > logit_thr``; where the row-ring kernel runs the last conv, the head is fused
-        into its epilogue and ``final`` is not materialised (RDP_FUSE_HEAD_EVAL=0: the separate
-        ``head_mask`` launch)."""
+        into its epilogue and ``final`` is not materialised (elsewhere the separate ``head_mask`` launch)."""
         C = _native()
         D = self.m.depth
         if not self.training and refresh_eval:
@@ -685,7 +614,7 @@ class UNetExecutor:
         self._conv_bn_relu(C, l0)
         pooled = self._conv_bn_relu(C, l1, self.pools[0] if D > 0 else None)
         # eval, bilinear decoder: each decoder input upsample is produced by the conv that makes `low`
-        eval_up = not self.training and self.m.bilinear and not self.fuse_up_bn
+        eval_up = not self.training and self.m.bilinear
         upsampled = False
         for i in range(1, D + 1):
             if not pooled:
@@ -695,13 +624,8 @@ class UNetExecutor:
             if i == D and eval_up:
                 upsampled = self._conv_bn_relu(C, lb, up=self.ups[0])
                 continue
-            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None,
-                                        apply=not (i == D and self.fuse_up_bn))
+            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None)
         low = self.skips[D]
-        low_layer = self.down_layers[D][1]
-        if self._skip_pending:  # the decoder reads the skip activations written on the side stream
-            _stream_wait(torch.cuda.current_stream(), self.side)
-            self._skip_pending = False
         for i in range(1, D + 1):
             lv = D - i
             u = self.ups[i - 1]
@@ -709,8 +633,6 @@ class UNetExecutor:
             ox = (u.shape[2] - 2 * low.shape[2]) // 2
             if upsampled:
                 upsampled = False
-            elif self.m.bilinear and self.fuse_up_bn:
-                C.upsample2_fwd(low_layer.y, u, oy, ox, low_layer.coef)  # BN + ReLU of low_layer on the fly
             elif self.m.bilinear:
                 C.upsample2_fwd(low, u, oy, ox)
             else:
@@ -726,9 +648,8 @@ class UNetExecutor:
             if not last and eval_up:
                 upsampled = self._conv_bn_relu(C, lb, up=self.ups[i])
             else:
-                self._conv_bn_relu(C, lb, apply=not ((last and self.fuse_head and head) or
-                                                     (not last and self.fuse_up_bn)))
-            low, low_layer = lb.a, lb
+                self._conv_bn_relu(C, lb, apply=not (last and self.fuse_head and head))
+            low = lb.a
         if not head:
             if mask_head is not None:
                 C.head_mask(self.final, *mask_head)
@@ -752,7 +673,7 @@ class UNetExecutor:
     def _conv_head_mask(self, C, L: _Layer, mask_head: tuple) -> bool:
         """Eval: the last conv + BN fold + ReLU + 1x1 head + threshold in one row-ring launch."""
         sp = L.spec
-        if self.training or not _FUSE_HEAD_EVAL or L.x2 is not None or sp.taps != 9 or sp.packed:
+        if self.training or L.x2 is not None or sp.taps != 9 or sp.packed:
             return False
         hw, hb, thr, mask = mask_head
         return bool(C.conv_head_mask(L.x1, self.m.fwd_weight(sp), L.coef, hw, hb, float(thr), mask))
@@ -835,22 +756,10 @@ class UNetExecutor:
         buf[: 2 * c].copy_(tot)
         return 1, self._sync_m[hw]
 
-    def _join_sides_into_side(self):
-        """Make the first side stream wait for the others (before a DDP bucket hook: the bucket's
-        all-reduce must see every wgrad issued so far, whichever side stream ran it)."""
-        for st in self.sides[1:]:
-            _stream_wait(self.side, st)
-
     def _on_wgrad_stream(self, fn):
-        """Run ``fn(slab)`` (a weight gradient) on the next side stream with that stream's slab."""
-        if len(self.sides) <= 1:
-            return self._on_side(lambda: fn(self.slab))
-        k = self._side_rr % len(self.sides)
-        self._side_rr += 1
-        st = self.sides[k]
-        _stream_wait(st, torch.cuda.current_stream())
-        with torch.cuda.stream(st):
-            return fn(self.slabs[k])
+        """Run ``fn(slab)`` (a weight gradient) on the side stream with its slab. (Several side streams,
+        one per consecutive wgrad, measured slower: every extra stream lands on another hardware queue.)"""
+        return self._on_side(lambda: fn(self.slab))
 
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream
@@ -865,7 +774,7 @@ class UNetExecutor:
         sp = L.spec
         st = self.m.store
         gw = st.flat_slice(sp.name + ".weight", st.grad)
-        if (self.fuse_first_wgrad and L is self.down_layers[0][0] and sp.packed and L.dx1 is None
+        if (self.dev.type == "cuda" and L is self.down_layers[0][0] and sp.packed and L.dx1 is None
                 and head_gscale is None and sp.cout == 64):
             # first layer: its pre-BN gradient feeds only the weight gradient, so the BN-backward apply
             # runs inside that wgrad (wgrad_first_bn) and dz is never stored
@@ -884,7 +793,6 @@ class UNetExecutor:
             else:
                 self._on_wgrad_stream(fused)
             if hooks is not None:
-                self._join_sides_into_side()
                 self._on_side(lambda: hooks(sp))
             return
         self._bn_bwd(C, L, head_gscale)
@@ -897,24 +805,17 @@ class UNetExecutor:
         else:
             self._on_wgrad_stream(lambda slab: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real,
                                                             slab, gw, 0, L.splits, 0))
-        owner = L.dx1_owner if self.dgrad_bnred else None
+        # dgrad into the da of a BN layer: where the row-ring kernel runs it (64 -> 64 channels), its
+        # epilogue also produces that layer's BN-backward partial sums (no bn_relu_bwd_reduce pass)
+        owner = L.dx1_owner
         if owner is not None and L.dx2 is None and sp.taps == 9 and not owner.bwd_rows:
             rows = C.conv_dgrad_bnred(L.dy, self.m.dgrad_weight(sp), L.dx1, owner.y, owner.coef, self.bn_partial)
-            if rows > 0:
-                owner.bwd_rows = rows
-                owner = True
-        if (owner is not None and owner is not True and L.dx2 is None and self.dgrad_pp_bnred
-                and not owner.bwd_rows):
-            # wider layers: the ping-pong dgrad's epilogue produces the owner's BN-backward partials
-            rows = C.conv_dgrad_pp_bnred(L.dy, self.m.dgrad_weight(sp), sp.taps, L.dx1, owner.y, owner.coef,
-                                         self.bn_partial)
             if rows > 0:
                 owner.bwd_rows = rows
                 owner = True
         if L.dx1 is not None and owner is not True:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:
-            self._join_sides_into_side()
             self._on_side(lambda: hooks(sp))  # the bucket's all-reduce waits for the wgrad too
 
     def backward(self, grad_hook=None, gscale: float = 1.0):
@@ -930,8 +831,7 @@ class UNetExecutor:
             self._backward(C, D, st, grad_hook, gscale)
         finally:
             if main is not None:
-                for side in self.sides:
-                    _stream_wait(main, side)  # join
+                _stream_wait(main, self.side)  # join
 
     def _backward(self, C, D, st, grad_hook, gscale):
         head_w = st.view("outc.conv.weight").reshape(-1)
@@ -962,12 +862,9 @@ class UNetExecutor:
             du = self.dups[i - 1]
             oy = (du.shape[1] - 2 * low_layer.a.shape[1]) // 2
             ox = (du.shape[2] - 2 * low_layer.a.shape[2]) // 2
-            if self.m.bilinear:
-                if self.fuse_pool:  # + the BN-backward reduction of low_layer (like the pool boundary)
-                    low_layer.bwd_rows = C.upsample2_bwd(du, low_layer.da, oy, ox, low_layer.y, low_layer.coef,
-                                                         self.bn_partial)
-                else:
-                    C.upsample2_bwd(du, low_layer.da, oy, ox)
+            if self.m.bilinear:  # + the BN-backward reduction of low_layer (like the pool boundary)
+                low_layer.bwd_rows = C.upsample2_bwd(du, low_layer.da, oy, ox, low_layer.y, low_layer.coef,
+                                                     self.bn_partial)
             else:
                 us = self.m.up_specs[i - 1]
                 dyT = self.dyTs[i - 1]
@@ -979,18 +876,14 @@ class UNetExecutor:
                 C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
                            self.kws)
                 if grad_hook is not None:
-                    self._join_sides_into_side()
                     self._on_side(lambda: grad_hook(us))
         for i in range(D, 0, -1):
             la, lb = self.down_layers[i]
             self._conv_bwd(C, lb, grad_hook)
             self._conv_bwd(C, la, grad_hook)
             prev = self.down_layers[i - 1][1]
-            if self.fuse_pool:
-                prev.bwd_rows = C.maxpool2_bwd_bn_reduce(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1],
-                                                         prev.da, prev.y, prev.coef, self.bn_partial)
-            else:
-                C.maxpool2_bwd(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1], prev.da)
+            prev.bwd_rows = C.maxpool2_bwd_bn_reduce(self.dpools[i - 1], self.skips[i - 1], self.dskips[i - 1],
+                                                     prev.da, prev.y, prev.coef, self.bn_partial)
         l0, l1 = self.down_layers[0]
         self._conv_bwd(C, l1, grad_hook)
         self._conv_bwd(C, l0, grad_hook)

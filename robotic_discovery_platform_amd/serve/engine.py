@@ -79,33 +79,11 @@ class FrameResult:
 
 
 def _stage(dst: torch.Tensor, src: np.ndarray) -> None:
-    """Copy a host frame into its pinned staging tensor (on every frame's latency path).
-
-    RDP_STAGE_TORCH: 0 (default) = numpy assignment; 1 = torch's OpenMP-threaded copy (640x480 RGB +
-    depth: ~26 us p50 vs ~140 us, but its spinning workers compete with the codec / gRPC threads).
-    Measured with the colour H2D enqueued before the depth is staged (same box, 4 interleaved rounds):
-    engine p50 0.591-0.594 vs 0.575-0.595 ms (a wash), engine 1681-1693 vs 1535-1660 FPS, pipelined
-    2942-2966 vs 2529-3003 FPS, e2e 814-1021 vs 529-1005 FPS -- the numpy copy is steadier and
-    faster under load. (A worker pool of numpy band copies took ~375 us: GIL hand-offs.) Negative-
-    stride views always take numpy's path; read-only arrays are only read (torch's one-time "not
-    writable" warning is silenced)."""
-    global _stage_warned
-    if _STAGE_MODE == 1 and all(st >= 0 for st in src.strides) and \
-            src.dtype == np.dtype(str(dst.dtype).replace("torch.", "")):
-        if src.flags.writeable or _stage_warned:
-            dst.copy_(torch.from_numpy(src))
-        else:
-            import warnings
-            with warnings.catch_warnings():
-                warnings.simplefilter("ignore")
-                dst.copy_(torch.from_numpy(src))
-            _stage_warned = True
-    else:
-        dst.numpy()[...] = src
-
-
-_stage_warned = False
-_STAGE_MODE = int(os.environ.get("RDP_STAGE_TORCH", "0"))
+    """Copy a host frame into its pinned staging tensor (on every frame's latency path). A numpy
+    assignment: torch's OpenMP-threaded copy was 4x faster alone but its spinning workers cost engine
+    and e2e throughput under load, and a worker pool of band copies paid GIL hand-offs
+    (profiles/dead_ends.md)."""
+    dst.numpy()[...] = src
 
 
 def _logit(p: float) -> float:

@@ -15,9 +15,6 @@ stream, while ~10 us of host time per launch stays ahead of the GPU even at bs 4
 therefore means eager launches for training; serving (N=1, latency-bound) keeps its graphs.
 With world > 1 the bucketed all-reduces overlap backward on RCCL's stream.
 
-``RDP_MAIN_PRIO=1`` runs the step on a high-priority stream (side stream at normal priority);
-measured neutral at bs 64 (2710 vs 2715 img/s), so off by default.
-
 Plan mode (``plan=True``; "auto" = on for single-process training without a graph): the third step
 is recorded by the native runtime (``csrc/bindings.cpp``: every kernel launch and cross-stream wait of
 the step, with its validated raw arguments and stream) and every later step is ONE ``plan_replay``
@@ -28,9 +25,8 @@ host-side decisions that change between steps, a constant learning rate and the 
 at every call. ``RDP_PLAN=0`` disables it. Measured (one MI355X, interleaved): host enqueue per bs-4
 step 1.55 -> 1.37 ms, step time unchanged (bs 4 2.53 ms, bs 64 20.1 ms either way) -- the remaining
 host cost is HIP's own ~7 us per kernel launch, which the GPU still outruns only in runs of
-sub-10-us kernels. ``RDP_PLAN_GRAPH=1`` additionally compiles each single-stream run of the plan into
-a hipGraph (``plan_compile``; bitwise equal, tests/test_unet_native_gpu.py): measured SLOWER (bs 4
-2.53 -> 2.68 ms, bs 64 20.3 -> 20.5 ms), so off by default.
+sub-10-us kernels. (Compiling each single-stream run of the plan into a hipGraph and a high-priority
+main stream measured slower / neutral: profiles/dead_ends.md.)
 
 ``EagerTrainer`` is the reference execution model (torch autograd + MIOpen) used for the CPU path,
 CPU/gloo DDP tests and as the measured comparison baseline.
@@ -86,21 +82,12 @@ class NativeTrainer:
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
         self.use_graph = bool(graph) and not self.ddp and torch.cuda.is_available()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.stream = None
-        if torch.cuda.is_available() and model.store.device.type == "cuda" and \
-                os.environ.get("RDP_MAIN_PRIO", "0") != "0":
-            lo, hi = torch.cuda.Stream.priority_range()
-            if hi != lo:
-                self.stream = torch.cuda.Stream(device=model.store.device, priority=hi)
         if plan == "auto":
             plan = os.environ.get("RDP_PLAN", "1") != "0"
-        self.use_plan = (bool(plan) and not self.ddp and not self.use_graph and self.stream is None
+        self.use_plan = (bool(plan) and not self.ddp and not self.use_graph
                          and torch.cuda.is_available() and model.store.device.type == "cuda")
         self.plan_id: Optional[int] = None
         self._plan_version = None
-        # RDP_PLAN_GRAPH=1: replay each single-stream run of launches of the plan as one hipGraph
-        self._plan_stream = (torch.cuda.Stream(device=model.store.device)
-                             if self.use_plan and os.environ.get("RDP_PLAN_GRAPH", "0") != "0" else None)
         self.steps = 0
 
     def __del__(self):
@@ -140,37 +127,25 @@ class NativeTrainer:
         if self.use_plan:
             from ..ops import native
             C = native(build_if_missing=False)
-            cur = torch.cuda.current_stream()
-            ps = self._plan_stream
-            if ps is not None:  # graph-compiled plans run on an owned stream (the null stream cannot be captured)
-                C.stream_wait(ps.cuda_stream, cur.cuda_stream)
-                ctx = torch.cuda.stream(ps)
-            else:
-                ctx = contextlib.nullcontext()
             version = (self.model.__dict__.get("_layout_version"), self.opt.hyper_key())
             if self.plan_id is not None and self._plan_version != version:
                 # buffers re-laid out or optimizer hyper-parameters changed (lr schedule, Adam
                 # load_state_dict): the recorded launches bake those in, so record again
                 C.plan_free(self.plan_id)
                 self.plan_id = None
-            with ctx:
-                if self.plan_id is not None:
-                    C.plan_replay(self.plan_id)
-                elif self.steps < 2:  # first steps eagerly (first-launch costs, flags that settle)
+            if self.plan_id is not None:
+                C.plan_replay(self.plan_id)
+            elif self.steps < 2:  # first steps eagerly (first-launch costs, flags that settle)
+                self._step_body()
+            else:
+                C.plan_begin()
+                try:
                     self._step_body()
-                else:
-                    C.plan_begin()
-                    try:
-                        self._step_body()
-                    except BaseException:
-                        C.plan_abort()
-                        raise
-                    self.plan_id = C.plan_end()
-                    self._plan_version = version
-                    if ps is not None:
-                        C.plan_compile(self.plan_id)
-            if ps is not None:
-                C.stream_wait(cur.cuda_stream, ps.cuda_stream)
+                except BaseException:
+                    C.plan_abort()
+                    raise
+                self.plan_id = C.plan_end()
+                self._plan_version = version
             self.steps += 1
             return self.ex.loss
         if self.use_graph:
@@ -188,12 +163,6 @@ class NativeTrainer:
                 torch.cuda.current_stream().wait_stream(s)
                 self.graph = g
             self.graph.replay()
-        elif self.stream is not None:
-            cur = torch.cuda.current_stream()
-            self.stream.wait_stream(cur)
-            with torch.cuda.stream(self.stream):
-                self._step_body()
-            cur.wait_stream(self.stream)
         else:
             self._step_body()
         self.steps += 1

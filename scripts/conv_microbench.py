@@ -18,7 +18,8 @@ from robotic_discovery_platform_amd.ops import native  # noqa: E402
 SHAPES = [  # (H, Cin1, Cin2, Cout)   spatial = H x H
     (256, 64, 0, 64), (128, 64, 0, 128), (128, 128, 0, 128), (64, 256, 0, 256), (32, 512, 0, 512),
     (16, 512, 0, 512), (32, 512, 512, 256), (64, 256, 256, 128), (128, 128, 128, 64), (256, 64, 64, 64),
-    (128, 128, 0, 64),
+    (128, 128, 0, 64), (64, 128, 0, 256), (32, 256, 0, 512), (32, 1024, 0, 512), (64, 512, 0, 256),
+    (32, 512, 0, 256), (64, 256, 0, 128), (128, 64, 0, 128),
 ]
 
 
@@ -32,7 +33,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--shapes", default=None, help="comma list of shape indices")
     ap.add_argument("--wgrad-blocks", type=int, default=2048,
-                    help="split-K grid target of the wgrad kernels (the training step uses 512, RDP_WGRAD_BLOCKS)")
+                    help="split-K grid target of the generic wgrad kernel (the training step uses 512)")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda")
@@ -57,19 +58,22 @@ def main():
             out = torch.zeros(Co * 9 * Cin, device=dev)
 
         def run(v):
-            # variant v >= 10000: same kernel with debug flags (v // 10000) (A/B in one process)
-            C.conv_set_debug_flags(v // 10000)
-            v = v % 10000
-            if a.wgrad:
+            if a.wgrad:  # v = variant (0 auto, 4 generic, 5 halo)
                 C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
             else:
                 C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, v, None, 0)  # v = bm_pref (1 halo, 128/256 igemm)
 
-        for v in variants:
-            run(v)
+        ok = []
+        for v in variants:  # a variant that does not apply to this shape (-1) is skipped
+            try:
+                run(v)
+                ok.append(v)
+            except RuntimeError:
+                pass
+        variants_s = ok
         torch.cuda.synchronize()
         for _ in range(a.rounds):
-            for v in variants:
+            for v in variants_s:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.reps):
@@ -81,7 +85,7 @@ def main():
         if a.wgrad:
             row["splits"] = splits
             row["wgrad_blocks"] = a.wgrad_blocks
-        for v in variants:
+        for v in variants_s:
             med = statistics.median(times[v])
             row[f"v{v}_us"] = round(med * 1e3, 1)
             row[f"v{v}_tflops"] = round(flops / (med * 1e-3) / 1e12, 1)

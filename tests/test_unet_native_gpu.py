@@ -125,9 +125,8 @@ def test_plan_replay_bitwise_equals_eager(bilinear, loss, monkeypatch):
     batches = [(torch.rand(2, 3, 64, 96, generator=g), (torch.rand(2, 1, 64, 96, generator=g) > 0.5).float())
                for _ in range(7)]
     runs = {}
-    for mode in ("eager", "plan", "plan_graph"):  # plan_graph: replay as per-stream hipGraphs (plan_compile)
+    for mode in ("eager", "plan"):
         plan = mode != "eager"
-        monkeypatch.setenv("RDP_PLAN_GRAPH", "1" if mode == "plan_graph" else "0")
         nat = UNetNative(3, 1, bilinear=bilinear, device=dev, init_from=ref)
         tr = NativeTrainer(nat, 2, 64, 96, lr=1e-3, loss=loss, plan=plan)
         assert tr.use_plan == plan
@@ -142,7 +141,7 @@ def test_plan_replay_bitwise_equals_eager(bilinear, loss, monkeypatch):
         runs[mode] = (torch.stack(ls), st.flat.clone(), st.exp_avg.clone(), st.exp_avg_sq.clone(),
                       nat.derived.clone(), [b.clone() for _, b in nat.named_buffers()])
     a = runs["eager"]
-    for mode in ("plan", "plan_graph"):
+    for mode in ("plan",):
         b = runs[mode]
         for u, v in zip(a[:5], b[:5]):
             assert torch.equal(u, v), mode
