@@ -985,20 +985,23 @@ py::object png_decode(py::bytes data) {
   return py::cast(t);
 }
 
-// Baseline JPEG -> (geometry int32[32], quantized coefficient planes int16, quant tables int32[3*64]) on
+// Baseline JPEG -> (meta int32[32 + 3*64] = geometry + quant tables, quantized coefficient planes int16) on
 // the CPU, entropy-decoded without the GIL (restart segments in parallel); None when the stream is not
 // one this decoder handles (progressive, arithmetic, 12-bit, ...): the caller falls back to PIL.
 // geometry: [0] W, [1] H, [2] ncomp, [3] hmax, [4] vmax, [5] total blocks; per component c at 8 + 8c:
 // h, v, blocks per line, block rows, first block, plane byte offset, downsampled width, height.
-py::object jpeg_decode(py::bytes data, bool parallel) {
+py::object jpeg_decode(py::bytes data, bool parallel, bool pin) {
   char* buf = nullptr;
   Py_ssize_t n = 0;
   if (PyBytes_AsStringAndSize(data.ptr(), &buf, &n) != 0) throw py::error_already_set();
   int hi[24];
   const long nco = rdp_jpeg_info((const uint8_t*)buf, n, hi);
   if (nco <= 0) return py::none();
-  auto geo = torch::zeros({32}, torch::kInt32);
-  int* g = geo.data_ptr<int>();
+  // geometry and quant tables share one int32[32 + 192] tensor (one H2D copy per frame); with `pin`
+  // both outputs come from the caching pinned-host allocator so the pipeline's copies are async DMA
+  auto opt = torch::TensorOptions().pinned_memory(pin);
+  auto meta = torch::zeros({32 + 192}, opt.dtype(torch::kInt32));
+  int* g = meta.data_ptr<int>();
   const int W = hi[0], H = hi[1], nc = hi[2], hmax = hi[3], vmax = hi[4];
   g[0] = W; g[1] = H; g[2] = nc; g[3] = hmax; g[4] = vmax;
   long blk = 0, pb = 0;
@@ -1012,17 +1015,16 @@ py::object jpeg_decode(py::bytes data, bool parallel) {
     pb += (long)bw * 8 * bh * 8;
   }
   g[5] = (int)blk;
-  auto coefs = torch::empty({nco}, torch::kInt16);
-  auto qt16 = torch::empty({3 * 64}, torch::kInt16);
+  auto coefs = torch::empty({nco}, opt.dtype(torch::kInt16));
+  uint16_t qt16[3 * 64];
   int r;
   {
     py::gil_scoped_release nogil;
-    r = rdp_jpeg_decode((const uint8_t*)buf, n, coefs.data_ptr<int16_t>(), nco, (uint16_t*)qt16.data_ptr(),
-                        parallel ? 1 : 0);
+    r = rdp_jpeg_decode((const uint8_t*)buf, n, coefs.data_ptr<int16_t>(), nco, qt16, parallel ? 1 : 0);
   }
   if (r != 0) return py::none();
-  auto qt = qt16.to(torch::kInt32).bitwise_and(0xFFFF);
-  return py::make_tuple(geo, coefs, qt);
+  for (int i = 0; i < 3 * 64; ++i) g[32 + i] = qt16[i];
+  return py::make_tuple(meta, coefs);
 }
 
 // Dequantisation + ISLOW 8x8 IDCT of every block into the component planes (`planes`, u8 scratch of
@@ -1153,7 +1155,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
         py::arg("presorted") = false);
   m.def("png_decode", &png_decode);
-  m.def("jpeg_decode", &jpeg_decode, py::arg("data"), py::arg("parallel") = true);
+  m.def("jpeg_decode", &jpeg_decode, py::arg("data"), py::arg("parallel") = true, py::arg("pin") = false);
   m.def("jpeg_to_rgb", on_device(&jpeg_to_rgb));
   m.def("jpeg_plane_bytes", &rdp_jpeg_plane_bytes);
   m.def("jpeg_max_coefs", &rdp_jpeg_max_coefs);

@@ -231,6 +231,12 @@ int parse(const uint8_t* d, long n, Jpeg& j) {
         if (j.ncomp == 1) {  // single component: blocks, not MCUs of the sampling factor
           j.comp[0].h = j.comp[0].v = j.hmax = j.vmax = 1;
         }
+        // luma at full resolution (the GPU colour stage reads Y unscaled); chroma-only subsampling
+        if (j.comp[0].h != j.hmax || j.comp[0].v != j.vmax) return -2;
+        for (int c = 1; c < j.ncomp; ++c) {  // chroma 4:4:4, 4:2:2 (h2v1) or 4:2:0 (h2v2): the fancy upsamplers
+          const int hr = j.hmax / j.comp[c].h, vr = j.vmax / j.comp[c].v;
+          if (j.hmax % j.comp[c].h || j.vmax % j.comp[c].v || (vr == 2 && hr != 2)) return -2;
+        }
         j.mcux = (j.width + 8 * j.hmax - 1) / (8 * j.hmax);
         j.mcuy = (j.height + 8 * j.vmax - 1) / (8 * j.vmax);
         long off = 0;

@@ -89,6 +89,7 @@ class ServeConfig:
     devices: str = ""  # comma-separated GPU indices for per-GPU replicas ("" = current device only; "all")
     replicas_per_device: int = 2  # independent stream pipelines (hipGraph + buffers) per GPU
     frame_errors: str = "degrade"  # "degrade": bad frame -> error status, stream goes on; "abort": reference
+    gpu_jpeg: bool = True  # baseline JPEGs: native entropy decode on the host, pixel stage in the frame graph
     hot_reload_alias: Optional[str] = None  # e.g. "staging": reload when alias moves
 
 

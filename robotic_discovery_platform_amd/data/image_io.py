@@ -20,10 +20,14 @@ from PIL import Image
 
 
 # ----------------------------------------------------------------------------- codecs
-def encode_jpeg(bgr: np.ndarray, quality: int = 95) -> bytes:
+def encode_jpeg(bgr: np.ndarray, quality: int = 95, restart_rows: int = 0) -> bytes:
+    """Baseline JPEG of a BGR frame (cv2.imencode('.jpg') equivalent). ``restart_rows`` > 0 puts a
+    restart marker after every that many MCU rows -- still a standard baseline stream that any decoder
+    reads; the server's native decoder (data/jpeg.py) decodes the segments in parallel."""
     rgb = np.ascontiguousarray(bgr[..., ::-1])
     buf = io.BytesIO()
-    Image.fromarray(rgb, "RGB").save(buf, format="JPEG", quality=quality)
+    kw = {"restart_marker_rows": int(restart_rows)} if restart_rows > 0 else {}
+    Image.fromarray(rgb, "RGB").save(buf, format="JPEG", quality=quality, **kw)
     return buf.getvalue()
 
 

@@ -25,25 +25,41 @@ import numpy as np
 
 @dataclass
 class JpegCoefs:
-    """One entropy-decoded frame: geometry int32[32], int16 coefficient planes, int32 quant tables."""
-    geo: "object"    # torch int32 [32] (bindings.cpp jpeg_decode layout)
+    """One entropy-decoded frame: ``meta`` int32[32 + 192] (geometry, then the three quantisation
+    tables in natural order; bindings.cpp jpeg_decode has the layout) and the int16 coefficient
+    planes. A stand-in for the HxWx3 array it decodes to (``shape`` / ``ndim``)."""
+    meta: "object"   # torch int32 [224]
     coefs: "object"  # torch int16 [n]
-    qt: "object"     # torch int32 [3 * 64], natural order
+    ndim = 3
+
+    @property
+    def geo(self):
+        return self.meta[:32]
+
+    @property
+    def qt(self):
+        return self.meta[32:]
 
     @property
     def width(self) -> int:
-        return int(self.geo[0])
+        return int(self.meta[0])
 
     @property
     def height(self) -> int:
-        return int(self.geo[1])
+        return int(self.meta[1])
+
+    @property
+    def blocks(self) -> int:
+        return int(self.meta[5])
 
     @property
     def shape(self):  # (H, W, 3), like the decoded array it stands for
         return (self.height, self.width, 3)
 
 
-def decode_coefs(data: bytes, parallel: bool = True) -> Optional[JpegCoefs]:
+def decode_coefs(data: bytes, parallel: bool = True, pin: bool = False) -> Optional[JpegCoefs]:
+    """Entropy-decode a baseline JPEG (None: not a stream the native decoder takes -> use PIL).
+    ``pin``: outputs in pinned host memory (the GPU pipeline copies them asynchronously)."""
     try:
         from ..ops import native
         C = native(build_if_missing=False)
@@ -51,7 +67,7 @@ def decode_coefs(data: bytes, parallel: bool = True) -> Optional[JpegCoefs]:
         return None
     if C is None or not hasattr(C, "jpeg_decode"):
         return None
-    r = C.jpeg_decode(bytes(data), parallel)
+    r = C.jpeg_decode(bytes(data), parallel, pin)
     if r is None:
         return None
     return JpegCoefs(*r)

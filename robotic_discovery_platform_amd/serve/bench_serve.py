@@ -103,14 +103,18 @@ def measure_engine_pipelined(model, scenes, frames: int = 200, warmup: int = 20,
             round(frames * streams / max(res.values()), 1)}
 
 
-def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8) -> dict:
+def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8, lockstep: bool = True,
+                    go=None) -> dict:
     """The load generator: one client stream (the reference client's encodings: JPEG colour, 16-bit
-    PNG depth), streamed throughput then lock-step round trips. Runs in its own process."""
+    PNG depth), streamed throughput then (``lockstep``) lock-step round trips. Runs in its own
+    process; ``go()`` (if given) blocks until every stream of a multi-stream run is ready."""
     import grpc
     from ..data.synthetic import make_scene
     from ..proto import vision as pb
     from .client import make_request
     reqs = [make_request(sc.color, sc.depth) for sc in (make_scene(i) for i in range(n_scenes))]
+    if go is not None:
+        go()
     out = {}
     with grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_receive_message_length", 64 << 20),
                                                                ("grpc.max_send_message_length", 64 << 20)]) as ch:
@@ -131,6 +135,8 @@ def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8) -> d
         t_end = time.perf_counter()
         out["e2e_fps"] = round(frames / (t_end - t_start), 1)
         out["e2e_server_proc_p50_ms"] = round(_pct(proc, 50), 3)  # processing only (proc_time_ms)
+        if not lockstep:
+            return out
         q: "queue.Queue" = queue.Queue()
         sent = []
 
@@ -151,9 +157,13 @@ def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8) -> d
     return out
 
 
-def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2):
-    """Server in this process, load generator in a separate client process (the reference's
-    topology: client.py and server.py are different processes), over loopback gRPC."""
+def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2, gpu_jpeg: bool = True,
+                streams: int = 1):
+    """Server in this process, load generator(s) in separate client processes (the reference's
+    topology: client.py and server.py are different processes), over loopback gRPC. ``gpu_jpeg``:
+    the server's JPEG path (native entropy decode + GPU pixel stage, as ``build_server``) or the host
+    PIL decode. ``streams`` > 1: that many concurrent client streams (processes started together),
+    aggregate frames/s = the sum of the streams' rates."""
     import grpc
     import json
     import subprocess
@@ -164,26 +174,52 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
     from .server import MetricsLog, VisionAnalysisService
     from concurrent import futures
     tmp = tempfile.mkdtemp(prefix="rdp_serve_")
-    engine = EnginePool(model, DEFAULT_K, 0.001, n=pool, graph=True)
+    engine = EnginePool(model, DEFAULT_K, 0.001, n=max(pool, 2 * streams), graph=True, rgb=True, jpeg=gpu_jpeg)
     svc = VisionAnalysisService(engine, MetricsLog(os.path.join(tmp, "metrics.csv")))
-    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10))
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=max(10, 2 * streams)))
     pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
     port = server.add_insecure_port("127.0.0.1:0")
     server.start()
     out = {}
+    sfx = "" if streams == 1 else f"_{streams}streams"
     try:
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
                    HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")  # the client never touches the GPU
-        r = subprocess.run([sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve", "--client-port",
-                            str(port), "--frames", str(frames), "--warmup", str(warmup)], env=env,
-                           capture_output=True, text=True, timeout=600)
-        if r.returncode != 0:
-            raise RuntimeError(f"client process failed: {r.stderr[-1500:]}")
-        out.update(json.loads(r.stdout.strip().splitlines()[-1]))
+        cmd = [sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve", "--client-port", str(port),
+               "--frames", str(frames), "--warmup", str(warmup), "--lockstep", str(int(streams == 1))]
+        procs = [subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                  stderr=subprocess.PIPE, text=True) for _ in range(streams)]
+        try:
+            for p in procs:  # every client has built its requests: start them together
+                if p.stdout.readline().strip() != "ready":
+                    raise RuntimeError(f"client process failed: {p.stderr.read()[-1500:]}")
+            for p in procs:
+                p.stdin.write("go\n")
+                p.stdin.flush()
+            res = []
+            for p in procs:
+                so, se = p.communicate(timeout=600)
+                if p.returncode != 0:
+                    raise RuntimeError(f"client process failed: {se[-1500:]}")
+                res.append(json.loads(so.strip().splitlines()[-1]))
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        if streams == 1:
+            out.update(res[0])
+        else:
+            out["e2e_fps" + sfx] = round(sum(r["e2e_fps"] for r in res), 1)
+            out["e2e_server_proc_p50_ms" + sfx] = round(float(np.median([r["e2e_server_proc_p50_ms"] for r in res])), 3)
         st = svc.latency_stats()
-        out["e2e_server_queue_p50_ms"] = round(st["queue_p50_ms"], 3)  # request read -> processing start
-        out["e2e_client"] = "separate process"
+        out["e2e_server_queue_p50_ms" + sfx] = round(st["queue_p50_ms"], 3)  # request read -> processing start
+        out["e2e_decode_color_p50_ms" + sfx] = round(st["decode_color_p50_ms"], 3)
+        out["e2e_decode_depth_p50_ms" + sfx] = round(st["decode_depth_p50_ms"], 3)
+        if streams == 1:
+            out["e2e_client"] = "separate process"
+        if not gpu_jpeg:
+            out = {k.replace("e2e_", "e2e_hostjpeg_"): v for k, v in out.items() if k != "e2e_client"}
         _progress(f"e2e: {out}")
     finally:
         # wait for the gRPC core to finish shutting down before its objects are collected: a
@@ -208,8 +244,11 @@ def measure_serving(dev: Optional[torch.device] = None, frames: int = 200, warmu
     res = {"serve_frame": "640x480 RGB-D -> 256x256 U-Net", "serve_weights": f"trained {train_steps} steps on synthetic"}
     res.update({"serve_" + k: v for k, v in measure_engine(model, scenes, frames, warmup).items()})
     _progress(f"engine done: {res}")
+    res.update({"serve_" + k: v for k, v in measure_engine_pipelined(model, scenes, frames, warmup, streams=4).items()})
     if e2e:
         res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup).items()})
+        res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup, gpu_jpeg=False).items()})
+        res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup, streams=4).items()})
         _progress("e2e done")
     return res
 
@@ -223,9 +262,16 @@ if __name__ == "__main__":
     ap.add_argument("--train-steps", type=int, default=200)
     ap.add_argument("--e2e", type=int, default=1)
     ap.add_argument("--client-port", type=int, default=0, help="internal: run as the e2e load-generator process")
+    ap.add_argument("--lockstep", type=int, default=1, help="internal: client also measures lock-step round trips")
     a = ap.parse_args()
     if a.client_port:
-        print(json.dumps(run_client_load(a.client_port, a.frames, a.warmup)), flush=True)
+        import sys
+
+        def go():
+            print("ready", flush=True)
+            sys.stdin.readline()
+        print(json.dumps(run_client_load(a.client_port, a.frames, a.warmup, lockstep=bool(a.lockstep), go=go)),
+              flush=True)
         raise SystemExit(0)
     print(json.dumps(measure_serving(torch.device("cuda"), a.frames, a.warmup, a.train_steps, bool(a.e2e))),
           flush=True)

@@ -39,6 +39,7 @@ import numpy as np
 import torch
 
 from ..config import GeometryConfig
+from ..data.jpeg import JpegCoefs, coefs_to_rgb_reference
 from ..geometry.curvature import CurvatureResult, GeometryEngine, compute_curvature_profile
 from ..utils import trace
 
@@ -78,6 +79,9 @@ class FrameResult:
     timings: dict = field(default_factory=dict)
 
 
+SRC_BGR, SRC_RGB, SRC_JPEG = 0, 1, 2  # colour sources of a frame graph
+
+
 def _stage(dst: torch.Tensor, src: np.ndarray) -> None:
     """Copy a host frame into its pinned staging tensor (on every frame's latency path). A numpy
     assignment: torch's OpenMP-threaded copy was 4x faster alone but its spinning workers cost engine
@@ -96,7 +100,7 @@ class FramePipeline:
 
     def __init__(self, model, K: np.ndarray, depth_scale: float, H: int = 480, W: int = 640, size: int = 256,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 device: Optional[torch.device] = None, rgb: bool = False):
+                 device: Optional[torch.device] = None, rgb: bool = False, jpeg: bool = False):
         from ..models.unet import UNetNative
         if not isinstance(model, UNetNative):
             raise TypeError("FramePipeline needs the native UNet (UNetNative); use CpuFramePipeline otherwise")
@@ -106,9 +110,9 @@ class FramePipeline:
         # everything below (buffers, stream, graph capture) belongs to the model's GPU, whatever device
         # the calling thread has current
         with torch.cuda.device(dev):
-            self._init(model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb)
+            self._init(model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb, jpeg)
 
-    def _init(self, model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb):
+    def _init(self, model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb, jpeg):
         from ..models.unet import UNetExecutor
         from ..ops import native
         self.C = native()
@@ -137,30 +141,40 @@ class FramePipeline:
         self.h_depth = torch.empty(H, W, dtype=torch.int16, pin_memory=True)
         self.h_mask = torch.empty(H, W, dtype=torch.uint8, pin_memory=True)
         self.h_res = torch.empty(self.geo.res.numel(), dtype=torch.float64, pin_memory=True)
+        # JPEG source (data/jpeg.py): entropy-decoded coefficients + geometry / quant tables in, the
+        # pixel stage (IDCT, chroma upsampling, YCbCr -> RGB) runs in the frame graph into d_color
+        self.d_coef = torch.empty(self.C.jpeg_max_coefs(H, W), dtype=torch.int16, device=dev)
+        self.d_meta = torch.zeros(32 + 192, dtype=torch.int32, device=dev)
+        self.d_planes = torch.empty(self.C.jpeg_plane_bytes(H, W), dtype=torch.uint8, device=dev)
         self.ev0 = torch.cuda.Event(enable_timing=True)
         self.ev1 = torch.cuda.Event(enable_timing=True)
-        self.graphs = {}  # channel order of the staged colour frame (0 BGR, 1 RGB) -> hipGraph
+        self.graphs = {}  # colour source (SRC_BGR / SRC_RGB arrays, SRC_JPEG coefficients) -> hipGraph
         self.use_graph = graph
         self.lock = threading.Lock()
-        # the graph for the channel order this pipeline will be fed (the gRPC server decodes to RGB) is
-        # captured here, at build time, never on a live request
+        # the graphs for the sources this pipeline will be fed (the gRPC server: JPEG coefficients, or
+        # RGB arrays for streams the native decoder does not take) are captured here, at build time,
+        # never on a live request
         if graph:
-            self._capture(int(rgb))
+            self._capture(SRC_RGB if rgb else SRC_BGR)
+            if jpeg:
+                self._capture(SRC_JPEG)
         else:
             self.refresh_weights()
 
     # ---------------------------------------------------------------- device program
-    def _device_program(self, rgb: int = 0):
-        self._net_program(rgb)
+    def _device_program(self, src: int = 0):
+        self._net_program(src)
         self._geo_program()
 
-    def _net_program(self, rgb: int = 0):
+    def _net_program(self, src: int = 0):
         # Measured dead end: the H2D / D2H copies captured INTO this graph, depth H2D and mask D2H
         # on a forked branch -- the memcpy nodes replay as blit kernels (20.7 + 17.7 us for colour /
         # depth instead of DMA-engine copies), the fork adds a ~67 us cross-queue gap, and two
         # pipelines no longer overlap: GPU p50 0.622 -> 0.648 ms, pipelined 2307 -> 1502 FPS.
         C, ex, m = self.C, self.ex, self.model
-        C.preprocess(self.d_color, *self.tab, ex.x_in, rgb)
+        if src == SRC_JPEG:
+            C.jpeg_to_rgb(self.d_coef, self.d_meta[:32], self.d_meta[32:], self.d_planes, self.d_color)
+        C.preprocess(self.d_color, *self.tab, ex.x_in, int(src != SRC_BGR))
         # BN-fold coefficients: see refresh_weights(); the head (+ threshold) is fused into the last conv
         ex.forward(head=False, refresh_eval=False,
                    mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
@@ -186,46 +200,58 @@ class FramePipeline:
     def graph(self):
         return self.graphs.get(0)
 
-    def _capture(self, rgb: int):
+    def _capture(self, src: int):
         if not self.graphs:
             self.refresh_weights()
         with torch.cuda.device(self.dev):
             with torch.cuda.stream(self.stream):
-                self._device_program(rgb)  # warm-up (lazy allocations, kernel loading)
+                self._device_program(src)  # warm-up (lazy allocations, kernel loading)
             self.stream.synchronize()
             g = torch.cuda.CUDAGraph()
             # thread-local capture: other server threads may use the GPU meanwhile (a late capture of
             # the other channel order happens on a live server)
             with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
-                self._device_program(rgb)
-        self.graphs[rgb] = g
+                self._device_program(src)
+        self.graphs[src] = g
 
     # ---------------------------------------------------------------- per frame
-    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, rgb: bool = False):
+    def submit(self, color_bgr, depth: np.ndarray, rgb: bool = False):
         """Stage a frame and enqueue its device work; returns immediately (call ``collect``).
-        ``rgb``: the colour frame is RGB (as the server decodes it), not OpenCV's BGR."""
+        ``color_bgr``: HxWx3 uint8 array -- OpenCV's BGR, or RGB with ``rgb`` (as the server decodes
+        it) -- or a ``JpegCoefs`` (entropy-decoded JPEG; the pixel stage runs in the frame graph)."""
         if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
         # colour staged and its H2D enqueued first; the depth frame is staged on the host while that
         # copy runs. (Measured alternative: the network and the geometry as two graphs with the depth
         # H2D on a copy stream under the network -- the cross-queue wait left a ~14 us gap between the
         # graphs, about what it hid.)
-        _stage(self.h_color, color_bgr)
         s = self.stream
-        with torch.cuda.device(self.dev), torch.cuda.stream(s):
-            self.ev0.record(s)
-            self.d_color.copy_(self.h_color, non_blocking=True)
+        if isinstance(color_bgr, JpegCoefs):
+            src = SRC_JPEG
+            n = color_bgr.coefs.numel()
+            if n > self.d_coef.numel() or color_bgr.blocks * 64 > n:
+                raise ValueError(f"JPEG coefficient planes ({n}) exceed the pipeline's capacity")
+            with torch.cuda.device(self.dev), torch.cuda.stream(s):
+                self.ev0.record(s)
+                self.d_meta.copy_(color_bgr.meta, non_blocking=True)
+                self.d_coef[:n].copy_(color_bgr.coefs, non_blocking=True)
+        else:
+            src = SRC_RGB if rgb else SRC_BGR
+            _stage(self.h_color, color_bgr)
+            with torch.cuda.device(self.dev), torch.cuda.stream(s):
+                self.ev0.record(s)
+                self.d_color.copy_(self.h_color, non_blocking=True)
         _stage(self.h_depth, depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16))
         with trace.range("serve.frame.enqueue"), torch.cuda.device(self.dev), torch.cuda.stream(s):
             self.d_depth.copy_(self.h_depth, non_blocking=True)
             if self.use_graph:
-                g = self.graphs.get(int(rgb))
-                if g is None:  # first frame in this channel order: capture its graph (stream-ordered)
-                    self._capture(int(rgb))
-                    g = self.graphs[int(rgb)]
+                g = self.graphs.get(src)
+                if g is None:  # first frame from this source: capture its graph (stream-ordered)
+                    self._capture(src)
+                    g = self.graphs[src]
                 g.replay()
             else:
-                self._device_program(int(rgb))
+                self._device_program(src)
             self.h_mask.copy_(self.mask, non_blocking=True)
             self.h_res.copy_(self.geo.res, non_blocking=True)
             self.ev1.record(s)
@@ -268,9 +294,11 @@ class CpuFramePipeline:
     def wait_idle(self):
         self._pending = None
 
-    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, rgb: bool = False):
+    def submit(self, color_bgr, depth: np.ndarray, rgb: bool = False):
         if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
+        if isinstance(color_bgr, JpegCoefs):  # (the server only sends these to GPU pipelines)
+            color_bgr, rgb = coefs_to_rgb_reference(color_bgr), True
         self._pending = (color_bgr[..., ::-1] if rgb else color_bgr, depth)
 
     def collect(self) -> FrameResult:
@@ -338,13 +366,14 @@ class EnginePool:
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 devices=None, rgb: bool = False):
+                 devices=None, rgb: bool = False, jpeg: bool = False):
         self.model = model
         self.rgb = rgb  # channel order of the frames this pool will be fed (graphs captured for it)
         self.args = dict(K=K, depth_scale=depth_scale, size=size, threshold=threshold, geo_cfg=geo_cfg)
         self.graph = graph
         self.n = max(1, n)
         self.gpu = _is_native(model)
+        self.jpeg = jpeg and self.gpu  # GPU pipelines also fed JpegCoefs (their graph captured at build)
         home = _model_device(model)
         devs = [torch.device(d) for d in (devices or [home])]
         self.devices = devs
@@ -360,7 +389,8 @@ class EnginePool:
     def _new(self, r: int, H, W):
         m = self.replicas[r]
         if self.gpu:
-            return FramePipeline(m, H=H, W=W, graph=self.graph, device=self.devices[r], rgb=self.rgb, **self.args)
+            return FramePipeline(m, H=H, W=W, graph=self.graph, device=self.devices[r], rgb=self.rgb,
+                                 jpeg=self.jpeg, **self.args)
         return CpuFramePipeline(m, H=H, W=W, **self.args)
 
     def _get(self, r: int, H, W) -> "queue.Queue":

@@ -32,9 +32,10 @@ import torch
 
 from ..config import ServeConfig
 from ..data.image_io import decode_image, encode_png
+from ..data.jpeg import decode_coefs
 from ..proto import vision as pb
 from ..utils import trace
-from .engine import EnginePool
+from .engine import EnginePool, _is_native
 
 log = logging.getLogger(__name__)
 
@@ -129,9 +130,30 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         self._stats_lock = threading.Lock()
         self.queue_ms: "collections.deque" = collections.deque(maxlen=4096)  # request read -> processing start
         self.proc_ms: "collections.deque" = collections.deque(maxlen=4096)  # processing start -> response ready
+        self.dec_color_ms: "collections.deque" = collections.deque(maxlen=4096)  # per-frame host decode times
+        self.dec_depth_ms: "collections.deque" = collections.deque(maxlen=4096)
         # shared host-codec pool: JPEG / 16-bit PNG decodes release the GIL, so colour and depth of a
         # frame, and up to `prefetch` frames of a stream, decode concurrently
         self._pool = futures.ThreadPoolExecutor(max_workers=decode_workers, thread_name_prefix="rdp-decode")
+        # colour frames of a GPU engine built for it: JPEG entropy decode only (pinned coefficients),
+        # the pixel stage runs in the frame graph (data/jpeg.py)
+        self._gpu_jpeg = bool(getattr(engine, "jpeg", False))
+
+    def _decode_color(self, data: bytes):
+        t = time.perf_counter()
+        out = None
+        if self._gpu_jpeg and data[:2] == b"\xff\xd8":
+            out = decode_coefs(data, parallel=True, pin=True)
+        if out is None:
+            out = decode_image(data, True, "RGB")  # no BGR flip: the engine takes RGB
+        self.dec_color_ms.append((time.perf_counter() - t) * 1e3)
+        return out
+
+    def _decode_depth(self, data: bytes):
+        t = time.perf_counter()
+        out = decode_image(data, False)
+        self.dec_depth_ms.append((time.perf_counter() - t) * 1e3)
+        return out
 
     def _decoded(self, request_iterator):
         """Yield (t_read, colour, depth, error, more) in request order; decoding runs ahead on the
@@ -157,8 +179,8 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     cb, db = req.color_image.data, req.depth_image.data
                     if self.faults is not None:
                         cb, db = self.faults.corrupt_request(i, cb, db)
-                    fc = self._pool.submit(decode_image, cb, True, "RGB")  # no BGR flip: the engine takes RGB
-                    fd = self._pool.submit(decode_image, db, False)
+                    fc = self._pool.submit(self._decode_color, cb)
+                    fd = self._pool.submit(self._decode_depth, db)
                     if not put((t, fc, fd, None)):
                         return
             except Exception as e:  # surface transport errors in the handler thread
@@ -232,8 +254,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
     def latency_stats(self) -> dict:
         with self._stats_lock:
             q, p = list(self.queue_ms), list(self.proc_ms)
+        dc, dd = list(self.dec_color_ms), list(self.dec_depth_ms)
         pct = (lambda v, k: float(np.percentile(v, k)) if v else float("nan"))
         return {"queue_p50_ms": pct(q, 50), "proc_p50_ms": pct(p, 50), "proc_p99_ms": pct(p, 99),
+                "decode_color_p50_ms": pct(dc, 50), "decode_depth_p50_ms": pct(dd, 50),
                 "frames": self.frames, "frame_failures": self.frame_failures}
 
     def AnalyzeActuatorPerformance(self, request_iterator, context):
@@ -349,7 +373,8 @@ def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_s
         return None
     metrics = MetricsLog(cfg.metrics_log)
     engine = EnginePool(model, K, ds, n=pool_size or cfg.replicas_per_device, threshold=cfg.mask_threshold,
-                        graph=cfg.graph, size=cfg.model_img_size, devices=devices, rgb=True)
+                        graph=cfg.graph, size=cfg.model_img_size, devices=devices, rgb=True,
+                        jpeg=cfg.gpu_jpeg and _is_native(model))
     service = VisionAnalysisService(engine, metrics, frame_errors=cfg.frame_errors, faults=faults)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.max_workers))
     pb.add_VisionAnalysisServiceServicer_to_server(service, server)
