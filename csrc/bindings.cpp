@@ -80,9 +80,9 @@ int rdp_jpeg_decode(const uint8_t*, long, int16_t*, long, uint16_t*, int);
 int rdp_jpeg_gpu(const void*, const int*, const int*, void*, int, int, int, void*, hipStream_t);
 long rdp_jpeg_plane_bytes(int, int);
 long rdp_jpeg_max_coefs(int, int);
-int rdp_png_decode(const uint8_t*, long, uint8_t*, long);
-long rdp_png_encode_gray8(const uint8_t*, int, int, int, uint8_t*, long);
-long rdp_png_encode_bound(int, int);
+int rdp_png_decode(const uint8_t*, long, uint8_t*, long, int);
+long rdp_png_encode_gray(const uint8_t*, int, int, int, int, int, uint8_t*, long);
+long rdp_png_encode_bound(int, int, int, int);
 int rdp_area_maxtap();
 int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
                        const double*, int, int, int, void*, hipStream_t);
@@ -968,8 +968,9 @@ void resize_area_u8(torch::Tensor in, torch::Tensor ys, torch::Tensor yn, torch:
 }
 
 // grayscale 8/16-bit PNG -> u8 / int16 (u16 bits) CPU tensor, decoded without the GIL; None when the
-// PNG is not one this reader handles (or is corrupt): the caller falls back to PIL
-py::object png_decode(py::bytes data) {
+// PNG is not one this reader handles (or is corrupt): the caller falls back to PIL. `parallel`: inflate
+// the bands of a banded stream (codecs.cpp) concurrently.
+py::object png_decode(py::bytes data, bool parallel) {
   char* buf = nullptr;
   Py_ssize_t n = 0;
   if (PyBytes_AsStringAndSize(data.ptr(), &buf, &n) != 0) throw py::error_already_set();
@@ -979,7 +980,8 @@ py::object png_decode(py::bytes data) {
   int r;
   {
     py::gil_scoped_release nogil;
-    r = rdp_png_decode((const uint8_t*)buf, n, (uint8_t*)t.data_ptr(), (long)t.numel() * t.element_size());
+    r = rdp_png_decode((const uint8_t*)buf, n, (uint8_t*)t.data_ptr(), (long)t.numel() * t.element_size(),
+                       parallel ? 1 : 0);
   }
   if (r != 0) return py::none();
   return py::cast(t);
@@ -1047,15 +1049,20 @@ void jpeg_to_rgb(torch::Tensor coefs, torch::Tensor geo, torch::Tensor qt, torch
 }
 
 // u8 [H, W] CPU tensor -> 8-bit grayscale PNG bytes (deflate level), encoded without the GIL
-py::bytes png_encode_gray8(torch::Tensor img, int level) {
-  TORCH_CHECK(!img.is_cuda() && img.scalar_type() == torch::kUInt8 && img.dim() == 2 && img.is_contiguous(),
-              "u8 HxW contiguous CPU tensor");
-  const int h = img.size(0), w = img.size(1);
-  std::string out((size_t)rdp_png_encode_bound(w, h), '\0');
+// u8 or int16 (u16 bits) [H, W] CPU tensor -> 8 / 16-bit grayscale PNG bytes, encoded without the GIL;
+// bands > 1: a banded stream with its rdPs index (codecs.cpp), bands deflated in parallel
+py::bytes png_encode(torch::Tensor img, int level, int bands) {
+  TORCH_CHECK(!img.is_cuda() && (img.scalar_type() == torch::kUInt8 || img.scalar_type() == torch::kInt16) &&
+                  img.dim() == 2 && img.is_contiguous(),
+              "u8 / int16 HxW contiguous CPU tensor");
+  const int h = img.size(0), w = img.size(1), bpp = (int)img.element_size();
+  TORCH_CHECK(h > 0 && w > 0 && level >= 0 && level <= 9 && bands >= 1, "png_encode: bad size / level / bands");
+  std::string out((size_t)rdp_png_encode_bound(w, h, bpp, bands), '\0');
   long len;
   {
     py::gil_scoped_release nogil;
-    len = rdp_png_encode_gray8(img.data_ptr<uint8_t>(), w, h, level, (uint8_t*)&out[0], (long)out.size());
+    len = rdp_png_encode_gray((const uint8_t*)img.data_ptr(), w, h, bpp, level, bands, (uint8_t*)&out[0],
+                              (long)out.size());
   }
   TORCH_CHECK(len > 0, "png encode failed");
   out.resize((size_t)len);
@@ -1154,12 +1161,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
         py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
         py::arg("presorted") = false);
-  m.def("png_decode", &png_decode);
+  m.def("png_decode", &png_decode, py::arg("data"), py::arg("parallel") = true);
   m.def("jpeg_decode", &jpeg_decode, py::arg("data"), py::arg("parallel") = true, py::arg("pin") = false);
   m.def("jpeg_to_rgb", on_device(&jpeg_to_rgb));
   m.def("jpeg_plane_bytes", &rdp_jpeg_plane_bytes);
   m.def("jpeg_max_coefs", &rdp_jpeg_max_coefs);
-  m.def("png_encode_gray8", &png_encode_gray8);
+  m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 1, py::arg("bands") = 1);
   m.def("resize_area_u8", on_device(&resize_area_u8));
   m.def("area_maxtap", &rdp_area_maxtap);
   m.def("geo_spline_res_len", &rdp_geo_spline_res_len);

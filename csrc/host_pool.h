@@ -1,0 +1,98 @@
+// A small native worker pool for host-side codec work that splits into independent pieces (JPEG
+// restart segments, PNG deflate bands). Shared by every concurrent caller (the server's codec
+// threads): a call queues helper tasks for its own job and takes part itself, so a job never waits on
+// another job's pieces and a busy pool degrades to the caller doing its job alone.
+#pragma once
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace rdp {
+
+class HostPool {
+ public:
+  explicit HostPool(int n) {
+    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { run(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  // run fn(0 .. n-1); the calling thread takes part, returns when all are done
+  void parallel_for(int n, const std::function<void(int)>& fn) {
+    if (n <= 1 || workers_.empty()) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    struct Job {
+      std::atomic<int> next{0}, done{0};
+      int n;
+      const std::function<void(int)>* fn;
+      std::mutex m;
+      std::condition_variable cv;
+    };
+    auto job = std::make_shared<Job>();
+    job->n = n;
+    job->fn = &fn;
+    // a helper that starts after the caller has finished everything claims no index (next >= n), so
+    // it never touches fn once the caller has returned
+    auto work = [job]() {
+      int i;
+      while ((i = job->next.fetch_add(1)) < job->n) {
+        (*job->fn)(i);
+        if (job->done.fetch_add(1) + 1 == job->n) {
+          std::lock_guard<std::mutex> g(job->m);
+          job->cv.notify_all();
+        }
+      }
+    };
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      const int helpers = std::min<int>(n - 1, (int)workers_.size());
+      for (int h = 0; h < helpers; ++h) q_.push_back(work);
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(job->m);
+    job->cv.wait(lk, [&] { return job->done.load() == job->n; });
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<void()> t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (stop_ && q_.empty()) return;
+        t = std::move(q_.front());
+        q_.pop_front();
+      }
+      t();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::deque<std::function<void()>> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+// one pool per process (inline: a single instance across the translation units of the library)
+inline HostPool& host_pool() {
+  static HostPool p((int)std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 2)));
+  return p;
+}
+
+}  // namespace rdp

@@ -15,14 +15,11 @@
 // the buffer.
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <cstring>
-#include <deque>
-#include <functional>
-#include <mutex>
-#include <thread>
 #include <vector>
+
+#include "host_pool.h"
 
 namespace {
 
@@ -388,83 +385,6 @@ int decode_segment(const Jpeg& j, const uint8_t* src, const uint8_t* end, long m
   return 0;
 }
 
-// ---- a small native worker pool for the restart segments (shared by concurrent decodes)
-class Pool {
- public:
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { run(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : workers_) t.join();
-  }
-  // run fn(0 .. n-1); the calling thread takes part, returns when all are done
-  void parallel_for(int n, const std::function<void(int)>& fn) {
-    if (n <= 1 || workers_.empty()) {
-      for (int i = 0; i < n; ++i) fn(i);
-      return;
-    }
-    struct Job {
-      std::atomic<int> next{0}, done{0};
-      int n;
-      const std::function<void(int)>* fn;
-      std::mutex m;
-      std::condition_variable cv;
-    };
-    auto job = std::make_shared<Job>();
-    job->n = n;
-    job->fn = &fn;
-    auto work = [job]() {
-      int i;
-      while ((i = job->next.fetch_add(1)) < job->n) {
-        (*job->fn)(i);
-        if (job->done.fetch_add(1) + 1 == job->n) {
-          std::lock_guard<std::mutex> g(job->m);
-          job->cv.notify_all();
-        }
-      }
-    };
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      const int helpers = std::min<int>(n - 1, (int)workers_.size());
-      for (int h = 0; h < helpers; ++h) q_.push_back(work);
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(job->m);
-    job->cv.wait(lk, [&] { return job->done.load() == job->n; });
-  }
-
- private:
-  void run() {
-    for (;;) {
-      std::function<void()> t;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-        if (stop_ && q_.empty()) return;
-        t = std::move(q_.front());
-        q_.pop_front();
-      }
-      t();
-    }
-  }
-  std::vector<std::thread> workers_;
-  std::deque<std::function<void()>> q_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stop_ = false;
-};
-
-Pool& pool() {
-  static Pool p((int)std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 2)));
-  return p;
-}
-
 }  // namespace
 
 extern "C" {
@@ -519,7 +439,7 @@ int rdp_jpeg_decode(const uint8_t* d, long n, int16_t* coefs, long ncoefs, uint1
     if (decode_segment(j, starts[s], se, m0, m1, coefs) != 0) bad.store(1);
   };
   if (parallel) {
-    pool().parallel_for((int)nseg, seg);
+    rdp::host_pool().parallel_for((int)nseg, seg);
   } else {
     for (int s = 0; s < nseg; ++s) seg(s);
   }

@@ -42,13 +42,17 @@ def _native():
         return None
 
 
-def encode_png(arr: np.ndarray, compress_level: int = 6) -> bytes:
-    """PNG of uint8 gray, uint8 BGR (stored as RGB) or uint16 gray (lossless 16-bit)."""
-    if arr.ndim == 2 and arr.dtype == np.uint8:
+def encode_png(arr: np.ndarray, compress_level: int = 6, bands: int = 1) -> bytes:
+    """PNG of uint8 gray, uint8 BGR (stored as RGB) or uint16 gray (lossless 16-bit). Grayscale goes
+    through the native encoder; ``bands`` > 1 writes a banded stream (an ordinary PNG for every reader,
+    which the native decoder inflates band-parallel: csrc/codecs.cpp)."""
+    if arr.ndim == 2 and arr.dtype in (np.uint8, np.uint16) and 0 <= compress_level <= 9:
         C = _native()
         if C is not None:
             import torch
-            return C.png_encode_gray8(torch.from_numpy(np.ascontiguousarray(arr)), int(compress_level))
+            a = np.ascontiguousarray(arr)
+            return C.png_encode(torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a),
+                                int(compress_level), max(1, int(bands)))
     buf = io.BytesIO()
     kw = dict(format="PNG", compress_level=compress_level)
     if arr.dtype == np.uint16:

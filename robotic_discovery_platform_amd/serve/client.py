@@ -76,14 +76,16 @@ def render_overlay(color_bgr: np.ndarray, resp, K: np.ndarray, dist: Optional[np
     return out
 
 
-def make_request(color_bgr: np.ndarray, depth_u16: np.ndarray, jpeg_quality: int = 95, restart_rows: int = 1):
-    """One request: colour as baseline JPEG with a restart marker per MCU row (the server entropy-
-    decodes the rows in parallel; other decoders read it as usual), depth as 16-bit PNG."""
+def make_request(color_bgr: np.ndarray, depth_u16: np.ndarray, jpeg_quality: int = 95, restart_rows: int = 1,
+                 png_bands: int = 8):
+    """One request: colour as baseline JPEG with a restart marker per MCU row, depth as a 16-bit PNG
+    in ``png_bands`` deflate bands -- both standard files any decoder reads, which the server's native
+    decoders split across threads (data/jpeg.py, csrc/codecs.cpp)."""
     h, w = color_bgr.shape[:2]
     dh, dw = depth_u16.shape[:2]
     jpg = encode_jpeg(color_bgr, jpeg_quality, restart_rows)
     return pb.AnalysisRequest(color_image=pb.Image(data=jpg, width=w, height=h),
-                              depth_image=pb.Image(data=encode_png(depth_u16, compress_level=1), width=dw,
+                              depth_image=pb.Image(data=encode_png(depth_u16, compress_level=1, bands=png_bands), width=dw,
                                                    height=dh))
 
 

@@ -243,7 +243,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                                        status=c.status, mask_coverage=r.coverage)
             if c.spline_points:
                 resp.spline_points.extend([pb.Point3D(x=p.x, y=p.y, z=p.z) for p in c.spline_points])
-            resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1)
+            resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1, bands=4)
         now = time.perf_counter()
         resp.proc_time_ms = (now - t_start) * 1e3
         with self._stats_lock:
