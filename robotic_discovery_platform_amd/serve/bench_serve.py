@@ -15,6 +15,7 @@ an actuator and the geometry stage sees realistic point counts), unless ``train_
 from __future__ import annotations
 
 import os
+import sys
 import queue
 import tempfile
 import threading
@@ -157,8 +158,62 @@ def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8, lock
     return out
 
 
+class NullPipeline:
+    """Host-path stand-in for a frame pipeline: accepts a frame, returns a fixed result (a 640x480
+    mask with an actuator-sized blob and a 50-point spline). With it the e2e bench measures the server's
+    host machinery alone -- gRPC, codecs, threads, GIL -- on any machine (``measure_e2e(model=None)``)."""
+
+    def __init__(self, H=480, W=640):
+        from ..geometry.curvature import CurvatureResult, Point
+        from .engine import FrameResult
+        m = np.zeros((H, W), np.uint8)
+        m[H // 4: 3 * H // 4, W // 3: 2 * W // 3] = 1
+        pts = [Point(float(i), float(i) * 0.5, 0.4) for i in range(50)]
+        self._res = FrameResult(m, 100.0 * m.mean(), CurvatureResult(0.01, 0.02, pts, "ok", 1000, 100))
+        self._n = 0
+
+    def submit(self, color, depth, rgb=False):
+        self._n += 1
+
+    def collect(self):
+        return self._res
+
+    def wait_idle(self):
+        pass
+
+    def refresh_weights(self):
+        pass
+
+
+class NullEngine:
+    """EnginePool interface over NullPipelines (see NullPipeline)."""
+
+    def __init__(self, n: int = 2, jpeg: bool = True):
+        from . import engine as E
+        self._E = E
+        self.jpeg, self.gpu, self.n = jpeg, False, n
+        self._pools = {}
+        self._lock = threading.Lock()
+
+    def _get(self, r, H, W):
+        with self._lock:
+            q = self._pools.get((H, W))
+            if q is None:
+                q = queue.Queue()
+                for _ in range(self.n):
+                    q.put(NullPipeline(H, W))
+                self._pools[(H, W)] = q
+            return q
+
+    def session(self):
+        return self._E.EngineSession(self, 0)
+
+    def process(self, color, depth):
+        return NullPipeline(*depth.shape[:2]).collect()
+
+
 def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2, gpu_jpeg: bool = True,
-                streams: int = 1):
+                streams: int = 1, switch_ms: float = 0.0):
     """Server in this process, load generator(s) in separate client processes (the reference's
     topology: client.py and server.py are different processes), over loopback gRPC. ``gpu_jpeg``:
     the server's JPEG path (native entropy decode + GPU pixel stage, as ``build_server``) or the host
@@ -174,7 +229,13 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
     from .server import MetricsLog, VisionAnalysisService
     from concurrent import futures
     tmp = tempfile.mkdtemp(prefix="rdp_serve_")
-    engine = EnginePool(model, DEFAULT_K, 0.001, n=max(pool, 2 * streams), graph=True, rgb=True, jpeg=gpu_jpeg)
+    old_switch = sys.getswitchinterval()
+    if switch_ms > 0:
+        sys.setswitchinterval(switch_ms * 1e-3)
+    if model is None:  # host path only
+        engine = NullEngine(n=max(pool, 2 * streams), jpeg=gpu_jpeg)
+    else:
+        engine = EnginePool(model, DEFAULT_K, 0.001, n=max(pool, 2 * streams), graph=True, rgb=True, jpeg=gpu_jpeg)
     svc = VisionAnalysisService(engine, MetricsLog(os.path.join(tmp, "metrics.csv")))
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=max(10, 2 * streams)))
     pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
@@ -214,8 +275,11 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
             out["e2e_server_proc_p50_ms" + sfx] = round(float(np.median([r["e2e_server_proc_p50_ms"] for r in res])), 3)
         st = svc.latency_stats()
         out["e2e_server_queue_p50_ms" + sfx] = round(st["queue_p50_ms"], 3)  # request read -> processing start
-        out["e2e_decode_color_p50_ms" + sfx] = round(st["decode_color_p50_ms"], 3)
-        out["e2e_decode_depth_p50_ms" + sfx] = round(st["decode_depth_p50_ms"], 3)
+        for k in ("decode_color", "decode_depth", "submit", "gpu", "respond", "hold"):  # server stages
+            for q in ("p50", "p99"):
+                v = st[f"{k}_{q}_ms"]
+                if v == v:
+                    out[f"e2e_stage_{k}_{q}_ms" + sfx] = round(v, 3)
         if streams == 1:
             out["e2e_client"] = "separate process"
         if not gpu_jpeg:
@@ -228,6 +292,7 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
         server.stop(0).wait()
         svc.close()
         del server
+        sys.setswitchinterval(old_switch)
     return out
 
 

@@ -130,29 +130,34 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         self._stats_lock = threading.Lock()
         self.queue_ms: "collections.deque" = collections.deque(maxlen=4096)  # request read -> processing start
         self.proc_ms: "collections.deque" = collections.deque(maxlen=4096)  # processing start -> response ready
-        self.dec_color_ms: "collections.deque" = collections.deque(maxlen=4096)  # per-frame host decode times
-        self.dec_depth_ms: "collections.deque" = collections.deque(maxlen=4096)
+        # per-stage times of every frame (ms; latency_stats() reports p50 / p99): decode_color /
+        # decode_depth (codec pool), submit (engine staging + graph launch, handler thread), gpu (the
+        # frame's device time), respond (mask PNG + response message, codec pool), hold (response
+        # ready -> handed to gRPC)
+        self.stage_ms = {k: collections.deque(maxlen=4096)
+                         for k in ("decode_color", "decode_depth", "submit", "gpu", "respond", "hold")}
         # shared host-codec pool: JPEG / 16-bit PNG decodes release the GIL, so colour and depth of a
         # frame, and up to `prefetch` frames of a stream, decode concurrently
         self._pool = futures.ThreadPoolExecutor(max_workers=decode_workers, thread_name_prefix="rdp-decode")
         # colour frames of a GPU engine built for it: JPEG entropy decode only (pinned coefficients),
         # the pixel stage runs in the frame graph (data/jpeg.py)
         self._gpu_jpeg = bool(getattr(engine, "jpeg", False))
+        self._pin = bool(getattr(engine, "gpu", False))  # pinned coefficient buffers: GPU engines only
 
     def _decode_color(self, data: bytes):
         t = time.perf_counter()
         out = None
         if self._gpu_jpeg and data[:2] == b"\xff\xd8":
-            out = decode_coefs(data, parallel=True, pin=True)
+            out = decode_coefs(data, parallel=True, pin=self._pin)
         if out is None:
             out = decode_image(data, True, "RGB")  # no BGR flip: the engine takes RGB
-        self.dec_color_ms.append((time.perf_counter() - t) * 1e3)
+        self.stage_ms["decode_color"].append((time.perf_counter() - t) * 1e3)
         return out
 
     def _decode_depth(self, data: bytes):
         t = time.perf_counter()
         out = decode_image(data, False)
-        self.dec_depth_ms.append((time.perf_counter() - t) * 1e3)
+        self.stage_ms["decode_depth"].append((time.perf_counter() - t) * 1e3)
         return out
 
     def _decoded(self, request_iterator):
@@ -229,6 +234,15 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             self.metrics.write(resp.mean_curvature, resp.max_curvature, r.coverage)
         self.frames += 1
 
+    def _respond_timed(self, r, t):
+        t0 = time.perf_counter()
+        resp, r = self._respond(r, t)
+        t1 = time.perf_counter()
+        self.stage_ms["respond"].append((t1 - t0) * 1e3)
+        if r is not None and "gpu_ms" in r.timings:
+            self.stage_ms["gpu"].append(r.timings["gpu_ms"])
+        return resp, r, t1
+
     def _respond(self, r, t):
         """FrameResult (or the frame's exception) -> AnalysisResponse; runs on the codec pool when
         streaming. ``t`` = (request read, processing start): proc_time_ms is the server's processing
@@ -254,11 +268,14 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
     def latency_stats(self) -> dict:
         with self._stats_lock:
             q, p = list(self.queue_ms), list(self.proc_ms)
-        dc, dd = list(self.dec_color_ms), list(self.dec_depth_ms)
+            st = {k: list(v) for k, v in self.stage_ms.items()}
         pct = (lambda v, k: float(np.percentile(v, k)) if v else float("nan"))
-        return {"queue_p50_ms": pct(q, 50), "proc_p50_ms": pct(p, 50), "proc_p99_ms": pct(p, 99),
-                "decode_color_p50_ms": pct(dc, 50), "decode_depth_p50_ms": pct(dd, 50),
-                "frames": self.frames, "frame_failures": self.frame_failures}
+        out = {"queue_p50_ms": pct(q, 50), "proc_p50_ms": pct(p, 50), "proc_p99_ms": pct(p, 99),
+               "frames": self.frames, "frame_failures": self.frame_failures}
+        for k, v in st.items():
+            out[f"{k}_p50_ms"] = pct(v, 50)
+            out[f"{k}_p99_ms"] = pct(v, 99)
+        return out
 
     def AnalyzeActuatorPerformance(self, request_iterator, context):
         """Responses leave in request order; one that is ready -- or any, when the client has not
@@ -276,12 +293,13 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                         raise r
                     self.frame_failures += 1
                     log.warning("frame failed (%s: %s): degraded response", type(r).__name__, r)
-                inflight.append(self._pool.submit(self._respond, r, times.pop(tag)))
+                inflight.append(self._pool.submit(self._respond_timed, r, times.pop(tag)))
 
         def ready(force: bool):
             while inflight and (force or inflight[0].done() or len(inflight) > self.prefetch):
-                resp, r = inflight.popleft().result()
+                resp, r, t_ready = inflight.popleft().result()
                 self._log(resp, r)
+                self.stage_ms["hold"].append((time.perf_counter() - t_ready) * 1e3)
                 yield resp
 
         frames = self._decoded(request_iterator)
@@ -294,7 +312,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     encode([(i, err)])
                 else:
                     with trace.range("serve.rpc.frame"):
-                        encode(sess.submit(color, self._as_u16(depth), tag=i, rgb=True))
+                        done = sess.submit(color, self._as_u16(depth), tag=i, rgb=True)
+                        self.stage_ms["submit"].append((time.perf_counter() - t_start) * 1e3)
+                        encode(done)
                     if not more():  # lock-step client: finish this frame now
                         encode(sess.drain())
                 yield from ready(force=not more())
