@@ -1093,7 +1093,10 @@ void mask_upsample(torch::Tensor m, torch::Tensor out, torch::Tensor count) {
 
 }  // namespace
 
+void register_serve_runtime(py::module_& m);  // serve_runtime.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  register_serve_runtime(m);
   m.doc() = "rdp MI355X (gfx950) HIP kernels";
   m.def("stream_wait", &stream_wait, "waiter stream waits for the work issued so far on waitee (recorded in plans)");
   m.def("plan_begin", &plan_begin);

@@ -1,0 +1,249 @@
+// Native per-frame serving runtime: the host side of one served frame, off the Python GIL.
+//
+// Reference per-frame path (/root/reference/services/vision_analysis/server.py:116-152): decode, model,
+// mask resize, geometry, then build the AnalysisResponse in Python. Here the device work is one
+// captured hipGraph per pipeline (serve/engine.py FramePipeline); what remained in Python per frame --
+// ~15 torch calls for staging copies, event records and the graph replay, then the response message
+// built field by field -- held the interpreter lock ~0.5 ms per frame, which capped a server process
+// at ~1,000 frames/s however many streams it served (profiles/serve_e2e.md). Two pieces move here:
+//
+//   FrameRunner      stage a frame into the pipeline's pinned buffers, enqueue H2D copies, launch the
+//                    graph exec, enqueue the D2H copies and the timing events -- one call with the GIL
+//                    released; wait() blocks on the frame's end event, also without the GIL.
+//   encode_response  mask PNG (banded, codecs.cpp) + the evofab.vision.AnalysisResponse wire encoding
+//                    (/root/reference/protos/vision.proto:29-37), byte-identical to protobuf's own
+//                    serializer (fields in number order, proto3 defaults omitted); the gRPC handler
+//                    yields the bytes (proto/vision.py passes them through).
+#include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+extern "C" long rdp_png_encode_gray(const uint8_t*, int, int, int, int, int, uint8_t*, long);
+extern "C" long rdp_png_encode_bound(int, int, int, int);
+
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceScope {  // make `dev` current for this thread, restore on exit
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) hip_check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+inline void* P(uintptr_t v) { return reinterpret_cast<void*>(v); }
+
+class FrameRunner {
+ public:
+  FrameRunner(int device, uintptr_t stream) : dev_(device), s_((hipStream_t)stream) {
+    DeviceScope g(dev_);
+    hip_check(hipEventCreate(&ev0_), "hipEventCreate");
+    hip_check(hipEventCreate(&ev1_), "hipEventCreate");
+  }
+  ~FrameRunner() {
+    (void)hipEventDestroy(ev0_);
+    (void)hipEventDestroy(ev1_);
+  }
+  // graph exec of colour source `src` (0 BGR, 1 RGB, 2 JPEG coefficients), owned by the pipeline's
+  // torch CUDAGraph (kept alive there)
+  void set_graph(int src, uintptr_t exec) {
+    if (src < 0 || src > 2) throw std::invalid_argument("src");
+    exec_[src] = (hipGraphExec_t)exec;
+  }
+  // pinned host staging / device buffers of the pipeline (sizes in bytes)
+  void set_buffers(uintptr_t d_color, uintptr_t h_color, size_t color_bytes, uintptr_t d_depth, uintptr_t h_depth,
+                   size_t depth_bytes, uintptr_t d_meta, size_t meta_bytes, uintptr_t d_coef, size_t coef_cap,
+                   uintptr_t d_mask, uintptr_t h_mask, size_t mask_bytes, uintptr_t d_res, uintptr_t h_res,
+                   size_t res_bytes) {
+    d_color_ = P(d_color); h_color_ = P(h_color); color_bytes_ = color_bytes;
+    d_depth_ = P(d_depth); h_depth_ = P(h_depth); depth_bytes_ = depth_bytes;
+    d_meta_ = P(d_meta); meta_bytes_ = meta_bytes; d_coef_ = P(d_coef); coef_cap_ = coef_cap;
+    d_mask_ = P(d_mask); h_mask_ = P(h_mask); mask_bytes_ = mask_bytes;
+    d_res_ = P(d_res); h_res_ = P(h_res); res_bytes_ = res_bytes;
+  }
+
+  // colour as an HxWx3 u8 array (src 0 BGR / 1 RGB), depth HxW 16-bit
+  void submit_array(int src, py::buffer color, py::buffer depth) {
+    py::buffer_info c = color.request(), d = depth.request();
+    check_contig(c, color_bytes_, "colour");
+    check_contig(d, depth_bytes_, "depth");
+    if (src != 0 && src != 1) throw std::invalid_argument("src must be 0 (BGR) or 1 (RGB)");
+    const void* cp = c.ptr;
+    const void* dp = d.ptr;
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
+    std::memcpy(h_color_, cp, color_bytes_);
+    hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
+    std::memcpy(h_depth_, dp, depth_bytes_);
+    launch_tail(src);
+  }
+
+  // colour as entropy-decoded JPEG (data/jpeg.py JpegCoefs: pinned meta + coefficient buffers; the caller
+  // keeps them alive until wait() returns)
+  void submit_jpeg(uintptr_t meta, size_t meta_bytes, uintptr_t coefs, size_t coef_bytes, py::buffer depth) {
+    py::buffer_info d = depth.request();
+    check_contig(d, depth_bytes_, "depth");
+    if (meta_bytes != meta_bytes_ || coef_bytes > coef_cap_) throw std::invalid_argument("JPEG buffers exceed the pipeline");
+    const void* dp = d.ptr;
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
+    hip_check(hipMemcpyAsync(d_meta_, P(meta), meta_bytes, hipMemcpyHostToDevice, s_), "H2D meta");
+    hip_check(hipMemcpyAsync(d_coef_, P(coefs), coef_bytes, hipMemcpyHostToDevice, s_), "H2D coefs");
+    std::memcpy(h_depth_, dp, depth_bytes_);
+    launch_tail(2);
+  }
+
+  // block until the frame's results are on the host; returns its device time (ms, event to event)
+  float wait() {
+    if (!recorded_) return 0.f;  // nothing submitted yet
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    hip_check(hipEventSynchronize(ev1_), "hipEventSynchronize");
+    float ms = 0.f;
+    hip_check(hipEventElapsedTime(&ms, ev0_, ev1_), "hipEventElapsedTime");
+    return ms;
+  }
+
+ private:
+  static void check_contig(const py::buffer_info& b, size_t bytes, const char* what) {
+    size_t n = (size_t)b.itemsize;
+    for (auto s : b.shape) n *= (size_t)s;
+    ssize_t expect = b.itemsize;
+    for (ssize_t i = b.ndim - 1; i >= 0; --i) {
+      if (b.shape[i] > 1 && b.strides[i] != expect) throw std::invalid_argument(std::string(what) + ": not C-contiguous");
+      expect *= b.shape[i];
+    }
+    if (n != bytes) throw std::invalid_argument(std::string(what) + ": size does not match the pipeline");
+  }
+  void launch_tail(int src) {
+    if (!exec_[src]) throw std::runtime_error("FrameRunner: no graph for this colour source");
+    hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, s_), "H2D depth");
+    hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
+    hip_check(hipMemcpyAsync(h_mask_, d_mask_, mask_bytes_, hipMemcpyDeviceToHost, s_), "D2H mask");
+    hip_check(hipMemcpyAsync(h_res_, d_res_, res_bytes_, hipMemcpyDeviceToHost, s_), "D2H result");
+    hip_check(hipEventRecord(ev1_, s_), "hipEventRecord");
+    recorded_ = true;
+  }
+
+  bool recorded_ = false;
+  int dev_;
+  hipStream_t s_;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  hipGraphExec_t exec_[3] = {nullptr, nullptr, nullptr};
+  void *d_color_ = nullptr, *h_color_ = nullptr, *d_depth_ = nullptr, *h_depth_ = nullptr;
+  void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
+  void *d_res_ = nullptr, *h_res_ = nullptr;
+  size_t color_bytes_ = 0, depth_bytes_ = 0, meta_bytes_ = 0, coef_cap_ = 0, mask_bytes_ = 0, res_bytes_ = 0;
+};
+
+// ---- protobuf wire format (proto3)
+void put_varint(std::string& o, uint64_t v) {
+  while (v >= 0x80) {
+    o.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  o.push_back((char)v);
+}
+void put_fixed64(std::string& o, int field, double v) {  // omitted when the bit pattern is zero (proto3)
+  uint64_t b;
+  std::memcpy(&b, &v, 8);
+  if (!b) return;
+  put_varint(o, (uint64_t)field << 3 | 1);
+  for (int i = 0; i < 8; ++i) o.push_back((char)(b >> (8 * i)));
+}
+void put_fixed32(std::string& o, int field, float v) {
+  uint32_t b;
+  std::memcpy(&b, &v, 4);
+  if (!b) return;
+  put_varint(o, (uint64_t)field << 3 | 5);
+  for (int i = 0; i < 4; ++i) o.push_back((char)(b >> (8 * i)));
+}
+void put_bytes(std::string& o, int field, const char* p, size_t n) {
+  if (!n) return;
+  put_varint(o, (uint64_t)field << 3 | 2);
+  put_varint(o, n);
+  o.append(p, n);
+}
+
+// AnalysisResponse bytes. mask: HxW u8 {0,1} (PNG-encoded as 0/255, `bands` deflate bands) or None;
+// points: [n, 3] float64 or None.
+py::bytes encode_response(double mean, double maxc, py::object points, const std::string& status, py::object mask,
+                          float coverage, float proc_ms, int level, int bands) {
+  std::vector<double> pts;
+  if (!points.is_none()) {
+    auto a = py::array_t<double, py::array::c_style | py::array::forcecast>::ensure(points);
+    if (!a || (a.size() && (a.ndim() != 2 || a.shape(1) != 3))) throw std::invalid_argument("points: [n, 3]");
+    pts.assign(a.data(), a.data() + a.size());
+  }
+  std::vector<uint8_t> img;
+  int h = 0, w = 0;
+  if (!mask.is_none()) {
+    auto m = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(mask);
+    if (!m || m.ndim() != 2) throw std::invalid_argument("mask: HxW u8");
+    h = (int)m.shape(0);
+    w = (int)m.shape(1);
+    img.assign(m.data(), m.data() + m.size());
+  }
+  std::string out;
+  {
+    py::gil_scoped_release nogil;
+    std::string png;
+    if (h > 0 && w > 0) {
+      for (auto& v : img) v = v ? 255 : 0;
+      png.resize((size_t)rdp_png_encode_bound(w, h, 1, bands));
+      const long n = rdp_png_encode_gray(img.data(), w, h, 1, level, bands, (uint8_t*)&png[0], (long)png.size());
+      if (n < 0) throw std::runtime_error("mask PNG encode failed");
+      png.resize((size_t)n);
+    }
+    out.reserve(png.size() + status.size() + pts.size() * 10 + 64);
+    put_fixed64(out, 1, mean);
+    put_fixed64(out, 2, maxc);
+    std::string sub;
+    for (size_t i = 0; i + 3 <= pts.size(); i += 3) {
+      sub.clear();
+      put_fixed64(sub, 1, pts[i]);
+      put_fixed64(sub, 2, pts[i + 1]);
+      put_fixed64(sub, 3, pts[i + 2]);
+      put_varint(out, 3 << 3 | 2);  // repeated Point3D: always present, even when empty
+      put_varint(out, sub.size());
+      out += sub;
+    }
+    put_bytes(out, 4, status.data(), status.size());
+    put_bytes(out, 5, png.data(), png.size());
+    put_fixed32(out, 6, coverage);
+    put_fixed32(out, 7, proc_ms);
+  }
+  return py::bytes(out);
+}
+
+}  // namespace
+
+void register_serve_runtime(py::module_& m) {
+  py::class_<FrameRunner>(m, "FrameRunner")
+      .def(py::init<int, uintptr_t>(), py::arg("device"), py::arg("stream"))
+      .def("set_graph", &FrameRunner::set_graph)
+      .def("set_buffers", &FrameRunner::set_buffers)
+      .def("submit_array", &FrameRunner::submit_array)
+      .def("submit_jpeg", &FrameRunner::submit_jpeg)
+      .def("wait", &FrameRunner::wait);
+  m.def("encode_response", &encode_response, py::arg("mean"), py::arg("max"), py::arg("points"), py::arg("status"),
+        py::arg("mask"), py::arg("coverage"), py::arg("proc_ms"), py::arg("level") = 1, py::arg("bands") = 4);
+}

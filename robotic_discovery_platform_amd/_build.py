@@ -72,7 +72,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time):
-            is_binding = os.path.basename(src) == "bindings.cpp"
+            is_binding = os.path.basename(src) in ("bindings.cpp", "serve_runtime.cpp")  # pybind11 sources
             cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
                    f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", CSRC, "-I", os.path.join(ROCM, "include")]
             if is_binding:

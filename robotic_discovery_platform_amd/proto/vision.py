@@ -84,11 +84,16 @@ class VisionAnalysisServiceServicer:
         raise NotImplementedError("Method not implemented!")
 
 
+def _serialize_response(m) -> bytes:
+    """A response message, or its wire bytes already encoded (the server's native fast path)."""
+    return m if isinstance(m, (bytes, bytearray)) else m.SerializeToString()
+
+
 def add_VisionAnalysisServiceServicer_to_server(servicer, server) -> None:
     import grpc
     handlers = {
         METHOD: grpc.stream_stream_rpc_method_handler(
             servicer.AnalyzeActuatorPerformance, request_deserializer=AnalysisRequest.FromString,
-            response_serializer=AnalysisResponse.SerializeToString),
+            response_serializer=_serialize_response),
     }
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(FULL_SERVICE, handlers),))

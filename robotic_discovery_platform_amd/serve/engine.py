@@ -77,6 +77,7 @@ class FrameResult:
     coverage: float                 # percent of pixels in the mask
     curvature: CurvatureResult
     timings: dict = field(default_factory=dict)
+    points: Optional[np.ndarray] = None  # spline points [n, 3] float64 (device fits; the server encodes them)
 
 
 SRC_BGR, SRC_RGB, SRC_JPEG = 0, 1, 2  # colour sources of a frame graph
@@ -151,6 +152,19 @@ class FramePipeline:
         self.graphs = {}  # colour source (SRC_BGR / SRC_RGB arrays, SRC_JPEG coefficients) -> hipGraph
         self.use_graph = graph
         self.lock = threading.Lock()
+        self._hold = None  # the submitted frame's JPEG buffers, alive until its copies are done
+        # native per-frame host path (csrc/serve_runtime.cpp): staging copies, H2D, graph launch, D2H and
+        # events in one call without the GIL; the Python path below stays for eager pipelines
+        self.runner = None
+        if graph and hasattr(self.C, "FrameRunner"):
+            r = self.C.FrameRunner(dev.index, self.stream.cuda_stream)
+            nb = lambda t: t.numel() * t.element_size()  # noqa: E731
+            r.set_buffers(self.d_color.data_ptr(), self.h_color.data_ptr(), nb(self.d_color),
+                          self.d_depth.data_ptr(), self.h_depth.data_ptr(), nb(self.d_depth),
+                          self.d_meta.data_ptr(), nb(self.d_meta), self.d_coef.data_ptr(), nb(self.d_coef),
+                          self.mask.data_ptr(), self.h_mask.data_ptr(), nb(self.mask),
+                          self.geo.res.data_ptr(), self.h_res.data_ptr(), nb(self.h_res))
+            self.runner = r
         # the graphs for the sources this pipeline will be fed (the gRPC server: JPEG coefficients, or
         # RGB arrays for streams the native decoder does not take) are captured here, at build time,
         # never on a live request
@@ -194,7 +208,11 @@ class FramePipeline:
 
     def wait_idle(self):
         """Block until this pipeline's last submitted frame has left the GPU (its result is dropped)."""
-        self.ev1.synchronize()
+        if self.runner is not None:
+            self.runner.wait()
+        else:
+            self.ev1.synchronize()
+        self._hold = None
 
     @property
     def graph(self):
@@ -213,6 +231,8 @@ class FramePipeline:
             with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self._device_program(src)
         self.graphs[src] = g
+        if self.runner is not None:
+            self.runner.set_graph(src, g.raw_cuda_graph_exec())
 
     # ---------------------------------------------------------------- per frame
     def submit(self, color_bgr, depth: np.ndarray, rgb: bool = False):
@@ -226,6 +246,8 @@ class FramePipeline:
         # H2D on a copy stream under the network -- the cross-queue wait left a ~14 us gap between the
         # graphs, about what it hid.)
         s = self.stream
+        if self.runner is not None:
+            return self._submit_native(color_bgr, depth, rgb)
         if isinstance(color_bgr, JpegCoefs):
             src = SRC_JPEG
             n = color_bgr.coefs.numel()
@@ -256,20 +278,44 @@ class FramePipeline:
             self.h_res.copy_(self.geo.res, non_blocking=True)
             self.ev1.record(s)
 
+    def _submit_native(self, color, depth: np.ndarray, rgb: bool):
+        d = depth if depth.dtype in (np.uint16, np.int16) else depth.astype(np.int16)
+        src = SRC_JPEG if isinstance(color, JpegCoefs) else (SRC_RGB if rgb else SRC_BGR)
+        if src not in self.graphs:  # first frame from this source: capture its graph (stream-ordered)
+            self._capture(src)
+        with trace.range("serve.frame.enqueue"):
+            if src == SRC_JPEG:
+                n = color.coefs.numel()
+                if n > self.d_coef.numel() or color.blocks * 64 > n:
+                    raise ValueError(f"JPEG coefficient planes ({n}) exceed the pipeline's capacity")
+                self._hold = color  # its (pinned) buffers must outlive the async copies
+                self.runner.submit_jpeg(color.meta.data_ptr(), color.meta.numel() * 4, color.coefs.data_ptr(),
+                                        n * 2, np.ascontiguousarray(d))
+            else:
+                self.runner.submit_array(src, np.ascontiguousarray(color), np.ascontiguousarray(d))
+
     def collect(self) -> FrameResult:
         t0 = time.perf_counter()
         with trace.range("serve.frame.wait_gpu"):
-            self.ev1.synchronize()
+            if self.runner is not None:
+                gpu_ms = self.runner.wait()
+                self._hold = None
+            else:
+                self.ev1.synchronize()
+                gpu_ms = self.ev0.elapsed_time(self.ev1)
         t1 = time.perf_counter()
         from ..geometry.curvature import coverage_from_device
-        count = coverage_from_device(self.h_res.numpy(), self.cfg)
+        h_res = self.h_res.numpy()
+        count = coverage_from_device(h_res, self.cfg)
         with trace.range("serve.frame.spline_fit"):  # device result -> CurvatureResult (host fit only as fallback)
-            res = self.geo.finish_device(self.h_res.numpy())
+            res = self.geo.finish_device(h_res)
+        pts = None
+        if int(h_res[0]) == 0 and res.status == "ok":  # fitted on the device: the points are in the result
+            pts = h_res[8:8 + 3 * self.cfg.num_samples].reshape(-1, 3).copy()
         t2 = time.perf_counter()
         cov = 100.0 * count / (self.H * self.W)
         return FrameResult(self.h_mask.numpy().copy(), cov, res,
-                           {"gpu_ms": self.ev0.elapsed_time(self.ev1), "wait_ms": (t1 - t0) * 1e3,
-                            "fit_ms": (t2 - t1) * 1e3})
+                           {"gpu_ms": gpu_ms, "wait_ms": (t1 - t0) * 1e3, "fit_ms": (t2 - t1) * 1e3}, pts)
 
     def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
         with self.lock:

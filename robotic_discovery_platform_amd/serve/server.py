@@ -143,6 +143,11 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         # the pixel stage runs in the frame graph (data/jpeg.py)
         self._gpu_jpeg = bool(getattr(engine, "jpeg", False))
         self._pin = bool(getattr(engine, "gpu", False))  # pinned coefficient buffers: GPU engines only
+        try:
+            from ..ops import native
+            self._encode = getattr(native(build_if_missing=False), "encode_response", None)
+        except Exception:  # pragma: no cover - no extension: message path
+            self._encode = None
 
     def _decode_color(self, data: bytes):
         t = time.perf_counter()
@@ -219,7 +224,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
     def analyze_frame(self, color: np.ndarray, depth: np.ndarray, t0: Optional[float] = None):
         t0 = time.perf_counter() if t0 is None else t0
         resp, r = self._respond(self._process(color, depth), (t0, t0))
-        self._log(resp, r)
+        self._log(r)
         return resp
 
     @staticmethod
@@ -229,19 +234,40 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
     def _process(self, color: np.ndarray, depth: np.ndarray):
         return self.engine.process(color, self._as_u16(depth))
 
-    def _log(self, resp, r):
+    def _log(self, r):
         if self.metrics is not None and r is not None:
-            self.metrics.write(resp.mean_curvature, resp.max_curvature, r.coverage)
+            c = r.curvature
+            self.metrics.write(c.mean_curvature, c.max_curvature, r.coverage)
         self.frames += 1
 
     def _respond_timed(self, r, t):
         t0 = time.perf_counter()
-        resp, r = self._respond(r, t)
+        resp, r = self._respond_wire(r, t)
         t1 = time.perf_counter()
         self.stage_ms["respond"].append((t1 - t0) * 1e3)
         if r is not None and "gpu_ms" in r.timings:
             self.stage_ms["gpu"].append(r.timings["gpu_ms"])
         return resp, r, t1
+
+    def _respond_wire(self, r, t):
+        """Streaming form of ``_respond``: the AnalysisResponse as wire bytes, mask PNG and message
+        encoded natively without the GIL (csrc/serve_runtime.cpp encode_response; byte-identical to the
+        message path, tests/test_serve_cpu.py). Error frames, and builds without the extension, take the
+        message path."""
+        if isinstance(r, Exception) or self._encode is None:
+            return self._respond(r, t)
+        c = r.curvature
+        pts = r.points
+        if pts is None and c.spline_points:
+            pts = np.array([(p.x, p.y, p.z) for p in c.spline_points], np.float64)
+        t_read, t_start = t
+        now = time.perf_counter()
+        payload = self._encode(c.mean_curvature, c.max_curvature, pts, c.status, r.mask, r.coverage,
+                               (now - t_start) * 1e3, 1, 4)
+        with self._stats_lock:
+            self.queue_ms.append((t_start - t_read) * 1e3)
+            self.proc_ms.append((now - t_start) * 1e3)
+        return payload, r
 
     def _respond(self, r, t):
         """FrameResult (or the frame's exception) -> AnalysisResponse; runs on the codec pool when
@@ -298,7 +324,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         def ready(force: bool):
             while inflight and (force or inflight[0].done() or len(inflight) > self.prefetch):
                 resp, r, t_ready = inflight.popleft().result()
-                self._log(resp, r)
+                self._log(r)
                 self.stage_ms["hold"].append((time.perf_counter() - t_ready) * 1e3)
                 yield resp
 

@@ -362,3 +362,40 @@ def test_png_forged_oversized_header_is_refused_before_allocation():
         assert _t.time() - t0 < 0.5
     with pytest.raises(Exception):
         decode_image(forged, False)
+
+
+@pytest.mark.parametrize("case", ["full", "zeros", "negzero", "nopoints", "nomask", "unicode"])
+def test_native_response_encoding_matches_protobuf(case):
+    """serve_runtime.cpp encode_response == AnalysisResponse(...).SerializeToString() byte for byte
+    (the streaming server yields those bytes; proto/vision.py passes them through)."""
+    from robotic_discovery_platform_amd.data.image_io import encode_png
+    from robotic_discovery_platform_amd.ops import native
+    from robotic_discovery_platform_amd.proto import vision as pb
+    C = native(build_if_missing=False)
+    if C is None or not hasattr(C, "encode_response"):
+        pytest.skip("native extension not built")
+    rng = np.random.default_rng(0)
+    mask = (rng.random((48, 64)) > 0.7).astype(np.uint8)
+    pts = rng.normal(size=(50, 3))
+    mean, mx, status, cov, proc = 0.0123, 0.456, "ok", 12.5, 1.75
+    if case == "zeros":
+        pts[3] = 0.0
+        mean, cov = 0.0, 0.0
+    elif case == "negzero":
+        mean, pts[0, 1] = -0.0, -0.0
+    elif case == "nopoints":
+        pts, status = None, "too_few_points"
+    elif case == "nomask":
+        mask = None
+    elif case == "unicode":
+        status = "erréur: → x"
+    got = C.encode_response(mean, mx, pts, status, mask, cov, proc, 1, 4)
+    ref = pb.AnalysisResponse(mean_curvature=mean, max_curvature=mx, status=status, mask_coverage=cov,
+                              proc_time_ms=proc)
+    if pts is not None:
+        ref.spline_points.extend([pb.Point3D(x=a, y=b, z=c) for a, b, c in pts])
+    if mask is not None:
+        ref.mask = encode_png(mask * np.uint8(255), compress_level=1, bands=4)
+    assert got == ref.SerializeToString()
+    back = pb.AnalysisResponse.FromString(got)
+    assert back.status == status and len(back.spline_points) == (0 if pts is None else 50)
