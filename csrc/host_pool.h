@@ -91,7 +91,7 @@ class HostPool {
 
 // one pool per process (inline: a single instance across the translation units of the library)
 inline HostPool& host_pool() {
-  static HostPool p((int)std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 2)));
+  static HostPool p((int)std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2)));
   return p;
 }
 

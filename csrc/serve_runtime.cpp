@@ -8,8 +8,11 @@
 // at ~1,000 frames/s however many streams it served (profiles/serve_e2e.md). Two pieces move here:
 //
 //   FrameRunner      stage a frame into the pipeline's pinned buffers, enqueue H2D copies, launch the
-//                    graph exec, enqueue the D2H copies and the timing events -- one call with the GIL
-//                    released; wait() blocks on the frame's end event, also without the GIL.
+//                    graph execs, enqueue the D2H copies and the timing events, with the GIL released.
+//                    A frame goes in two calls on the pipeline's stream: the colour half (H2D + the
+//                    network graph) as soon as the colour frame is decoded, the depth half (H2D + the
+//                    geometry graph + D2H) when the depth frame is -- so the network runs while the
+//                    depth PNG is still inflating. wait() blocks on the frame's end event.
 //   encode_response  mask PNG (banded, codecs.cpp) + the evofab.vision.AnalysisResponse wire encoding
 //                    (/root/reference/protos/vision.proto:29-37), byte-identical to protobuf's own
 //                    serializer (fields in number order, proto3 defaults omitted); the gRPC handler
@@ -60,11 +63,11 @@ class FrameRunner {
     (void)hipEventDestroy(ev0_);
     (void)hipEventDestroy(ev1_);
   }
-  // graph exec of colour source `src` (0 BGR, 1 RGB, 2 JPEG coefficients), owned by the pipeline's
-  // torch CUDAGraph (kept alive there)
-  void set_graph(int src, uintptr_t exec) {
-    if (src < 0 || src > 2) throw std::invalid_argument("src");
-    exec_[src] = (hipGraphExec_t)exec;
+  // graph execs, owned by the pipeline's torch CUDAGraphs (kept alive there): slots 0..2 = the network
+  // graph of colour source 0 BGR / 1 RGB / 2 JPEG coefficients, slot 3 = the geometry graph
+  void set_graph(int slot, uintptr_t exec) {
+    if (slot < 0 || slot > 3) throw std::invalid_argument("slot");
+    exec_[slot] = (hipGraphExec_t)exec;
   }
   // pinned host staging / device buffers of the pipeline (sizes in bytes)
   void set_buffers(uintptr_t d_color, uintptr_t h_color, size_t color_bytes, uintptr_t d_depth, uintptr_t h_depth,
@@ -78,37 +81,56 @@ class FrameRunner {
     d_res_ = P(d_res); h_res_ = P(h_res); res_bytes_ = res_bytes;
   }
 
-  // colour as an HxWx3 u8 array (src 0 BGR / 1 RGB), depth HxW 16-bit
-  void submit_array(int src, py::buffer color, py::buffer depth) {
-    py::buffer_info c = color.request(), d = depth.request();
+  // colour half, from an HxWx3 u8 array (src 0 BGR / 1 RGB)
+  void submit_array(int src, py::buffer color) {
+    py::buffer_info c = color.request();
     check_contig(c, color_bytes_, "colour");
-    check_contig(d, depth_bytes_, "depth");
     if (src != 0 && src != 1) throw std::invalid_argument("src must be 0 (BGR) or 1 (RGB)");
+    need(src);
     const void* cp = c.ptr;
-    const void* dp = d.ptr;
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
     std::memcpy(h_color_, cp, color_bytes_);
     hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
-    std::memcpy(h_depth_, dp, depth_bytes_);
-    launch_tail(src);
+    hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
   }
 
-  // colour as entropy-decoded JPEG (data/jpeg.py JpegCoefs: pinned meta + coefficient buffers; the caller
-  // keeps them alive until wait() returns)
-  void submit_jpeg(uintptr_t meta, size_t meta_bytes, uintptr_t coefs, size_t coef_bytes, py::buffer depth) {
-    py::buffer_info d = depth.request();
-    check_contig(d, depth_bytes_, "depth");
+  // colour half, from an entropy-decoded JPEG (data/jpeg.py JpegCoefs: pinned meta + coefficient
+  // buffers; the caller keeps them alive until wait() returns)
+  void submit_jpeg(uintptr_t meta, size_t meta_bytes, uintptr_t coefs, size_t coef_bytes) {
     if (meta_bytes != meta_bytes_ || coef_bytes > coef_cap_) throw std::invalid_argument("JPEG buffers exceed the pipeline");
-    const void* dp = d.ptr;
+    need(2);
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
     hip_check(hipMemcpyAsync(d_meta_, P(meta), meta_bytes, hipMemcpyHostToDevice, s_), "H2D meta");
     hip_check(hipMemcpyAsync(d_coef_, P(coefs), coef_bytes, hipMemcpyHostToDevice, s_), "H2D coefs");
+    hip_check(hipGraphLaunch(exec_[2], s_), "hipGraphLaunch");
+  }
+
+  // depth half (HxW 16-bit): H2D, the geometry graph, the result read-back and the frame's end event
+  void submit_depth(py::buffer depth) {
+    py::buffer_info d = depth.request();
+    check_contig(d, depth_bytes_, "depth");
+    need(3);
+    const void* dp = d.ptr;
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
     std::memcpy(h_depth_, dp, depth_bytes_);
-    launch_tail(2);
+    hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, s_), "H2D depth");
+    hip_check(hipGraphLaunch(exec_[3], s_), "hipGraphLaunch");
+    hip_check(hipMemcpyAsync(h_mask_, d_mask_, mask_bytes_, hipMemcpyDeviceToHost, s_), "D2H mask");
+    hip_check(hipMemcpyAsync(h_res_, d_res_, res_bytes_, hipMemcpyDeviceToHost, s_), "D2H result");
+    hip_check(hipEventRecord(ev1_, s_), "hipEventRecord");
+    recorded_ = true;
+  }
+
+  // a frame whose depth half never came (its decode failed): drain the colour half
+  void abort() {
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
   }
 
   // block until the frame's results are on the host; returns its device time (ms, event to event)
@@ -133,21 +155,15 @@ class FrameRunner {
     }
     if (n != bytes) throw std::invalid_argument(std::string(what) + ": size does not match the pipeline");
   }
-  void launch_tail(int src) {
-    if (!exec_[src]) throw std::runtime_error("FrameRunner: no graph for this colour source");
-    hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, s_), "H2D depth");
-    hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
-    hip_check(hipMemcpyAsync(h_mask_, d_mask_, mask_bytes_, hipMemcpyDeviceToHost, s_), "D2H mask");
-    hip_check(hipMemcpyAsync(h_res_, d_res_, res_bytes_, hipMemcpyDeviceToHost, s_), "D2H result");
-    hip_check(hipEventRecord(ev1_, s_), "hipEventRecord");
-    recorded_ = true;
+  void need(int slot) const {
+    if (!exec_[slot]) throw std::runtime_error("FrameRunner: graph slot " + std::to_string(slot) + " not set");
   }
 
   bool recorded_ = false;
   int dev_;
   hipStream_t s_;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
-  hipGraphExec_t exec_[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t exec_[4] = {nullptr, nullptr, nullptr, nullptr};
   void *d_color_ = nullptr, *h_color_ = nullptr, *d_depth_ = nullptr, *h_depth_ = nullptr;
   void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
   void *d_res_ = nullptr, *h_res_ = nullptr;
@@ -243,6 +259,8 @@ void register_serve_runtime(py::module_& m) {
       .def("set_buffers", &FrameRunner::set_buffers)
       .def("submit_array", &FrameRunner::submit_array)
       .def("submit_jpeg", &FrameRunner::submit_jpeg)
+      .def("submit_depth", &FrameRunner::submit_depth)
+      .def("abort", &FrameRunner::abort)
       .def("wait", &FrameRunner::wait);
   m.def("encode_response", &encode_response, py::arg("mean"), py::arg("max"), py::arg("points"), py::arg("status"),
         py::arg("mask"), py::arg("coverage"), py::arg("proc_ms"), py::arg("level") = 1, py::arg("bands") = 4);

@@ -175,6 +175,15 @@ class NullPipeline:
     def submit(self, color, depth, rgb=False):
         self._n += 1
 
+    def submit_color(self, color, rgb=False):
+        pass
+
+    def submit_depth(self, depth):
+        self._n += 1
+
+    def abort(self):
+        pass
+
     def collect(self):
         return self._res
 

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import collections
 import contextlib
+from concurrent import futures
 import math
 import queue
 import threading
@@ -80,7 +81,8 @@ class FrameResult:
     points: Optional[np.ndarray] = None  # spline points [n, 3] float64 (device fits; the server encodes them)
 
 
-SRC_BGR, SRC_RGB, SRC_JPEG = 0, 1, 2  # colour sources of a frame graph
+SRC_BGR, SRC_RGB, SRC_JPEG = 0, 1, 2  # colour sources of a network graph
+GEO, GEO_SLOT = "geo", 3  # the geometry graph (FrameRunner slot 3)
 
 
 def _stage(dst: torch.Tensor, src: np.ndarray) -> None:
@@ -153,6 +155,7 @@ class FramePipeline:
         self.use_graph = graph
         self.lock = threading.Lock()
         self._hold = None  # the submitted frame's JPEG buffers, alive until its copies are done
+        self._pending_src = None  # colour half submitted, depth half not yet
         # native per-frame host path (csrc/serve_runtime.cpp): staging copies, H2D, graph launch, D2H and
         # events in one call without the GIL; the Python path below stays for eager pipelines
         self.runner = None
@@ -176,12 +179,13 @@ class FramePipeline:
             self.refresh_weights()
 
     # ---------------------------------------------------------------- device program
-    def _device_program(self, src: int = 0):
-        self._net_program(src)
-        self._geo_program()
-
+    # A frame is two captured graphs on the pipeline's stream: the network graph of its colour source
+    # (JPEG pixel stage, preprocess, U-Net, fused head + threshold -> 256x256 mask) and the geometry
+    # graph (mask upsample, back-projection, edge bins, device spline fit). The server enqueues the
+    # first as soon as the colour frame is decoded and the second when the depth PNG is, so the network
+    # runs while the depth frame is still inflating on the host.
     def _net_program(self, src: int = 0):
-        # Measured dead end: the H2D / D2H copies captured INTO this graph, depth H2D and mask D2H
+        # Measured dead end: the H2D / D2H copies captured INTO the frame graph, depth H2D and mask D2H
         # on a forked branch -- the memcpy nodes replay as blit kernels (20.7 + 17.7 us for colour /
         # depth instead of DMA-engine copies), the fork adds a ~67 us cross-queue gap, and two
         # pipelines no longer overlap: GPU p50 0.622 -> 0.648 ms, pipelined 2307 -> 1502 FPS.
@@ -209,100 +213,123 @@ class FramePipeline:
     def wait_idle(self):
         """Block until this pipeline's last submitted frame has left the GPU (its result is dropped)."""
         if self.runner is not None:
-            self.runner.wait()
+            self.runner.abort()  # stream drain: also covers a colour half without its depth half
         else:
-            self.ev1.synchronize()
+            self.stream.synchronize()
         self._hold = None
+        self._pending_src = None
 
     @property
     def graph(self):
-        return self.graphs.get(0)
+        return self.graphs.get(SRC_BGR)
+
+    def _capture_one(self, key, program):
+        with torch.cuda.device(self.dev):
+            with torch.cuda.stream(self.stream):
+                program()  # warm-up (lazy allocations, kernel loading)
+            self.stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            # thread-local capture: other server threads may use the GPU meanwhile (a late capture of
+            # another colour source happens on a live server)
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+                program()
+        self.graphs[key] = g
+        if self.runner is not None:
+            self.runner.set_graph(GEO_SLOT if key == GEO else key, g.raw_cuda_graph_exec())
 
     def _capture(self, src: int):
         if not self.graphs:
             self.refresh_weights()
-        with torch.cuda.device(self.dev):
-            with torch.cuda.stream(self.stream):
-                self._device_program(src)  # warm-up (lazy allocations, kernel loading)
-            self.stream.synchronize()
-            g = torch.cuda.CUDAGraph()
-            # thread-local capture: other server threads may use the GPU meanwhile (a late capture of
-            # the other channel order happens on a live server)
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
-                self._device_program(src)
-        self.graphs[src] = g
-        if self.runner is not None:
-            self.runner.set_graph(src, g.raw_cuda_graph_exec())
+        self._capture_one(src, lambda: self._net_program(src))
+        if GEO not in self.graphs:
+            self._capture_one(GEO, self._geo_program)
 
     # ---------------------------------------------------------------- per frame
     def submit(self, color_bgr, depth: np.ndarray, rgb: bool = False):
         """Stage a frame and enqueue its device work; returns immediately (call ``collect``).
         ``color_bgr``: HxWx3 uint8 array -- OpenCV's BGR, or RGB with ``rgb`` (as the server decodes
         it) -- or a ``JpegCoefs`` (entropy-decoded JPEG; the pixel stage runs in the frame graph)."""
-        if color_bgr.shape != (self.H, self.W, 3) or depth.shape != (self.H, self.W):
+        if depth.shape != (self.H, self.W):
             raise ValueError(f"frame shape {color_bgr.shape}/{depth.shape} != pipeline ({self.H},{self.W})")
-        # colour staged and its H2D enqueued first; the depth frame is staged on the host while that
-        # copy runs. (Measured alternative: the network and the geometry as two graphs with the depth
-        # H2D on a copy stream under the network -- the cross-queue wait left a ~14 us gap between the
-        # graphs, about what it hid.)
-        s = self.stream
-        if self.runner is not None:
-            return self._submit_native(color_bgr, depth, rgb)
-        if isinstance(color_bgr, JpegCoefs):
-            src = SRC_JPEG
-            n = color_bgr.coefs.numel()
-            if n > self.d_coef.numel() or color_bgr.blocks * 64 > n:
-                raise ValueError(f"JPEG coefficient planes ({n}) exceed the pipeline's capacity")
-            with torch.cuda.device(self.dev), torch.cuda.stream(s):
-                self.ev0.record(s)
-                self.d_meta.copy_(color_bgr.meta, non_blocking=True)
-                self.d_coef[:n].copy_(color_bgr.coefs, non_blocking=True)
-        else:
-            src = SRC_RGB if rgb else SRC_BGR
-            _stage(self.h_color, color_bgr)
-            with torch.cuda.device(self.dev), torch.cuda.stream(s):
-                self.ev0.record(s)
-                self.d_color.copy_(self.h_color, non_blocking=True)
-        _stage(self.h_depth, depth.view(np.int16) if depth.dtype == np.uint16 else depth.astype(np.int16))
-        with trace.range("serve.frame.enqueue"), torch.cuda.device(self.dev), torch.cuda.stream(s):
-            self.d_depth.copy_(self.h_depth, non_blocking=True)
-            if self.use_graph:
-                g = self.graphs.get(src)
-                if g is None:  # first frame from this source: capture its graph (stream-ordered)
-                    self._capture(src)
-                    g = self.graphs[src]
-                g.replay()
-            else:
-                self._device_program(src)
-            self.h_mask.copy_(self.mask, non_blocking=True)
-            self.h_res.copy_(self.geo.res, non_blocking=True)
-            self.ev1.record(s)
+        self.submit_color(color_bgr, rgb)
+        self.submit_depth(depth)
 
-    def _submit_native(self, color, depth: np.ndarray, rgb: bool):
-        d = depth if depth.dtype in (np.uint16, np.int16) else depth.astype(np.int16)
+    def submit_color(self, color, rgb: bool = False):
+        """First half of ``submit``: stage the colour frame and enqueue the network graph."""
+        if color.shape != (self.H, self.W, 3):
+            raise ValueError(f"colour frame {color.shape} != pipeline ({self.H},{self.W})")
         src = SRC_JPEG if isinstance(color, JpegCoefs) else (SRC_RGB if rgb else SRC_BGR)
-        if src not in self.graphs:  # first frame from this source: capture its graph (stream-ordered)
+        if src == SRC_JPEG:
+            n = color.coefs.numel()
+            if n > self.d_coef.numel() or color.blocks * 64 > n:
+                raise ValueError(f"JPEG coefficient planes ({n}) exceed the pipeline's capacity")
+        if self.use_graph and src not in self.graphs:  # first frame from this source (stream-ordered)
             self._capture(src)
-        with trace.range("serve.frame.enqueue"):
-            if src == SRC_JPEG:
-                n = color.coefs.numel()
-                if n > self.d_coef.numel() or color.blocks * 64 > n:
-                    raise ValueError(f"JPEG coefficient planes ({n}) exceed the pipeline's capacity")
-                self._hold = color  # its (pinned) buffers must outlive the async copies
-                self.runner.submit_jpeg(color.meta.data_ptr(), color.meta.numel() * 4, color.coefs.data_ptr(),
-                                        n * 2, np.ascontiguousarray(d))
+        with trace.range("serve.frame.enqueue_color"):
+            if self.runner is not None:
+                if src == SRC_JPEG:
+                    self._hold = color  # its (pinned) buffers must outlive the async copies
+                    self.runner.submit_jpeg(color.meta.data_ptr(), color.meta.numel() * 4, color.coefs.data_ptr(),
+                                            color.coefs.numel() * 2)
+                else:
+                    self.runner.submit_array(src, np.ascontiguousarray(color))
             else:
-                self.runner.submit_array(src, np.ascontiguousarray(color), np.ascontiguousarray(d))
+                s = self.stream
+                if src != SRC_JPEG:
+                    _stage(self.h_color, color)
+                with torch.cuda.device(self.dev), torch.cuda.stream(s):
+                    self.ev0.record(s)
+                    if src == SRC_JPEG:
+                        self._hold = color
+                        self.d_meta.copy_(color.meta, non_blocking=True)
+                        self.d_coef[:color.coefs.numel()].copy_(color.coefs, non_blocking=True)
+                    else:
+                        self.d_color.copy_(self.h_color, non_blocking=True)
+                    if self.use_graph:
+                        self.graphs[src].replay()
+                    else:
+                        self._net_program(src)
+        self._pending_src = src
+
+    def submit_depth(self, depth: np.ndarray):
+        """Second half of ``submit``: stage the depth frame, enqueue the geometry graph and the result
+        read-back."""
+        if self._pending_src is None:
+            raise RuntimeError("submit_depth without submit_color")
+        if depth.shape != (self.H, self.W):
+            raise ValueError(f"depth frame {depth.shape} != pipeline ({self.H},{self.W})")
+        d = depth.view(np.int16) if depth.dtype == np.uint16 else (
+            depth if depth.dtype == np.int16 else depth.astype(np.int16))
+        with trace.range("serve.frame.enqueue_depth"):
+            if self.runner is not None:
+                self.runner.submit_depth(np.ascontiguousarray(d))
+            else:
+                s = self.stream
+                _stage(self.h_depth, d)
+                with torch.cuda.device(self.dev), torch.cuda.stream(s):
+                    self.d_depth.copy_(self.h_depth, non_blocking=True)
+                    if self.use_graph:
+                        self.graphs[GEO].replay()
+                    else:
+                        self._geo_program()
+                    self.h_mask.copy_(self.mask, non_blocking=True)
+                    self.h_res.copy_(self.geo.res, non_blocking=True)
+                    self.ev1.record(s)
+        self._pending_src = None
+
+    def abort(self):
+        """Drop a frame whose depth half will not come (its decode failed)."""
+        self.wait_idle()
 
     def collect(self) -> FrameResult:
         t0 = time.perf_counter()
         with trace.range("serve.frame.wait_gpu"):
             if self.runner is not None:
                 gpu_ms = self.runner.wait()
-                self._hold = None
             else:
                 self.ev1.synchronize()
                 gpu_ms = self.ev0.elapsed_time(self.ev1)
+            self._hold = None
         t1 = time.perf_counter()
         from ..geometry.curvature import coverage_from_device
         h_res = self.h_res.numpy()
@@ -314,6 +341,7 @@ class FramePipeline:
             pts = h_res[8:8 + 3 * self.cfg.num_samples].reshape(-1, 3).copy()
         t2 = time.perf_counter()
         cov = 100.0 * count / (self.H * self.W)
+        # gpu_ms: colour-half start -> results on the host (includes any wait for the depth half)
         return FrameResult(self.h_mask.numpy().copy(), cov, res,
                            {"gpu_ms": gpu_ms, "wait_ms": (t1 - t0) * 1e3, "fit_ms": (t2 - t1) * 1e3}, pts)
 
@@ -346,6 +374,19 @@ class CpuFramePipeline:
         if isinstance(color_bgr, JpegCoefs):  # (the server only sends these to GPU pipelines)
             color_bgr, rgb = coefs_to_rgb_reference(color_bgr), True
         self._pending = (color_bgr[..., ::-1] if rgb else color_bgr, depth)
+
+    def submit_color(self, color, rgb: bool = False):
+        if color.shape != (self.H, self.W, 3):
+            raise ValueError(f"colour frame {color.shape} != pipeline ({self.H},{self.W})")
+        self._color = (color, rgb)
+
+    def submit_depth(self, depth: np.ndarray):
+        color, rgb = self._color
+        self._color = None
+        self.submit(color, depth, rgb)
+
+    def abort(self):
+        self._color = self._pending = None
 
     def collect(self) -> FrameResult:
         color_bgr, depth = self._pending
@@ -501,17 +542,23 @@ class EngineSession:
         self.pool, self.replica, self.depth = pool, replica, max(1, depth)
         self.inflight: "collections.deque" = collections.deque()
 
-    def submit(self, color_bgr: np.ndarray, depth: np.ndarray, tag=None, rgb: bool = False) -> list:
+    def submit(self, color_bgr, depth, tag=None, rgb: bool = False) -> list:
         """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect.
-        ``rgb``: the colour frame is in RGB order (else OpenCV BGR)."""
+        ``rgb``: the colour frame is in RGB order (else OpenCV BGR). ``depth`` may be a
+        ``concurrent.futures.Future`` of the depth frame (the server's decode): the colour half of the
+        frame is then enqueued first and the depth half when the future resolves."""
         out = []
-        if color_bgr.ndim != 3 or color_bgr.shape[2] != 3 or color_bgr.shape[:2] != depth.shape[:2]:
+        split = isinstance(depth, futures.Future)
+        dshape = None if split else depth.shape[:2]
+        if color_bgr.ndim != 3 or color_bgr.shape[2] != 3 or (dshape is not None and color_bgr.shape[:2] != dshape):
+            if split:
+                depth.cancel()
             out += self.drain()  # results stay in submission order
-            out.append((tag, ValueError(f"colour {color_bgr.shape} and depth {depth.shape} frame sizes differ")))
+            out.append((tag, ValueError(f"colour {color_bgr.shape} and depth {dshape} frame sizes differ")))
             return out
         while len(self.inflight) >= self.depth:
             out.append(self._collect_one())
-        q = self.pool._get(self.replica, *depth.shape[:2])
+        q = self.pool._get(self.replica, *color_bgr.shape[:2])
         try:
             p = q.get_nowait()
         except queue.Empty:
@@ -519,7 +566,18 @@ class EngineSession:
                 out.append(self._collect_one())
             p = q.get()
         try:
-            p.submit(color_bgr, depth, rgb)
+            if split:
+                p.submit_color(color_bgr, rgb)
+                try:
+                    d = depth.result()
+                    if d.shape[:2] != color_bgr.shape[:2]:
+                        raise ValueError(f"colour {color_bgr.shape} and depth {d.shape} frame sizes differ")
+                    p.submit_depth(d)
+                except BaseException:
+                    p.abort()
+                    raise
+            else:
+                p.submit(color_bgr, depth, rgb)
         except Exception as e:
             q.put(p)
             out += self.drain()

@@ -161,14 +161,15 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
 
     def _decode_depth(self, data: bytes):
         t = time.perf_counter()
-        out = decode_image(data, False)
+        out = self._as_u16(decode_image(data, False))
         self.stage_ms["decode_depth"].append((time.perf_counter() - t) * 1e3)
         return out
 
     def _decoded(self, request_iterator):
-        """Yield (t_read, colour, depth, error, more) in request order; decoding runs ahead on the
-        codec pool. ``error`` is the decode exception of a bad frame (colour/depth None then);
-        ``more()`` tells whether the client has already sent the next frame."""
+        """Yield (t_read, colour, depth future, error, more) in request order; decoding runs ahead on
+        the codec pool. ``error`` is the colour decode exception of a bad frame (colour None then; a
+        depth decode error surfaces as that frame's result); ``more()`` tells whether the client has
+        already sent the next frame."""
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         END = object()
         stop = threading.Event()  # the handler is gone (stream ended early): the reader must not block
@@ -208,12 +209,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     raise item[3]
                 t, fc, fd, _ = item
                 try:
-                    color, depth = fc.result(), fd.result()
-                    err = None
+                    color, err = fc.result(), None
                 except Exception as e:
-                    color = depth = None
-                    err = e
-                yield t, color, depth, err, lambda: q.qsize() > 0
+                    color, err = None, e
+                yield t, color, fd, err, lambda: q.qsize() > 0
         finally:
             stop.set()
 
@@ -338,7 +337,8 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     encode([(i, err)])
                 else:
                     with trace.range("serve.rpc.frame"):
-                        done = sess.submit(color, self._as_u16(depth), tag=i, rgb=True)
+                        # colour half enqueued now, depth half when its PNG is inflated
+                        done = sess.submit(color, depth, tag=i, rgb=True)
                         self.stage_ms["submit"].append((time.perf_counter() - t_start) * 1e3)
                         encode(done)
                     if not more():  # lock-step client: finish this frame now

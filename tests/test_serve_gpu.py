@@ -310,3 +310,39 @@ def test_frame_pipeline_jpeg_source_matches_array_source():
     with pytest.raises(ValueError):
         small = decode_coefs(encode_jpeg(np.zeros((240, 320, 3), np.uint8)), pin=True)
         pj.submit(small, np.zeros((480, 640), np.uint16))
+
+
+def test_session_split_submit_and_failed_depth_half():
+    """The server's split submission (colour half now, depth half from a future): same result as the
+    one-shot submit; a failed depth decode gives that frame an error and leaves the pipeline usable."""
+    from concurrent.futures import Future
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K, make_scene
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.serve.engine import EnginePool
+    torch.manual_seed(0)
+    nat = UNetNative(3, 1, device=torch.device("cuda")).eval()
+    with torch.no_grad():
+        nat.store.view("outc.conv.bias").fill_(0.0)
+    pool = EnginePool(nat, DEFAULT_K, 0.001, n=2, graph=True, rgb=True)
+    assert all(p.runner is not None for p in list(pool._pools.values())[0].queue)  # native host path
+    sc = make_scene(2)
+    rgb = np.ascontiguousarray(sc.color[..., ::-1])
+    ref = pool.process(sc.color, sc.depth)
+
+    def fut(v=None, exc=None):
+        f = Future()
+        f.set_exception(exc) if exc is not None else f.set_result(v)
+        return f
+    s = pool.session()
+    out = []
+    out += s.submit(rgb, fut(sc.depth), tag=0, rgb=True)
+    out += s.submit(rgb, fut(exc=ValueError("corrupt depth PNG")), tag=1, rgb=True)
+    out += s.submit(rgb, fut(sc.depth[:100]), tag=2, rgb=True)  # size mismatch found at the depth half
+    out += s.submit(rgb, fut(sc.depth), tag=3, rgb=True)
+    out += s.drain()
+    res = dict(out)
+    assert sorted(res) == [0, 1, 2, 3]
+    assert isinstance(res[1], ValueError) and isinstance(res[2], ValueError)
+    for k in (0, 3):
+        assert np.array_equal(res[k].mask, ref.mask) and res[k].coverage == ref.coverage
+        assert res[k].curvature.mean_curvature == ref.curvature.mean_curvature
