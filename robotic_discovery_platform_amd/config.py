@@ -90,6 +90,7 @@ class ServeConfig:
     replicas_per_device: int = 2  # independent stream pipelines (hipGraph + buffers) per GPU
     frame_errors: str = "degrade"  # "degrade": bad frame -> error status, stream goes on; "abort": reference
     gpu_jpeg: bool = True  # baseline JPEGs: native entropy decode on the host, pixel stage in the frame graph
+    workers: int = 1  # server processes sharing the port (SO_REUSEPORT): one interpreter lock each
     hot_reload_alias: Optional[str] = None  # e.g. "staging": reload when alias moves
 
 

@@ -221,6 +221,118 @@ class NullEngine:
         return NullPipeline(*depth.shape[:2]).collect()
 
 
+def _client_env():
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    return dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")  # the client never touches the GPU
+
+
+def _run_clients(ports, frames, warmup, lockstep, env=None) -> list:
+    """One load-generator process per entry of ``ports`` (stream k -> ports[k]), started together."""
+    import json
+    import subprocess
+    env = env or _client_env()
+    procs = [subprocess.Popen([sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve",
+                               "--client-port", str(pt), "--frames", str(frames), "--warmup", str(warmup),
+                               "--lockstep", str(int(lockstep))],
+                              env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for pt in ports]
+    try:
+        for p in procs:  # every client has built its requests: start them together
+            if p.stdout.readline().strip() != "ready":
+                raise RuntimeError(f"client process failed: {p.stderr.read()[-1500:]}")
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        res = []
+        for p in procs:
+            so, se = p.communicate(timeout=600)
+            if p.returncode != 0:
+                raise RuntimeError(f"client process failed: {se[-1500:]}")
+            res.append(json.loads(so.strip().splitlines()[-1]))
+        return res
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+
+
+def measure_e2e_procs(model, frames: int = 200, warmup: int = 20, procs: int = 2, streams: int = 4,
+                      hw_queues: int = 0) -> dict:
+    """``ServeConfig.workers`` topology: ``procs`` server processes on one GPU (each its own engine replica
+    and interpreter lock), ``streams`` client streams spread round-robin over them. Aggregate frames/s
+    = the sum of the streams' rates."""
+    import json
+    import subprocess
+    tmp = tempfile.mkdtemp(prefix="rdp_serve_procs_")
+    wpath = os.path.join(tmp, "weights.pt")
+    torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()}, wpath)
+    env = dict(_client_env(), HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", ""),
+               CUDA_VISIBLE_DEVICES=os.environ.get("CUDA_VISIBLE_DEVICES", ""))
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if not env[k]:
+            env.pop(k)
+    if hw_queues > 0:  # hardware queues per server process (HIP default 4)
+        env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
+    per = max(1, -(-streams // procs))
+    servers = [subprocess.Popen([sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve",
+                                 "--server-child", wpath, "--pool", str(2 * per)],
+                                env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                text=True) for _ in range(procs)]
+    out = {}
+    try:
+        ports = []
+        for p in servers:
+            line = p.stdout.readline().strip()
+            if not line.startswith("port "):
+                raise RuntimeError(f"server process failed: {p.stderr.read()[-1500:]}")
+            ports.append(int(line.split()[1]))
+        res = _run_clients([ports[k % procs] for k in range(streams)], frames, warmup, lockstep=False)
+        sfx = f"_{streams}streams_{procs}procs" + (f"_{hw_queues}hwq" if hw_queues else "")
+        out["e2e_fps" + sfx] = round(sum(r["e2e_fps"] for r in res), 1)
+        out["e2e_server_proc_p50_ms" + sfx] = round(float(np.median([r["e2e_server_proc_p50_ms"] for r in res])), 3)
+        stats = []
+        for p in servers:
+            so, _ = p.communicate("", timeout=120)
+            stats.append(json.loads(so.strip().splitlines()[-1]))
+        for k in ("decode_color", "decode_depth", "gpu", "respond"):
+            out[f"e2e_stage_{k}_p50_ms" + sfx] = round(float(np.median([st[f"{k}_p50_ms"] for st in stats])), 3)
+        _progress(f"e2e procs: {out}")
+    finally:
+        for p in servers:
+            if p.poll() is None:
+                p.kill()
+    return out
+
+
+def _server_child(wpath: str, pool: int) -> None:
+    """``--server-child``: one server process of ``measure_e2e_procs``; prints its port, serves until
+    stdin closes, then prints its latency stats."""
+    import json
+    import grpc
+    from concurrent import futures
+    from ..data.synthetic import DEFAULT_K
+    from ..models.unet import UNetNative
+    from ..proto import vision as pb
+    from .engine import EnginePool
+    from .server import VisionAnalysisService
+    dev = torch.device("cuda")
+    model = UNetNative(3, 1, device=dev)
+    model.load_state_dict(torch.load(wpath, map_location="cpu", weights_only=True))
+    model.eval()
+    engine = EnginePool(model, DEFAULT_K, 0.001, n=pool, graph=True, rgb=True, jpeg=True)
+    svc = VisionAnalysisService(engine, None)
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10))
+    pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
+    port = server.add_insecure_port("127.0.0.1:0")
+    server.start()
+    print(f"port {port}", flush=True)
+    sys.stdin.read()
+    server.stop(0).wait()
+    svc.close()
+    print(json.dumps(svc.latency_stats()), flush=True)
+
+
 def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 2, gpu_jpeg: bool = True,
                 streams: int = 1, switch_ms: float = 0.0):
     """Server in this process, load generator(s) in separate client processes (the reference's
@@ -256,27 +368,7 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
                    HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")  # the client never touches the GPU
-        cmd = [sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve", "--client-port", str(port),
-               "--frames", str(frames), "--warmup", str(warmup), "--lockstep", str(int(streams == 1))]
-        procs = [subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                                  stderr=subprocess.PIPE, text=True) for _ in range(streams)]
-        try:
-            for p in procs:  # every client has built its requests: start them together
-                if p.stdout.readline().strip() != "ready":
-                    raise RuntimeError(f"client process failed: {p.stderr.read()[-1500:]}")
-            for p in procs:
-                p.stdin.write("go\n")
-                p.stdin.flush()
-            res = []
-            for p in procs:
-                so, se = p.communicate(timeout=600)
-                if p.returncode != 0:
-                    raise RuntimeError(f"client process failed: {se[-1500:]}")
-                res.append(json.loads(so.strip().splitlines()[-1]))
-        finally:
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
+        res = _run_clients([port] * streams, frames, warmup, lockstep=streams == 1, env=env)
         if streams == 1:
             out.update(res[0])
         else:
@@ -323,6 +415,7 @@ def measure_serving(dev: Optional[torch.device] = None, frames: int = 200, warmu
         res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup).items()})
         res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup, gpu_jpeg=False).items()})
         res.update({"serve_" + k: v for k, v in measure_e2e(model, scenes, frames, warmup, streams=4).items()})
+        res.update({"serve_" + k: v for k, v in measure_e2e_procs(model, frames, warmup, procs=2, streams=4).items()})
         _progress("e2e done")
     return res
 
@@ -337,7 +430,12 @@ if __name__ == "__main__":
     ap.add_argument("--e2e", type=int, default=1)
     ap.add_argument("--client-port", type=int, default=0, help="internal: run as the e2e load-generator process")
     ap.add_argument("--lockstep", type=int, default=1, help="internal: client also measures lock-step round trips")
+    ap.add_argument("--server-child", default=None, help="internal: run as a measure_e2e_procs server process")
+    ap.add_argument("--pool", type=int, default=4)
     a = ap.parse_args()
+    if a.server_child:
+        _server_child(a.server_child, a.pool)
+        raise SystemExit(0)
     if a.client_port:
         import sys
 

@@ -432,7 +432,14 @@ def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_s
 
 
 def serve(cfg: Optional[ServeConfig] = None, block: bool = True):
+    """Run the service. ``cfg.workers`` > 1: that many server processes (spawned before anything
+    touches the GPU) bind the same port with SO_REUSEPORT -- the kernel spreads client connections
+    over them -- each with its own engine replica and its own interpreter lock; the per-frame Python
+    work of one process caps it at ~1,500-1,800 frames/s (profiles/serve_e2e.md). ``block``: wait for
+    the workers to exit (else return the worker processes)."""
     cfg = cfg or ServeConfig()
+    if cfg.workers > 1:
+        return _serve_workers(cfg, block)
     from .faults import from_env
     out = build_server(cfg, faults=from_env())
     if out is None:
@@ -445,3 +452,31 @@ def serve(cfg: Optional[ServeConfig] = None, block: bool = True):
     if block:
         server.wait_for_termination()
     return server, service, watcher, port
+
+
+def _worker_main(cfg: ServeConfig) -> None:
+    import dataclasses
+    serve(dataclasses.replace(cfg, workers=1), block=True)
+
+
+def _serve_workers(cfg: ServeConfig, block: bool = True):
+    import multiprocessing as mp
+    if cfg.port == 0:
+        raise ValueError("workers > 1 need a fixed port (every worker binds it with SO_REUSEPORT)")
+    ctx = mp.get_context("spawn")  # fresh interpreters: the parent never initialises the GPU
+    procs = [ctx.Process(target=_worker_main, args=(cfg,), name=f"rdp-serve-{i}", daemon=False)
+             for i in range(cfg.workers)]
+    for p in procs:
+        p.start()
+    log.info("VisionAnalysisService: %d worker processes on %s:%d", cfg.workers, cfg.host, cfg.port)
+    if not block:
+        return procs
+    try:
+        for p in procs:
+            p.join()
+    except KeyboardInterrupt:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            p.join()
+    return [p.exitcode for p in procs]

@@ -11,7 +11,7 @@ for f in sorted(glob.glob(f'{d}/set*/pmc_counter_collection.csv')):
         meta[k] = (r['Kernel_Name'][:32], r['Grid_Size'], int(r['End_Timestamp']) - int(r['Start_Timestamp']))
     for k, v in acc.items():
         name, grid, dur = meta[k]
-        if 'conv' not in name: continue
+        if 'conv' not in name and 'wgrad' not in name: continue
         for c, x in v.items(): per[(name, grid)][c].append(x)
         per[(name, grid)]['dur_us'].append(dur / 1e3)
 for (name, grid), v in per.items():

@@ -399,3 +399,39 @@ def test_native_response_encoding_matches_protobuf(case):
     assert got == ref.SerializeToString()
     back = pb.AnalysisResponse.FromString(got)
     assert back.status == status and len(back.spline_points) == (0 if pts is None else 50)
+
+
+def test_serve_workers_share_port(tmp_path):
+    """ServeConfig.workers: spawned server processes bind one port (SO_REUSEPORT); concurrent client
+    streams are answered."""
+    import socket
+    import grpc
+    from robotic_discovery_platform_amd.proto import vision as pb
+    from robotic_discovery_platform_amd.serve.client import make_request
+    from robotic_discovery_platform_amd.serve.server import serve
+    _setup_store(tmp_path)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cfg = _serve_cfg(tmp_path, port=port, workers=2)
+    procs = serve(cfg, block=False)
+    try:
+        sc = make_scene(1)
+        req = make_request(sc.color, sc.depth)
+        got = []
+
+        def stream():
+            with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+                grpc.channel_ready_future(ch).result(timeout=120)
+                stub = pb.VisionAnalysisServiceStub(ch)
+                got.append([r.status for r in stub.AnalyzeActuatorPerformance(iter([req] * 3), timeout=120)])
+        ths = [threading.Thread(target=stream) for _ in range(3)]
+        [t.start() for t in ths]
+        [t.join(180) for t in ths]
+        assert len(got) == 3 and all(len(g) == 3 and not any(x.startswith("error") for x in g) for g in got)
+        assert all(p.is_alive() for p in procs)
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            p.join(30)
