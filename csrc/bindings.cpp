@@ -31,6 +31,7 @@ int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStre
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
                    float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
+long rdp_conv_wgrad_halo_slab_elems(int, int, int, int, int);
 int rdp_wgrad_first_bn(const void*, long, int, const void*, long, int, const void*, long, int, const float*, const float*,
                        float*, long, float*, int, int, int, int, int, int, hipStream_t);
 int rdp_bn_finalize(const float*, int, int, long, const float*, const float*, float*, float*, long long*, float, float,
@@ -1116,6 +1117,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", on_device(&conv_wgrad));
   m.def("wgrad_first_bn", on_device(&wgrad_first_bn));
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
+  m.def("wgrad_halo_slab_elems", &rdp_conv_wgrad_halo_slab_elems);
   m.def("bn_finalize", on_device(&bn_finalize));
   m.def("bn_eval_coef", on_device(&bn_eval_coef));
   m.def("bn_relu_apply", on_device(&bn_relu_apply));

@@ -951,8 +951,12 @@ extern "C" int rdp_wgrad_first_bn(const void* x, long xbytes, int xpitch, const 
   return splits;
 }
 
-// Slab size needed (elements) for a given configuration.
-// Slab size needed (elements) for a given configuration.
+// Slab size (elements) for the generic kernel's `splits` pixel splits. The halo / row-ring kernels choose
+// their own split count, capped by the slab they are given: the training step shares one slab of the
+// largest generic size, which caps the deep layers' halo wgrads at 4-15 splits (~120 blocks). That is
+// deliberate: sized for a full wave of halo blocks (rdp_conv_wgrad_halo_slab_elems) the wgrads run ~1.8x
+// faster alone but the step got slower -- bs 64 3,120-3,131 vs 3,160-3,181 img/s, bs 4 1,405-1,409 vs
+// 1,591 (same box, 2 rounds): the side-stream wgrads then take every CU from the main stream's convs.
 extern "C" long rdp_conv_wgrad_slab_elems(int N, int H, int W, int Cin, int Cout, int taps, int packed, int splits) {
   const int ncols = packed ? 72 : taps * Cin;
   const int ncols_pad = (ncols + 255) / 256 * 256;
@@ -961,4 +965,18 @@ extern "C" long rdp_conv_wgrad_slab_elems(int N, int H, int W, int Cin, int Cout
   pps = (pps + 63) / 64 * 64;
   const long sp = (M + pps - 1) / pps;
   return sp * Cout * ncols_pad;
+}
+
+// Slab the halo / row-ring wgrad needs for one resident wave of blocks (its own split choice
+// unconstrained); 0 where the dispatch does not pick those kernels. (conv_microbench.py sizes with it.)
+extern "C" long rdp_conv_wgrad_halo_slab_elems(int N, int H, int W, int Cin, int Cout) {
+  const long M = (long)N * H * W;
+  const bool halo = Cin % 64 == 0 && Cout % 64 == 0 && (W % 64 == 0 || (W >= 32 && 64 % W == 0 && (H * W) % 64 == 0));
+  if (!halo) return 0;
+  const int BN = Cout % 128 == 0 ? 128 : 64;
+  const long tiles = (long)(Cin / 64) * (Cout / BN);
+  const long target = BN == 64 ? 512 : 256;
+  long hsp = std::max<long>(1, (target + tiles - 1) / tiles);
+  hsp = std::min<long>(hsp, std::max<long>(1, M / 64));
+  return hsp * Cout * 9L * Cin;
 }

@@ -465,9 +465,6 @@ class UNetExecutor:
         N = self.N
         D = self.m.depth
 
-        def like(x):        N = self.N
-        D = self.m.depth
-
         def like(x):
             return torch.zeros_like(x)
 

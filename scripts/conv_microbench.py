@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--halo-slab", type=int, default=1, help="wgrad: slab for the halo kernel's full split count")
     ap.add_argument("--shapes", default=None, help="comma list of shape indices")
     ap.add_argument("--wgrad-blocks", type=int, default=2048,
                     help="split-K grid target of the generic wgrad kernel (the training step uses 512)")
@@ -54,7 +55,10 @@ def main():
             dy = torch.randn(N, H, H, Co, device=dev).to(torch.bfloat16)
             tiles = ((9 * Cin + 255) // 256) * (Co // 64)
             splits = max(1, min((a.wgrad_blocks + tiles - 1) // tiles, N * H * H // 2048))
-            slab = torch.zeros(C.wgrad_slab_elems(N, H, H, Cin, Co, 9, 0, splits), device=dev)
+            # sized for the halo kernel's own full-occupancy split choice too (the training step gives it
+            # less on purpose: csrc/conv_wgrad.hip rdp_conv_wgrad_slab_elems)
+            slab = torch.zeros(max(C.wgrad_slab_elems(N, H, H, Cin, Co, 9, 0, splits),
+                                   C.wgrad_halo_slab_elems(N, H, H, Cin, Co) if a.halo_slab else 0), device=dev)
             out = torch.zeros(Co * 9 * Cin, device=dev)
 
         def run(v):
