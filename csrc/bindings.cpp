@@ -24,7 +24,7 @@ int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
 int rdp_geo_edges(const void*, const void*, int, int, double, double, double, double, double, int*, double*, double*,
                   double*, int, int*, double*, int, int*, int, double, int, double*, int, int*, const void*, int, int,
-                  int*, double*, int*, int, hipStream_t);
+                  int*, double*, int*, int, void*, hipStream_t);
 int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, const int*, const int*, const float*, int,
                    int, int, void*, hipStream_t);
 int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
@@ -872,8 +872,16 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
                torch::Tensor work_i, torch::Tensor work_d, torch::Tensor pts, torch::Tensor npts, torch::Tensor out,
                torch::Tensor kout, int nbins, double top, int min_points, c10::optional<torch::Tensor> edges,
                c10::optional<torch::Tensor> hdr, c10::optional<torch::Tensor> m256, c10::optional<torch::Tensor> cov,
-               c10::optional<torch::Tensor> sorted, c10::optional<torch::Tensor> gperm) {
+               c10::optional<torch::Tensor> sorted, c10::optional<torch::Tensor> gperm,
+               c10::optional<torch::Tensor> mask_host) {
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == torch::kUInt8 && mask.dim() == 2 && mask.is_contiguous(), "mask");
+  void* mhost = nullptr;
+  if (mask_host && mask_host->defined()) {  // pinned / mapped host memory the kernel writes directly
+    TORCH_CHECK(!mask_host->is_cuda() && mask_host->scalar_type() == torch::kUInt8 && mask_host->is_contiguous() &&
+                    mask_host->numel() == mask.numel(), "mask_host: host u8 tensor of the mask's size");
+    TORCH_CHECK(m256 && m256->defined(), "mask_host needs the serving form (m256)");
+    mhost = mask_host->data_ptr();
+  }
   TORCH_CHECK(depth.is_cuda() && depth.element_size() == 2 && depth.sizes() == mask.sizes() && depth.is_contiguous(),
               "depth u16");
   const int H = mask.size(0), W = mask.size(1);
@@ -918,7 +926,8 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
                               work_d.data_ptr<double>(), work_d.data_ptr<double>() + nblk, pts.data_ptr<double>(), H * W,
                               npts.data_ptr<int>(), out.data_ptr<double>(), out.size(1), kout.data_ptr<int>(), nbins,
                               top, min_points, pack ? edges->data_ptr<double>() : nullptr, pack ? edges->size(0) : 0,
-                              pack ? hdr->data_ptr<int>() : nullptr, mp, mh, mw, covp, sp, gp, secap, unplanned_stream());
+                              pack ? hdr->data_ptr<int>() : nullptr, mp, mh, mw, covp, sp, gp, secap, mhost,
+                              unplanned_stream());
   TORCH_CHECK(r >= 0, "geo_edges: nbins must be in [1, 128]");
 }
 
@@ -1167,7 +1176,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cy"), py::arg("scale"), py::arg("work_i"), py::arg("work_d"), py::arg("pts"), py::arg("npts"),
         py::arg("out"), py::arg("kout"), py::arg("nbins"), py::arg("top"), py::arg("min_points"),
         py::arg("edges") = py::none(), py::arg("hdr") = py::none(), py::arg("m256") = py::none(),
-        py::arg("cov") = py::none(), py::arg("sorted") = py::none(), py::arg("gperm") = py::none());
+        py::arg("cov") = py::none(), py::arg("sorted") = py::none(), py::arg("gperm") = py::none(),
+        py::arg("mask_host") = py::none());
   m.def("geo_nblocks", &geo_nblocks);
   m.def("geo_spline", on_device(&geo_spline), py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),

@@ -59,6 +59,7 @@ struct GeoSrc {
   int mh, mw;
   double sy, sx;
   uint8_t* mask_out;
+  uint8_t* mask_host;  // optional second copy of mask_out in host memory (the serving read-back, zero-copy)
   int* cov;  // [nblk] coverage counts (serving form)
   int* zero;  // [nzero] ints zeroed by block 0
   int nzero;
@@ -86,7 +87,10 @@ __global__ __launch_bounds__(GEO_THREADS) void geo_count_kernel(const uint8_t* _
   double lo = 1e300, hi = -1e300;
   for (int p = r0 * W + threadIdx.x; p < r1 * W; p += GEO_THREADS) {
     const uint8_t mv = src_mask(gs, mask, p, W);
-    if (gs.m256) gs.mask_out[p] = mv;
+    if (gs.m256) {
+      gs.mask_out[p] = mv;
+      if (gs.mask_host) gs.mask_host[p] = mv;
+    }
     cov += mv != 0;
     if (mv > 0 && depth[p] > 0) {
       ++cnt;
@@ -556,7 +560,7 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
                   double scale, int* counts, double* xmin, double* xmax, double* pts, int cap, int* npts,
                   double* out, int kcap, int* kout, int nbins, double top, int min_points, double* edges,
                   int ecap, int* hdr, const void* m256, int mh, int mw, int* cov, double* sorted, int* gperm,
-                  int secap, hipStream_t s) {
+                  int secap, void* mask_host, hipStream_t s) {
   if (nbins > 128 || nbins < 1) return -1;
   const int nblk = rdp_geo_nblocks(H);
   GeoCam cam{fx, fy, cx, cy, scale};
@@ -572,6 +576,7 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
   gs.sy = m256 ? 1.0 / ((double)H / (double)mh) : 0.0;  // as cv::resize INTER_NEAREST (serve_kernels.hip)
   gs.sx = m256 ? 1.0 / ((double)W / (double)mw) : 0.0;
   gs.mask_out = (uint8_t*)mask;
+  gs.mask_host = (uint8_t*)mask_host;
   gs.cov = cov;
   gs.zero = gb.cnt;  // cnt + cursor (256 ints), consumed two kernels later
   gs.nzero = 256;

@@ -58,10 +58,17 @@ class FrameRunner {
     DeviceScope g(dev_);
     hip_check(hipEventCreate(&ev0_), "hipEventCreate");
     hip_check(hipEventCreate(&ev1_), "hipEventCreate");
+    // the depth frame's H2D runs on its own stream, under the network graph; the geometry graph waits
+    // for it (a GPU-side dependency only: no system-scope fence)
+    hip_check(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipEventCreateWithFlags(&evd_, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate");
   }
   ~FrameRunner() {
     (void)hipEventDestroy(ev0_);
     (void)hipEventDestroy(ev1_);
+    (void)hipEventDestroy(evd_);
+    (void)hipStreamDestroy(cs_);
+    for (void* p : host_) (void)hipHostFree(p);
   }
   // graph execs, owned by the pipeline's torch CUDAGraphs (kept alive there): slots 0..2 = the network
   // graph of colour source 0 BGR / 1 RGB / 2 JPEG coefficients, slot 3 = the geometry graph
@@ -69,7 +76,21 @@ class FrameRunner {
     if (slot < 0 || slot > 3) throw std::invalid_argument("slot");
     exec_[slot] = (hipGraphExec_t)exec;
   }
-  // pinned host staging / device buffers of the pipeline (sizes in bytes)
+  void depth_stream(bool on) { depth_stream_ = on; }
+
+  // fine-grained (coherent) host memory that kernels write directly -- the frame's mask and result
+  // vector, so no read-back copies follow the geometry graph (freed with the runner)
+  uintptr_t alloc_host(size_t bytes) {
+    DeviceScope g(dev_);
+    void* p = nullptr;
+    hip_check(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
+    std::memset(p, 0, bytes);
+    host_.push_back(p);
+    return (uintptr_t)p;
+  }
+
+  // pinned host staging / device buffers of the pipeline (sizes in bytes; mask / result sizes 0: the
+  // geometry kernels write them to host memory themselves)
   void set_buffers(uintptr_t d_color, uintptr_t h_color, size_t color_bytes, uintptr_t d_depth, uintptr_t h_depth,
                    size_t depth_bytes, uintptr_t d_meta, size_t meta_bytes, uintptr_t d_coef, size_t coef_cap,
                    uintptr_t d_mask, uintptr_t h_mask, size_t mask_bytes, uintptr_t d_res, uintptr_t h_res,
@@ -118,10 +139,16 @@ class FrameRunner {
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
     std::memcpy(h_depth_, dp, depth_bytes_);
-    hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, s_), "H2D depth");
+    if (depth_stream_) {
+      hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, cs_), "H2D depth");
+      hip_check(hipEventRecord(evd_, cs_), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(s_, evd_, 0), "hipStreamWaitEvent");
+    } else {
+      hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, s_), "H2D depth");
+    }
     hip_check(hipGraphLaunch(exec_[3], s_), "hipGraphLaunch");
-    hip_check(hipMemcpyAsync(h_mask_, d_mask_, mask_bytes_, hipMemcpyDeviceToHost, s_), "D2H mask");
-    hip_check(hipMemcpyAsync(h_res_, d_res_, res_bytes_, hipMemcpyDeviceToHost, s_), "D2H result");
+    if (mask_bytes_) hip_check(hipMemcpyAsync(h_mask_, d_mask_, mask_bytes_, hipMemcpyDeviceToHost, s_), "D2H mask");
+    if (res_bytes_) hip_check(hipMemcpyAsync(h_res_, d_res_, res_bytes_, hipMemcpyDeviceToHost, s_), "D2H result");
     hip_check(hipEventRecord(ev1_, s_), "hipEventRecord");
     recorded_ = true;
   }
@@ -130,6 +157,7 @@ class FrameRunner {
   void abort() {
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
+    hip_check(hipStreamSynchronize(cs_), "hipStreamSynchronize");
     hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
   }
 
@@ -160,9 +188,12 @@ class FrameRunner {
   }
 
   bool recorded_ = false;
+  bool depth_stream_ = true;
   int dev_;
   hipStream_t s_;
-  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr, evd_ = nullptr;
+  hipStream_t cs_ = nullptr;
+  std::vector<void*> host_;
   hipGraphExec_t exec_[4] = {nullptr, nullptr, nullptr, nullptr};
   void *d_color_ = nullptr, *h_color_ = nullptr, *d_depth_ = nullptr, *h_depth_ = nullptr;
   void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
@@ -257,6 +288,8 @@ void register_serve_runtime(py::module_& m) {
       .def(py::init<int, uintptr_t>(), py::arg("device"), py::arg("stream"))
       .def("set_graph", &FrameRunner::set_graph)
       .def("set_buffers", &FrameRunner::set_buffers)
+      .def("alloc_host", &FrameRunner::alloc_host)
+      .def("set_depth_stream", [](FrameRunner& r, bool on) { r.depth_stream(on); })
       .def("submit_array", &FrameRunner::submit_array)
       .def("submit_jpeg", &FrameRunner::submit_jpeg)
       .def("submit_depth", &FrameRunner::submit_depth)

@@ -152,21 +152,26 @@ class GeometryEngine:
         self._serving_form = False
 
     def launch_frame(self, m256_dev: torch.Tensor, mask_out: torch.Tensor, depth_dev: torch.Tensor, K: np.ndarray,
-                     scale: float):
+                     scale: float, mask_host: Optional[torch.Tensor] = None):
         """Serving form: ``mask_out`` (H x W) is produced here by nearest-upsampling the model-resolution
         mask ``m256_dev`` (no separate upsample kernel), with the coverage count per row block, and no
-        packed edge list; follow with ``launch_spline()`` (its result then carries the coverage)."""
+        packed edge list; follow with ``launch_spline()`` (its result then carries the coverage).
+        ``mask_host``: a host-memory copy of the mask written by the same kernel (no read-back copy)."""
         c = self.cfg
         self.C.geo_edges(mask_out, depth_dev, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]),
                          float(scale), self.work_i, self.work_d, self.pts, self.npts, self.out, self.kout, c.num_bins,
-                         c.top_k_percent, c.min_points, None, None, m256_dev, self.cov, self.sorted, self.gperm)
+                         c.top_k_percent, c.min_points, None, None, m256_dev, self.cov, self.sorted, self.gperm,
+                         mask_host)
         self._serving_form = True  # the select kernel also wrote the x-sorted edge points
 
-    def launch_spline(self):
-        """Enqueue the on-device spline stage after ``launch`` (no host sync; graph-capturable)."""
+    def launch_spline(self, res_out: Optional[torch.Tensor] = None):
+        """Enqueue the on-device spline stage after ``launch`` (no host sync; graph-capturable).
+        ``res_out``: where the result vector goes instead of ``self.res`` (e.g. host memory the kernel
+        writes directly: nothing on the device reads it back)."""
         c = self.cfg
         serving = getattr(self, "_serving_form", False)
-        self.C.geo_spline(self.out, self.kout, self.npts, self.sorted, self.gperm, self.u, self.res, c.smoothing,
+        self.C.geo_spline(self.out, self.kout, self.npts, self.sorted, self.gperm, self.u,
+                          self.res if res_out is None else res_out, c.smoothing,
                           c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points,
                           self.cov if serving else None, presorted=serving)
 

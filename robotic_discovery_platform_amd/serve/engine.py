@@ -85,6 +85,14 @@ SRC_BGR, SRC_RGB, SRC_JPEG = 0, 1, 2  # colour sources of a network graph
 GEO, GEO_SLOT = "geo", 3  # the geometry graph (FrameRunner slot 3)
 
 
+def _host_tensor(runner, shape, dtype) -> torch.Tensor:
+    """A CPU tensor over fine-grained host memory owned by ``runner`` (kernels write it directly)."""
+    import ctypes
+    n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    buf = (ctypes.c_uint8 * n).from_address(runner.alloc_host(n))
+    return torch.from_numpy(np.frombuffer(buf, dtype=dtype).reshape(shape))
+
+
 def _stage(dst: torch.Tensor, src: np.ndarray) -> None:
     """Copy a host frame into its pinned staging tensor (on every frame's latency path). A numpy
     assignment: torch's OpenMP-threaded copy was 4x faster alone but its spinning workers cost engine
@@ -159,15 +167,23 @@ class FramePipeline:
         # native per-frame host path (csrc/serve_runtime.cpp): staging copies, H2D, graph launch, D2H and
         # events in one call without the GIL; the Python path below stays for eager pipelines
         self.runner = None
+        self.zero_copy = False  # the geometry kernels write the mask / result straight to host memory
         if graph and hasattr(self.C, "FrameRunner"):
             r = self.C.FrameRunner(dev.index, self.stream.cuda_stream)
+            # mask + result vector in fine-grained host memory the kernels write: no read-back copies
+            # after the geometry graph (the copy's launch after a graph cost ~30 us of idle GPU)
+            self.h_mask = _host_tensor(r, (H, W), np.uint8)
+            self.h_res = _host_tensor(r, (self.geo.res.numel(),), np.float64)
+            self.zero_copy = True
             nb = lambda t: t.numel() * t.element_size()  # noqa: E731
             r.set_buffers(self.d_color.data_ptr(), self.h_color.data_ptr(), nb(self.d_color),
                           self.d_depth.data_ptr(), self.h_depth.data_ptr(), nb(self.d_depth),
                           self.d_meta.data_ptr(), nb(self.d_meta), self.d_coef.data_ptr(), nb(self.d_coef),
-                          self.mask.data_ptr(), self.h_mask.data_ptr(), nb(self.mask),
-                          self.geo.res.data_ptr(), self.h_res.data_ptr(), nb(self.h_res))
+                          self.mask.data_ptr(), self.h_mask.data_ptr(), 0,
+                          self.geo.res.data_ptr(), self.h_res.data_ptr(), 0)
             self.runner = r
+            if os.environ.get("RDP_AB_DSTREAM") is not None:  # TEMP A/B
+                r.set_depth_stream(os.environ["RDP_AB_DSTREAM"] == "1")
         # the graphs for the sources this pipeline will be fed (the gRPC server: JPEG coefficients, or
         # RGB arrays for streams the native decoder does not take) are captured here, at build time,
         # never on a live request
@@ -199,8 +215,10 @@ class FramePipeline:
                               self.thr_logit, self.m256))
 
     def _geo_program(self):
-        self.geo.launch_frame(self.m256.view(self.S, self.S), self.mask, self.d_depth, self.K, self.scale)
-        self.geo.launch_spline()
+        zc = self.zero_copy
+        self.geo.launch_frame(self.m256.view(self.S, self.S), self.mask, self.d_depth, self.K, self.scale,
+                              mask_host=self.h_mask if zc else None)
+        self.geo.launch_spline(res_out=self.h_res if zc else None)
 
     def refresh_weights(self):
         """Recompute the BN-fold coefficients from the current weights / running stats (after a
@@ -312,8 +330,9 @@ class FramePipeline:
                         self.graphs[GEO].replay()
                     else:
                         self._geo_program()
-                    self.h_mask.copy_(self.mask, non_blocking=True)
-                    self.h_res.copy_(self.geo.res, non_blocking=True)
+                    if not self.zero_copy:
+                        self.h_mask.copy_(self.mask, non_blocking=True)
+                        self.h_res.copy_(self.geo.res, non_blocking=True)
                     self.ev1.record(s)
         self._pending_src = None
 
