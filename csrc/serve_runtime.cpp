@@ -76,6 +76,9 @@ class FrameRunner {
     if (slot < 0 || slot > 3) throw std::invalid_argument("slot");
     exec_[slot] = (hipGraphExec_t)exec;
   }
+  // Measured (same box, 2 rounds): the copy stream vs the depth H2D in order on the frame stream --
+  // engine GPU p50 0.515-0.524 vs 0.536 ms, pipelined 3,025-3,105 vs 2,837-2,926 FPS, e2e 4 streams in
+  // one process 1,886-2,582 vs 1,506-1,562 FPS, 2 processes x 2 streams 3,353-3,420 vs 3,177-3,433.
   void depth_stream(bool on) { depth_stream_ = on; }
 
   // fine-grained (coherent) host memory that kernels write directly -- the frame's mask and result
@@ -289,7 +292,8 @@ void register_serve_runtime(py::module_& m) {
       .def("set_graph", &FrameRunner::set_graph)
       .def("set_buffers", &FrameRunner::set_buffers)
       .def("alloc_host", &FrameRunner::alloc_host)
-      .def("set_depth_stream", [](FrameRunner& r, bool on) { r.depth_stream(on); })
+      .def("set_depth_stream", [](FrameRunner& r, bool on) { r.depth_stream(on); },
+           "depth H2D on the copy stream (default) or in order on the frame stream")
       .def("submit_array", &FrameRunner::submit_array)
       .def("submit_jpeg", &FrameRunner::submit_jpeg)
       .def("submit_depth", &FrameRunner::submit_depth)

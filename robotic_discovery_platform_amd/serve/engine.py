@@ -182,8 +182,6 @@ class FramePipeline:
                           self.mask.data_ptr(), self.h_mask.data_ptr(), 0,
                           self.geo.res.data_ptr(), self.h_res.data_ptr(), 0)
             self.runner = r
-            if os.environ.get("RDP_AB_DSTREAM") is not None:  # TEMP A/B
-                r.set_depth_stream(os.environ["RDP_AB_DSTREAM"] == "1")
         # the graphs for the sources this pipeline will be fed (the gRPC server: JPEG coefficients, or
         # RGB arrays for streams the native decoder does not take) are captured here, at build time,
         # never on a live request
