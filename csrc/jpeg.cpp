@@ -176,6 +176,9 @@ int parse(const uint8_t* d, long n, Jpeg& j) {
         j.width = be16(s + 3);
         j.ncomp = s[5];
         if (j.width <= 0 || j.height <= 0) return -2;  // DNL-defined height: unsupported
+        // untrusted header: PIL's decompression-bomb bound (Image.MAX_IMAGE_PIXELS) before anything is
+        // allocated from it -- the coefficient planes of a forged 65535 x 65535 header would be 25 GB
+        if ((long)j.width * j.height > 89478485L) return -1;
         if (j.ncomp != 1 && j.ncomp != 3) return -2;
         if (sl < 6 + 3 * j.ncomp) return -1;
         for (int c = 0; c < j.ncomp; ++c) {

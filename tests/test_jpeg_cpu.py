@@ -111,3 +111,11 @@ def test_cpu_pipeline_takes_coefficients():
     a = p.collect()
     b = p.process(decode_image(data, True, "BGR"), depth)
     np.testing.assert_array_equal(a.mask, b.mask)
+
+
+def test_forged_huge_header_is_refused():
+    """An SOF claiming 65535 x 65535 (a 25 GB coefficient allocation) is rejected before allocating."""
+    data = bytearray(_jpeg(_frame(16, 16), quality=90))
+    i = data.index(b"\xff\xc0")
+    data[i + 5:i + 9] = b"\xff\xff\xff\xff"  # height, width
+    assert decode_coefs(bytes(data)) is None
