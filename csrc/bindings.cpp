@@ -18,7 +18,7 @@ int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, con
                    float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
-                     hipStream_t);
+                     const float*, const float*, hipStream_t);
 long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
@@ -29,7 +29,7 @@ int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, 
                    int, int, void*, hipStream_t);
 int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
-                   float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+                   float*, int, int, int, int, int, int, int, int, int, int, const float*, const float*, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
 long rdp_conv_wgrad_halo_slab_elems(int, int, int, int, int);
 int rdp_wgrad_first_bn(const void*, long, int, const void*, long, int, const void*, long, int, const float*, const float*,
@@ -403,9 +403,19 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
 }
 
 
+// in_coef (optional, fp32 [4C] of x1's producer BN): x1 is that layer's pre-BN output and the kernel
+// forms relu(bn(x1)) itself (the row-ring kernel, 64 -> 64 channels; other shapes raise)
 int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor dy, int taps, int packed, int cin_real,
-               torch::Tensor slab, torch::Tensor out, int accumulate, int splits, int variant) {
+               torch::Tensor slab, torch::Tensor out, int accumulate, int splits, int variant,
+               c10::optional<torch::Tensor> in_coef) {
   Act a1 = act(x1, "x1"), a2;
+  const float *isc = nullptr, *ish = nullptr;
+  if (in_coef && in_coef->defined()) {
+    check_f32(*in_coef, "in_coef");
+    TORCH_CHECK(in_coef->numel() >= 4l * a1.C, "in_coef: [4 C] f32");
+    isc = in_coef->data_ptr<float>() + 2 * a1.C;
+    ish = in_coef->data_ptr<float>() + 3 * a1.C;
+  }
   if (x2) a2 = act(*x2, "x2");
   Act d = act(dy, "dy");
   TORCH_CHECK(d.N == a1.N && d.H == a1.H && d.W == a1.W, "dy spatial mismatch");
@@ -431,7 +441,7 @@ int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor 
     const long sln = slab.numel();
     float* const outp = out.data_ptr<float>();
     r = RDP_PLAN(rdp_conv_wgrad(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, pdy, bdy, d.pitch, slp, sln, outp, acc, nn,
-                                a1.H, a1.W, d.C, taps, packed, cin_real, splits, variant, st));
+                                a1.H, a1.W, d.C, taps, packed, cin_real, splits, variant, isc, ish, st));
     TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
   }
   return r;
@@ -516,7 +526,29 @@ int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch:
   if (chunk_images(per_img, a.N) < a.N) return -1;
   return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                           o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
-                          0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), st));
+                          0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), nullptr, nullptr, st));
+}
+
+// Training forward of a 3x3 64 -> 64 conv whose input is the producer layer's PRE-BN output x_pre: the
+// row-ring kernel applies the producer's BN + ReLU (in_coef: its [mean|invstd|scale|shift]) to the
+// staged rows itself, so the activation is never written (conv_ring.hip BNIN). Writes y and this
+// conv's BN statistic rows; returns the rows, or -1 when the ring kernel does not apply (nothing
+// launched: the caller runs bn_relu_apply + conv_fwd).
+int conv_fwd_bnin(torch::Tensor x_pre, torch::Tensor w, torch::Tensor y, torch::Tensor stats, torch::Tensor in_coef) {
+  Act a = act(x_pre, "x_pre"), o = act(y, "y");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && w.size(0) == o.C, "conv_fwd_bnin: shape mismatch");
+  check_f32(stats, "stats");
+  check_f32(in_coef, "in_coef");
+  TORCH_CHECK(in_coef.numel() >= 4l * a.C, "in_coef: [4 C] f32");
+  // (the ring grid writes <= 256 blocks x 4 pixel-group rows of 2 * C)
+  if (a.C != 64 || o.C != 64 || a.W % 64 || a.H % 2 || stats.numel() < 1024l * 2 * o.C) return -1;
+  const long per_img = std::max((long)a.H * a.W * a.pitch, (long)o.H * o.W * o.pitch) * 2;
+  if (chunk_images(per_img, a.N) < a.N) return -1;
+  const float* c = in_coef.data_ptr<float>();
+  return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
+                                   o.pitch, nullptr, 0, 0, o.C, o.C, stats.data_ptr<float>(), a.N, a.H, a.W, nullptr,
+                                   nullptr, 0, 256, nullptr, 0, nullptr, c + 2 * a.C, c + 3 * a.C, st));
 }
 
 int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, int relu, torch::Tensor partial) {
@@ -1130,7 +1162,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return rdp_conv_ws_elems(N, H, W, C1, C2, Cout, taps, packed, bm_pref);
   });
   m.def("conv_stats_rows", &conv_stats_rows);
-  m.def("conv_wgrad", on_device(&conv_wgrad));
+  m.def("conv_wgrad", on_device(&conv_wgrad), py::arg("x1"), py::arg("x2"), py::arg("dy"), py::arg("taps"),
+        py::arg("packed"), py::arg("cin_real"), py::arg("slab"), py::arg("out"), py::arg("accumulate"),
+        py::arg("splits"), py::arg("variant"), py::arg("in_coef") = py::none());
+  m.def("conv_fwd_bnin", on_device(&conv_fwd_bnin));
   m.def("wgrad_first_bn", on_device(&wgrad_first_bn));
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
   m.def("wgrad_halo_slab_elems", &rdp_conv_wgrad_halo_slab_elems);

@@ -54,6 +54,10 @@ struct RingArgs {
   // eval MaxPool2d(2) of the output (POOL variant): pool [N][H/2][W/2][64] with pixel pitch ppitch
   u16* pool;
   int ppitch;
+  // BNIN: the input is the previous layer's pre-BN output; its BN + ReLU (scale, shift per input
+  // channel) is applied to the staged rows in LDS
+  const float* iscale;
+  const float* ishift;
   int H, W, WS;  // WS = W / 64 segments per image row
   int nrows;     // N * WS * H: input rows in column order (R = column * H + h)
   int npairs;    // nrows / 2: steps (two output rows each)
@@ -75,7 +79,12 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 // one row of 2x2 windows (rows 2P, 2P + 1 with H even): horizontal pairs are neighbouring lanes (DPP
 // swap), vertical pairs are the orow = 0 / 1 waves of a pixel group, exchanged through LDS (step-parity
 // double buffer) and finished by the orow = 0 waves after the next barrier.
-template <int COUT, bool BNR = false, bool HEAD = false, bool POOL = false>
+// BNIN (training forward, COUT = 64): the input rows are the producer layer's pre-BN output y and
+// a = relu(y * scale + shift), rounded to bf16 exactly as bn_relu_apply_kernel does, is formed in LDS
+// once per staged element -- by the wave whose DMA staged it, right after its own vmcnt wait, so the
+// step's existing barrier publishes it -- instead of a separate apply pass writing and re-reading a
+// (padding chunks stay zero: the conv pads the post-ReLU activation).
+template <int COUT, bool BNR = false, bool HEAD = false, bool POOL = false, bool BNIN = false>
 __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
   constexpr int PXW = 128 / NPG, NI = PXW / 16;  // pixels per wave (one output row half or whole)
@@ -186,6 +195,46 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   if constexpr (BNR) {
     for (int c = threadIdx.x; c < 4 * COUT; c += 512) efold[c] = a.bncoef[c];
   }
+  if constexpr (BNIN) {  // input BN [scale | shift] (64 input channels), visible before the first transform
+    for (int c = threadIdx.x; c < 64; c += 512) { efold[c] = a.iscale[c]; efold[64 + c] = a.ishift[c]; }
+    __syncthreads();
+  }
+  // BNIN: this lane's chunk of piece pj of input row R (staged by this wave): y -> relu(y*scale+shift)
+  auto bn_chunk = [&](int R, int pj) {
+    int m0, w0;
+    row_base(R, m0, w0);
+    const int j = pj * 8 + (lane >> 3);
+    if (!((m0 >= 0) & (j < 66) & inb(w0 - 1 + j, a.W))) return;  // padding: stays zero
+    uint4* p = (uint4*)(ring + ((R + NX) % NX) * XREG + pj * 1024 + lane * 16);
+    const uint4 v = *p;
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    const float* sc = efold + 8 * gch;
+    const float* sh = efold + 64 + 8 * gch;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = fmaxf(fmaf(__uint_as_float(wv[k] << 16), sc[2 * k], sh[2 * k]), 0.f);
+      const float hi = fmaxf(fmaf(__uint_as_float(wv[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]), 0.f);
+      o[k] = pack2bf(lo, hi);
+    }
+    *p = make_uint4(o[0], o[1], o[2], o[3]);
+  };
+  auto bn_stage = [&](int P) {  // the pieces this wave staged for stage P (see issue)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int p = wave + 8 * t;
+      if (p >= PIECES) continue;
+      const int rr = p >= 9 ? 1 : 0;
+      bn_chunk(2 * P + 1 + rr, p - 9 * rr);
+    }
+  };
+  auto bn_row = [&](int R) {  // the prologue pieces this wave staged for row R (see issue_row)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int pj = wave + 8 * t;
+      if (pj < 9) bn_chunk(R, pj);
+    }
+  };
 
   // slot NX stays zero: the padding row read by a column's first / last output row, so the tap loop
   // has no branches and the compiler can overlap one tap's fragment reads with the previous MFMAs
@@ -266,6 +315,14 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
       if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NS) : "memory");
       else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    if constexpr (BNIN) {  // this wave's DMAs of stage P (and at the start the prologue rows) have landed
+      if (ks == 0) {
+        bn_row(2 * P0 - 1);
+        bn_row(2 * P0);
+      }
+      bn_stage(P);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     raw_barrier();
     if constexpr (HEAD) head_finish((ks - 1) & 1);
@@ -486,13 +543,13 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
                                 void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                                 int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                                 int erelu, int max_blocks, const void* bn_y_, int bn_ypitch, const float* bn_coef,
-                                hipStream_t s);
+                                const float* iscale, const float* ishift, hipStream_t s);
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
                              void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                              int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                              int erelu, int max_blocks, hipStream_t s) {
   return rdp_conv_ring_ex(x, xbytes, C, pitch, w, wbytes, ldw, y, ybytes, ypitch, y2, ybytes2, ypitch2, Cy1, Cout,
-                          stats, N, H, W, escale, eshift, erelu, max_blocks, nullptr, 0, nullptr, s);
+                          stats, N, H, W, escale, eshift, erelu, max_blocks, nullptr, 0, nullptr, nullptr, nullptr, s);
 }
 
 // Eval conv (64 -> 64, BN folded + ReLU) fused with the serving 1x1 head: writes only the u8 mask
@@ -510,6 +567,7 @@ extern "C" int rdp_conv_ring_head(const void* x, long xbytes, int C, int pitch, 
   a.bny = nullptr; a.bnypitch = 0; a.bncoef = nullptr;
   a.hw = hw; a.hb = hb; a.hthr = hthr; a.hmask = (uint8_t*)mask;
   a.pool = nullptr; a.ppitch = 0;
+  a.iscale = nullptr; a.ishift = nullptr;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -539,6 +597,7 @@ extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, 
   a.bny = nullptr; a.bnypitch = 0; a.bncoef = nullptr;
   a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
   a.pool = (u16*)pool; a.ppitch = ppitch;
+  a.iscale = nullptr; a.ishift = nullptr;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -558,9 +617,10 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
                                 void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                                 int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                                 int erelu, int max_blocks, const void* bn_y_, int bn_ypitch, const float* bn_coef,
-                                hipStream_t s) {
+                                const float* iscale, const float* ishift, hipStream_t s) {
   const u16* bn_y = (const u16*)bn_y_;
   if (bn_y && (!stats || escale || y2 || bn_ypitch % 4 || Cout != 64)) return -1;
+  if (iscale && (!ishift || bn_y || escale || y2 || Cout != 64)) return -1;
   if (C != 64 || (Cout != 64 && Cout != 128) || W % 64 || H % 2 || ldw < 576 || Cy1 % 32) return -1;
   if (y2 == nullptr && Cy1 != Cout) return -1;
   if (xbytes >= (1l << 31) || ybytes >= (1l << 31) || ybytes2 >= (1l << 31) || wbytes >= (1l << 31)) return -1;
@@ -574,6 +634,7 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   a.bny = bn_y; a.bnypitch = bn_ypitch; a.bncoef = bn_coef;
   a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
   a.pool = nullptr; a.ppitch = 0;
+  a.iscale = iscale; a.ishift = ishift;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -588,6 +649,10 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   }
   if (bn_y) {
     hipLaunchKernelGGL((conv_ring_kernel<64, true>), dim3(grid), dim3(512), 0, s, a);
+    return grid * 4;
+  }
+  if (iscale) {
+    hipLaunchKernelGGL((conv_ring_kernel<64, false, false, false, true>), dim3(grid), dim3(512), 0, s, a);
     return grid * 4;
   }
   hipLaunchKernelGGL((conv_ring_kernel<64>), dim3(grid), dim3(512), 0, s, a);

@@ -325,6 +325,11 @@ class _Layer:
     dx2: Optional[torch.Tensor] = None
     splits: int = 1
     bwd_rows: int = 0  # BN-backward partial rows already produced by a fused producer of da
+    # training: this conv reads its producer's PRE-BN output and applies that BN + ReLU itself (the
+    # row-ring kernels, 64 -> 64 channels at W % 64 == 0): bnin = the producer layer, whose `a` is never
+    # written; consumer_bnin marks the producer (no bn_relu_apply pass)
+    bnin: Optional["_Layer"] = None
+    consumer_bnin: bool = False
 
 
 def _stream_wait(waiter: "torch.cuda.Stream", waitee: "torch.cuda.Stream"):
@@ -409,6 +414,17 @@ class UNetExecutor:
             self.up_layers.append((la, lb))
             low = lb.a
         self.final = low
+        # BN + ReLU of the first layer of the full-resolution DoubleConvs (inc, up4) applied by the
+        # consumer conv instead of a separate pass (training; the forward and the weight-gradient
+        # row-ring kernels stage the pre-BN rows and form the activation in LDS)
+        if training and dev.type == "cuda" and os.environ.get("RDP_AB_BNIN", "1") == "1":  # TEMP A/B
+            pairs = [self.down_layers[0]] + ([self.up_layers[-1]] if self.up_layers else [])
+            for la, lb in pairs:
+                n, h, w, c = la.y.shape
+                if (lb.x1 is la.a and lb.x2 is None and c == 64 and lb.spec.cout == 64 and lb.spec.taps == 9
+                        and not lb.spec.packed and w % 64 == 0 and h % 2 == 0 and n * h * w * c * 2 < (1 << 31)):
+                    lb.bnin = la
+                    la.consumer_bnin = True
         M = N * H * W
         self.M = M
         self.logits = torch.zeros(M, dtype=torch.float32, device=dev)
@@ -570,7 +586,11 @@ class UNetExecutor:
                 return True
             C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool)
             return pool is not None
-        rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
+        if L.bnin is not None:  # the producer's BN + ReLU applied by this conv (row-ring BNIN)
+            rows = C.conv_fwd_bnin(L.bnin.y, w, L.y, self.stats, L.bnin.coef)
+            assert rows > 0, "conv_fwd_bnin: ring kernel not applicable"
+        else:
+            rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
         g = m.store.view(sp.bn + ".weight")
         b = m.store.view(sp.bn + ".bias")
         if self.training:
@@ -582,7 +602,7 @@ class UNetExecutor:
         if pool is not None:
             C.bn_relu_apply_pool(L.y, L.a, pool, L.coef)
             return True
-        if apply:
+        if apply and not L.consumer_bnin:
             C.bn_relu_apply(L.y, L.a, L.coef, 1)
         return False
 
@@ -799,6 +819,10 @@ class UNetExecutor:
         # all wgrads share the slab, so they stay serialized on the one side stream
         if self.slab_main is not None and L is self.down_layers[0][0]:
             C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab_main, gw, 0, L.splits, 0)
+        elif L.bnin is not None:  # x = relu(bn(producer y)), formed by the row-ring wgrad itself
+            src = L.bnin
+            self._on_wgrad_stream(lambda slab: C.conv_wgrad(src.y, None, L.dy, sp.taps, 0, sp.cin_real, slab, gw, 0,
+                                                            L.splits, 0, src.coef))
         else:
             self._on_wgrad_stream(lambda slab: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real,
                                                             slab, gw, 0, L.splits, 0))

@@ -387,6 +387,54 @@ def test_conv_dgrad_bnred(C, N, H, W, Cout):
     assert relerr(p[1], (g * (y.float() - mean) * inv).sum((0, 1, 2))) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 32, 128), (3, 16, 64)])
+def test_conv_bnin_fwd_and_wgrad(C, N, H, W):
+    """Row-ring forward / weight gradient that apply the producer's BN + ReLU to the staged pre-BN rows
+    (BNIN): bitwise equal to bn_relu_apply followed by the same ring kernels."""
+    torch.manual_seed(23)
+    dev = "cuda"
+    y_pre = bf(torch.randn(N, H, W, 64, device=dev) * 1.5 + 0.2)
+    mean = y_pre.float().mean((0, 1, 2))
+    inv = 1.0 / (y_pre.float().var((0, 1, 2), unbiased=False) + 1e-5).sqrt()
+    scale = (torch.rand(64, device=dev) + 0.5) * inv
+    shift = torch.randn(64, device=dev) * 0.3 - mean * scale
+    coef = torch.cat([mean, inv, scale, shift]).contiguous()
+    a = torch.empty_like(y_pre)
+    C.bn_relu_apply(y_pre, a, coef, 1)
+    w = bf(torch.randn(64, 64, 3, 3, device=dev) * 0.05)
+    wk = ohwi(w).contiguous()
+    y_ref, y_out = (torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev) for _ in range(2))
+    st_ref, st = (torch.zeros(1024 * 2 * 64, device=dev) for _ in range(2))
+    rows_ref = C.conv_fwd(a, None, wk, 9, 0, y_ref, None, st_ref, 6, None, 0)  # ring kernel on a
+    rows = C.conv_fwd_bnin(y_pre, wk, y_out, st, coef)
+    torch.cuda.synchronize()
+    assert rows == rows_ref > 0
+    assert torch.equal(y_out, y_ref) and torch.equal(st[: rows * 128], st_ref[: rows * 128])
+    assert relerr(nchw(y_out), F.conv2d(nchw(a).float(), w.float(), padding=1)) < 1e-2
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 64, 64, 9, 0, 64), device=dev)
+    g_ref, g = (torch.full((64 * 9 * 64,), 7.0, device=dev) for _ in range(2))
+    C.conv_wgrad(a, None, dy, 9, 0, 64, slab, g_ref, 0, 64, 0)
+    C.conv_wgrad(y_pre, None, dy, 9, 0, 64, slab, g, 0, 64, 0, coef)
+    torch.cuda.synchronize()
+    assert torch.equal(g, g_ref)
+    wt = torch.zeros(64, 64, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(nchw(a).float(), wt, padding=1).backward(nchw(dy).float())
+    assert relerr(g, wt.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
+
+
+def test_conv_bnin_not_applicable(C):
+    dev = "cuda"
+    y_pre = bf(torch.randn(1, 16, 48, 64, device=dev))  # W % 64 != 0: no ring kernel
+    coef = torch.ones(256, device=dev)
+    y = torch.empty_like(y_pre)
+    wk = bf(torch.randn(64, 576, device=dev))
+    assert C.conv_fwd_bnin(y_pre, wk, y, torch.zeros(1024 * 128, device=dev), coef) == -1
+    slab = torch.zeros(C.wgrad_slab_elems(1, 16, 48, 64, 64, 9, 0, 8), device=dev)
+    with pytest.raises(RuntimeError):
+        C.conv_wgrad(y_pre, None, y_pre, 9, 0, 64, slab, torch.zeros(64 * 576, device=dev), 0, 8, 0, coef)
+
+
 def test_maxpool_fwd_bwd_with_skip(C):
     torch.manual_seed(6)
     dev = "cuda"
