@@ -404,7 +404,8 @@ def test_conv_bnin_fwd_and_wgrad(C, N, H, W):
     w = bf(torch.randn(64, 64, 3, 3, device=dev) * 0.05)
     wk = ohwi(w).contiguous()
     y_ref, y_out = (torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev) for _ in range(2))
-    st_ref, st = (torch.zeros(1024 * 2 * 64, device=dev) for _ in range(2))
+    rows_cap = max(1024, C.conv_stats_rows(N * H * W, 64, 0))
+    st_ref, st = (torch.zeros(rows_cap * 2 * 64, device=dev) for _ in range(2))
     rows_ref = C.conv_fwd(a, None, wk, 9, 0, y_ref, None, st_ref, 6, None, 0)  # ring kernel on a
     rows = C.conv_fwd_bnin(y_pre, wk, y_out, st, coef)
     torch.cuda.synchronize()
