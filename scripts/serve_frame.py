@@ -4,23 +4,26 @@
 Frames are delimited by ``preprocess_kernel`` (one per frame). Prints, per kernel position of the
 frame, the start offset and duration of the second-to-last complete frame plus the median duration
 over the last (up to) 50 frames with the same kernel sequence, and the summed kernel time.
-usage: serve_frame.py <kernel_trace.csv>
+usage: serve_frame.py <kernel_trace.csv> [first_frame]
+first_frame: take the reference frame and the median window from frames [first, first + 50) instead of
+the last 50 (e.g. the sequential engine phase of bench_serve, before the pipelined frames overlap).
 """
 import csv
 import statistics
 import sys
 
 
-def main(path):
+def main(path, first=None):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("preprocess_kernel")]
     if len(idx) < 3:
         print("fewer than 3 frames in the trace")
         return
     frames = [rows[a:b] for a, b in zip(idx[:-1], idx[1:])]
-    ref = frames[-2]
+    win = frames[-51:-1] if first is None else frames[first:first + 50]
+    ref = win[-1]
     sig = [r["Kernel_Name"] for r in ref]
-    same = [f for f in frames[-51:-1] if [r["Kernel_Name"] for r in f] == sig]
+    same = [f for f in win if [r["Kernel_Name"] for r in f] == sig]
     t0 = int(ref[0]["Start_Timestamp"])
     tot = tmed = 0.0
     print(f"{'start us':>9} {'dur us':>7} {'med us':>7} {'grid':>8} kernel   (median over {len(same)} frames)")
@@ -36,4 +39,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
