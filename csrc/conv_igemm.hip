@@ -376,7 +376,7 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
 // cout halves of the weight fragments stay in registers (HOLDB: no re-read in phase 3); BN = 128
 // runs a 3-stage K ring (NST). (A 512 x 64 form and a BN-backward reduction in the dgrad epilogue
 // were measured slower: profiles/dead_ends.md.)
-template <int BN>
+template <int BN, bool SPLIT = false>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   // 256-pixel tile, wave (wm, wn) = 128 pixels x BN/4 couts
   constexpr int NST = BN == 128 ? 3 : 2;
@@ -413,13 +413,17 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   const auto ry1 = make_rsrc(a.y1, a.ybytes1);
   const auto ry2 = make_rsrc(a.y2 ? a.y2 : a.y1, a.y2 ? a.ybytes2 : 0u);
 
-  // DMA state of the tile being staged (see conv_igemm_kernel::set_tile)
+  // DMA state of the tile being staged (see conv_igemm_kernel::set_tile). Split-K (ksplit > 1):
+  // work item = (tile, split) as in conv_igemm_kernel, K steps [ks0, ks0 + nks) of the tile.
+  const int tiles1 = SPLIT ? a.ntiles / a.ksplit : a.ntiles;
   uint32_t pb1[NROW], pb2[NROW], nmask[NROW], woff[WPIECES];
   int itap = 0, icc = 0;
   auto set_tile = [&](int t) {
-    const int tile = (int)lid + t * (int)G;
-    itap = 0;
-    icc = 0;
+    const int item = (int)lid + t * (int)G;
+    const int tile = SPLIT ? item % tiles1 : item;
+    const int ks0 = SPLIT ? (item / tiles1) * a.nks : 0;
+    itap = ks0 / a.cpt;
+    icc = ks0 - itap * a.cpt;
     const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 #pragma unroll
     for (int f = 0; f < WPIECES; ++f) {
       const int n = tn * BN + (wave * WPIECES + f) * 8 + (lane >> 3);
-      woff[f] = (uint32_t)(n * a.ldw + gch * 8) * 2u;
+      woff[f] = (uint32_t)(n * a.ldw + gch * 8 + ks0 * 64) * 2u;  // + the split's first K column
     }
   };
   auto issue = [&](int ks, char* buf) {
@@ -509,6 +513,23 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 
   auto epilogue = [&]() {
     const int item = (int)lid + t * (int)G;
+    if constexpr (SPLIT) {  // fp32 partial tile -> slab[split][m][n]; conv_splitk_reduce_kernel finishes
+      const int tile = item % tiles1, split = item / tiles1;
+      const int tm = tile / a.tilesN, tn = tile - tm * a.tilesN;
+      const auto rk = make_rsrc(a.kslab, (uint32_t)((long)a.ksplit * a.M * a.Cout * 4));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = tn * BN + wco + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int m = tm * BM + wpx + i * 16 + (lane & 15);
+          const uint32_t off = m < a.M ? (uint32_t)(((long)split * a.M + m) * a.Cout + n) * 4u : RDP_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rk, off, 0, 0);
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      return;
+    }
     const int tm = item / a.tilesN, tn = item - tm * a.tilesN;
     const int m0 = tm * BM, n0 = tn * BN;
     const int gq = lane >> 4;
@@ -655,13 +676,28 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   }
 }
 
+static int launch_split_reduce(const ConvArgs& a, hipStream_t s, int* pooled);
+
+// ksplit > 1 (a.kslab set, ksplit divides nks, slab within 2 GiB -- the caller's plan): fp32
+// partial tiles, then the shared split-K reduce (stats / eval epilogue / fused pool or upsample).
 template <int BN>
-static int launch_pp(ConvArgs a, hipStream_t s) {
+static int launch_pp(ConvArgs a, hipStream_t s, int ksplit = 1, int* pooled = nullptr) {
   constexpr int BM = 256;
   if (a.packed || a.Cout % BN || a.Cy1 % 32) return -1;
   const int tilesM = (a.M + BM - 1) / BM;
   a.tilesN = a.Cout / BN;
   a.ntiles = tilesM * a.tilesN;
+  if (ksplit > 1) {
+    if (!a.kslab || a.nks % ksplit) return -1;
+    a.ksplit = ksplit;
+    a.nks /= ksplit;
+    a.ntiles *= ksplit;
+    ConvArgs k = a;
+    k.stats = nullptr;  // statistics come from the reduce
+    const int grid = k.ntiles < 256 ? k.ntiles : 256;
+    hipLaunchKernelGGL((conv_pp_kernel<BN, true>), dim3(grid), dim3(512), 0, s, k);
+    return launch_split_reduce(a, s, pooled);
+  }
   a.ksplit = 1;
   a.pool = nullptr;
   a.up = nullptr;
@@ -876,6 +912,29 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_up_kernel(const ConvAr
   }
 }
 
+// The reduce + epilogue launch after a split-K conv: returns the stats rows written (0 with the fused
+// upsample / pool, whose *pooled is set)
+static int launch_split_reduce(const ConvArgs& a, hipStream_t s, int* pooled) {
+  const int rpb = 256 / (a.Cout / 4);
+  int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
+  nblk = nblk < 512 ? nblk : 512;
+  if (a.up) {  // fused eval upsample: bands of UP_TY output rows x UP_CG channels
+    const int nb = (a.uH + UP_TY - 1) / UP_TY;
+    const size_t lds = (size_t)(UP_TY / 2 + 2) * a.W * UP_CG * 2;
+    hipLaunchKernelGGL(conv_splitk_reduce_up_kernel, dim3(a.N * nb, a.Cout / UP_CG), dim3(256), lds, s, a);
+    if (pooled) *pooled = 1;
+    return 0;
+  }
+  if (a.pool) {  // fused eval MaxPool2d(2): one work row per 2x2 window, no stats rows
+    nblk = (a.M / 4 + rpb - 1) / rpb;
+    nblk = nblk < 2048 ? nblk : 2048;
+    if (pooled) *pooled = 1;
+  }
+  const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
+  hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
+  return nblk;
+}
+
 // Split-K when the tile grid leaves most CUs idle: the smallest divisor of the K steps that gives
 // >= 256 work items with >= 4 K steps each, as long as the fp32 slab fits `ws_elems`.
 static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long ws_elems) {
@@ -891,6 +950,32 @@ static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long 
   return ks;
 }
 
+// Split-K ping-pong plan for the small-M / long-K convs (reference-batch training, deep layers): the
+// 256 x BN tile grid alone leaves most CUs idle, so the K steps are split over d work items (the
+// smallest divisor of nks giving >= 256 items, one block per CU, each >= PP_SPLIT_MIN_KS K steps)
+// when the fp32 slab d * M * Cout fits. Returns d (0: no split-K ping-pong plan).
+constexpr int PP_SPLIT_MIN_KS = 8;
+static int pp_split_plan(int M, int Cout, int BN, int nks, long ws_elems) {
+  if (Cout % BN) return 0;
+  const long tiles = (long)(M + 255) / 256 * (Cout / BN);
+  if (tiles >= 256) return 0;
+  for (int d = 2; d <= nks / PP_SPLIT_MIN_KS; ++d) {
+    if (nks % d) continue;
+    if ((long)d * M * Cout > ws_elems) return 0;
+    if (tiles * d >= 256) return d;
+  }
+  return 0;
+}
+
+static bool pp_split_enabled() {  // RDP_PP_SPLIT=0: the 128 x 128 split-K kernel instead (A/B)
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("RDP_PP_SPLIT");
+    on = e ? atoi(e) != 0 : 1;
+  }
+  return on != 0;
+}
+
 template <int BM, int BN, int NWV = 4>
 static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, int* pooled = nullptr) {
   const int tilesM = (a.M + BM - 1) / BM;
@@ -902,24 +987,7 @@ static int launch_cfg(ConvArgs a, int max_blocks, long ws_elems, hipStream_t s, 
     a.ntiles *= a.ksplit;
     const int grid = a.ntiles < max_blocks ? a.ntiles : max_blocks;
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, NWV>), dim3(grid), dim3(64 * NWV), 0, s, a);
-    const int rpb = 256 / (a.Cout / 4);
-    int nblk = (a.M + rpb - 1) / rpb;  // <= 512 stats rows: within conv_stats_rows()'s bound
-    nblk = nblk < 512 ? nblk : 512;
-    if (a.up) {  // fused eval upsample: bands of UP_TY output rows x UP_CG channels
-      const int nb = (a.uH + UP_TY - 1) / UP_TY;
-      const size_t lds = (size_t)(UP_TY / 2 + 2) * a.W * UP_CG * 2;
-      hipLaunchKernelGGL(conv_splitk_reduce_up_kernel, dim3(a.N * nb, a.Cout / UP_CG), dim3(256), lds, s, a);
-      if (pooled) *pooled = 1;
-      return 0;
-    }
-    if (a.pool) {  // fused eval MaxPool2d(2): one work row per 2x2 window, no stats rows
-      nblk = (a.M / 4 + rpb - 1) / rpb;
-      nblk = nblk < 2048 ? nblk : 2048;
-      if (pooled) *pooled = 1;
-    }
-    const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
-    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
-    return nblk;
+    return launch_split_reduce(a, s, pooled);
   }
   a.pool = nullptr;  // the non-split epilogue does not pool / upsample (the caller launches them)
   a.up = nullptr;
@@ -1055,6 +1123,21 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
     if (Cout % 128 == 0 && Cy1 % 32 == 0 && tiles128 >= 256 && C1 + C2 >= 128 && escale == nullptr)
       return launch_pp<128>(a, s);
   }
+  // bm_pref 7 / 8: force the split-K ping-pong 256 x 128 / 256 x 256 kernel (pp_split_plan's split)
+  if (bm_pref == 7 || bm_pref == 8) {
+    const int d = pp_split_plan(a.M, Cout, bm_pref == 7 ? 128 : 256, a.nks, wse);
+    if (d < 2 || packed || Cy1 % 32) return -1;
+    return bm_pref == 7 ? launch_pp<128>(a, s, d, pooled) : launch_pp<256>(a, s, d, pooled);
+  }
+  // auto, small M x long K (training): split-K ping-pong 256 x 128 where its plan exists and the 128 x 128
+  // kernel would split K too (measured, scripts/conv_microbench.py --batch 4 --ws 1, one MI355X: 32^2
+  // 1024->512 63.5 -> 53.2 us, 512->512 39.9 -> 36.7, 512+512->256 39.0 -> 36.7, 64^2 256->128 31.5 ->
+  // 29.4; where the 128 x 128 grid needs no split (64^2 256->256) the unsplit kernel wins, 32.9 vs 39.5)
+  if (bm_pref == 0 && !packed && escale == nullptr && Cout % 128 == 0 && Cy1 % 32 == 0 && C1 + C2 >= 128 &&
+      (long)(a.M + 127) / 128 * (Cout / 128) < 192 && pp_split_enabled()) {
+    const int d = pp_split_plan(a.M, Cout, 128, a.nks, wse);
+    if (d > 1) return launch_pp<128>(a, s, d, pooled);
+  }
   const int max_blocks = 256 * per_cu;
   // bm_pref 2 / 3: 8-wave blocks (64 x 32 per wave; twice the waves per SIMD to hide the per-step
   // barrier + DMA latency, 1.5x the LDS fragment reads per MFMA) for the 128x128 / 256x64 tiles
@@ -1079,5 +1162,12 @@ extern "C" long rdp_conv_ws_elems(int N, int H, int W, int C1, int C2, int Cout,
   const int BM = ((pref == 128 || pref == 0) && Cout % 128 == 0) ? 128 : 256, BN = BM == 128 ? 128 : 64;
   const int ntiles = (M + BM - 1) / BM * (Cout / BN);
   const int d = choose_ksplit(ntiles, nks, M, Cout, packed, 1L << 29);
-  return d > 1 ? (long)d * M * Cout : 0;
+  long need = d > 1 ? (long)d * M * Cout : 0;
+  // the split-K ping-pong plan (auto at >= 128 input channels, or forced by bm_pref 7 / 8)
+  if ((pref == 0 && C1 + C2 >= 128 && Cout % 128 == 0 && (long)(M + 127) / 128 * (Cout / 128) < 192) || pref == 7 ||
+      pref == 8) {
+    const int dp = pp_split_plan(M, Cout, pref == 8 ? 256 : 128, nks, 1L << 29);
+    if (dp > 1 && (long)dp * M * Cout > need) need = (long)dp * M * Cout;
+  }
+  return need;
 }

@@ -20,6 +20,7 @@ SHAPES = [  # (H, Cin1, Cin2, Cout)   spatial = H x H
     (16, 512, 0, 512), (32, 512, 512, 256), (64, 256, 256, 128), (128, 128, 128, 64), (256, 64, 64, 64),
     (128, 128, 0, 64), (64, 128, 0, 256), (32, 256, 0, 512), (32, 1024, 0, 512), (64, 512, 0, 256),
     (32, 512, 0, 256), (64, 256, 0, 128), (128, 64, 0, 128),
+    (32, 512, 0, 1024), (64, 256, 0, 512), (16, 512, 0, 1024),  # dgrads of the Up convs' concat inputs
 ]
 
 
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--halo-slab", type=int, default=1, help="wgrad: slab for the halo kernel's full split count")
     ap.add_argument("--shapes", default=None, help="comma list of shape indices")
+    ap.add_argument("--ws", type=int, default=0, help="fwd: pass a split-K workspace (the training step has one)")
     ap.add_argument("--wgrad-blocks", type=int, default=2048,
                     help="split-K grid target of the generic wgrad kernel (the training step uses 512)")
     a = ap.parse_args()
@@ -51,6 +53,10 @@ def main():
         stats = torch.zeros(C.conv_stats_rows(N * H * H, Co, 0) * 2 * Co, device=dev)
         flops = 2.0 * N * H * H * 9 * Cin * Co
         times = {v: [] for v in variants}
+        ws = None
+        if a.ws and not a.wgrad:
+            n_ws = max(C.conv_ws_elems(N, H, H, C1, C2, Co, 9, 0, v) for v in variants)
+            ws = torch.zeros(max(n_ws, 1), device=dev) if n_ws else None
         if a.wgrad:
             dy = torch.randn(N, H, H, Co, device=dev).to(torch.bfloat16)
             tiles = ((9 * Cin + 255) // 256) * (Co // 64)
@@ -65,7 +71,8 @@ def main():
             if a.wgrad:  # v = variant (0 auto, 4 generic, 5 halo)
                 C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
             else:
-                C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, v, None, 0)  # v = bm_pref (1 halo, 128/256 igemm)
+                # v = bm_pref (1 halo, 2 igemm 128x128 8-wave, 4 / 5 ping-pong, 7 / 8 split-K ping-pong)
+                C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, v, None, 0, ws)
 
         ok = []
         for v in variants:  # a variant that does not apply to this shape (-1) is skipped

@@ -855,6 +855,56 @@ def test_conv_pingpong_bitwise(C, N, H, W, C1, C2, Cout, pref):
             assert torch.equal(d1, e1) and torch.equal(d2, e2)
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pref", [
+    (4, 32, 32, 512, 512, 512, 7), (4, 32, 32, 512, 0, 512, 7), (4, 64, 64, 256, 256, 256, 7),
+    (4, 32, 32, 512, 0, 512, 8), (4, 32, 32, 256, 0, 512, 0), (5, 37, 29, 256, 0, 512, 7),
+    (4, 32, 32, 512, 0, 256, 0)])
+def test_conv_pingpong_splitk(C, N, H, W, C1, C2, Cout, pref):
+    """bm_pref 7 / 8 (and auto at the reference batch): the ping-pong kernel with K split over work
+    items (fp32 partial tiles + conv_splitk_reduce_kernel) vs fp32 torch: output, BN partial sums, a
+    ragged last tile (M = 5365), the concat input, split destinations (dgrad) and the eval BN fold;
+    two launches bitwise equal."""
+    torch.manual_seed(13)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    n_ws = C.conv_ws_elems(N, H, W, C1, C2, Cout, 9, 0, pref)
+    assert n_ws > 0, "shape should have a split-K plan"
+    ws = torch.full((n_ws,), float("nan"), device=dev)  # every slab element is written before it is read
+    rows = C.conv_stats_rows(N * H * W, Cout, pref)
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.conv2d(xin, w.float(), padding=1)
+    ys = []
+    for _ in range(2):
+        y = torch.full((N, H, W, Cout), 7.0, dtype=torch.bfloat16, device=dev)
+        st = torch.zeros(rows * 2 * Cout, device=dev)
+        r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, st, pref, None, 0, ws)
+        assert 0 < r <= rows
+        ys.append((y, st[: r * 2 * Cout].view(r, 2, Cout).sum(0)))
+    y, s = ys[0]
+    assert relerr(nchw(y), ref) < 1e-2
+    assert torch.equal(ys[1][0], y)
+    yq = nchw(y).float()
+    assert torch.allclose(s[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    # split destinations (the dgrad of a concat input)
+    y1 = torch.empty(N, H, W, Cout // 2, dtype=torch.bfloat16, device=dev)
+    y2 = torch.empty(N, H, W, Cout // 2, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, y1, y2, None, pref if pref else 7, None, 0, ws)
+    assert torch.equal(torch.cat([y1, y2], 3), y)
+    # eval BN fold + ReLU through the same reduce
+    if pref:
+        g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+        rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+        coef = torch.zeros(4 * Cout, device=dev)
+        C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+        a = torch.empty_like(y)
+        C.conv_fwd(x1, x2, wk, 9, 0, a, None, None, pref, coef, 1, ws)
+        assert relerr(nchw(a), F.relu(F.batch_norm(ref, rm, rv, g, b, False, 0.0, 1e-5))) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 6, 64), (1, 4, 128), (3, 2, 192), (1, 10, 64)])
 def test_conv_ring_fwd_stats_eval_dgrad(C, N, H, W):
     """Row-ring kernel (64 -> 64, W % 64 == 0): forward + BN stats, eval BN fold + ReLU, and the
