@@ -1132,9 +1132,10 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // auto, small M x long K (training): split-K ping-pong 256 x 128 where its plan exists and the 128 x 128
   // kernel would split K too (measured, scripts/conv_microbench.py --batch 4 --ws 1, one MI355X: 32^2
   // 1024->512 63.5 -> 53.2 us, 512->512 39.9 -> 36.7, 512+512->256 39.0 -> 36.7, 64^2 256->128 31.5 ->
-  // 29.4; where the 128 x 128 grid needs no split (64^2 256->256) the unsplit kernel wins, 32.9 vs 39.5)
+  // 29.4; where the 128 x 128 grid needs no split (64^2 256->256) the unsplit kernel wins, 32.9 vs 39.5,
+  // and at M = 1024 (16^2 512->1024: 29.5 vs 31.0 us) the 128 x 128 split does)
   if (bm_pref == 0 && !packed && escale == nullptr && Cout % 128 == 0 && Cy1 % 32 == 0 && C1 + C2 >= 128 &&
-      (long)(a.M + 127) / 128 * (Cout / 128) < 192 && pp_split_enabled()) {
+      a.M >= 4096 && (long)(a.M + 127) / 128 * (Cout / 128) < 192 && pp_split_enabled()) {
     const int d = pp_split_plan(a.M, Cout, 128, a.nks, wse);
     if (d > 1) return launch_pp<128>(a, s, d, pooled);
   }
@@ -1164,7 +1165,8 @@ extern "C" long rdp_conv_ws_elems(int N, int H, int W, int C1, int C2, int Cout,
   const int d = choose_ksplit(ntiles, nks, M, Cout, packed, 1L << 29);
   long need = d > 1 ? (long)d * M * Cout : 0;
   // the split-K ping-pong plan (auto at >= 128 input channels, or forced by bm_pref 7 / 8)
-  if ((pref == 0 && C1 + C2 >= 128 && Cout % 128 == 0 && (long)(M + 127) / 128 * (Cout / 128) < 192) || pref == 7 ||
+  if ((pref == 0 && C1 + C2 >= 128 && Cout % 128 == 0 && M >= 4096 && (long)(M + 127) / 128 * (Cout / 128) < 192) ||
+      pref == 7 ||
       pref == 8) {
     const int dp = pp_split_plan(M, Cout, pref == 8 ? 256 : 128, nks, 1L << 29);
     if (dp > 1 && (long)dp * M * Cout > need) need = (long)dp * M * Cout;
