@@ -256,13 +256,23 @@ class UNetNative(nn.Module):
         # re-records when this changes)
         self.__dict__["_layout_version"] = self.__dict__.get("_layout_version", 0) + 1
         seg_size = C.wseg_size()
-        raw = bytearray()
         import struct
-        for s in segs:
-            rec = struct.pack("<qqiiii", *s)
-            raw += rec + b"\0" * (seg_size - len(rec))
-        self._segs = torch.tensor(list(raw), dtype=torch.uint8).to(st.device)
-        self._nseg = len(segs)
+
+        def table(ss):
+            raw = bytearray()
+            for s in ss:
+                rec = struct.pack("<qqiiii", *s)
+                raw += rec + b"\0" * (seg_size - len(rec))
+            return torch.tensor(list(raw) or [0], dtype=torch.uint8).to(st.device), len(ss)
+
+        self._segs, self._nseg = table(segs)
+        # the conv dgrad layouts (kind 0 with 9 or 1 taps of a ConvSpec) are read only by backward; the
+        # packed first layer and the transposed decoder's forward weights by the next forward
+        n_conv = len(self.specs)
+        bwd = [s for i, s in enumerate(segs) if i < n_conv and not self.specs[i].packed]
+        fwd = [s for i, s in enumerate(segs) if not (i < n_conv and not self.specs[i].packed)]
+        self._segs_fwd, self._nseg_fwd = table(fwd)
+        self._segs_bwd, self._nseg_bwd = table(bwd)
         self.refresh_weights()
 
     def refresh_weights(self):
@@ -850,6 +860,9 @@ class UNetExecutor:
         D = self.m.depth
         st = self.m.store
         main = torch.cuda.current_stream() if self.overlap_wgrad else None
+        pend = self.m.__dict__.pop("_wprep_pending", None)
+        if pend is not None:  # the dgrad weights rebuilt on a side stream after the last Adam step
+            _stream_wait(torch.cuda.current_stream(), pend)
         try:
             self._backward(C, D, st, grad_hook, gscale)
         finally:
@@ -951,12 +964,24 @@ class NativeAdam:
         self.m = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
 
-    def step(self, gscale: float = 1.0):
+    def step(self, gscale: float = 1.0, side: Optional["torch.cuda.Stream"] = None):
+        """``side``: the training executor's weight-gradient stream. The dgrad weight layouts are then
+        rebuilt there, off the critical path, overlapping the next forward (which reads only the packed
+        first layer and the transposed decoder's weights, rebuilt here); the next backward waits for
+        them (:meth:`UNetExecutor.backward`)."""
         C = _native()
         st = self.m.store
+        m = self.m
         C.adam(st.flat, st.grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr, self.betas[0], self.betas[1], self.eps,
                self.wd, gscale, st.step, False)
-        C.wprep(st.flat, self.m.derived, self.m._segs, self.m._nseg, st.step)  # + the step counter advance
+        if side is None or m._nseg_bwd == 0:
+            C.wprep(st.flat, m.derived, m._segs, m._nseg, st.step)  # + the step counter advance
+            return
+        C.wprep(st.flat, m.derived, m._segs_fwd, m._nseg_fwd, st.step)
+        _stream_wait(side, torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            C.wprep(st.flat, m.derived, m._segs_bwd, m._nseg_bwd)
+        m.__dict__["_wprep_pending"] = side
 
     def hyper_key(self) -> tuple:
         """The hyper-parameters a recorded launch plan bakes in (NativeTrainer re-records on change)."""

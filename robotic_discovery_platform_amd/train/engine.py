@@ -112,12 +112,18 @@ class NativeTrainer:
                 ex.backward(grad_hook=self._hook)  # every layer's hook fires inside, the head's first
                 self.bucketer.finish()
             with trace.range("train.adam"):
-                self.opt.step(gscale=1.0 / self.world)
+                self.opt.step(gscale=1.0 / self.world, side=self._wprep_side())
         else:
             with trace.range("train.backward"):
                 ex.backward()
             with trace.range("train.adam"):
-                self.opt.step()
+                self.opt.step(side=self._wprep_side())
+
+    def _wprep_side(self):
+        """The stream for the dgrad weight re-layout after Adam (NativeAdam.step): the executor's wgrad
+        stream, idle during the next forward; inline under graph capture (no work left unjoined)."""
+        # (measured: bs 64 3,198 / 3,195 vs 3,187 / 3,188 img/s inline, bs 4 within noise; interleaved)
+        return None if self.use_graph else getattr(self.ex, "side", None)
 
     def set_batch(self, x: torch.Tensor, target: torch.Tensor):
         self.ex.set_input(x, target)
