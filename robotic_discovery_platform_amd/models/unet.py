@@ -209,7 +209,15 @@ class UNetNative(nn.Module):
         mod, leaf = self._holder(path)
         return mod._buffers[leaf]
 
+    def _join_wprep(self):
+        """Order the current stream after a dgrad re-layout still running on a training executor's side
+        stream (NativeAdam.step with ``side``) before the masters / derived buffers are touched here."""
+        pend = self.__dict__.pop("_wprep_pending", None)
+        if pend is not None:
+            _stream_wait(torch.cuda.current_stream(), pend)
+
     def load_state_dict(self, sd, strict: bool = True):  # keep flat-buffer views intact
+        self._join_wprep()
         own = dict(self.named_parameters())
         ownb = dict(self.named_buffers())
         missing = [k for k in list(own) + list(ownb) if k not in sd]
@@ -277,6 +285,7 @@ class UNetNative(nn.Module):
 
     def refresh_weights(self):
         """Rebuild the bf16 shadow + derived layouts from the fp32 master (after load / manual edits)."""
+        self._join_wprep()
         C = _native()
         C.cast_bf16(self.store.flat, self.store.shadow)
         C.wprep(self.store.flat, self.derived, self._segs, self._nseg)

@@ -177,3 +177,46 @@ def test_plan_rerecords_after_load_state_dict():
     want = tr2.step().clone()
     torch.cuda.synchronize()
     assert torch.equal(got[0][0], want[0])
+
+
+@pytest.mark.parametrize("bilinear", [True, False])
+def test_side_stream_wprep_matches_inline(bilinear):
+    """NativeTrainer rebuilds the dgrad weight layouts on the wgrad side stream after Adam (overlapping
+    the next forward): after every step the derived buffer equals a fresh inline re-layout of the
+    masters, the trained state is bitwise that of inline re-layout (graph mode, which keeps it inline),
+    and a load_state_dict right after a step waits for the side re-layout."""
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.train.engine import NativeTrainer
+    torch.manual_seed(6)
+    dev = torch.device("cuda")
+    ref = UNetRef(3, 1, bilinear=bilinear)
+    x = torch.rand(2, 3, 64, 64, device=dev)
+    y = (torch.rand(2, 1, 64, 64, device=dev) > 0.5).float()
+    nat = UNetNative(3, 1, bilinear=bilinear, device=dev, init_from=ref)
+    tr = NativeTrainer(nat, 2, 64, 64, lr=1e-3, plan=False)
+    assert tr._wprep_side() is not None
+    tr.set_batch(x, y)
+    for _ in range(3):
+        tr.step()
+        torch.cuda.synchronize()
+        d_side = nat.derived.clone()
+        nat.refresh_weights()  # inline re-layout from the same masters
+        torch.cuda.synchronize()
+        assert torch.equal(d_side, nat.derived)
+    nat2 = UNetNative(3, 1, bilinear=bilinear, device=dev, init_from=ref)
+    tr2 = NativeTrainer(nat2, 2, 64, 64, lr=1e-3, plan=False)
+    tr2._wprep_side = lambda: None  # inline re-layout after Adam
+    tr2.set_batch(x, y)
+    for _ in range(3):
+        tr2.step()
+    torch.cuda.synchronize()
+    assert torch.equal(nat.store.flat, nat2.store.flat) and torch.equal(nat.derived, nat2.derived)
+    sd = {k: v.clone() for k, v in UNetRef(3, 1, bilinear=bilinear).state_dict().items()}
+    tr.step()
+    nat.load_state_dict(sd)  # right behind the side re-layout of the step
+    torch.cuda.synchronize()
+    fresh = UNetNative(3, 1, bilinear=bilinear, device=dev, init_from=UNetRef(3, 1, bilinear=bilinear))
+    fresh.load_state_dict(sd)
+    torch.cuda.synchronize()
+    assert torch.equal(nat.derived, fresh.derived)
