@@ -69,7 +69,7 @@ int rdp_head_mask(const void*, int, const float*, const float*, float, void*, in
 int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, int*, int,
              hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
-int rdp_wprep(const float*, void*, const void*, int, int*, hipStream_t);
+int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
 int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
 double rdp_splev1(const double*, int, const double*, int, double, int);
@@ -838,7 +838,8 @@ void cast_bf16(torch::Tensor p, torch::Tensor out) {
   RDP_PLAN(rdp_cast_bf16(p.data_ptr<float>(), out.data_ptr(), p.numel(), st));
 }
 
-void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg, c10::optional<torch::Tensor> step) {
+void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg, c10::optional<torch::Tensor> step,
+           int blocks) {
   check_f32(master, "master");
   TORCH_CHECK(out.scalar_type() == torch::kBFloat16, "wprep out bf16");
   TORCH_CHECK(segs.is_cuda() && segs.numel() * segs.element_size() >= (long)nseg * rdp_wseg_size(), "segs");
@@ -847,7 +848,7 @@ void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg
     TORCH_CHECK(step->scalar_type() == torch::kInt32 && step->is_cuda(), "step int32");
     sp = (int*)step->data_ptr();
   }
-  RDP_PLAN(rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, sp, st));
+  RDP_PLAN(rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, sp, blocks, st));
 }
 
 void check_cpu_f64(const torch::Tensor& t, const char* name) {
@@ -1204,7 +1205,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("inc") = true);
   m.def("cast_bf16", on_device(&cast_bf16));
   m.def("wprep", on_device(&wprep), py::arg("master"), py::arg("out"), py::arg("segs"), py::arg("nseg"),
-        py::arg("step") = py::none());
+        py::arg("step") = py::none(), py::arg("blocks") = 0);
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
   m.def("geo_edges", on_device(&geo_edges), py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),

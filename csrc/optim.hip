@@ -124,8 +124,10 @@ int rdp_cast_bf16(const float* p, void* out, long n, hipStream_t s) {
   return 0;
 }
 
-// segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps} (32 bytes each)
-int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* step, hipStream_t s) {
+// segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps} (32 bytes each);
+// blocks: blocks per segment (0: 1152, enough for the largest layer; the caller passes the table's own
+// need -- e.g. 32 for the packed first layer alone -- so a small table is not a 1152-block launch)
+int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* step, int blocks, hipStream_t s) {
   if (nseg <= 0) {
     if (step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
     return 0;
@@ -133,7 +135,7 @@ int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* s
   // blocks per segment: the largest layer (512 x 1024 x 9) has 1152 64x64 tiles; at 128 blocks per
   // segment every block of it walked 9 tiles back to back (latency-bound: 68 us per step, a fixed
   // cost at every batch size). Blocks of smaller segments past their tile count exit at once.
-  constexpr int gx = 1152;
+  const int gx = blocks > 0 ? std::min(blocks, 1152) : 1152;
   hipLaunchKernelGGL(wprep_kernel, dim3(gx, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, step);
   return 0;
 }

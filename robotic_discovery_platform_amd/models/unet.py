@@ -273,7 +273,13 @@ class UNetNative(nn.Module):
                 raw += rec + b"\0" * (seg_size - len(rec))
             return torch.tensor(list(raw) or [0], dtype=torch.uint8).to(st.device), len(ss)
 
+        def blocks(ss):  # wprep blocks per segment this table needs (64 x 64 tiles / 256-element chunks)
+            need = [(co * 128 + 255) // 256 if kind == 1 else taps * ((co + 63) // 64) * ((ci + 63) // 64)
+                    for _, _, kind, co, ci, taps in ss]
+            return min(max(need + [1]), 1152)
+
         self._segs, self._nseg = table(segs)
+        self._wblk = blocks(segs)
         # the conv dgrad layouts (kind 0 with 9 or 1 taps of a ConvSpec) are read only by backward; the
         # packed first layer and the transposed decoder's forward weights by the next forward
         n_conv = len(self.specs)
@@ -281,6 +287,7 @@ class UNetNative(nn.Module):
         fwd = [s for i, s in enumerate(segs) if not (i < n_conv and not self.specs[i].packed)]
         self._segs_fwd, self._nseg_fwd = table(fwd)
         self._segs_bwd, self._nseg_bwd = table(bwd)
+        self._wblk_fwd, self._wblk_bwd = blocks(fwd), blocks(bwd)
         self.refresh_weights()
 
     def refresh_weights(self):
@@ -288,7 +295,7 @@ class UNetNative(nn.Module):
         self._join_wprep()
         C = _native()
         C.cast_bf16(self.store.flat, self.store.shadow)
-        C.wprep(self.store.flat, self.derived, self._segs, self._nseg)
+        C.wprep(self.store.flat, self.derived, self._segs, self._nseg, None, self._wblk)
 
     def fwd_weight(self, sp: ConvSpec) -> torch.Tensor:
         if sp.packed:
@@ -445,6 +452,13 @@ class UNetExecutor:
                         and not lb.spec.packed and w % 64 == 0 and h % 2 == 0 and n * h * w * c * 2 < (1 << 31)):
                     lb.bnin = la
                     la.consumer_bnin = True
+        # training, bilinear decoder: the BN + ReLU of the layer under each Up block is applied by the
+        # upsample itself on its 4 source taps (that layer's activation is never written; its backward
+        # reads only y). Pays at small batch, where each of the 4 apply launches is mostly launch /
+        # dependent-load latency; at bs 64 the 4x re-application cost 0.3-0.5 % (profiles/dead_ends.md).
+        fu = os.environ.get("RDP_FUSE_UP_BN")
+        self.fuse_up_bn = (training and model.bilinear and dev.type == "cuda" and
+                           (fu == "1" if fu is not None else N * H * W <= (1 << 20)))
         M = N * H * W
         self.M = M
         self.logits = torch.zeros(M, dtype=torch.float32, device=dev)
@@ -653,6 +667,7 @@ class UNetExecutor:
         # eval, bilinear decoder: each decoder input upsample is produced by the conv that makes `low`
         eval_up = not self.training and self.m.bilinear
         upsampled = False
+        fuse_up = self.fuse_up_bn and head
         for i in range(1, D + 1):
             if not pooled:
                 C.maxpool2_fwd(self.skips[i - 1], self.pools[i - 1])
@@ -661,8 +676,9 @@ class UNetExecutor:
             if i == D and eval_up:
                 upsampled = self._conv_bn_relu(C, lb, up=self.ups[0])
                 continue
-            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None)
+            pooled = self._conv_bn_relu(C, lb, self.pools[i] if i < D else None, apply=not (i == D and fuse_up))
         low = self.skips[D]
+        low_layer = self.down_layers[D][1] if D else None
         for i in range(1, D + 1):
             lv = D - i
             u = self.ups[i - 1]
@@ -670,6 +686,8 @@ class UNetExecutor:
             ox = (u.shape[2] - 2 * low.shape[2]) // 2
             if upsampled:
                 upsampled = False
+            elif fuse_up:  # relu(bn(y)) of the layer below formed on the upsample's source taps
+                C.upsample2_fwd(low_layer.y, u, oy, ox, low_layer.coef)
             elif self.m.bilinear:
                 C.upsample2_fwd(low, u, oy, ox)
             else:
@@ -685,8 +703,9 @@ class UNetExecutor:
             if not last and eval_up:
                 upsampled = self._conv_bn_relu(C, lb, up=self.ups[i])
             else:
-                self._conv_bn_relu(C, lb, apply=not (last and self.fuse_head and head))
+                self._conv_bn_relu(C, lb, apply=not ((last and self.fuse_head and head) or (not last and fuse_up)))
             low = lb.a
+            low_layer = lb
         if not head:
             if mask_head is not None:
                 C.head_mask(self.final, *mask_head)
@@ -984,12 +1003,12 @@ class NativeAdam:
         C.adam(st.flat, st.grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr, self.betas[0], self.betas[1], self.eps,
                self.wd, gscale, st.step, False)
         if side is None or m._nseg_bwd == 0:
-            C.wprep(st.flat, m.derived, m._segs, m._nseg, st.step)  # + the step counter advance
+            C.wprep(st.flat, m.derived, m._segs, m._nseg, st.step, m._wblk)  # + the step counter advance
             return
-        C.wprep(st.flat, m.derived, m._segs_fwd, m._nseg_fwd, st.step)
+        C.wprep(st.flat, m.derived, m._segs_fwd, m._nseg_fwd, st.step, m._wblk_fwd)
         _stream_wait(side, torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            C.wprep(st.flat, m.derived, m._segs_bwd, m._nseg_bwd)
+            C.wprep(st.flat, m.derived, m._segs_bwd, m._nseg_bwd, None, m._wblk_bwd)
         m.__dict__["_wprep_pending"] = side
 
     def hyper_key(self) -> tuple:
