@@ -958,7 +958,8 @@ static int choose_ksplit(int ntiles, int nks, int M, int Cout, int packed, long 
 // when the fp32 slab d * M * Cout fits. Returns d (0: no split-K ping-pong plan).
 constexpr int PP_SPLIT_MIN_KS = 8;
 static int pp_split_plan(int M, int Cout, int BN, int nks, long ws_elems) {
-  if (Cout % BN) return 0;
+  // (the split-K reduce kernel maps a power-of-two channel count, 64..1024, onto its threads)
+  if (Cout % BN || Cout > 1024 || (Cout & (Cout - 1))) return 0;
   const long tiles = (long)(M + 255) / 256 * (Cout / BN);
   if (tiles >= 256) return 0;
   for (int d = 2; d <= nks / PP_SPLIT_MIN_KS; ++d) {
