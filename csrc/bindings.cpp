@@ -18,7 +18,7 @@ int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, con
                    float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
-                     const float*, const float*, hipStream_t);
+                     const float*, const float*, void*, long, int, hipStream_t);
 long rdp_conv_ws_elems(int, int, int, int, int, int, int, int, int);
 int rdp_geo_nblocks(int);
 long rdp_geo_work_ints(int, int);
@@ -526,16 +526,26 @@ int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch:
   if (chunk_images(per_img, a.N) < a.N) return -1;
   return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                           o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
-                          0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), nullptr, nullptr, st));
+                          0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), nullptr, nullptr, nullptr, 0, 0, st));
 }
 
 // Training forward of a 3x3 64 -> 64 conv whose input is the producer layer's PRE-BN output x_pre: the
 // row-ring kernel applies the producer's BN + ReLU (in_coef: its [mean|invstd|scale|shift]) to the
 // staged rows itself, so the activation is never written (conv_ring.hip BNIN). Writes y and this
 // conv's BN statistic rows; returns the rows, or -1 when the ring kernel does not apply (nothing
-// launched: the caller runs bn_relu_apply + conv_fwd).
-int conv_fwd_bnin(torch::Tensor x_pre, torch::Tensor w, torch::Tensor y, torch::Tensor stats, torch::Tensor in_coef) {
+// launched: the caller runs bn_relu_apply + conv_fwd). a_out (optional): the activation is also
+// written there (bitwise what bn_relu_apply writes), for a plain weight-gradient pass.
+int conv_fwd_bnin(torch::Tensor x_pre, torch::Tensor w, torch::Tensor y, torch::Tensor stats, torch::Tensor in_coef,
+                  c10::optional<torch::Tensor> a_out) {
   Act a = act(x_pre, "x_pre"), o = act(y, "y");
+  void* aptr = nullptr;
+  long abytes = 0;
+  int apitch = 0;
+  if (a_out && a_out->defined()) {
+    Act q = act(*a_out, "a_out");
+    TORCH_CHECK(q.N == a.N && q.H == a.H && q.W == a.W && q.C == a.C, "conv_fwd_bnin: a_out shape");
+    aptr = q.ptr; abytes = q.bytes; apitch = q.pitch;
+  }
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
   TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && w.size(0) == o.C, "conv_fwd_bnin: shape mismatch");
   check_f32(stats, "stats");
@@ -548,7 +558,8 @@ int conv_fwd_bnin(torch::Tensor x_pre, torch::Tensor w, torch::Tensor y, torch::
   const float* c = in_coef.data_ptr<float>();
   return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                                    o.pitch, nullptr, 0, 0, o.C, o.C, stats.data_ptr<float>(), a.N, a.H, a.W, nullptr,
-                                   nullptr, 0, 256, nullptr, 0, nullptr, c + 2 * a.C, c + 3 * a.C, st));
+                                   nullptr, 0, 256, nullptr, 0, nullptr, c + 2 * a.C, c + 3 * a.C, aptr, abytes, apitch,
+                                   st));
 }
 
 int bn_relu_bwd_reduce(torch::Tensor da, torch::Tensor y, torch::Tensor coef, int relu, torch::Tensor partial) {
@@ -1166,7 +1177,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", on_device(&conv_wgrad), py::arg("x1"), py::arg("x2"), py::arg("dy"), py::arg("taps"),
         py::arg("packed"), py::arg("cin_real"), py::arg("slab"), py::arg("out"), py::arg("accumulate"),
         py::arg("splits"), py::arg("variant"), py::arg("in_coef") = py::none());
-  m.def("conv_fwd_bnin", on_device(&conv_fwd_bnin));
+  m.def("conv_fwd_bnin", on_device(&conv_fwd_bnin), py::arg("x_pre"), py::arg("w"), py::arg("y"), py::arg("stats"),
+        py::arg("in_coef"), py::arg("a_out") = py::none());
   m.def("wgrad_first_bn", on_device(&wgrad_first_bn));
   m.def("wgrad_slab_elems", &wgrad_slab_elems);
   m.def("wgrad_halo_slab_elems", &rdp_conv_wgrad_halo_slab_elems);

@@ -58,6 +58,11 @@ struct RingArgs {
   // channel) is applied to the staged rows in LDS
   const float* iscale;
   const float* ishift;
+  // BNIN, optional: the formed activation of the rows this block owns is also stored here (pixel pitch
+  // apitch), so the layer's weight gradient can run the plain ring kernel on it (nullptr: not stored)
+  u16* aout;
+  uint32_t abytes;
+  int apitch;
   int H, W, WS;  // WS = W / 64 segments per image row
   int nrows;     // N * WS * H: input rows in column order (R = column * H + h)
   int npairs;    // nrows / 2: steps (two output rows each)
@@ -83,7 +88,9 @@ RDP_DEV uint32_t rdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, 
 // a = relu(y * scale + shift), rounded to bf16 exactly as bn_relu_apply_kernel does, is formed in LDS
 // once per staged element -- by the wave whose DMA staged it, right after its own vmcnt wait, so the
 // step's existing barrier publishes it -- instead of a separate apply pass writing and re-reading a
-// (padding chunks stay zero: the conv pads the post-ReLU activation).
+// (padding chunks stay zero: the conv pads the post-ReLU activation). With aout, the interior chunks of
+// the rows the block owns (2 P0 .. 2 (P0 + nks) - 1) are also stored there; every staged chunk issues
+// its store (the others at an out-of-range offset) so the per-wave vmcnt counts below stay fixed.
 template <int COUT, bool BNR = false, bool HEAD = false, bool POOL = false, bool BNIN = false>
 __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   constexpr int NCG = COUT / 32, NPG = 8 / NCG;  // waves per channel group / per pixel group
@@ -200,11 +207,13 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     __syncthreads();
   }
   // BNIN: this lane's chunk of piece pj of input row R (staged by this wave): y -> relu(y*scale+shift)
+  const auto ra = make_rsrc(a.aout, a.aout ? a.abytes : 0u);
+  const int rown0 = 2 * P0, rown1 = 2 * (P0 + nks);  // rows this block owns (activation store)
   auto bn_chunk = [&](int R, int pj) {
     int m0, w0;
     row_base(R, m0, w0);
     const int j = pj * 8 + (lane >> 3);
-    if (!((m0 >= 0) & (j < 66) & inb(w0 - 1 + j, a.W))) return;  // padding: stays zero
+    const bool ok = (m0 >= 0) & (j < 66) & inb(w0 - 1 + j, a.W);  // else padding: stays zero
     uint4* p = (uint4*)(ring + ((R + NX) % NX) * XREG + pj * 1024 + lane * 16);
     const uint4 v = *p;
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
@@ -217,7 +226,10 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
       const float hi = fmaxf(fmaf(__uint_as_float(wv[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]), 0.f);
       o[k] = pack2bf(lo, hi);
     }
-    *p = make_uint4(o[0], o[1], o[2], o[3]);
+    const uint4 ov = make_uint4(o[0], o[1], o[2], o[3]);
+    if (ok) *p = ov;
+    const bool st = ok & (j >= 1) & (j <= 64) & (R >= rown0) & (R < rown1);
+    bstore16(ra, st ? (uint32_t)((m0 + j - 1) * a.apitch + gch * 8) * 2u : RDP_OOB, ov);
   };
   auto bn_stage = [&](int P) {  // the pieces this wave staged for stage P (see issue)
 #pragma unroll
@@ -306,14 +318,17 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     // (unless this is the last step) stage P+1 -- leave exactly those in flight.
     // (HEAD: no activation stores; the mask stores of cg = 0 are not counted, which only makes the
     // wait stricter)
+    // BNIN: also the activation stores of step ks - 1's transform, younger than stage P's DMAs: at
+    // least AS per wave per stage (2 or 3 pieces) and AS0 at step 0 (+ the 1-2 pieces of each prologue row)
     constexpr int NS = HEAD ? 0 : NI;  // counted output stores per step
+    constexpr int AS = BNIN ? 2 : 0, AS0 = BNIN ? 4 : 0;
     if (ks + 1 < nks) {
-      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2 * NS) : "memory");
-      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + NS) : "memory");
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + 2 * NS + AS) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW + NS + AS0) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
     } else {
-      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NS) : "memory");
-      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NS) : "memory");
+      if (ks >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NS + AS) : "memory");
+      else if (ks == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NS + AS0) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     if constexpr (BNIN) {  // this wave's DMAs of stage P (and at the start the prologue rows) have landed
@@ -543,13 +558,15 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
                                 void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                                 int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                                 int erelu, int max_blocks, const void* bn_y_, int bn_ypitch, const float* bn_coef,
-                                const float* iscale, const float* ishift, hipStream_t s);
+                                const float* iscale, const float* ishift, void* aout, long abytes, int apitch,
+                                hipStream_t s);
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,
                              void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                              int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                              int erelu, int max_blocks, hipStream_t s) {
   return rdp_conv_ring_ex(x, xbytes, C, pitch, w, wbytes, ldw, y, ybytes, ypitch, y2, ybytes2, ypitch2, Cy1, Cout,
-                          stats, N, H, W, escale, eshift, erelu, max_blocks, nullptr, 0, nullptr, nullptr, nullptr, s);
+                          stats, N, H, W, escale, eshift, erelu, max_blocks, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+                          0, 0, s);
 }
 
 // Eval conv (64 -> 64, BN folded + ReLU) fused with the serving 1x1 head: writes only the u8 mask
@@ -568,6 +585,7 @@ extern "C" int rdp_conv_ring_head(const void* x, long xbytes, int C, int pitch, 
   a.hw = hw; a.hb = hb; a.hthr = hthr; a.hmask = (uint8_t*)mask;
   a.pool = nullptr; a.ppitch = 0;
   a.iscale = nullptr; a.ishift = nullptr;
+  a.aout = nullptr; a.abytes = 0; a.apitch = 0;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -598,6 +616,7 @@ extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, 
   a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
   a.pool = (u16*)pool; a.ppitch = ppitch;
   a.iscale = nullptr; a.ishift = nullptr;
+  a.aout = nullptr; a.abytes = 0; a.apitch = 0;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;
@@ -617,8 +636,10 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
                                 void* y, long ybytes, int ypitch, void* y2, long ybytes2, int ypitch2, int Cy1,
                                 int Cout, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                                 int erelu, int max_blocks, const void* bn_y_, int bn_ypitch, const float* bn_coef,
-                                const float* iscale, const float* ishift, hipStream_t s) {
+                                const float* iscale, const float* ishift, void* aout, long abytes, int apitch,
+                                hipStream_t s) {
   const u16* bn_y = (const u16*)bn_y_;
+  if (aout && (!iscale || abytes >= (1l << 31) || apitch % 8)) return -1;
   if (bn_y && (!stats || escale || y2 || bn_ypitch % 4 || Cout != 64)) return -1;
   if (iscale && (!ishift || bn_y || escale || y2 || Cout != 64)) return -1;
   if (C != 64 || (Cout != 64 && Cout != 128) || W % 64 || H % 2 || ldw < 576 || Cy1 % 32) return -1;
@@ -635,6 +656,7 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   a.hw = nullptr; a.hb = nullptr; a.hthr = 0.f; a.hmask = nullptr;
   a.pool = nullptr; a.ppitch = 0;
   a.iscale = iscale; a.ishift = ishift;
+  a.aout = (u16*)aout; a.abytes = (uint32_t)abytes; a.apitch = apitch;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;

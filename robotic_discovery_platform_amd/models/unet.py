@@ -452,6 +452,9 @@ class UNetExecutor:
                         and not lb.spec.packed and w % 64 == 0 and h % 2 == 0 and n * h * w * c * 2 < (1 << 31)):
                     lb.bnin = la
                     la.consumer_bnin = True
+        # ... and the forward also stores that activation (one extra write) so the weight gradient runs the
+        # plain row-ring kernel instead of re-forming it
+        self.bnin_write_a = os.environ.get("RDP_BNIN_WRITE_A", "1") == "1"
         # training, bilinear decoder: the BN + ReLU of the layer under each Up block is applied by the
         # upsample itself on its 4 source taps (that layer's activation is never written; its backward
         # reads only y). Pays at small batch, where each of the 4 apply launches is mostly launch /
@@ -621,7 +624,7 @@ class UNetExecutor:
             C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool)
             return pool is not None
         if L.bnin is not None:  # the producer's BN + ReLU applied by this conv (row-ring BNIN)
-            rows = C.conv_fwd_bnin(L.bnin.y, w, L.y, self.stats, L.bnin.coef)
+            rows = C.conv_fwd_bnin(L.bnin.y, w, L.y, self.stats, L.bnin.coef, L.bnin.a if self.bnin_write_a else None)
             assert rows > 0, "conv_fwd_bnin: ring kernel not applicable"
         else:
             rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
@@ -859,7 +862,7 @@ class UNetExecutor:
         # all wgrads share the slab, so they stay serialized on the one side stream
         if self.slab_main is not None and L is self.down_layers[0][0]:
             C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab_main, gw, 0, L.splits, 0)
-        elif L.bnin is not None:  # x = relu(bn(producer y)), formed by the row-ring wgrad itself
+        elif L.bnin is not None and not self.bnin_write_a:  # x = relu(bn(producer y)), formed by the ring wgrad
             src = L.bnin
             self._on_wgrad_stream(lambda slab: C.conv_wgrad(src.y, None, L.dy, sp.taps, 0, sp.cin_real, slab, gw, 0,
                                                             L.splits, 0, src.coef))

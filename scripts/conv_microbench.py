@@ -50,7 +50,7 @@ def main():
         Cin = C1 + C2
         w = (torch.randn(Co, 9 * Cin, device=dev) * 0.02).to(torch.bfloat16)
         y = torch.empty(N, H, H, Co, dtype=torch.bfloat16, device=dev)
-        stats = torch.zeros(C.conv_stats_rows(N * H * H, Co, 0) * 2 * Co, device=dev)
+        stats = torch.zeros(max(C.conv_stats_rows(N * H * H, Co, 0), 1024) * 2 * Co, device=dev)
         flops = 2.0 * N * H * H * 9 * Cin * Co
         times = {v: [] for v in variants}
         ws = None
@@ -67,9 +67,22 @@ def main():
                                    C.wgrad_halo_slab_elems(N, H, H, Cin, Co) if a.halo_slab else 0), device=dev)
             out = torch.zeros(Co * 9 * Cin, device=dev)
 
+        # v = 9: the BN-on-input row-ring path (x1 = producer's pre-BN y; 64 -> 64 at W % 64 == 0)
+        # ([mean | invstd | scale | shift] of the producer's BN)
+        coef = torch.cat([torch.zeros(2 * C1, device=dev), torch.rand(C1, device=dev) + 0.5,
+                          torch.randn(C1, device=dev) * 0.1]).float()
+
+        a_st = torch.empty_like(x1)
+
         def run(v):
-            if a.wgrad:  # v = variant (0 auto, 4 generic, 5 halo)
-                C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
+            if a.wgrad:  # v = variant (0 auto, 4 generic, 5 halo, 9 BN-on-input ring)
+                if v == 9:
+                    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, 0, coef)
+                else:
+                    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
+            elif v in (9, 10):  # 10: BN-on-input forward that also stores the activation
+                if C.conv_fwd_bnin(x1, w, y, stats, coef, a_st if v == 10 else None) <= 0:
+                    raise RuntimeError("bnin n/a")
             else:
                 # v = bm_pref (1 halo, 2 igemm 128x128 8-wave, 4 / 5 ping-pong, 7 / 8 split-K ping-pong)
                 C.conv_fwd(x1, x2, w, 9, 0, y, None, stats, v, None, 0, ws)

@@ -412,6 +412,14 @@ def test_conv_bnin_fwd_and_wgrad(C, N, H, W):
     assert rows == rows_ref > 0
     assert torch.equal(y_out, y_ref) and torch.equal(st[: rows * 128], st_ref[: rows * 128])
     assert relerr(nchw(y_out), F.conv2d(nchw(a).float(), w.float(), padding=1)) < 1e-2
+    # with a_out: the same outputs, and the formed activation written bitwise as bn_relu_apply writes it
+    a_out = torch.full_like(y_pre, 3.0)
+    y_out.zero_()
+    st.zero_()
+    assert C.conv_fwd_bnin(y_pre, wk, y_out, st, coef, a_out) == rows
+    torch.cuda.synchronize()
+    assert torch.equal(y_out, y_ref) and torch.equal(st[: rows * 128], st_ref[: rows * 128])
+    assert torch.equal(a_out, a)
     dy = bf(torch.randn(N, H, W, 64, device=dev))
     slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 64, 64, 9, 0, 64), device=dev)
     g_ref, g = (torch.full((64 * 9 * 64,), 7.0, device=dev) for _ in range(2))
