@@ -8,7 +8,7 @@ for f in sorted(glob.glob(f'{d}/set*/pmc_counter_collection.csv')):
     for r in csv.DictReader(open(f)):
         k = (r['Dispatch_Id'])
         acc[k][r['Counter_Name']] += float(r['Counter_Value'])
-        meta[k] = (r['Kernel_Name'][:32], r['Grid_Size'], int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+        meta[k] = (r['Kernel_Name'][:64], r['Grid_Size'], int(r['End_Timestamp']) - int(r['Start_Timestamp']))
     for k, v in acc.items():
         name, grid, dur = meta[k]
         if 'conv' not in name and 'wgrad' not in name: continue
