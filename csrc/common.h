@@ -33,8 +33,12 @@ RDP_DEV u16 f2bf(float f) {
   __bf16 b = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 at -O3 (keeps NaN a NaN)
   return __builtin_bit_cast(u16, b);
 }
+// one v_cvt_pk_bf16_f32 (lo, hi) per pair: composing two scalar f2bf conversions let the SLP vectorizer
+// pair the wrong operands (two converts + four shuffle ops per two pairs)
+typedef __bf16 rdp_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float rdp_f32x2 __attribute__((ext_vector_type(2)));
 RDP_DEV uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((rdp_f32x2){lo, hi}, rdp_bf16x2));
 }
 
 // ---- 16/8-byte buffer loads/stores ----
