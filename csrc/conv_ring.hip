@@ -209,7 +209,12 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
   // BNIN: this lane's chunk of piece pj of input row R (staged by this wave): y -> relu(y*scale+shift)
   const auto ra = make_rsrc(a.aout, a.aout ? a.abytes : 0u);
   const int rown0 = 2 * P0, rown1 = 2 * (P0 + nks);  // rows this block owns (activation store)
-  auto bn_chunk = [&](int R, int pj) {
+  // cf = this lane's [scale x 8 | shift x 8] (its chunk's channels 8 gch ..), read once per stage
+  auto bn_coefs = [&](float (&cf)[16]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { cf[k] = efold[8 * gch + k]; cf[8 + k] = efold[64 + 8 * gch + k]; }
+  };
+  auto bn_chunk = [&](int R, int pj, const float (&cf)[16]) {
     int m0, w0;
     row_base(R, m0, w0);
     const int j = pj * 8 + (lane >> 3);
@@ -217,8 +222,8 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     uint4* p = (uint4*)(ring + ((R + NX) % NX) * XREG + pj * 1024 + lane * 16);
     const uint4 v = *p;
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-    const float* sc = efold + 8 * gch;
-    const float* sh = efold + 64 + 8 * gch;
+    const float* sc = cf;
+    const float* sh = cf + 8;
     uint32_t o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -232,19 +237,23 @@ __global__ __launch_bounds__(512, 2) void conv_ring_kernel(const RingArgs a) {
     bstore16(ra, st ? (uint32_t)((m0 + j - 1) * a.apitch + gch * 8) * 2u : RDP_OOB, ov);
   };
   auto bn_stage = [&](int P) {  // the pieces this wave staged for stage P (see issue)
+    float cf[16];
+    bn_coefs(cf);
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int p = wave + 8 * t;
       if (p >= PIECES) continue;
       const int rr = p >= 9 ? 1 : 0;
-      bn_chunk(2 * P + 1 + rr, p - 9 * rr);
+      bn_chunk(2 * P + 1 + rr, p - 9 * rr, cf);
     }
   };
   auto bn_row = [&](int R) {  // the prologue pieces this wave staged for row R (see issue_row)
+    float cf[16];
+    bn_coefs(cf);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int pj = wave + 8 * t;
-      if (pj < 9) bn_chunk(R, pj);
+      if (pj < 9) bn_chunk(R, pj, cf);
     }
   };
 
