@@ -18,6 +18,7 @@ execution model is MI355X-first:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -358,10 +359,16 @@ class _Layer:
     consumer_bnin: bool = False
 
 
+# observers of every cross-stream wait (parallel.ddp.StreamOrderChecker, tests)
+_STREAM_OBSERVERS: List = []
+
+
 def _stream_wait(waiter: "torch.cuda.Stream", waitee: "torch.cuda.Stream"):
     """``waiter.wait_stream(waitee)`` through the native runtime, so that a launch plan being recorded
     (NativeTrainer plan mode, csrc/bindings.cpp) also holds the cross-stream dependency."""
     _native().stream_wait(waiter.cuda_stream, waitee.cuda_stream)
+    for o in _STREAM_OBSERVERS:
+        o.wait(waiter, waitee)
 
 
 class UNetExecutor:
@@ -820,6 +827,21 @@ class UNetExecutor:
         one per consecutive wgrad, measured slower: every extra stream lands on another hardware queue.)"""
         return self._on_side(lambda: fn(self.slab))
 
+    @contextlib.contextmanager
+    def comm_stream(self):
+        """Make the current stream one ordered after EVERY gradient issued so far -- the main stream's
+        (BN, head, bias gradients) and the wgrad side stream's (conv weight gradients) -- for the DDP
+        bucket all-reduces (parallel.ddp.FlatBucketer ``launch_ctx``): the side stream after a fork
+        from the main stream. Without a side stream the current stream already is."""
+        if self.side is None:
+            yield
+            return
+        cur = torch.cuda.current_stream()
+        if cur != self.side:
+            _stream_wait(self.side, cur)
+        with torch.cuda.stream(self.side):
+            yield
+
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream
         (fork); without a side stream it runs inline. (One fork per two weight gradients, which saves
@@ -834,13 +856,14 @@ class UNetExecutor:
         sp = L.spec
         st = self.m.store
         gw = st.flat_slice(sp.name + ".weight", st.grad)
+        main = torch.cuda.current_stream() if self.dev.type == "cuda" else None
         if (self.dev.type == "cuda" and L is self.down_layers[0][0] and sp.packed and L.dx1 is None
                 and head_gscale is None and sp.cout == 64):
             # first layer: its pre-BN gradient feeds only the weight gradient, so the BN-backward apply
             # runs inside that wgrad (wgrad_first_bn) and dz is never stored
             self._bn_bwd(C, L, None, apply=False)
             if hooks is not None:
-                hooks(BNHook(sp))
+                hooks(BNHook(sp), main)
 
             def fused(slab):
                 r = C.wgrad_first_bn(L.x1, L.da, L.y, L.coef, L.coef2, slab, gw, sp.cin_real, 0, L.splits)
@@ -852,16 +875,18 @@ class UNetExecutor:
                 fused(self.slab_main)
             else:
                 self._on_wgrad_stream(fused)
-            if hooks is not None:
-                self._on_side(lambda: hooks(sp))
+            if hooks is not None:  # the weight gradient is final once its stream's work so far has run
+                hooks(sp, main if self.slab_main is not None or self.side is None else self.side)
             return
         self._bn_bwd(C, L, head_gscale)
         if hooks is not None:  # gamma / beta gradients are final (main stream)
-            hooks(BNHook(sp))
+            hooks(BNHook(sp), main)
         # wgrad (latency-bound on x / dY streams) overlaps the main stream's dgrad + next BN backward;
         # all wgrads share the slab, so they stay serialized on the one side stream
+        wstream = self.side if self.side is not None else main
         if self.slab_main is not None and L is self.down_layers[0][0]:
             C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab_main, gw, 0, L.splits, 0)
+            wstream = main
         elif L.bnin is not None and not self.bnin_write_a:  # x = relu(bn(producer y)), formed by the ring wgrad
             src = L.bnin
             self._on_wgrad_stream(lambda slab: C.conv_wgrad(src.y, None, L.dy, sp.taps, 0, sp.cin_real, slab, gw, 0,
@@ -879,11 +904,13 @@ class UNetExecutor:
                 owner = True
         if L.dx1 is not None and owner is not True:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
-        if hooks is not None:
-            self._on_side(lambda: hooks(sp))  # the bucket's all-reduce waits for the wgrad too
+        if hooks is not None:  # the weight gradient is final once its stream's work so far has run
+            hooks(sp, wstream)
 
     def backward(self, grad_hook=None, gscale: float = 1.0):
-        """Full backward; ``grad_hook(spec)`` fires after each conv layer's grads are final.
+        """Full backward; ``grad_hook(spec, stream)`` fires as each layer's gradients are issued: they
+        are final once the work issued so far on ``stream`` has run (a collective reading them must be
+        issued from a stream ordered after it: :meth:`comm_stream`).
 
         Weight gradients run on a side stream (``overlap_wgrad``) and join the caller's stream at
         the end, so the optimizer (or a graph capture) sees every gradient complete."""
@@ -919,7 +946,7 @@ class UNetExecutor:
                        hgb, self.dice_w, self.dice_eps, gscale)
         self._head_fwd_grads = False
         if grad_hook is not None:  # the head's gradients are final now: its bucket may go first
-            grad_hook(HEAD_SPEC)
+            grad_hook(HEAD_SPEC, torch.cuda.current_stream() if self.dev.type == "cuda" else None)
         for i in range(D, 0, -1):
             la, lb = self.up_layers[i - 1]
             self._conv_bwd(C, lb, grad_hook, head_gscale if i == D else None)
@@ -942,8 +969,8 @@ class UNetExecutor:
                                                    st.flat_slice(us.name + ".weight", st.grad), 0, ns, 0))
                 C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
                            self.kws)
-                if grad_hook is not None:
-                    self._on_side(lambda us=us: grad_hook(us))
+                if grad_hook is not None:  # bias (main) + weight (side, forked after the bias)
+                    grad_hook(us, self.side if self.side is not None else torch.cuda.current_stream())
         for i in range(D, 0, -1):
             la, lb = self.down_layers[i]
             self._conv_bwd(C, lb, grad_hook)

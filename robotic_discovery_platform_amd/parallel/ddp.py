@@ -9,8 +9,14 @@ Design (MI355X-first):
     Backward produces gradients in exactly the reverse order, so buckets are contiguous reverse
     ranges of that buffer -- no gradient copies, no per-parameter launches.
   * A bucket is launched (``all_reduce(SUM, async_op=True)``) as soon as the last parameter in it is
-    final; RCCL's internal stream waits on the compute stream at issue time and runs concurrently
+    final; RCCL's internal stream waits on the ISSUING stream at issue time and runs concurrently
     with the remaining backward kernels. ``finish()`` makes the compute stream wait for all buckets.
+  * Stream ordering: RCCL (and gloo's CUDA path) orders a collective after the current stream only.
+    The native executor produces gradients on two streams (BN / head gradients on the main stream,
+    conv weight gradients on the wgrad side stream), so a bucket may only be issued from a stream
+    that is ordered after EVERY producer of its gradients. ``launch_ctx`` supplies that stream
+    (the executor's: the side stream after a fork from main, ``UNetExecutor.comm_stream``); the
+    bf16 narrowing copy runs there too. :class:`StreamOrderChecker` verifies it with vector clocks.
   * A parameter of at least half a bucket that would overflow the open bucket starts a new one, so
     the small decoder layers whose gradients are final first (outc, up4 .. up1.conv.3, 12.5 MB) go
     out before the 18.9 MB up1.conv.0 gradient exists.
@@ -25,7 +31,8 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+import contextlib
+from typing import Callable, ContextManager, Dict, Iterable, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -41,8 +48,13 @@ class FlatBucketer:
     """Reverse-order contiguous gradient buckets over a flat buffer."""
 
     def __init__(self, grad_flat: torch.Tensor, param_ranges: Sequence[Tuple[str, int, int]],
-                 bucket_mb: float = 16.0, group=None, comm_dtype: Optional[torch.dtype] = None):
+                 bucket_mb: float = 16.0, group=None, comm_dtype: Optional[torch.dtype] = None,
+                 launch_ctx: Optional[Callable[[], ContextManager]] = None):
         self.grad = grad_flat
+        # context that makes the current stream one ordered after every gradient producer (None: the
+        # caller's current stream already is, e.g. single-stream autograd)
+        self.launch_ctx = launch_ctx
+        self.checker: Optional["StreamOrderChecker"] = None
         self.group = group
         self.comm_dtype = comm_dtype if comm_dtype not in (None, grad_flat.dtype) else None
         # bf16 mirror of the whole gradient buffer (buckets are slices of it, like of ``grad``)
@@ -95,14 +107,22 @@ class FlatBucketer:
         self.handles = []
 
     def _launch(self, b: int):
-        lo, hi = self.buckets[b]
-        buf = self.grad[lo:hi]
-        if self.comm is not None:
-            buf = self.comm[lo:hi]
-            buf.copy_(self.grad[lo:hi])  # narrowing cast on the stream that produced the gradients
-        self.handles.append((b, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
+        with (self.launch_ctx() if self.launch_ctx is not None else contextlib.nullcontext()):
+            if self.checker is not None:
+                self.checker.check_launch(self.bucket_params[b], torch.cuda.current_stream())
+            lo, hi = self.buckets[b]
+            buf = self.grad[lo:hi]
+            if self.comm is not None:
+                buf = self.comm[lo:hi]
+                buf.copy_(self.grad[lo:hi])  # narrowing cast, ordered after every producer (launch_ctx)
+            self.handles.append((b, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
 
-    def mark_ready(self, names: Iterable[str]):
+    def mark_ready(self, names: Iterable[str], stream=None):
+        """``names`` are final once the work issued so far on ``stream`` (their producer; None: the
+        current stream) has run."""
+        names = list(names)
+        if self.checker is not None:
+            self.checker.produced(names, stream)
         for n in names:
             b = self.param_bucket[n]
             self.pending[b] -= 1
@@ -120,6 +140,64 @@ class FlatBucketer:
                 lo, hi = self.buckets[b]
                 self.grad[lo:hi].copy_(self.comm[lo:hi])  # widen the reduced sums back to fp32
         self.handles = []
+
+
+class StreamOrderChecker:
+    """Vector-clock model of HIP stream ordering, to prove every bucket is issued after its producers.
+
+    Each stream keeps a clock {stream: count}. Producing gradients on stream ``p`` ticks ``p``'s own
+    entry and stamps the gradients with (p, count); ``waiter`` waiting on ``waitee`` (an event recorded
+    on waitee, waited on waiter: ``stream_wait``) merges waitee's clock into waiter's. A collective
+    issued on stream ``s`` reads its bucket correctly iff ``clock[s][p] >= count`` for every stamped
+    gradient. Install with :meth:`install` (hooks ``UNetExecutor``'s stream waits)."""
+
+    def __init__(self):
+        self.clock: Dict[int, Dict[int, int]] = {}
+        self.stamp: Dict[str, Tuple[int, int]] = {}
+        self.launches = 0
+        self.violations: List[str] = []
+
+    @staticmethod
+    def _key(stream) -> int:
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
+
+    def _vc(self, k: int) -> Dict[int, int]:
+        return self.clock.setdefault(k, {k: 0})
+
+    def produced(self, names: Iterable[str], stream=None):
+        k = self._key(stream)
+        vc = self._vc(k)
+        vc[k] = vc.get(k, 0) + 1
+        for n in names:
+            self.stamp[n] = (k, vc[k])
+
+    def wait(self, waiter, waitee):
+        w, e = self._vc(self._key(waiter)), self._vc(self._key(waitee))
+        for s, c in e.items():
+            if w.get(s, 0) < c:
+                w[s] = c
+
+    def check_launch(self, names: Iterable[str], stream=None):
+        self.launches += 1
+        vc = self._vc(self._key(stream))
+        for n in names:
+            st = self.stamp.get(n)
+            if st is not None and vc.get(st[0], 0) < st[1]:
+                self.violations.append(f"{n}: produced on stream {st[0]:#x} at {st[1]}, bucket issued on a stream "
+                                       f"ordered only up to {vc.get(st[0], 0)}")
+
+    def install(self):
+        """Observe every cross-stream wait the native executor issues (``models.unet._stream_wait``)."""
+        from ..models import unet
+        unet._STREAM_OBSERVERS.append(self)
+        return self
+
+    def uninstall(self):
+        from ..models import unet
+        if self in unet._STREAM_OBSERVERS:
+            unet._STREAM_OBSERVERS.remove(self)
 
 
 def broadcast_module_state(tensors: Iterable[torch.Tensor], src: int = 0, group=None):

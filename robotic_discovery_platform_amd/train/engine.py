@@ -75,8 +75,11 @@ class NativeTrainer:
             broadcast_module_state([st.flat] + [b for _, b in model.named_buffers()])
             model.refresh_weights()
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
+            # buckets are issued from a stream ordered after both gradient streams (main: BN / head,
+            # side: conv weights), never from whichever stream a hook happens to run on
             self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb,
-                                         comm_dtype=torch.bfloat16 if grad_comm == "bf16" else None)
+                                         comm_dtype=torch.bfloat16 if grad_comm == "bf16" else None,
+                                         launch_ctx=self.ex.comm_stream)
             self.ex.set_sync_bn(enabled=sync_bn)
         if graph == "auto":
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
@@ -98,9 +101,10 @@ class NativeTrainer:
             except Exception:  # interpreter teardown
                 pass
 
-    def _hook(self, spec):
-        """Gradient hook of one layer (head, BN, conv or ConvTranspose2d: ``spec.param_names()``)."""
-        self.bucketer.mark_ready(spec.param_names())
+    def _hook(self, spec, stream=None):
+        """Gradient hook of one layer (head, BN, conv or ConvTranspose2d: ``spec.param_names()``), final
+        once the work issued so far on ``stream`` has run."""
+        self.bucketer.mark_ready(spec.param_names(), stream)
 
     def _step_body(self):
         ex = self.ex

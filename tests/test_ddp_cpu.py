@@ -263,3 +263,66 @@ def test_bucket_big_param_starts_new_bucket():
     ranges = [("a", 0, 1000), ("b", 1000, 1100), ("c", 1100, 1200)]  # reverse order: c, b, a
     b = FlatBucketer(torch.zeros(1200), ranges, bucket_mb=400 * 4 / 2 ** 20)
     assert b.bucket_params == [["c", "b"], ["a"]]
+
+
+# ----------------------------------------------------------------------------- stream ordering model
+def _simulate_issue(bilinear: bool, ordered: bool):
+    """The native executor's two-stream protocol on fake stream ids, checked by StreamOrderChecker:
+    BN / head gradients on the main stream, each conv / ConvTranspose weight gradient on the side
+    stream after a fork from main; buckets issued either on the comm stream (side after a fork from
+    main: ``UNetExecutor.comm_stream``) or, unordered, on the stream the hook runs on (main)."""
+    from robotic_discovery_platform_amd.models.unet import (ALIGN, BNHook, ConvSpec, UpTSpec, backward_hook_order,
+                                                             unet_conv_specs)
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer, StreamOrderChecker
+    MAIN, SIDE = 1, 2
+    ref = UNetRef(3, 1, bilinear=bilinear)
+    ranges, off = [], 0
+    for n, p in ref.named_parameters():
+        ranges.append((n, off, off + p.numel()))
+        off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+    ck = StreamOrderChecker()
+    b = FlatBucketer(torch.zeros(off), ranges, 16.0)
+    b.checker = ck
+
+    def launch(k):
+        if ordered:
+            ck.wait(SIDE, MAIN)
+            ck.check_launch(b.bucket_params[k], SIDE)
+        else:
+            ck.check_launch(b.bucket_params[k], MAIN)
+    b._launch = launch
+    specs = unet_conv_specs(4, 64, 3, bilinear)
+    ups = [] if bilinear else [UpTSpec(f"up{i}.up", 64 * 2 ** (5 - i), 64 * 2 ** (4 - i)) for i in range(1, 5)]
+    b.reset()
+    for sp in backward_hook_order(specs, ups, 4):
+        if isinstance(sp, (ConvSpec, UpTSpec)):  # weight gradient forked onto the side stream
+            ck.wait(SIDE, MAIN)
+            b.mark_ready(sp.param_names(), SIDE)
+        else:  # head, BN gamma / beta: main stream
+            assert isinstance(sp, BNHook) or sp.name == "outc"
+            b.mark_ready(sp.param_names(), MAIN)
+    return ck, len(b.buckets)
+
+
+@pytest.mark.parametrize("bilinear", [True, False])
+def test_stream_order_checker_on_executor_protocol(bilinear):
+    ck, nb = _simulate_issue(bilinear, ordered=True)
+    assert ck.launches == nb and ck.violations == []
+    ck, nb = _simulate_issue(bilinear, ordered=False)  # round-3 race: issued from main behind side wgrads
+    assert ck.launches == nb and ck.violations
+
+
+def test_stream_order_checker_clocks():
+    from robotic_discovery_platform_amd.parallel.ddp import StreamOrderChecker
+    ck = StreamOrderChecker()
+    ck.produced(["w"], 2)           # produced on stream 2
+    ck.check_launch(["w"], 1)       # stream 1 never waited on 2
+    assert len(ck.violations) == 1
+    ck.wait(3, 2)                   # 3 waits on 2, 1 waits on 3: transitively ordered
+    ck.wait(1, 3)
+    ck.check_launch(["w"], 1)
+    assert len(ck.violations) == 1
+    ck.produced(["w"], 2)           # re-produced later on 2: the old wait no longer covers it
+    ck.check_launch(["w"], 1)
+    assert len(ck.violations) == 2

@@ -137,7 +137,7 @@ def _order_worker(rank, port, out):
         tr = NativeTrainer(nat, 2, 64, 64, lr=1e-3, graph=False, bucket_mb=16.0, ddp_force=True)
         hooks, launches = [], []
         hook0, launch0 = tr._hook, tr.bucketer._launch
-        tr._hook = lambda sp: (hooks.append(sp.name), hook0(sp))
+        tr._hook = lambda sp, st=None: (hooks.append(sp.name), hook0(sp, st))
         tr.bucketer._launch = lambda b: (launches.append((b, len(hooks))), launch0(b))
         x, t = _data(2)
         tr.set_batch(x.to(dev), t.to(dev))
