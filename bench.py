@@ -57,7 +57,8 @@ def parse():
                    help="1: run the DDP path (RCCL process group, bucketed all-reduce hooks) even at world 1")
     p.add_argument("--extras", type=int, default=-1,
                    help="also report ref_batch_imgs_per_s (bs 4 step) and train_model_imgs_per_s (train_model on an "
-                        "on-disk synthetic PNG dataset, incl. data gather/H2D); default: on for 1-GPU native runs")
+                        "on-disk synthetic PNG dataset, incl. data gather/H2D) and transposed_imgs_per_s (the "
+                        "transposed-conv decoder at the same batch); default: on for 1-GPU native runs")
     p.add_argument("--serve", type=int, default=-1,
                    help="also measure e2e serving FPS / p50 latency (default: on for single-GPU runs)")
     return p.parse_args()
@@ -149,6 +150,29 @@ def measure_ref_batch(args, dev, steps: int = 50, warmup: int = 10) -> dict:
     return {"ref_batch_imgs_per_s": round(4 * steps / dt, 2), "ref_batch_ms_per_step": round(dt / steps * 1e3, 3)}
 
 
+def measure_transposed(args, dev, steps: int = 20, warmup: int = 5) -> dict:
+    """BASELINE.json's north-star decoder ("transposed-conv decoder", the reference's
+    ``bilinear=False`` path, fixed: ``segmentation_model.py:63-65,75-76``) through the same timed step
+    at the headline's per-GPU batch: forward, BCE, backward, Adam, device syncs around the K steps."""
+    if args.decoder == "transposed":
+        return {}
+    from robotic_discovery_platform_amd.train.engine import build_bench_step
+    step = build_bench_step(batch=args.batch, size=args.size, decoder="transposed", device=dev, world=1,
+                            graph="auto", bucket_mb=args.bucket_mb, loss=args.loss)
+    for _ in range(warmup):
+        step()
+    sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync(dev)
+    dt = time.perf_counter() - t0
+    return {"transposed_imgs_per_s": round(args.batch * steps / dt, 2),
+            "transposed_ms_per_step": round(dt / steps * 1e3, 3),
+            "transposed_config": f"UNet(3,1) transposed decoder (fixed), 31.04M params, bs {args.batch}, "
+                                 f"{steps} timed steps"}
+
+
 def measure_train_model(args, dev, samples: int = 160, epochs: int = 3) -> dict:
     """``train_model`` (the train_segmenter.py entry point) on an on-disk synthetic PNG dataset at the
     reference's batch 4: device-resident data build, per-epoch shuffled batches gathered on the GPU,
@@ -214,8 +238,8 @@ def main():
     extra = {}
     extras = args.extras if args.extras >= 0 else int(world == 1 and args.impl == "native" and dev.type == "cuda")
     if extras and rank == 0:
-        progress.phase = "extras (reference batch, train_model)"
-        for fn in (measure_ref_batch, measure_train_model):
+        progress.phase = "extras (reference batch, transposed decoder, train_model)"
+        for fn in (measure_ref_batch, measure_transposed, measure_train_model):
             try:  # never let it break the training result line
                 extra.update(fn(args, dev))
             except Exception as e:  # pragma: no cover - reported in the JSON

@@ -29,7 +29,7 @@ int rdp_preprocess(const void*, int, int, const int*, const int*, const float*, 
                    int, int, void*, hipStream_t);
 int rdp_mask_upsample(const void*, int, int, void*, int, int, unsigned*, hipStream_t);
 int rdp_conv_wgrad(const void*, const void*, long, long, int, int, int, int, const void*, long, int, float*, long,
-                   float*, int, int, int, int, int, int, int, int, int, int, const float*, const float*, hipStream_t);
+                   float*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 long rdp_conv_wgrad_slab_elems(int, int, int, int, int, int, int, int);
 long rdp_conv_wgrad_halo_slab_elems(int, int, int, int, int);
 int rdp_wgrad_first_bn(const void*, long, int, const void*, long, int, const void*, long, int, const float*, const float*,
@@ -133,18 +133,26 @@ auto on_device(R (*fn)(A...)) {
 // step, with idle gaps wherever a run of short kernels outpaced it). Unlike a hipGraph, replay keeps
 // the eager launch order on the same two streams / hardware queues (graph replay spread the side
 // branch over extra queues and measured slower, train/engine.py).
+//
+// A plan may also hold host call points (kind 2, ``plan_mark``): work the runtime cannot replay itself
+// (the DDP bucket all-reduces, issued through torch.distributed). Recording marks the point, then runs
+// that work with recording paused (``plan_pause`` / ``plan_resume``); replay calls back into Python with
+// the mark's tag at the same position in the launch sequence, so the collectives keep their place
+// between the recorded kernels.
 struct PlanOp {
-  int kind;        // 0: launch, 1: waiter waits for everything issued so far on waitee
+  int kind;        // 0: launch, 1: waiter waits for everything issued so far on waitee, 2: host call
   hipStream_t s;   // launch stream / waiter
   hipStream_t s2;  // waitee
   hipEvent_t ev;
   std::function<long(hipStream_t)> fn;
+  int tag = -1;    // kind 2: the caller's call-point id
 };
 struct Plan {
   std::vector<PlanOp> ops;
 };
 std::vector<std::unique_ptr<Plan>> g_plans;
 Plan* g_rec = nullptr;
+Plan* g_paused = nullptr;  // the plan being recorded while a host call point runs
 
 template <class F>
 long plan_launch(F&& f) {
@@ -198,7 +206,7 @@ void stream_wait(long waiter, long waitee) {
 }
 
 void plan_begin() {
-  TORCH_CHECK(g_rec == nullptr, "plan_begin: already recording");
+  TORCH_CHECK(g_rec == nullptr && g_paused == nullptr, "plan_begin: already recording");
   g_plans.emplace_back(new Plan());
   g_rec = g_plans.back().get();
 }
@@ -210,6 +218,10 @@ int plan_end() {
 }
 
 void plan_abort() {
+  if (g_paused) {
+    g_rec = g_paused;
+    g_paused = nullptr;
+  }
   if (g_rec) {
     for (auto& op : g_rec->ops) if (op.ev) hipEventDestroy(op.ev);
     g_rec->ops.clear();
@@ -217,15 +229,39 @@ void plan_abort() {
   }
 }
 
-void plan_replay(int id) {
+bool plan_recording() { return g_rec != nullptr; }
+
+void plan_mark(int tag) {
+  TORCH_CHECK(g_rec != nullptr, "plan_mark: not recording");
+  PlanOp op{2, nullptr, nullptr, nullptr, nullptr};
+  op.tag = tag;
+  g_rec->ops.push_back(std::move(op));
+}
+
+void plan_pause() {
+  TORCH_CHECK(g_rec != nullptr && g_paused == nullptr, "plan_pause: not recording");
+  g_paused = g_rec;
+  g_rec = nullptr;
+}
+
+void plan_resume() {
+  TORCH_CHECK(g_paused != nullptr && g_rec == nullptr, "plan_resume: not paused");
+  g_rec = g_paused;
+  g_paused = nullptr;
+}
+
+void plan_replay(int id, py::object host_call) {
   TORCH_CHECK(id >= 0 && id < (int)g_plans.size() && g_plans[id], "plan_replay: bad plan id");
-  TORCH_CHECK(g_rec == nullptr, "plan_replay while recording");
+  TORCH_CHECK(g_rec == nullptr && g_paused == nullptr, "plan_replay while recording");
   for (auto& op : g_plans[id]->ops) {
     if (op.kind == 0) {
       op.fn(op.s);
-    } else {
+    } else if (op.kind == 1) {
       hipEventRecord(op.ev, op.s2);
       hipStreamWaitEvent(op.s, op.ev, 0);
+    } else {
+      TORCH_CHECK(!host_call.is_none(), "plan_replay: the plan has host call points, pass a callback");
+      host_call(op.tag);
     }
   }
 }
@@ -403,19 +439,9 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
 }
 
 
-// in_coef (optional, fp32 [4C] of x1's producer BN): x1 is that layer's pre-BN output and the kernel
-// forms relu(bn(x1)) itself (the row-ring kernel, 64 -> 64 channels; other shapes raise)
 int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor dy, int taps, int packed, int cin_real,
-               torch::Tensor slab, torch::Tensor out, int accumulate, int splits, int variant,
-               c10::optional<torch::Tensor> in_coef) {
+               torch::Tensor slab, torch::Tensor out, int accumulate, int splits, int variant) {
   Act a1 = act(x1, "x1"), a2;
-  const float *isc = nullptr, *ish = nullptr;
-  if (in_coef && in_coef->defined()) {
-    check_f32(*in_coef, "in_coef");
-    TORCH_CHECK(in_coef->numel() >= 4l * a1.C, "in_coef: [4 C] f32");
-    isc = in_coef->data_ptr<float>() + 2 * a1.C;
-    ish = in_coef->data_ptr<float>() + 3 * a1.C;
-  }
   if (x2) a2 = act(*x2, "x2");
   Act d = act(dy, "dy");
   TORCH_CHECK(d.N == a1.N && d.H == a1.H && d.W == a1.W, "dy spatial mismatch");
@@ -441,7 +467,7 @@ int conv_wgrad(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor 
     const long sln = slab.numel();
     float* const outp = out.data_ptr<float>();
     r = RDP_PLAN(rdp_conv_wgrad(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, pdy, bdy, d.pitch, slp, sln, outp, acc, nn,
-                                a1.H, a1.W, d.C, taps, packed, cin_real, splits, variant, isc, ish, st));
+                                a1.H, a1.W, d.C, taps, packed, cin_real, splits, variant, st));
     TORCH_CHECK(r >= 0, "conv_wgrad: unsupported shape or slab too small (code ", r, ")");
   }
   return r;
@@ -1030,8 +1056,8 @@ void resize_area_u8(torch::Tensor in, torch::Tensor ys, torch::Tensor yn, torch:
 
 // grayscale 8/16-bit PNG -> u8 / int16 (u16 bits) CPU tensor, decoded without the GIL; None when the
 // PNG is not one this reader handles (or is corrupt): the caller falls back to PIL. `parallel`: inflate
-// the bands of a banded stream (codecs.cpp) concurrently.
-py::object png_decode(py::bytes data, bool parallel) {
+// the bands of a banded stream (codecs.cpp) concurrently (2: only that way, else None -- tests).
+py::object png_decode(py::bytes data, int parallel) {
   char* buf = nullptr;
   Py_ssize_t n = 0;
   if (PyBytes_AsStringAndSize(data.ptr(), &buf, &n) != 0) throw py::error_already_set();
@@ -1042,7 +1068,7 @@ py::object png_decode(py::bytes data, bool parallel) {
   {
     py::gil_scoped_release nogil;
     r = rdp_png_decode((const uint8_t*)buf, n, (uint8_t*)t.data_ptr(), (long)t.numel() * t.element_size(),
-                       parallel ? 1 : 0);
+                       parallel);
   }
   if (r != 0) return py::none();
   return py::cast(t);
@@ -1163,7 +1189,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_begin", &plan_begin);
   m.def("plan_end", &plan_end);
   m.def("plan_abort", &plan_abort);
-  m.def("plan_replay", &plan_replay);
+  m.def("plan_replay", &plan_replay, py::arg("id"), py::arg("host_call") = py::none());
+  m.def("plan_recording", &plan_recording);
+  m.def("plan_mark", &plan_mark, "record a host call point (replay calls host_call(tag) there)");
+  m.def("plan_pause", &plan_pause);
+  m.def("plan_resume", &plan_resume);
   m.def("plan_size", &plan_size);
   m.def("plan_free", &plan_free);
   m.def("conv_fwd", on_device(&conv_fwd), py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
@@ -1176,7 +1206,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_stats_rows", &conv_stats_rows);
   m.def("conv_wgrad", on_device(&conv_wgrad), py::arg("x1"), py::arg("x2"), py::arg("dy"), py::arg("taps"),
         py::arg("packed"), py::arg("cin_real"), py::arg("slab"), py::arg("out"), py::arg("accumulate"),
-        py::arg("splits"), py::arg("variant"), py::arg("in_coef") = py::none());
+        py::arg("splits"), py::arg("variant"));
   m.def("conv_fwd_bnin", on_device(&conv_fwd_bnin), py::arg("x_pre"), py::arg("w"), py::arg("y"), py::arg("stats"),
         py::arg("in_coef"), py::arg("a_out") = py::none());
   m.def("wgrad_first_bn", on_device(&wgrad_first_bn));
@@ -1231,7 +1261,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
         py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
         py::arg("presorted") = false);
-  m.def("png_decode", &png_decode, py::arg("data"), py::arg("parallel") = true);
+  m.def("png_decode", &png_decode, py::arg("data"), py::arg("parallel") = 1,
+        "parallel: 0 serial inflate, 1 banded (rdPs index) with serial fallback, 2 banded only (tests)");
   m.def("jpeg_decode", &jpeg_decode, py::arg("data"), py::arg("parallel") = true, py::arg("pin") = false);
   m.def("jpeg_to_rgb", on_device(&jpeg_to_rgb));
   m.def("jpeg_plane_bytes", &rdp_jpeg_plane_bytes);

@@ -148,11 +148,29 @@ bool inflate_band(const uint8_t* in, size_t in_len, uint8_t* out, size_t out_len
   zs.next_out = out;
   zs.avail_out = (uInt)out_len;
   const int zr = inflate(&zs, final ? Z_FINISH : Z_SYNC_FLUSH);
-  const bool ok = zs.avail_out == 0 && (final ? zr == Z_STREAM_END : (zr == Z_OK || zr == Z_BUF_ERROR ||
-                                                                       zr == Z_STREAM_END));
+  bool ok = zs.avail_out == 0 && (final ? zr == Z_STREAM_END : (zr == Z_OK || zr == Z_BUF_ERROR ||
+                                                                 zr == Z_STREAM_END));
   const bool ended = zr == Z_STREAM_END;
+  if (ok && !final && zs.avail_in > 0) {
+    // the band's rows are full: what is left of its input (the flush's empty stored block) must
+    // decode to nothing -- input that would produce more bytes belongs to no row
+    uint8_t spare = 0;
+    zs.next_out = &spare;
+    zs.avail_out = 1;
+    const int z2 = inflate(&zs, Z_SYNC_FLUSH);
+    ok = zs.avail_out == 1 && (z2 == Z_OK || z2 == Z_BUF_ERROR);
+  }
+  // every byte of the band's input consumed, as the serial decoder (libpng / cv2) would read it
+  ok = ok && zs.avail_in == 0;
   inflateEnd(&zs);
   return ok && (final || !ended);  // a non-final band must not carry the final block
+}
+
+// the zlib stream header (RFC 1950): deflate, window <= 32 KiB, valid check bits, no preset dictionary
+bool zlib_header_ok(const std::vector<uint8_t>& z) {
+  if (z.size() < 6) return false;
+  const unsigned cmf = z[0], flg = z[1];
+  return (cmf & 15) == 8 && (cmf >> 4) <= 7 && ((cmf << 8) | flg) % 31 == 0 && !(flg & 0x20);
 }
 
 // parallel decode along the rdPs index; false: fall back to the serial decoder
@@ -250,9 +268,10 @@ int rdp_png_decode(const uint8_t* d, long n, uint8_t* out, long out_bytes, int p
   }
   if (!end && z.empty()) return -1;
   std::vector<Band> bands;
-  if (parallel && idx >= 0 && parse_index(d + idx, idx_len, hd.h, z.size(), bands) &&
+  if (parallel && idx >= 0 && zlib_header_ok(z) && parse_index(d + idx, idx_len, hd.h, z.size(), bands) &&
       decode_banded(z, bands, hd, bpp, stride, out))
     return 0;
+  if (parallel == 2) return -3;  // banded path only (tests): not taken
   const size_t raw_len = (stride + 1) * hd.h;
   std::vector<uint8_t> raw(raw_len);
   z_stream zs;

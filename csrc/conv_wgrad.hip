@@ -430,15 +430,9 @@ struct WgradRingArgs {
   int cinTiles, coutTiles, splits, pos_per_split, npos;
   int WS;                           // 64-pixel segments per image row
   uint32_t fh_m, fh_s, fs_m, fs_s;  // fast div by H and by WS
-  const float* iscale;              // BNIN: x1 is the producer's pre-BN output; BN + ReLU applied in LDS
-  const float* ishift;
 };
 
-// BNIN: x is the producer layer's pre-BN output (the forward ring conv took it the same way,
-// conv_ring.hip): each staged x chunk becomes relu(y * scale + shift), bf16-rounded as
-// bn_relu_apply_kernel rounds it, in LDS -- by the wave that staged it, after its own vmcnt wait and
-// before the step's barrier -- so the activation a is never written to HBM.
-template <int BN, bool BNIN = false>
+template <int BN>
 __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradRingArgs a) {
   constexpr int NWV = BN / 16;
   constexpr int XREG = 72 * 128;   // one staged input row region: pixels w0-1 .. w0+70 (66 used)
@@ -448,10 +442,9 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradR
   constexpr int XPIECES = 9, NPIECES = XPIECES + 8 * (BN / 64);
   constexpr int PPW = (NPIECES + NWV - 1) / NWV;
   constexpr int MINPW = NPIECES / NWV;  // DMAs issued per step by the wave that issues fewest
-  __shared__ __attribute__((aligned(16))) char smem[NX * XREG + ND * DT + (BNIN ? 128 * 4 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[NX * XREG + ND * DT];
   char* const xring = smem;
   char* const dring = smem + NX * XREG;
-  float* const icoef = (float*)(smem + NX * XREG + ND * DT);  // BNIN: [scale | shift] of the 64 channels
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -513,37 +506,6 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradR
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (BNIN) {
-    for (int c = threadIdx.x; c < 64; c += BN * 4) { icoef[c] = a.iscale[ch0 + c]; icoef[64 + c] = a.ishift[ch0 + c]; }
-    __syncthreads();
-  }
-  // BNIN: this wave's staged chunks of input row P -> relu(y * scale + shift) (padding stays zero)
-  auto bn_row = [&](int P) {
-    int m0, h, w0;
-    locate(P, m0, h, w0);
-#pragma unroll
-    for (int t = 0; t < PPW; ++t) {
-      const int piece = wave + t * NWV;
-      if (piece >= XPIECES) continue;
-      const int j = piece * 8 + rowl;
-      if (!((j < 66) & inb(w0 - 1 + j, a.W) & inb(h, a.H))) continue;
-      const int g = cpos ^ swz(j);
-      uint4* p = (uint4*)(xring + ((P + NX) % NX) * XREG + piece * 1024 + lane * 16);
-      const uint4 v = *p;
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-      const float* sc = icoef + 8 * g;
-      const float* sh = icoef + 64 + 8 * g;
-      uint32_t o[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float lo = fmaxf(fmaf(__uint_as_float(wv[k] << 16), sc[2 * k], sh[2 * k]), 0.f);
-        const float hi = fmaxf(fmaf(__uint_as_float(wv[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]), 0.f);
-        o[k] = pack2bf(lo, hi);
-      }
-      *p = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-  };
-
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tpp = lane & 3;
   const int cf = wave & 3, cg = wave >> 2;
   const int ca = 2 * cf + (tpp >> 1);
@@ -562,14 +524,6 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_ring_kernel(const WgradR
     // step ks's data: everything but the (up to MINPW-per-wave) DMAs of step ks + 1
     if (ks + 1 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(MINPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    if constexpr (BNIN) {  // this wave's DMAs of row P + 1 (at the start: rows P - 1, P too) have landed
-      if (ks == 0) {
-        bn_row(P - 1);
-        bn_row(P);
-      }
-      bn_row(P + 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
     raw_barrier();
     if (ks + 2 < nks) { issue(P + 3, true, false); issue(P + 2, false, true); }
     int m0, h, w0;
@@ -708,8 +662,7 @@ extern "C" void rdp_wgrad_reduce(float* slab, float* out, int splits, int Cout, 
 extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
                               int pitch2, const void* dy, long dybytes, int dypitch, float* slab, long slab_elems,
                               float* out, int accumulate, int N, int H, int W, int Cout, int taps, int packed,
-                              int cin_real, int splits, int variant, const float* iscale, const float* ishift,
-                              hipStream_t s) {
+                              int cin_real, int splits, int variant, hipStream_t s) {
   WgradArgs a;
   a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
   a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
@@ -726,9 +679,6 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   }
   if (Cout % 64) return -1;
   if (xbytes1 >= (1l << 31) || xbytes2 >= (1l << 31) || dybytes >= (1l << 31)) return -1;
-  // BN on the input (the row-ring kernel only): 64 -> 64 channels, one source, W % 64 == 0
-  if (iscale && (!ishift || packed || taps != 9 || C1 != 64 || C2 != 0 || Cout != 64 || W % 64 || variant != 0))
-    return -4;
   // halo-reuse kernel: 3x3, whole 64-pixel row segments
   const bool halo_ok = !packed && taps == 9 && (W % 64 == 0 || (W >= 32 && 64 % W == 0 && (H * W) % 64 == 0)) &&
                        variant != 4;
@@ -759,7 +709,6 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
     FastDiv fw = make_fastdiv(W), fh = make_fastdiv(H);
     h.fw_m = fw.m; h.fw_s = fw.s; h.fh_m = fh.m; h.fh_s = fh.s;
     const int nblk = tiles * h.splits;
-    if (iscale && !(variant == 0 && W % 64 == 0 && BN == 64 && C2 == 0 && C1 == 64)) return -4;  // BNIN: ring only
     if (variant == 0 && W % 64 == 0 && BN == 64) {  // row-ring variant: same split of the positions
       WgradRingArgs g;
       g.x1 = h.x1; g.x2 = h.x2; g.xbytes1 = h.xbytes1; g.xbytes2 = h.xbytes2;
@@ -770,9 +719,7 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
       g.pos_per_split = h.segs_per_split; g.npos = h.nseg; g.WS = W / 64;
       FastDiv fs = make_fastdiv(W / 64);
       g.fh_m = fh.m; g.fh_s = fh.s; g.fs_m = fs.m; g.fs_s = fs.s;
-      g.iscale = iscale; g.ishift = ishift;
-      if (iscale) hipLaunchKernelGGL((conv_wgrad_ring_kernel<64, true>), dim3(nblk), dim3(256), 0, s, g);
-      else hipLaunchKernelGGL((conv_wgrad_ring_kernel<64>), dim3(nblk), dim3(256), 0, s, g);
+      hipLaunchKernelGGL((conv_wgrad_ring_kernel<64>), dim3(nblk), dim3(256), 0, s, g);
     } else {
       const bool mr = W < 64;
       if (BN == 128 && mr) hipLaunchKernelGGL((conv_wgrad_halo_kernel<128, true>), dim3(nblk), dim3(512), 0, s, h);

@@ -111,11 +111,39 @@ struct Jpeg {
 
 inline int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
-// 0 ok, -1 corrupt, -2 unsupported
+// EXIF orientation (TIFF tag 0x0112 of IFD0) of an APP1 payload; 1 (upright) when absent / unreadable
+int exif_orientation(const uint8_t* s, int sl) {
+  if (sl < 14 || std::memcmp(s, "Exif\0\0", 6) != 0) return 1;
+  const uint8_t* t = s + 6;
+  const long tl = sl - 6;
+  const bool le = t[0] == 'I' && t[1] == 'I';
+  if (!le && !(t[0] == 'M' && t[1] == 'M')) return 1;
+  auto u16 = [&](long o) { return le ? (t[o] | (t[o + 1] << 8)) : ((t[o] << 8) | t[o + 1]); };
+  auto u32 = [&](long o) {
+    return le ? ((uint32_t)t[o] | ((uint32_t)t[o + 1] << 8) | ((uint32_t)t[o + 2] << 16) | ((uint32_t)t[o + 3] << 24))
+              : (((uint32_t)t[o] << 24) | ((uint32_t)t[o + 1] << 16) | ((uint32_t)t[o + 2] << 8) | (uint32_t)t[o + 3]);
+  };
+  const long ifd = u32(4);
+  if (ifd < 8 || ifd + 2 > tl) return 1;
+  const int cnt = u16(ifd);
+  for (int e = 0; e < cnt; ++e) {
+    const long o = ifd + 2 + 12l * e;
+    if (o + 12 > tl) return 1;
+    if (u16(o) == 0x0112) return u16(o + 8);
+  }
+  return 1;
+}
+
+// 0 ok, -1 corrupt, -2 unsupported (the caller decodes with PIL). The GPU pixel stage converts YCbCr;
+// streams libjpeg (and so the reference's cv2.imdecode) takes as RGB -- an Adobe APP14 marker with
+// transform 0, or no JFIF marker and component ids 'R', 'G', 'B' -- and streams with an EXIF rotation
+// (cv2.imdecode applies it) are left to the fallback.
 int parse(const uint8_t* d, long n, Jpeg& j) {
   if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return -1;
   long p = 2;
   bool sof = false;
+  bool jfif = false;
+  int adobe = -1;  // APP14 "Adobe" colour transform (-1: no such marker)
   while (p + 4 <= n) {
     if (d[p] != 0xFF) return -1;
     int m = d[p + 1];
@@ -194,8 +222,23 @@ int parse(const uint8_t* d, long n, Jpeg& j) {
       case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9: case 0xCA: case 0xCB: case 0xCD:
       case 0xCE: case 0xCF:
         return -2;  // progressive / lossless / hierarchical / arithmetic
+      case 0xE0:  // APP0
+        if (sl >= 5 && std::memcmp(s, "JFIF\0", 5) == 0) jfif = true;
+        break;
+      case 0xE1:  // APP1: EXIF orientation other than upright -> the fallback rotates like cv2.imdecode
+        if (exif_orientation(s, sl) != 1) return -2;
+        break;
+      case 0xEE:  // APP14
+        if (sl >= 12 && std::memcmp(s, "Adobe", 5) == 0) adobe = s[11];
+        break;
       case 0xDA: {  // SOS
         if (!sof || sl < 1) return -1;
+        if (j.ncomp == 3) {  // libjpeg's colour-space guess (jdapimin.c default_decompress_parms)
+          const bool rgb = jfif ? false
+                         : adobe >= 0 ? adobe == 0
+                         : (j.comp[0].id == 'R' && j.comp[1].id == 'G' && j.comp[2].id == 'B');
+          if (rgb) return -2;
+        }
         const int ns = s[0];
         if (ns != j.ncomp || sl < 1 + 2 * ns + 3) return -2;  // one interleaved scan only
         for (int k = 0; k < ns; ++k) {

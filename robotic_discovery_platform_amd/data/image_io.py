@@ -16,7 +16,7 @@ import io
 from typing import Tuple
 
 import numpy as np
-from PIL import Image
+from PIL import Image, ImageOps
 
 
 # ----------------------------------------------------------------------------- codecs
@@ -76,6 +76,8 @@ def decode_image(data: bytes, color: bool = True, order: str = "BGR") -> np.ndar
     im = Image.open(io.BytesIO(data))
     if color:
         im.load()
+        if im.getexif().get(0x0112, 1) != 1:  # cv2.imdecode(IMREAD_COLOR) applies the EXIF orientation
+            im = ImageOps.exif_transpose(im)
         rgb = np.asarray(im if im.mode == "RGB" else im.convert("RGB"))
         return rgb if order == "RGB" else rgb[..., ::-1].copy()
     if im.mode in ("I;16", "I;16B", "I;16L", "I"):

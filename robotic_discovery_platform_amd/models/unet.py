@@ -353,8 +353,8 @@ class _Layer:
     splits: int = 1
     bwd_rows: int = 0  # BN-backward partial rows already produced by a fused producer of da
     # training: this conv reads its producer's PRE-BN output and applies that BN + ReLU itself (the
-    # row-ring kernels, 64 -> 64 channels at W % 64 == 0): bnin = the producer layer, whose `a` is never
-    # written; consumer_bnin marks the producer (no bn_relu_apply pass)
+    # row-ring kernels, 64 -> 64 channels at W % 64 == 0): bnin = the producer layer, whose `a` that
+    # kernel also writes; consumer_bnin marks the producer (no bn_relu_apply pass)
     bnin: Optional["_Layer"] = None
     consumer_bnin: bool = False
 
@@ -460,8 +460,7 @@ class UNetExecutor:
                     lb.bnin = la
                     la.consumer_bnin = True
         # ... and the forward also stores that activation (one extra write) so the weight gradient runs the
-        # plain row-ring kernel instead of re-forming it
-        self.bnin_write_a = os.environ.get("RDP_BNIN_WRITE_A", "1") == "1"
+        # plain row-ring kernel on it (re-forming it in the wgrad measured 1 % slower: dead_ends.md)
         # training, bilinear decoder: the BN + ReLU of the layer under each Up block is applied by the
         # upsample itself on its 4 source taps (that layer's activation is never written; its backward
         # reads only y). Pays at small batch, where each of the 4 apply launches is mostly launch /
@@ -631,7 +630,7 @@ class UNetExecutor:
             C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool)
             return pool is not None
         if L.bnin is not None:  # the producer's BN + ReLU applied by this conv (row-ring BNIN)
-            rows = C.conv_fwd_bnin(L.bnin.y, w, L.y, self.stats, L.bnin.coef, L.bnin.a if self.bnin_write_a else None)
+            rows = C.conv_fwd_bnin(L.bnin.y, w, L.y, self.stats, L.bnin.coef, L.bnin.a)
             assert rows > 0, "conv_fwd_bnin: ring kernel not applicable"
         else:
             rows = C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.y, None, self.stats, 0, None, 0, self.kws)
@@ -887,10 +886,6 @@ class UNetExecutor:
         if self.slab_main is not None and L is self.down_layers[0][0]:
             C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real, self.slab_main, gw, 0, L.splits, 0)
             wstream = main
-        elif L.bnin is not None and not self.bnin_write_a:  # x = relu(bn(producer y)), formed by the ring wgrad
-            src = L.bnin
-            self._on_wgrad_stream(lambda slab: C.conv_wgrad(src.y, None, L.dy, sp.taps, 0, sp.cin_real, slab, gw, 0,
-                                                            L.splits, 0, src.coef))
         else:
             self._on_wgrad_stream(lambda slab: C.conv_wgrad(L.x1, L.x2, L.dy, sp.taps, int(sp.packed), sp.cin_real,
                                                             slab, gw, 0, L.splits, 0))

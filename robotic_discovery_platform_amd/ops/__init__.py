@@ -1,8 +1,8 @@
 """Native HIP/CDNA4 op library (``robotic_discovery_platform_amd/_C.so``).
 
 ``native()`` returns the compiled extension. On a GPU box it MUST be present: there is no silent
-eager fallback for GPU tensors -- the plain-torch implementations in :mod:`.reference` are test
-oracles and the CPU path only.
+eager fallback for GPU tensors -- the plain-torch model (:mod:`..models.unet_ref`) and the numpy /
+scipy geometry (:mod:`..geometry.reference`) are test oracles and the CPU path only.
 """
 from __future__ import annotations
 

@@ -55,6 +55,9 @@ class FlatBucketer:
         # caller's current stream already is, e.g. single-stream autograd)
         self.launch_ctx = launch_ctx
         self.checker: Optional["StreamOrderChecker"] = None
+        # host_call(fn) runs a bucket launch; a launch-plan recorder (NativeTrainer) replaces it to keep
+        # the launch as a host call point of the plan (csrc/bindings.cpp plan_mark)
+        self.host_call: Optional[Callable[[Callable[[], None]], None]] = None
         self.group = group
         self.comm_dtype = comm_dtype if comm_dtype not in (None, grad_flat.dtype) else None
         # bf16 mirror of the whole gradient buffer (buckets are slices of it, like of ``grad``)
@@ -127,7 +130,10 @@ class FlatBucketer:
             b = self.param_bucket[n]
             self.pending[b] -= 1
             if self.pending[b] == 0:
-                self._launch(b)
+                if self.host_call is not None:
+                    self.host_call(lambda b=b: self._launch(b))
+                else:
+                    self._launch(b)
 
     def finish(self):
         for b, p in enumerate(self.pending):  # anything never marked (unused params) goes now

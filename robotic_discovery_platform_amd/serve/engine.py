@@ -183,8 +183,9 @@ class FramePipeline:
                           self.geo.res.data_ptr(), self.h_res.data_ptr(), 0)
             self.runner = r
         # the graphs for the sources this pipeline will be fed (the gRPC server: JPEG coefficients, or
-        # RGB arrays for streams the native decoder does not take) are captured here, at build time,
-        # never on a live request
+        # RGB arrays for streams the native decoder does not take) are captured here, at build time --
+        # for the configured frame size when the server starts; a pipeline for another frame size is
+        # built (and captured) by the first request of that size (EnginePool bounds how many exist)
         if graph:
             self._capture(SRC_RGB if rgb else SRC_BGR)
             if jpeg:
@@ -463,6 +464,11 @@ class EnginePool:
       each with its own ``n`` pipelines (executor buffers, HIP stream, hipGraph) per frame size.
       Streams are assigned to replicas round-robin when they open (``session()``); replicas never
       communicate, so N GPUs serve N times the streams.
+    * Frame sizes: the configured (H, W) keeps its pipelines; at most ``max_sizes`` other sizes have
+      pipelines at once per replica (each holds full-size device buffers and captured graphs), the
+      least recently used idle one is dropped for a new size, and a new size with every other size's
+      pipelines busy is refused (the frame gets an error status) -- a client varying the frame size
+      cannot grow device memory without bound.
     * ``session()`` gives a stream double-buffering: frame i+1 is staged and replayed on a second
       pipeline (own stream) while frame i's result is still on the device, so H2D, graph and D2H of
       consecutive frames overlap and the host tail of frame i overlaps the GPU work of frame i+1.
@@ -470,8 +476,10 @@ class EnginePool:
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 devices=None, rgb: bool = False, jpeg: bool = False):
+                 devices=None, rgb: bool = False, jpeg: bool = False, max_sizes: int = 3):
         self.model = model
+        self.home_size = (H, W)
+        self.max_sizes = max(0, max_sizes)
         self.rgb = rgb  # channel order of the frames this pool will be fed (graphs captured for it)
         self.args = dict(K=K, depth_scale=depth_scale, size=size, threshold=threshold, geo_cfg=geo_cfg)
         self.graph = graph
@@ -483,7 +491,7 @@ class EnginePool:
         self.devices = devs
         self.replicas = [model if devs[i] == home and i == 0 else replicate_model(model, devs[i])
                          for i in range(len(devs))]
-        self._pools = {}
+        self._pools: "collections.OrderedDict" = collections.OrderedDict()  # (r, H, W) -> Queue, LRU order
         self._mk_lock = threading.Lock()
         self._rr = 0
         self.sessions_opened = [0] * len(self.replicas)
@@ -499,12 +507,24 @@ class EnginePool:
 
     def _get(self, r: int, H, W) -> "queue.Queue":
         with self._mk_lock:
-            q = self._pools.get((r, H, W))
-            if q is None:
-                q = queue.Queue()
-                for _ in range(self.n):
-                    q.put(self._new(r, H, W))
-                self._pools[(r, H, W)] = q
+            key = (r, H, W)
+            q = self._pools.get(key)
+            if q is not None:
+                self._pools.move_to_end(key)
+                return q
+            if (H, W) != self.home_size:
+                other = [k for k in self._pools if k[0] == r and k[1:] != self.home_size]
+                if len(other) >= self.max_sizes:
+                    # drop the least recently used size whose pipelines are all idle (in the queue)
+                    victim = next((k for k in other if self._pools[k].qsize() == self.n), None)
+                    if victim is None:
+                        raise RuntimeError(f"frame size {H}x{W}: {len(other)} other frame sizes are in flight "
+                                           f"on this replica (max_sizes={self.max_sizes})")
+                    del self._pools[victim]
+            q = queue.Queue()
+            for _ in range(self.n):
+                q.put(self._new(r, H, W))
+            self._pools[key] = q
             return q
 
     def session(self) -> "EngineSession":
@@ -575,7 +595,14 @@ class EngineSession:
             return out
         while len(self.inflight) >= self.depth:
             out.append(self._collect_one())
-        q = self.pool._get(self.replica, *color_bgr.shape[:2])
+        try:
+            q = self.pool._get(self.replica, *color_bgr.shape[:2])
+        except RuntimeError as e:  # too many frame sizes in flight: this frame fails, the stream goes on
+            if split:
+                depth.cancel()
+            out += self.drain()
+            out.append((tag, e))
+            return out
         try:
             p = q.get_nowait()
         except queue.Empty:
@@ -595,8 +622,10 @@ class EngineSession:
                     raise
             else:
                 p.submit(color_bgr, depth, rgb)
-        except Exception as e:
+        except BaseException as e:  # the pipeline goes back to its pool whatever was raised
             q.put(p)
+            if not isinstance(e, Exception):
+                raise
             out += self.drain()
             out.append((tag, e))
             return out

@@ -48,8 +48,12 @@ class MetricsLog:
     def __init__(self, path: str):
         self.path = path
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-        if not os.path.exists(path):
-            with open(path, "w") as f:
+        try:  # exactly one writer creates the file and its header (server worker processes race here)
+            fd = os.open(path, os.O_WRONLY | os.O_APPEND | os.O_CREAT | os.O_EXCL, 0o644)
+        except FileExistsError:
+            pass
+        else:
+            with os.fdopen(fd, "w") as f:
                 f.write(CSV_HEADER)
         self._f = open(path, "a", buffering=1)
         self._lock = threading.Lock()
@@ -464,6 +468,7 @@ def _serve_workers(cfg: ServeConfig, block: bool = True):
     if cfg.port == 0:
         raise ValueError("workers > 1 need a fixed port (every worker binds it with SO_REUSEPORT)")
     ctx = mp.get_context("spawn")  # fresh interpreters: the parent never initialises the GPU
+    MetricsLog(cfg.metrics_log).close()  # the CSV and its header exist before any worker appends
     procs = [ctx.Process(target=_worker_main, args=(cfg,), name=f"rdp-serve-{i}", daemon=False)
              for i in range(cfg.workers)]
     for p in procs:

@@ -15,14 +15,17 @@ stream, while ~10 us of host time per launch stays ahead of the GPU even at bs 4
 therefore means eager launches for training; serving (N=1, latency-bound) keeps its graphs.
 With world > 1 the bucketed all-reduces overlap backward on RCCL's stream.
 
-Plan mode (``plan=True``; "auto" = on for single-process training without a graph): the third step
+Plan mode (``plan=True``; "auto" = on unless a graph or SyncBN is used): the third step
 is recorded by the native runtime (``csrc/bindings.cpp``: every kernel launch and cross-stream wait of
 the step, with its validated raw arguments and stream) and every later step is ONE ``plan_replay``
 call that re-issues the same launches on the same two streams from C++. The executor's Python
 (~8 us of host time per launch) then runs once instead of every step; at small batch the host no
 longer falls behind the GPU. Requirements, all true of the training step: static buffers, no
 host-side decisions that change between steps, a constant learning rate and the same current stream
-at every call. ``RDP_PLAN=0`` disables it. Measured (one MI355X, interleaved): host enqueue per bs-4
+at every call. ``RDP_PLAN=0`` disables it. Under DDP the bucket all-reduces (and ``finish``'s waits / bf16 widening)
+are torch.distributed calls the runtime cannot replay: each is recorded as a host call point of the
+plan (``plan_mark``), run with recording paused, and replay calls back into Python at that point, so
+every collective keeps its place between the recorded kernels. Measured (one MI355X, interleaved): host enqueue per bs-4
 step 1.55 -> 1.37 ms, step time unchanged (bs 4 2.53 ms, bs 64 20.1 ms either way) -- the remaining
 host cost is HIP's own ~7 us per kernel launch, which the GPU still outruns only in runs of
 sub-10-us kernels. (Compiling each single-stream run of the plan into a hipGraph and a high-priority
@@ -87,9 +90,13 @@ class NativeTrainer:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         if plan == "auto":
             plan = os.environ.get("RDP_PLAN", "1") != "0"
-        self.use_plan = (bool(plan) and not self.ddp and not self.use_graph
+        # SyncBN's statistics all-reduces sit inside the executor's kernel sequence: no plan with it
+        self.use_plan = (bool(plan) and not (self.ddp and sync_bn) and not self.use_graph
                          and torch.cuda.is_available() and model.store.device.type == "cuda")
         self.plan_id: Optional[int] = None
+        self._plan_calls: list = []  # host call points of the recorded plan (DDP collectives), by tag
+        if self.bucketer is not None and self.use_plan:
+            self.bucketer.host_call = self._host_call
         self._plan_version = None
         self.steps = 0
 
@@ -100,6 +107,25 @@ class NativeTrainer:
                 native(build_if_missing=False).plan_free(self.plan_id)
             except Exception:  # interpreter teardown
                 pass
+
+    def _host_call(self, fn):
+        """Run ``fn`` (torch.distributed work); while a plan is being recorded, also make it a host call
+        point of the plan, run with recording paused."""
+        from ..ops import native
+        C = native(build_if_missing=False)
+        if not C.plan_recording():
+            fn()
+            return
+        C.plan_mark(len(self._plan_calls))
+        self._plan_calls.append(fn)
+        C.plan_pause()
+        try:
+            fn()
+        finally:
+            C.plan_resume()
+
+    def _plan_host(self, tag: int):
+        self._plan_calls[tag]()
 
     def _hook(self, spec, stream=None):
         """Gradient hook of one layer (head, BN, conv or ConvTranspose2d: ``spec.param_names()``), final
@@ -114,7 +140,10 @@ class NativeTrainer:
             self.bucketer.reset()
             with trace.range("train.backward+allreduce"):
                 ex.backward(grad_hook=self._hook)  # every layer's hook fires inside, the head's first
-                self.bucketer.finish()
+                if self.use_plan:
+                    self._host_call(self.bucketer.finish)
+                else:
+                    self.bucketer.finish()
             with trace.range("train.adam"):
                 self.opt.step(gscale=1.0 / self.world, side=self._wprep_side())
         else:
@@ -144,10 +173,15 @@ class NativeTrainer:
                 C.plan_free(self.plan_id)
                 self.plan_id = None
             if self.plan_id is not None:
-                C.plan_replay(self.plan_id)
+                if self.bucketer is not None:
+                    self.bucketer.reset()
+                    C.plan_replay(self.plan_id, self._plan_host)
+                else:
+                    C.plan_replay(self.plan_id)
             elif self.steps < 2:  # first steps eagerly (first-launch costs, flags that settle)
                 self._step_body()
             else:
+                self._plan_calls = []
                 C.plan_begin()
                 try:
                     self._step_body()

@@ -75,11 +75,8 @@ def main():
         a_st = torch.empty_like(x1)
 
         def run(v):
-            if a.wgrad:  # v = variant (0 auto, 4 generic, 5 halo, 9 BN-on-input ring)
-                if v == 9:
-                    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, 0, coef)
-                else:
-                    C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
+            if a.wgrad:  # v = variant (0 auto, 4 generic, 5 halo)
+                C.conv_wgrad(x1, x2, dy, 9, 0, 0, slab, out, 0, splits, v)
             elif v in (9, 10):  # 10: BN-on-input forward that also stores the activation
                 if C.conv_fwd_bnin(x1, w, y, stats, coef, a_st if v == 10 else None) <= 0:
                     raise RuntimeError("bnin n/a")

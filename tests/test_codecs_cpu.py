@@ -62,17 +62,34 @@ def test_roundtrip_and_pil_agree(dtype, hw, bands):
 
 
 def test_banded_path_is_taken():
-    """A banded file with a broken zlib header: the serial inflate rejects it, the band decoder (which
-    starts after the header) does not -- so a good decode here came from the parallel path."""
+    """Our banded files decode through the parallel band path (mode 2: banded only). A broken zlib
+    header (or a preset-dictionary flag) is rejected there too, as libpng rejects it."""
     a = _img(480, 640, np.uint16)
     data = encode_png(a, 1, bands=8)
+    np.testing.assert_array_equal(C.png_decode(data, 2).numpy().view(np.uint16), a)
     for t, p, n in _chunks(data):
         if t == b"IDAT":
             z = bytearray(data[p + 8:p + 8 + n])
-    z[1] ^= 0x1F  # header check bits now wrong
-    bad = _rechunk(data, b"IDAT", bytes(z))
-    assert C.png_decode(bad, False) is None
-    np.testing.assert_array_equal(C.png_decode(bad, True).numpy().view(np.uint16), a)
+    for flip in (0x1F, 0x20):  # check bits wrong / FDICT set
+        zb = bytearray(z)
+        zb[1] ^= flip
+        bad = _rechunk(data, b"IDAT", bytes(zb))
+        assert C.png_decode(bad, 0) is None and C.png_decode(bad, 2) is None and C.png_decode(bad, 1) is None
+
+
+def test_banded_band_input_fully_consumed():
+    """Every band's compressed bytes must be consumed: a band index whose first band stops short of the
+    data (rows full early) is not taken, and the serial decode stays authoritative."""
+    a = _img(256, 320, np.uint16)
+    data = encode_png(a, 1, bands=4)
+    for t, p, n in _chunks(data):
+        if t == b"rdPs":
+            idx = bytearray(data[p + 8:p + 8 + n])
+    # move band 1's start one byte later: band 0 keeps a trailing byte it never decodes
+    off = int.from_bytes(idx[20:24], "big")
+    idx[20:24] = (off + 1).to_bytes(4, "big")
+    bad = _rechunk(data, b"rdPs", bytes(idx))
+    assert C.png_decode(bad, 2) is None
 
 
 def test_bad_index_falls_back_to_serial():

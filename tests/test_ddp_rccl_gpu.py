@@ -33,7 +33,10 @@ def _data(n=4, hw=64, seed=5):
     return torch.rand(n, 3, hw, hw, generator=g), (torch.rand(n, 1, hw, hw, generator=g) > 0.6).float()
 
 
-def _worker(rank, port, comm, out):
+STEPS = 5  # a launch plan is recorded at the third step and replayed from the fourth
+
+
+def _worker(rank, port, comm, out, plan=True):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
     dev = torch.device("cuda", 0)
@@ -46,16 +49,20 @@ def _worker(rank, port, comm, out):
         from robotic_discovery_platform_amd.train.engine import NativeTrainer
         torch.manual_seed(7)
         nat = UNetNative(3, 1, device=dev, init_from=UNetRef(3, 1))
-        tr = NativeTrainer(nat, 4, 64, 64, lr=1e-3, graph=False, bucket_mb=4.0, ddp_force=True, grad_comm=comm)
+        tr = NativeTrainer(nat, 4, 64, 64, lr=1e-3, graph=False, bucket_mb=4.0, ddp_force=True, grad_comm=comm,
+                           plan=plan)
         assert tr.ddp and tr.bucketer is not None and len(tr.bucketer.buckets) >= 4
+        assert tr.use_plan == plan
         assert tr.ex.side is not None  # hooks fire from the wgrad side stream
         x, t = _data()
         tr.set_batch(x.to(dev), t.to(dev))
         grads = []
-        for _ in range(3):
+        for _ in range(STEPS):
             tr.step()
             grads.append(nat.store.grad.clone())
         torch.cuda.synchronize()
+        if plan:  # the replayed steps ran the recorded plan with the all-reduces as host call points
+            assert tr.plan_id is not None and len(tr._plan_calls) == len(tr.bucketer.buckets) + 1
         torch.save({"flat": nat.store.flat.cpu(), "grads": [g.cpu() for g in grads]}, out)
     finally:
         dist.destroy_process_group()
@@ -73,7 +80,7 @@ def _plain(comm):
     x, t = _data()
     ex.set_input(x.to(dev), t.to(dev))
     grads = []
-    for _ in range(3):
+    for _ in range(STEPS):
         ex.forward()
         ex.backward()
         if comm == "bf16":
@@ -84,10 +91,12 @@ def _plain(comm):
     return nat.store.flat.cpu(), [g.cpu() for g in grads]
 
 
-@pytest.mark.parametrize("comm", ["fp32", "bf16"])
-def test_rccl_world1_ddp_step_matches_plain_step(tmp_path, comm):
+@pytest.mark.parametrize("comm,plan", [("fp32", True), ("bf16", True), ("fp32", False)])
+def test_rccl_world1_ddp_step_matches_plain_step(tmp_path, comm, plan):
+    """DDP step (eager or launch-plan replay with the bucket all-reduces as host call points) under
+    nccl at world 1 == the plain step, bit for bit."""
     out = str(tmp_path / f"ddp_{comm}.pt")
-    mp.spawn(_worker, args=(_free_port(), comm, out), nprocs=1, join=True)
+    mp.spawn(_worker, args=(_free_port(), comm, out, plan), nprocs=1, join=True)
     got = torch.load(out, weights_only=True)
     flat, grads = _plain(comm)
     for i, (a, b) in enumerate(zip(got["grads"], grads)):

@@ -119,3 +119,79 @@ def test_forged_huge_header_is_refused():
     i = data.index(b"\xff\xc0")
     data[i + 5:i + 9] = b"\xff\xff\xff\xff"  # height, width
     assert decode_coefs(bytes(data)) is None
+
+
+# ------------------------------------------------------------------ colour space / orientation fallbacks
+def _segments(data):
+    """(marker, payload-with-length) list up to SOS, and the rest (SOS .. EOI)."""
+    p, segs = 2, []
+    while True:
+        m = data[p + 1]
+        ln = (data[p + 2] << 8) | data[p + 3]
+        if m == 0xDA:
+            return segs, data[p:]
+        segs.append((m, data[p + 2:p + 2 + ln]))
+        p += 2 + ln
+
+
+def _assemble(segs, rest):
+    return b"\xff\xd8" + b"".join(bytes([0xFF, m]) + pl for m, pl in segs) + rest
+
+
+def _adobe(transform):
+    body = b"Adobe" + bytes([0, 100, 0, 0, 0, 0, transform])
+    return (0xEE, bytes([0, len(body) + 2]) + body)
+
+
+def test_adobe_rgb_jpeg_falls_back_to_libjpeg_semantics():
+    """An Adobe APP14 marker with transform 0 (no JFIF) means RGB components: libjpeg -- and the
+    reference's cv2.imdecode -- skip the YCbCr conversion, so the native (YCbCr) path must decline."""
+    segs, rest = _segments(_jpeg(_frame(48, 64, 3), quality=92, subsampling=0))
+    segs = [s for s in segs if s[0] != 0xE0]  # drop JFIF
+    for transform, native_ok in ((0, False), (1, True)):
+        data = _assemble([_adobe(transform)] + segs, rest)
+        jc = decode_coefs(data, parallel=False)
+        assert (jc is not None) == native_ok
+        want = _pil(data)
+        assert np.array_equal(decode_image(data, True, "RGB"), want)
+        if native_ok:
+            assert np.array_equal(coefs_to_rgb_reference(jc), want)
+
+
+def test_rgb_component_ids_fall_back():
+    """No JFIF / Adobe marker and component ids 'R', 'G', 'B': libjpeg decodes without conversion."""
+    segs, rest = _segments(_jpeg(_frame(40, 56, 4), quality=92, subsampling=0))
+    segs = [s for s in segs if s[0] != 0xE0]
+    out = []
+    for m, pl in segs:
+        if m in (0xC0, 0xC1):
+            pl = bytearray(pl)
+            for c in range(3):
+                pl[2 + 6 + 3 * c] = b"RGB"[c]
+            pl = bytes(pl)
+        out.append((m, pl))
+    rest = bytearray(rest)  # SOS: ff da len(2) ns (id, tables) x 3
+    for k in range(3):
+        rest[5 + 2 * k] = b"RGB"[k]
+    data = _assemble(out, bytes(rest))
+    assert decode_coefs(data, parallel=False) is None
+    assert np.array_equal(decode_image(data, True, "RGB"), _pil(data))
+
+
+def test_exif_rotated_jpeg_is_transposed_like_cv2():
+    """cv2.imdecode(IMREAD_COLOR) applies the EXIF orientation: the native path declines such streams
+    and the fallback rotates (orientation 6: 90 degrees clockwise)."""
+    rgb = _frame(24, 40, 5)
+    ex = Image.Exif()
+    ex[0x0112] = 6
+    buf = io.BytesIO()
+    Image.fromarray(rgb, "RGB").save(buf, format="JPEG", quality=95, exif=ex.tobytes())
+    data = buf.getvalue()
+    assert decode_coefs(data, parallel=False) is None
+    out = decode_image(data, True, "RGB")
+    assert out.shape == (40, 24, 3)
+    assert np.array_equal(out, np.rot90(_pil(data), k=-1))
+    ex[0x0112] = 1  # upright EXIF: the native path takes it
+    buf = io.BytesIO()
+    Image.fromarray(rgb, "RGB").save(buf, format="JPEG", quality=95, exif=ex.tobytes())
+    assert decode_coefs(buf.getvalue(), parallel=False) is not None

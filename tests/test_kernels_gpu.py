@@ -420,16 +420,6 @@ def test_conv_bnin_fwd_and_wgrad(C, N, H, W):
     torch.cuda.synchronize()
     assert torch.equal(y_out, y_ref) and torch.equal(st[: rows * 128], st_ref[: rows * 128])
     assert torch.equal(a_out, a)
-    dy = bf(torch.randn(N, H, W, 64, device=dev))
-    slab = torch.zeros(C.wgrad_slab_elems(N, H, W, 64, 64, 9, 0, 64), device=dev)
-    g_ref, g = (torch.full((64 * 9 * 64,), 7.0, device=dev) for _ in range(2))
-    C.conv_wgrad(a, None, dy, 9, 0, 64, slab, g_ref, 0, 64, 0)
-    C.conv_wgrad(y_pre, None, dy, 9, 0, 64, slab, g, 0, 64, 0, coef)
-    torch.cuda.synchronize()
-    assert torch.equal(g, g_ref)
-    wt = torch.zeros(64, 64, 3, 3, device=dev, requires_grad=True)
-    F.conv2d(nchw(a).float(), wt, padding=1).backward(nchw(dy).float())
-    assert relerr(g, wt.grad.permute(0, 2, 3, 1).reshape(-1)) < 2e-3
 
 
 def test_conv_bnin_not_applicable(C):
@@ -439,9 +429,6 @@ def test_conv_bnin_not_applicable(C):
     y = torch.empty_like(y_pre)
     wk = bf(torch.randn(64, 576, device=dev))
     assert C.conv_fwd_bnin(y_pre, wk, y, torch.zeros(1024 * 128, device=dev), coef) == -1
-    slab = torch.zeros(C.wgrad_slab_elems(1, 16, 48, 64, 64, 9, 0, 8), device=dev)
-    with pytest.raises(RuntimeError):
-        C.conv_wgrad(y_pre, None, y_pre, 9, 0, 64, slab, torch.zeros(64 * 576, device=dev), 0, 8, 0, coef)
 
 
 def test_maxpool_fwd_bwd_with_skip(C):

@@ -435,3 +435,39 @@ def test_serve_workers_share_port(tmp_path):
             p.terminate()
         for p in procs:
             p.join(30)
+
+
+def test_metrics_log_header_written_once(tmp_path):
+    """Several writers opening the same CSV (server worker processes): one header, no truncation."""
+    from robotic_discovery_platform_amd.serve.server import CSV_HEADER, MetricsLog
+    path = str(tmp_path / "logs" / "m.csv")
+    a = MetricsLog(path)
+    a.write(1.0, 2.0, 3.0, ts=10.0)
+    b = MetricsLog(path)  # a second worker starting late must not rewrite the header
+    b.write(4.0, 5.0, 6.0, ts=11.0)
+    a.close()
+    b.close()
+    lines = open(path).read().splitlines(keepends=True)
+    assert lines[0] == CSV_HEADER and len(lines) == 3 and lines.count(CSV_HEADER) == 1
+
+
+def test_engine_pool_bounds_frame_sizes():
+    """Pipelines for non-configured frame sizes are LRU-bounded per replica (idle ones evicted); a new
+    size while every other size is busy is refused for that frame only."""
+    from robotic_discovery_platform_amd.serve.engine import EnginePool
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
+    pool = EnginePool(UNetRef(3, 1, base_width=8, depth=2).eval(), DEFAULT_K, 0.001, H=48, W=64, n=1, graph=False,
+                      max_sizes=2)
+    for hw in ((32, 32), (40, 40), (48, 48)):
+        pool._get(0, *hw)
+    assert set(k[1:] for k in pool._pools) == {(48, 64), (40, 40), (48, 48)}  # (32, 32) evicted, home kept
+    held = pool._get(0, 40, 40).get()  # (40, 40) busy
+    q48 = pool._get(0, 48, 48)
+    held48 = q48.get()  # both other sizes busy: a third size is refused
+    with pytest.raises(RuntimeError):
+        pool._get(0, 24, 24)
+    q48.put(held48)
+    pool._get(0, 24, 24)  # (48, 48) idle again: it is the one evicted
+    assert set(k[1:] for k in pool._pools) == {(48, 64), (40, 40), (24, 24)}
+    pool._get(0, 40, 40).put(held)

@@ -220,30 +220,3 @@ def test_side_stream_wprep_matches_inline(bilinear):
     fresh.load_state_dict(sd)
     torch.cuda.synchronize()
     assert torch.equal(nat.derived, fresh.derived)
-
-
-def test_bnin_stored_activation_matches_reformed(monkeypatch):
-    """The full-resolution BN-on-input convs either store the activation they form (weight gradient on
-    it with the plain row-ring kernel) or leave it unwritten (the weight gradient re-forms it): the
-    trained state after 3 steps is bitwise the same."""
-    from robotic_discovery_platform_amd.models.unet import UNetNative
-    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
-    from robotic_discovery_platform_amd.train.engine import NativeTrainer
-    torch.manual_seed(8)
-    dev = torch.device("cuda")
-    ref = UNetRef(3, 1)
-    x = torch.rand(2, 3, 64, 128, device=dev)
-    y = (torch.rand(2, 1, 64, 128, device=dev) > 0.5).float()
-    out = {}
-    for wa in ("0", "1"):
-        monkeypatch.setenv("RDP_BNIN_WRITE_A", wa)
-        nat = UNetNative(3, 1, device=dev, init_from=ref)
-        tr = NativeTrainer(nat, 2, 64, 128, lr=1e-3, plan=False)
-        assert tr.ex.bnin_write_a == (wa == "1")
-        assert any(lb.bnin is not None for _, lb in [tr.ex.down_layers[0]])
-        tr.set_batch(x, y)
-        ls = [tr.step().clone() for _ in range(3)]
-        torch.cuda.synchronize()
-        out[wa] = (torch.stack(ls), nat.store.flat.clone(), nat.store.exp_avg.clone())
-    for u, v in zip(out["0"], out["1"]):
-        assert torch.equal(u, v)
