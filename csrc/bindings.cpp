@@ -8,6 +8,9 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <link.h>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <vector>
@@ -66,7 +69,7 @@ int rdp_head_bwd(const void*, int, const float*, const float*, const float*, con
 int rdp_head_bn_bwd_apply(const void*, int, const float*, const float*, const float*, const float*, const float*,
                           const float*, void*, int, int, float, float, float, hipStream_t);
 int rdp_head_mask(const void*, int, const float*, const float*, float, void*, int, hipStream_t);
-int rdp_adam(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, int*, int,
+int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float, float, float, float, float, int*, int,
              hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
@@ -275,6 +278,70 @@ void plan_free(int id) {
   if (id < 0 || id >= (int)g_plans.size() || !g_plans[id]) return;
   for (auto& op : g_plans[id]->ops) if (op.ev) hipEventDestroy(op.ev);
   g_plans[id].reset();
+}
+
+// ---- RCCL collectives enqueued straight onto HIP streams ---------------------------------------------
+// The DDP gradient buckets are all-reduced with ncclAllReduce on the communicator of a dedicated
+// torch.distributed (nccl = RCCL) process group (ProcessGroupNCCL._comm_ptr), issued on the executor's
+// stream in stream order -- no ProcessGroupNCCL work objects, events or host waits per bucket -- and
+// recorded into launch plans like a kernel launch, so a DDP step replays from C++ with its collectives
+// in place. The entry points are resolved from the librccl instance torch itself loaded (the
+// communicator belongs to it), never from another copy of the library.
+typedef int (*NcclAllReduceFn)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef int (*NcclAsyncErrFn)(void*, int*);
+typedef const char* (*NcclErrStrFn)(int);
+struct RcclApi {
+  NcclAllReduceFn all_reduce = nullptr;
+  NcclAsyncErrFn async_err = nullptr;
+  NcclErrStrFn err_str = nullptr;
+  std::string path;
+} g_rccl;
+
+int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* out) {
+  if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+    *(std::string*)out = info->dlpi_name;
+    return 1;
+  }
+  return 0;
+}
+
+std::string comm_bind() {
+  if (g_rccl.all_reduce) return g_rccl.path;
+  std::string path;
+  dl_iterate_phdr(find_loaded_rccl, &path);
+  TORCH_CHECK(!path.empty(), "comm_bind: RCCL is not loaded in this process (create the nccl process group first)");
+  void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_NOLOAD);
+  TORCH_CHECK(h != nullptr, "comm_bind: dlopen ", path);
+  g_rccl.all_reduce = (NcclAllReduceFn)dlsym(h, "ncclAllReduce");
+  g_rccl.async_err = (NcclAsyncErrFn)dlsym(h, "ncclCommGetAsyncError");
+  g_rccl.err_str = (NcclErrStrFn)dlsym(h, "ncclGetErrorString");
+  TORCH_CHECK(g_rccl.all_reduce && g_rccl.async_err && g_rccl.err_str, "comm_bind: RCCL symbols in ", path);
+  g_rccl.path = path;
+  return path;
+}
+
+long rccl_check(int r, void* comm) {
+  constexpr int kInProgress = 7;  // ncclInProgress: a non-blocking communicator is still enqueuing
+  while (r == kInProgress) {
+    int e = 0;
+    g_rccl.async_err(comm, &e);
+    r = e;
+  }
+  TORCH_CHECK(r == 0, "ncclAllReduce: ", g_rccl.err_str(r));
+  return 0;
+}
+
+// in-place SUM all-reduce of `buf` (fp32 or bf16) over `comm`, on the current stream
+void comm_all_reduce(torch::Tensor buf, long comm) {
+  TORCH_CHECK(g_rccl.all_reduce != nullptr, "comm_all_reduce: call comm_bind() first");
+  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous(), "comm_all_reduce: contiguous device tensor");
+  const int dt = buf.scalar_type() == torch::kFloat ? 7 : buf.scalar_type() == torch::kBFloat16 ? 9 : -1;
+  TORCH_CHECK(dt >= 0 && comm != 0, "comm_all_reduce: fp32 / bf16 buffer and a communicator");
+  void* const p = buf.data_ptr();
+  const size_t n = (size_t)buf.numel();
+  void* const c = (void*)comm;
+  const NcclAllReduceFn fn = g_rccl.all_reduce;
+  RDP_PLAN(rccl_check(fn(p, p, n, dt, /*ncclSum*/ 0, c, st), c));
 }
 
 struct Act {
@@ -856,7 +923,10 @@ void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_t
 
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
           double lr, double b1, double b2, double eps, double wd, double gscale, torch::Tensor step, bool inc) {
-  check_f32(p, "p"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v");
+  check_f32(p, "p"); check_f32(m, "m"); check_f32(v, "v");
+  const bool gbf = g.scalar_type() == torch::kBFloat16;  // bf16 gradients (the DDP bf16 all-reduce buffer)
+  if (!gbf) check_f32(g, "g");
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous(), "g: contiguous device tensor");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam numel");
   TORCH_CHECK(step.scalar_type() == torch::kInt32 && step.is_cuda(), "step int32");
   void* sh = nullptr;
@@ -864,7 +934,8 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c1
     TORCH_CHECK(shadow->scalar_type() == torch::kBFloat16 && shadow->numel() == p.numel(), "shadow");
     sh = shadow->data_ptr();
   }
-  TORCH_CHECK(RDP_PLAN(rdp_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sh, p.numel(),
+  const void* gp = g.data_ptr();
+  TORCH_CHECK(RDP_PLAN(rdp_adam(p.data_ptr<float>(), gp, gbf ? 1 : 0, m.data_ptr<float>(), v.data_ptr<float>(), sh, p.numel(),
                        (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale,
                        (int*)step.data_ptr(), inc ? 1 : 0, st)) == 0, "adam: numel must be a multiple of 4");
 }
@@ -1191,6 +1262,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_abort", &plan_abort);
   m.def("plan_replay", &plan_replay, py::arg("id"), py::arg("host_call") = py::none());
   m.def("plan_recording", &plan_recording);
+  m.def("comm_bind", &comm_bind, "resolve RCCL from the library torch loaded; returns its path");
+  m.def("comm_all_reduce", on_device(&comm_all_reduce), py::arg("buf"), py::arg("comm"),
+        "in-place SUM all-reduce over an RCCL communicator on the current stream (recorded in plans)");
   m.def("plan_mark", &plan_mark, "record a host call point (replay calls host_call(tag) there)");
   m.def("plan_pause", &plan_pause);
   m.def("plan_resume", &plan_resume);

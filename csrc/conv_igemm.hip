@@ -718,6 +718,10 @@ extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, 
                                   const float* escale, const float* eshift, int erelu, void* pool, int ppitch,
                                   hipStream_t s);
 extern "C" int rdp_conv_halo_tiles(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed);
+extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const void* x1, long xbytes1, int pitch1,
+                              const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, float* stats,
+                              int N, int H, int W, const float* escale, const float* eshift, int erelu, int max_blocks,
+                              hipStream_t s);
 extern "C" int rdp_conv_first(const void* x, long xbytes, int pitch, const void* w, long wbytes, void* y, long ybytes,
                               int ypitch, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                               int erelu, hipStream_t s);
@@ -1046,6 +1050,22 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
       const int r = rdp_conv_ring(x1, xbytes1, C1, pitch1, w, wbytes, ldw, y1, ybytes1, ypitch1, y2, ybytes2,
                                   ypitch2, Cy1, Cout, stats, N, H, W, escale, eshift, erelu, 256, s);
       if (r >= 0 || pref == 6) return r;
+    }
+  }
+  // two-source row ring (conv_ring.hip conv_ring2_kernel): 128 input channels (two 64-channel sources,
+  // or one 128-channel tensor as its two halves) -> 64, 3x3, one destination; 14 = force
+  {
+    const int pref = bm_pref % 1000;
+    const long ring_pairs = W % 64 == 0 ? (long)N * (W / 64) * H / 2 : 0;
+    const bool two = C1 == 64 && C2 == 64 && x2 != nullptr, one = C1 == 128 && C2 == 0 && x2 == nullptr;
+    static const bool ring2_auto = getenv("RDP_RING2") == nullptr || atoi(getenv("RDP_RING2")) != 0;  // A/B
+    if ((pref == 14 || (pref == 0 && ring2_auto && ring_pairs >= 256)) && taps == 9 && !packed && Cout == 64 && (two || one) &&
+        y2 == nullptr && !(pool && pooled) && !(up && pooled)) {
+      const void* s1 = two ? x2 : (const void*)((const u16*)x1 + 64);
+      const long b1 = two ? xbytes2 : xbytes1 - 128;
+      const int r = rdp_conv_ring2(x1, xbytes1, pitch1, s1, b1, two ? pitch2 : pitch1, w, wbytes, ldw, y1, ybytes1,
+                                   ypitch1, stats, N, H, W, escale, eshift, erelu, 256, s);
+      if (r >= 0 || pref == 14) return r;
     }
   }
   {

@@ -689,3 +689,294 @@ extern "C" int rdp_conv_ring_ex(const void* x, long xbytes, int C, int pitch, co
   hipLaunchKernelGGL((conv_ring_kernel<64>), dim3(grid), dim3(512), 0, s, a);
   return grid * 4;
 }
+
+// ---- two-source (128 -> 64) row ring ---------------------------------------------------------------
+// The first conv of up4 (/root/reference/pkg/segmentation_model.py:62,75-76: DoubleConv(128, 64) on
+// cat([skip, up]) at 256^2) and the second conv of up3 (128 -> 64 at 128^2) as a row ring: the 9 taps of
+// 128 input channels, 64 outputs. The whole weight tensor (64 x 1152 bf16) does not fit one wave's
+// registers, so K is split over wave pairs: 8 waves = 2 channel groups (32 outputs) x 2 K-halves (the
+// 64 channels of source 0 / source 1: the skip and the upsample, or the two halves of one 128-channel
+// tensor) x 2 output rows of the step; every wave keeps its 32 x 576 weights in VGPRs (144) and
+// computes all 64 pixels of its row over its K-half. The two partial tiles of a (channel group, row)
+// meet in LDS: each wave hands its partner the fp32 half of the tile the partner finishes (32 pixels),
+// one barrier later adds the partner's half of its own, and runs the epilogue (bf16 store, BN
+// statistics or eval BN fold + ReLU) on its 32 pixels. A ring slot holds one input row of both
+// sources (2 x 72 x 128 B); 6 slots = the 4 rows of a step + the next stage's 2 rows in flight, so
+// the ring + exchange tile + zero row fit the 160 KiB LDS with one 512-thread block per CU.
+struct Ring2Args {
+  const u16* x0;
+  const u16* x1;
+  uint32_t xbytes0, xbytes1;
+  int pitch0, pitch1;
+  const u16* w;  // [64][ldw], k = tap * 128 + 64 * source + cin
+  uint32_t wbytes;
+  int ldw;
+  u16* y;
+  uint32_t ybytes;
+  int ypitch;
+  float* stats;  // [gridDim.x * 4][2][64] partial (sum, sumsq) or nullptr
+  const float* escale;
+  const float* eshift;
+  int erelu;
+  int H, W, WS, nrows, npairs, pairs_per_block;
+  uint32_t fh_m, fh_s, fs_m, fs_s;
+};
+
+__global__ __launch_bounds__(512, 2) void conv_ring2_kernel(const Ring2Args a) {
+  constexpr int XREG = 72 * 128;          // one source of one staged row
+  constexpr int SLOT = 2 * XREG;          // both sources
+  constexpr int NX = 6;                   // 4 rows in use + the next stage's 2
+  constexpr int PIECES = 36;              // 1-KiB DMA pieces per stage: 2 rows x 2 sources x 9
+  constexpr int MINPW = PIECES / 8;       // pieces of the wave that issues fewest
+  constexpr int XCH = 2 * 2 * 2 * 2 * 2 * 64 * 16;  // exchange: [orow][cg][dst half][i2][j] x 64 lanes x 16 B
+  __shared__ __attribute__((aligned(16))) char ring[NX * SLOT + XREG + XCH + 2 * 64 * 4];
+  char* const zslot = ring + NX * SLOT;
+  f32x4* const xch = (f32x4*)(ring + NX * SLOT + XREG);
+  float* const efold = (float*)(ring + NX * SLOT + XREG + XCH);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave & 1, kh = (wave >> 1) & 1, orow = wave >> 2;
+
+  const int P0 = blockIdx.x * a.pairs_per_block;
+  const int nks = min(a.npairs, P0 + a.pairs_per_block) - P0;
+  if (nks <= 0) return;
+
+  const auto rx0 = make_rsrc(a.x0, a.xbytes0);
+  const auto rx1 = make_rsrc(a.x1, a.xbytes1);
+  const auto rw = make_rsrc(a.w, a.wbytes);
+  const auto ry = make_rsrc(a.y, a.ybytes);
+
+  // weights: wa[ks][j] = W[32 cg + 16 j + (lane & 15)][tap * 128 + 64 kh + 32 (ks & 1) + 8 (lane >> 4) .. +7]
+  bf16x8 wa[18][2];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 32 * cg + 16 * j + (lane & 15);
+      const uint32_t off = (uint32_t)(n * a.ldw + (ks >> 1) * 128 + 64 * kh + 32 * (ks & 1) + 8 * (lane >> 4)) * 2u;
+      wa[ks][j] = __builtin_bit_cast(bf16x8, bload16(rw, off));
+    }
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(wa[ks][j]));  // loads waited here, not in the loop
+
+  // DMA lane geometry: LDS row pj * 8 + lrow, global 16-B chunk gch of it; per source the lane part
+  // of the global offset (elements): lrow * pitch + 8 gch (the pieces add scalar parts only)
+  const int lrow = lane >> 3;
+  const int gch = (lane & 7) ^ lrow;
+  const int lofs0 = lrow * a.pitch0 + gch * 8, lofs1 = lrow * a.pitch1 + gch * 8;
+  auto row_base = [&](int R, int& m0, int& w0) {
+    if (R < 0 || R >= a.nrows) { m0 = -1; w0 = 0; return; }
+    const uint32_t col = rdiv((uint32_t)R, a.fh_m, a.fh_s);
+    const int h = R - (int)col * a.H;
+    const uint32_t n = rdiv(col, a.fs_m, a.fs_s);
+    const int ws = (int)col - (int)n * a.WS;
+    w0 = ws * 64;
+    m0 = ((int)n * a.H + h) * a.W + w0;
+  };
+  // piece q (0..17) of row R: source q / 9, LDS row group q % 9
+  auto dma_piece = [&](int R, int q, int lr) {
+    int m0, w0;
+    row_base(R, m0, w0);
+    const int src = q >= 9 ? 1 : 0, pj = q - 9 * src;  // wave-uniform
+    const int j = pj * 8 + lr;
+    const bool ok = (m0 >= 0) & (j < 66) & inb(w0 - 1 + j, a.W);
+    const int pitch = src ? a.pitch1 : a.pitch0;
+    const uint32_t off = ok ? (uint32_t)((m0 + pj * 8 - 1) * pitch + (src ? lofs1 : lofs0)) * 2u : RDP_OOB;
+    dma16_async(src ? rx1 : rx0, (lds_void*)(ring + ((R + NX) % NX) * SLOT + src * XREG + pj * 1024), off);
+  };
+  // (lr re-derived per call behind an opaque asm: per-piece lane values are recomputed, not hoisted
+  // out of the step loop into registers the weights need)
+  auto issue = [&](int P) {  // stage P = rows 2P + 1, 2P + 2: wave w issues pieces w, w + 8, ...
+    int lr = lrow;
+    asm volatile("" : "+v"(lr));
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int p = wave + 8 * t;
+      if (p >= PIECES) continue;
+      const int rr = p >= 18 ? 1 : 0;
+      dma_piece(2 * P + 1 + rr, p - 18 * rr, lr);
+    }
+  };
+  auto issue_row = [&](int R) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int q = wave + 8 * t;
+      if (q < 18) dma_piece(R, q, lrow);
+    }
+  };
+
+  for (int o = threadIdx.x * 16; o < XREG; o += 512 * 16) *(uint4*)(zslot + o) = make_uint4(0, 0, 0, 0);
+  if (a.escale) {
+    for (int c = threadIdx.x; c < 64; c += 512) { efold[c] = a.escale[c]; efold[64 + c] = a.eshift[c]; }
+  }
+
+  issue_row(2 * P0 - 1);
+  issue_row(2 * P0);
+  issue(P0);
+
+  const int gq = lane >> 4;
+  const int coff = 16 * (gq & 1) + 8 * (gq >> 1);
+  int lpart[3][2];
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int r = (lane & 15) + d;
+      lpart[d][h2] = r * 128 + 16 * ((gq + 4 * h2) ^ (r & 7));
+    }
+  f32x4 acc[2][4];
+  float s1[2][4], s2[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+  constexpr int NS = 2;  // output stores per wave per step (its 2 fragments of 16 pixels)
+
+  for (int ks = 0; ks < nks; ++ks) {
+    const int P = P0 + ks;
+    // stage P landed; younger than it: only the NS stores of step ks - 1
+    if (ks == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NS) : "memory");
+    raw_barrier();  // every wave's stage P visible; every wave done with step ks - 1 (ring rows, exchange)
+    asm volatile("" ::: "memory");  // no LDS access of this step moves above the barrier
+    if (ks + 1 < nks) issue(P + 1);
+
+    const int R0 = 2 * P + orow;
+    const int h = R0 - (int)rdiv((uint32_t)R0, a.fh_m, a.fh_s) * a.H;
+    const bool top = h == 0, bottom = h == a.H - 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto src_base = [&](int tap) {
+      const int dr = tap / 3 - 1;
+      const bool pad = (dr < 0 && top) || (dr > 0 && bottom);  // wave-uniform
+      return pad ? zslot : ring + ((R0 + dr + NX) % NX) * SLOT + kh * XREG;
+    };
+    // fragment i of K-step kk: LDS row 16 i + (lane & 15) + ds + 1 of the tap's slot; the swizzle only
+    // sees the row's low 3 bits, so the lane part is one of 6 offsets and 16 i a 2-KiB immediate
+    auto read_frag = [&](int kk, bf16x8 (&fb)[4]) {  // kk = 2 tap + K-half of the source's 64 channels
+      const char* xb = src_base(kk >> 1) + lpart[(kk >> 1) % 3][kk & 1];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fb[i] = *(const bf16x8*)(xb + 2048 * i);
+    };
+    // 18 K-steps of 4 fragment reads + 8 MFMAs (no second fragment set: the registers hold the weights;
+    // the SIMD's other wave covers the read latency)
+#pragma unroll
+    for (int kk = 0; kk < 18; ++kk) {
+      bf16x8 fb[4];
+      read_frag(kk, fb);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk][j], fb[i], acc[j][i], 0, 0, 0);
+    }
+
+    // exchange: this wave finishes pixels 32 kh .. 32 kh + 31 (fragments 2 kh, 2 kh + 1); the partner
+    // (same cg / row, other K-half) finishes the rest. kh is wave-uniform: scalar branches pick the
+    // register sets (no dynamic register indexing, no second copy of the tile)
+    const int xo = (orow * 2 + cg) * 2;  // [orow][cg] base, then [dst half][i2][j]
+    auto give = [&](int ib) {  // fragments ib, ib + 1 -> the partner's slots
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) xch[(((xo + (1 - kh)) * 2 + i2) * 2 + j) * 64 + lane] = acc[j][ib + i2];
+    };
+    if (kh == 0) give(2);
+    else give(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    asm volatile("" ::: "memory");
+
+    int m0, w0;
+    row_base(R0, m0, w0);
+    auto finish = [&](int ib) {  // fragments ib, ib + 1 (+ the partner's partials) -> epilogue
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const int i = ib + i2;
+        uint2 v[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 o = acc[j][i] + xch[(((xo + kh) * 2 + i2) * 2 + j) * 64 + lane];
+          if (a.escale) {
+            const int c = 32 * cg + 16 * j + 4 * gq;
+            const float4 sc = *(const float4*)(efold + c), sh = *(const float4*)(efold + 64 + c);
+            o[0] = fmaf(o[0], sc.x, sh.x); o[1] = fmaf(o[1], sc.y, sh.y);
+            o[2] = fmaf(o[2], sc.z, sh.z); o[3] = fmaf(o[3], sc.w, sh.w);
+            if (a.erelu) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+            }
+          }
+          v[j].x = pack2bf(o[0], o[1]);
+          v[j].y = pack2bf(o[2], o[3]);
+          if (a.stats) {
+            const float q0 = __uint_as_float(v[j].x << 16), q1 = __uint_as_float(v[j].x & 0xffff0000u);
+            const float q2 = __uint_as_float(v[j].y << 16), q3 = __uint_as_float(v[j].y & 0xffff0000u);
+            s1[j][0] += q0; s2[j][0] += q0 * q0;
+            s1[j][1] += q1; s2[j][1] += q1 * q1;
+            s1[j][2] += q2; s2[j][2] += q2 * q2;
+            s1[j][3] += q3; s2[j][3] += q3 * q3;
+          }
+        }
+        const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
+        const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
+        const int m = m0 + 16 * i + (lane & 15);
+        bstore16(ry, (uint32_t)(m * a.ypitch + 32 * cg + coff) * 2u, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
+      }
+    };
+    if (kh == 0) finish(0);
+    else finish(2);
+  }
+
+  if (a.stats) {  // one partial row per (block, row of the step, pixel half); cg = 0 / 1 fill its halves
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] = row16_sum(s1[j][r]);
+        s2[j][r] = row16_sum(s2[j][r]);
+      }
+    if ((lane & 15) == 0) {
+      float* row = a.stats + (size_t)(blockIdx.x * 4 + orow * 2 + kh) * 2 * 64;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = 32 * cg + 16 * j + 4 * gq;
+        *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+        *(float4*)(row + 64 + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+      }
+    }
+  }
+}
+
+// Two-source row ring (see conv_ring2_kernel): x0 / x1 = the two 64-channel sources (for one
+// 128-channel tensor: its two halves), 64 outputs, 3x3, W % 64 == 0, even H. Returns the stats rows
+// written (grid * 4), or -1 when not applicable.
+extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const void* x1, long xbytes1, int pitch1,
+                              const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, float* stats,
+                              int N, int H, int W, const float* escale, const float* eshift, int erelu, int max_blocks,
+                              hipStream_t s) {
+  if (W % 64 || H % 2 || ldw < 1152 || ypitch % 8 || pitch0 % 8 || pitch1 % 8) return -1;
+  if (xbytes0 >= (1l << 31) || xbytes1 >= (1l << 31) || ybytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+  if ((escale == nullptr) != (eshift == nullptr)) return -1;
+  Ring2Args a;
+  a.x0 = (const u16*)x0; a.x1 = (const u16*)x1;
+  a.xbytes0 = (uint32_t)xbytes0; a.xbytes1 = (uint32_t)xbytes1; a.pitch0 = pitch0; a.pitch1 = pitch1;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+  a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  a.H = H; a.W = W; a.WS = W / 64;
+  a.nrows = N * a.WS * H;
+  a.npairs = a.nrows / 2;
+  const int blocks = std::max(1, std::min(max_blocks > 0 ? max_blocks : 256, a.npairs));
+  a.pairs_per_block = (a.npairs + blocks - 1) / blocks;
+  const int grid = (a.npairs + a.pairs_per_block - 1) / a.pairs_per_block;
+  const FastDiv fh = make_fastdiv((uint32_t)H), fs = make_fastdiv((uint32_t)a.WS);
+  a.fh_m = fh.m; a.fh_s = fh.s; a.fs_m = fs.m; a.fs_s = fs.s;
+  hipLaunchKernelGGL(conv_ring2_kernel, dim3(grid), dim3(512), 0, s, a);
+  return grid * 4;
+}

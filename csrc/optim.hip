@@ -14,7 +14,10 @@
 #include <algorithm>
 #include <stdlib.h>
 
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// G = float (the flat fp32 gradient) or u16: bf16 gradients straight from the DDP bf16 all-reduce
+// buffer (parallel/ddp.py comm_dtype), widened here instead of by a separate pass.
+template <typename G>
+__global__ void adam_kernel(float* __restrict__ p, const G* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, u16* __restrict__ shadow, long n, float lr, float b1, float b2,
                             float eps, float wd, float gscale, const int* __restrict__ step) {
   const int t = step[0] + 1;
@@ -24,7 +27,14 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   const float bc2s = sqrtf(bc2);
   const long n4 = n >> 2;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 pp = ((float4*)p)[i], gg = ((const float4*)g)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    float4 pp = ((float4*)p)[i], gg, mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    if constexpr (sizeof(G) == 4) {
+      gg = ((const float4*)g)[i];
+    } else {
+      const uint2 gb = ((const uint2*)g)[i];
+      gg = make_float4(__uint_as_float(gb.x << 16), __uint_as_float(gb.x & 0xffff0000u),
+                       __uint_as_float(gb.y << 16), __uint_as_float(gb.y & 0xffff0000u));
+    }
     float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -107,13 +117,18 @@ __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ ma
 
 extern "C" {
 // inc = 0: the caller advances the step counter later on this stream (rdp_wprep with step)
-int rdp_adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2,
-             float eps, float wd, float gscale, int* step, int inc, hipStream_t s) {
+// g_bf16: g is bf16 (u16) instead of fp32
+int rdp_adam(float* p, const void* g, int g_bf16, float* m, float* v, void* shadow, long n, float lr, float b1,
+             float b2, float eps, float wd, float gscale, int* step, int inc, hipStream_t s) {
   if (n % 4) return -1;
   const long n4 = n / 4;
   const int grid = (int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 8192));
-  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, s, p, g, m, v, (u16*)shadow, n, lr, b1, b2, eps, wd, gscale,
-                     step);
+  if (g_bf16)
+    hipLaunchKernelGGL(adam_kernel<u16>, dim3(grid), dim3(256), 0, s, p, (const u16*)g, m, v, (u16*)shadow, n, lr, b1,
+                       b2, eps, wd, gscale, step);
+  else
+    hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(256), 0, s, p, (const float*)g, m, v, (u16*)shadow, n, lr,
+                       b1, b2, eps, wd, gscale, step);
   if (inc) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   return 0;
 }

@@ -841,6 +841,12 @@ class UNetExecutor:
         with torch.cuda.stream(self.side):
             yield
 
+    def join_comm(self):
+        """Order the current stream after the collectives issued on :meth:`comm_stream` (native RCCL issue
+        has no work handles to wait on: stream order is the dependency)."""
+        if self.side is not None:
+            _stream_wait(torch.cuda.current_stream(), self.side)
+
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream
         (fork); without a side stream it runs inline. (One fork per two weight gradients, which saves
@@ -1017,15 +1023,18 @@ class NativeAdam:
         self.m = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
 
-    def step(self, gscale: float = 1.0, side: Optional["torch.cuda.Stream"] = None):
-        """``side``: the training executor's weight-gradient stream. The dgrad weight layouts are then
+    def step(self, gscale: float = 1.0, side: Optional["torch.cuda.Stream"] = None,
+             grad: Optional[torch.Tensor] = None):
+        """``grad``: the gradients to apply (default the store's fp32 grad; the DDP bf16 all-reduce buffer
+        is read as is). ``side``: the training executor's weight-gradient stream. The dgrad weight layouts are then
         rebuilt there, off the critical path, overlapping the next forward (which reads only the packed
         first layer and the transposed decoder's weights, rebuilt here); the next backward waits for
         them (:meth:`UNetExecutor.backward`)."""
         C = _native()
         st = self.m.store
         m = self.m
-        C.adam(st.flat, st.grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr, self.betas[0], self.betas[1], self.eps,
+        C.adam(st.flat, st.grad if grad is None else grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr,
+               self.betas[0], self.betas[1], self.eps,
                self.wd, gscale, st.step, False)
         if side is None or m._nseg_bwd == 0:
             C.wprep(st.flat, m.derived, m._segs, m._nseg, st.step, m._wblk)  # + the step counter advance

@@ -24,6 +24,12 @@ Design (MI355X-first):
     ring all-reduce moves 2(n-1)/n of the bucket per GPU, so ~16 MB buckets (≈4-5 per step) keep
     every bucket well above the latency-bound regime while still giving backward-overlap.
   * The 1/world averaging is folded into the fused Adam kernel (gscale), not a separate pass.
+  * Native RCCL issue (``native_comm``, the default for the nccl backend on GPUs): each bucket is
+    all-reduced by ``ncclAllReduce`` on a dedicated process group's communicator, enqueued by the
+    native runtime straight onto the issuing HIP stream (``csrc/bindings.cpp`` comm_all_reduce) --
+    stream order is the dependency, no per-bucket ProcessGroupNCCL work objects, events or waits,
+    and the launch is recorded into the step's launch plan like a kernel. ``RDP_DDP_COMM=torch``
+    issues through torch.distributed instead (gloo always does).
   * ``comm_dtype=torch.bfloat16`` (SURVEY.md §7.4 option): each ready bucket is cast into a bf16
     mirror of the gradient buffer on the producing stream and all-reduced there (half the xGMI bytes:
     34.5 MB instead of 69 MB per step for the bilinear U-Net); ``finish()`` widens the reduced sums
@@ -49,8 +55,13 @@ class FlatBucketer:
 
     def __init__(self, grad_flat: torch.Tensor, param_ranges: Sequence[Tuple[str, int, int]],
                  bucket_mb: float = 16.0, group=None, comm_dtype: Optional[torch.dtype] = None,
-                 launch_ctx: Optional[Callable[[], ContextManager]] = None):
+                 launch_ctx: Optional[Callable[[], ContextManager]] = None, native_comm: Optional[int] = None,
+                 join: Optional[Callable[[], None]] = None):
         self.grad = grad_flat
+        # RCCL communicator (ncclComm_t as int) for native issue, and the callable that orders the
+        # caller's stream after the issuing stream once every bucket is out (native mode has no handles)
+        self.native_comm = native_comm
+        self.join = join
         # context that makes the current stream one ordered after every gradient producer (None: the
         # caller's current stream already is, e.g. single-stream autograd)
         self.launch_ctx = launch_ctx
@@ -115,6 +126,15 @@ class FlatBucketer:
                 self.checker.check_launch(self.bucket_params[b], torch.cuda.current_stream())
             lo, hi = self.buckets[b]
             buf = self.grad[lo:hi]
+            if self.native_comm is not None:
+                from ..ops import native
+                C = native(build_if_missing=False)
+                if self.comm is not None:
+                    buf = self.comm[lo:hi]
+                    C.cast_bf16(self.grad[lo:hi], buf)  # narrowing cast, ordered after every producer
+                C.comm_all_reduce(buf, self.native_comm)
+                self.handles.append((b, None))
+                return
             if self.comm is not None:
                 buf = self.comm[lo:hi]
                 buf.copy_(self.grad[lo:hi])  # narrowing cast, ordered after every producer (launch_ctx)
@@ -136,10 +156,17 @@ class FlatBucketer:
                     self._launch(b)
 
     def finish(self):
+        """Every bucket issued; the caller's stream is ordered after the reductions. With native issue
+        and bf16 comm the reduced sums stay in ``comm`` (bf16) for the optimizer to read directly."""
         for b, p in enumerate(self.pending):  # anything never marked (unused params) goes now
             if p > 0:
                 self.pending[b] = 0
                 self._launch(b)
+        if self.native_comm is not None:
+            if self.join is not None:
+                self.join()
+            self.handles = []
+            return
         for b, h in self.handles:
             h.wait()  # the caller's stream now waits for the collective (RCCL: no host block)
             if self.comm is not None:
@@ -204,6 +231,32 @@ class StreamOrderChecker:
         from ..models import unet
         if self in unet._STREAM_OBSERVERS:
             unet._STREAM_OBSERVERS.remove(self)
+
+
+_GRAD_GROUPS: Dict[int, object] = {}
+
+
+def native_comm_group(device: torch.device):
+    """(process group, ncclComm_t as int) for natively issued gradient all-reduces on ``device``: a
+    dedicated nccl group (created once per device; collective -- every rank calls this in the same
+    order) with BLOCKING communicators (eager-init groups default to non-blocking ones, whose calls
+    may return ncclInProgress), initialised by one all-reduce before its communicator is taken."""
+    from torch._C._distributed_c10d import ProcessGroupNCCL
+    key = device.index or 0
+    if key not in _GRAD_GROUPS:
+        opts = ProcessGroupNCCL.Options()
+        opts.config.blocking = 1
+        grp = dist.new_group(backend="nccl", pg_options=opts)
+        dist.all_reduce(torch.zeros(1, device=device), group=grp)
+        torch.cuda.synchronize(device)
+        with torch.cuda.device(device):
+            ptr = int(grp._get_backend(device)._comm_ptr())
+        if ptr == 0:
+            raise RuntimeError("native_comm_group: the RCCL communicator is not initialised")
+        from ..ops import native
+        native(build_if_missing=False).comm_bind()
+        _GRAD_GROUPS[key] = (grp, ptr)
+    return _GRAD_GROUPS[key]
 
 
 def broadcast_module_state(tensors: Iterable[torch.Tensor], src: int = 0, group=None):

@@ -45,7 +45,7 @@ import torch.nn as nn
 
 from ..models.unet import NativeAdam, UNetNative
 from ..models.unet_ref import UNetRef
-from ..parallel.ddp import FlatBucketer, broadcast_module_state, dist_info
+from ..parallel.ddp import FlatBucketer, broadcast_module_state, dist_info, native_comm_group
 from ..utils import trace
 
 
@@ -80,9 +80,13 @@ class NativeTrainer:
             ranges = [(n, st.offsets[n], st.offsets[n] + _numel(st.shapes[n])) for n in st.names]
             # buckets are issued from a stream ordered after both gradient streams (main: BN / head,
             # side: conv weights), never from whichever stream a hook happens to run on
-            self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb,
+            group, comm_ptr, join = None, None, None
+            if self._native_comm_wanted(model):
+                group, comm_ptr = native_comm_group(model.store.device)
+                join = self.ex.join_comm
+            self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb, group=group,
                                          comm_dtype=torch.bfloat16 if grad_comm == "bf16" else None,
-                                         launch_ctx=self.ex.comm_stream)
+                                         launch_ctx=self.ex.comm_stream, native_comm=comm_ptr, join=join)
             self.ex.set_sync_bn(enabled=sync_bn)
         if graph == "auto":
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
@@ -95,8 +99,8 @@ class NativeTrainer:
                          and torch.cuda.is_available() and model.store.device.type == "cuda")
         self.plan_id: Optional[int] = None
         self._plan_calls: list = []  # host call points of the recorded plan (DDP collectives), by tag
-        if self.bucketer is not None and self.use_plan:
-            self.bucketer.host_call = self._host_call
+        if self.bucketer is not None and self.use_plan and self.bucketer.native_comm is None:
+            self.bucketer.host_call = self._host_call  # torch.distributed issue: plan host call points
         self._plan_version = None
         self.steps = 0
 
@@ -107,6 +111,17 @@ class NativeTrainer:
                 native(build_if_missing=False).plan_free(self.plan_id)
             except Exception:  # interpreter teardown
                 pass
+
+    @staticmethod
+    def _native_comm_wanted(model) -> bool:
+        """RCCL issued natively (parallel.ddp native_comm_group) unless RDP_DDP_COMM=torch: nccl backend,
+        GPU parameters and the executor's wgrad side stream to issue from."""
+        import torch.distributed as dist
+        mode = os.environ.get("RDP_DDP_COMM", "native")
+        if mode not in ("native", "torch"):
+            raise ValueError(f"RDP_DDP_COMM must be 'native' or 'torch', got {mode!r}")
+        return (mode == "native" and model.store.device.type == "cuda" and dist.get_backend() == "nccl"
+                and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0")
 
     def _host_call(self, fn):
         """Run ``fn`` (torch.distributed work); while a plan is being recorded, also make it a host call
@@ -140,12 +155,14 @@ class NativeTrainer:
             self.bucketer.reset()
             with trace.range("train.backward+allreduce"):
                 ex.backward(grad_hook=self._hook)  # every layer's hook fires inside, the head's first
-                if self.use_plan:
+                if self.use_plan and self.bucketer.native_comm is None:
                     self._host_call(self.bucketer.finish)
-                else:
+                else:  # native issue: finish is only the stream join (recorded in the plan)
                     self.bucketer.finish()
             with trace.range("train.adam"):
-                self.opt.step(gscale=1.0 / self.world, side=self._wprep_side())
+                # native bf16 comm: Adam reads the reduced bf16 sums straight from the comm buffer
+                g = self.bucketer.comm if self.bucketer.native_comm is not None else None
+                self.opt.step(gscale=1.0 / self.world, side=self._wprep_side(), grad=g)
         else:
             with trace.range("train.backward"):
                 ex.backward()
@@ -173,7 +190,7 @@ class NativeTrainer:
                 C.plan_free(self.plan_id)
                 self.plan_id = None
             if self.plan_id is not None:
-                if self.bucketer is not None:
+                if self._plan_calls:
                     self.bucketer.reset()
                     C.plan_replay(self.plan_id, self._plan_host)
                 else:

@@ -941,6 +941,52 @@ def test_conv_ring_fwd_stats_eval_dgrad(C, N, H, W):
     assert relerr(nchw(dx), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 6, 64), (1, 4, 128), (3, 2, 192), (1, 10, 64), (4, 64, 128)])
+@pytest.mark.parametrize("form", ["concat", "one128"])
+def test_conv_ring2_128_to_64(C, N, H, W, form):
+    """Two-source row ring (128 -> 64, K split over wave pairs that meet in LDS): up4 conv0 on the concat
+    [skip, up] (two 64-channel sources) and up3 conv1 on one 128-channel tensor (its two halves), forward +
+    BN partial sums and eval BN fold + ReLU, against torch fp32; forced (pref 14) == auto dispatch where
+    the grid fills the chip (>= 256 row pairs) bitwise."""
+    torch.manual_seed(13)
+    dev = "cuda"
+    if form == "concat":
+        x1, x2 = bf(torch.randn(N, H, W, 64, device=dev)), bf(torch.randn(N, H, W, 64, device=dev))
+        xin = torch.cat([x1, x2], -1)
+    else:
+        x1, x2 = bf(torch.randn(N, H, W, 128, device=dev)), None
+        xin = x1
+    w = bf(torch.randn(64, 128, 3, 3, device=dev) / 34)
+    wk = ohwi(w).contiguous()
+    ref = F.conv2d(nchw(xin).float(), w.float(), padding=1)
+    rows = C.conv_stats_rows(N * H * W, 64, 0)
+    auto = N * (W // 64) * H // 2 >= 256
+    outs = []
+    for pref in ((14, 0) if auto else (14,)):
+        y = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+        stats = torch.zeros(rows * 2 * 64, device=dev)
+        r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, stats, pref, None, 0)
+        assert 0 < r <= rows
+        assert relerr(nchw(y), ref) < 1e-2
+        yq = nchw(y).float()
+        st = stats.view(rows, 2, 64)[:r].sum(0)
+        assert torch.allclose(st[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        assert torch.allclose(st[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+        outs.append(y)
+    if auto:
+        assert torch.equal(outs[0], outs[1])
+    # the implicit GEMM (256 x 64 tile) computes the same conv: equal up to fp32 summation order
+    yi = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, yi, None, torch.zeros(rows * 2 * 64, device=dev), 256, None, 0)
+    assert relerr(nchw(outs[0]), nchw(yi).float()) < 1e-2
+    # eval: BN fold + ReLU in the epilogue
+    sc, sh = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
+    aff = torch.cat([torch.zeros(64, device=dev), torch.ones(64, device=dev), sc, sh])
+    ye = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, ye, None, None, 14, aff, 1)
+    assert relerr(nchw(ye), torch.relu(ref * sc[None, :, None, None] + sh[None, :, None, None])) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,split", [(2, 4, 64, False), (1, 6, 128, True), (2, 2, 64, True)])
 def test_conv_ring_cout128(C, N, H, W, split):
     """Row-ring kernel with 128 outputs (down1 conv0 forward; up4 conv0 dgrad into the two halves of
