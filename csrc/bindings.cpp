@@ -80,6 +80,7 @@ int rdp_fit_curvature(const double*, int, double, int, int, double, double*, dou
 int rdp_geo_spline_res_len(int);
 int rdp_png_info(const uint8_t*, long, int*, int*, int*);
 long rdp_jpeg_info(const uint8_t*, long, int*);
+void rdp_jpeg_meta(const int*, int*);
 int rdp_jpeg_decode(const uint8_t*, long, int16_t*, long, uint16_t*, int);
 int rdp_jpeg_gpu(const void*, const int*, const int*, void*, int, int, int, void*, hipStream_t);
 long rdp_jpeg_plane_bytes(int, int);
@@ -1162,19 +1163,7 @@ py::object jpeg_decode(py::bytes data, bool parallel, bool pin) {
   auto opt = torch::TensorOptions().pinned_memory(pin);
   auto meta = torch::zeros({32 + 192}, opt.dtype(torch::kInt32));
   int* g = meta.data_ptr<int>();
-  const int W = hi[0], H = hi[1], nc = hi[2], hmax = hi[3], vmax = hi[4];
-  g[0] = W; g[1] = H; g[2] = nc; g[3] = hmax; g[4] = vmax;
-  long blk = 0, pb = 0;
-  for (int c = 0; c < nc; ++c) {
-    const int h = hi[9 + 5 * c], v = hi[10 + 5 * c], bw = hi[11 + 5 * c], bh = hi[12 + 5 * c];
-    int* q = g + 8 + 8 * c;
-    q[0] = h; q[1] = v; q[2] = bw; q[3] = bh; q[4] = (int)blk; q[5] = (int)pb;
-    q[6] = (W * h + hmax - 1) / hmax;
-    q[7] = (H * v + vmax - 1) / vmax;
-    blk += (long)bw * bh;
-    pb += (long)bw * 8 * bh * 8;
-  }
-  g[5] = (int)blk;
+  rdp_jpeg_meta(hi, g);
   auto coefs = torch::empty({nco}, opt.dtype(torch::kInt16));
   uint16_t qt16[3 * 64];
   int r;

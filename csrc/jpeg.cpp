@@ -454,6 +454,26 @@ long rdp_jpeg_info(const uint8_t* d, long n, int* info) {
   return j.total_coefs;
 }
 
+// The pixel stage's geometry block (meta int32[32]: W, H, ncomp, hmax, vmax, total blocks; per component
+// c at 8 + 8c: h, v, blocks per line, block rows, first block, plane byte offset, downsampled width,
+// height) from rdp_jpeg_info's header summary `hi`.
+void rdp_jpeg_meta(const int* hi, int* g) {
+  const int W = hi[0], H = hi[1], nc = hi[2], hmax = hi[3], vmax = hi[4];
+  for (int i = 0; i < 32; ++i) g[i] = 0;
+  g[0] = W; g[1] = H; g[2] = nc; g[3] = hmax; g[4] = vmax;
+  long blk = 0, pb = 0;
+  for (int c = 0; c < nc; ++c) {
+    const int h = hi[9 + 5 * c], v = hi[10 + 5 * c], bw = hi[11 + 5 * c], bh = hi[12 + 5 * c];
+    int* q = g + 8 + 8 * c;
+    q[0] = h; q[1] = v; q[2] = bw; q[3] = bh; q[4] = (int)blk; q[5] = (int)pb;
+    q[6] = (W * h + hmax - 1) / hmax;
+    q[7] = (H * v + vmax - 1) / vmax;
+    blk += (long)bw * bh;
+    pb += (long)bw * 8 * bh * 8;
+  }
+  g[5] = (int)blk;
+}
+
 // Entropy-decode into `coefs` (rdp_jpeg_info's count, int16, plane after plane, blocks row-major,
 // natural order, quantized) and the component quantisation tables into qt[3][64] (natural order).
 // Restart segments are decoded in parallel when `parallel`. 0 ok, -1 corrupt, -2 unsupported.

@@ -21,16 +21,24 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "host_pool.h"
+
 namespace py = pybind11;
 
 extern "C" long rdp_png_encode_gray(const uint8_t*, int, int, int, int, int, uint8_t*, long);
 extern "C" long rdp_png_encode_bound(int, int, int, int);
+extern "C" long rdp_jpeg_info(const uint8_t*, long, int*);
+extern "C" void rdp_jpeg_meta(const int*, int*);
+extern "C" int rdp_jpeg_decode(const uint8_t*, long, int16_t*, long, uint16_t*, int);
+extern "C" int rdp_png_info(const uint8_t*, long, int*, int*, int*);
+extern "C" int rdp_png_decode(const uint8_t*, long, uint8_t*, long, int);
 
 namespace {
 
@@ -51,6 +59,9 @@ struct DeviceScope {  // make `dev` current for this thread, restore on exit
 };
 
 inline void* P(uintptr_t v) { return reinterpret_cast<void*>(v); }
+
+std::string encode_wire(double mean, double maxc, const double* pts, size_t npts, const std::string& status,
+                        const uint8_t* mask01, int h, int w, float coverage, float proc_ms, int level, int bands);
 
 class FrameRunner {
  public:
@@ -142,6 +153,11 @@ class FrameRunner {
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
     std::memcpy(h_depth_, dp, depth_bytes_);
+    launch_depth_half();
+  }
+
+ private:
+  void launch_depth_half() {  // h_depth_ staged; the device is current
     if (depth_stream_) {
       hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, cs_), "H2D depth");
       hip_check(hipEventRecord(evd_, cs_), "hipEventRecord");
@@ -154,6 +170,119 @@ class FrameRunner {
     if (res_bytes_) hip_check(hipMemcpyAsync(h_res_, d_res_, res_bytes_, hipMemcpyDeviceToHost, s_), "D2H result");
     hip_check(hipEventRecord(ev1_, s_), "hipEventRecord");
     recorded_ = true;
+  }
+
+ public:
+  // ---- whole requests natively (the gRPC fast path) ---------------------------------------------------
+  // The colour JPEG and depth PNG bytes of an AnalysisRequest: the JPEG is entropy-decoded into this
+  // runner's pinned coefficient buffers and its network graph launched while the depth PNG inflates in
+  // parallel (host pool), then the geometry half -- one call, no interpreter lock. collect_encoded()
+  // waits for the frame and builds the AnalysisResponse wire bytes from the result the geometry kernels
+  // wrote to host memory. Frames this path does not take (JPEG the native decoder declines, other frame
+  // sizes, non-16-bit depth) return a code and nothing is launched: the caller decodes them itself.
+  enum { kOk = 0, kNotNative = 1, kSize = 2, kCorrupt = 3 };
+  void configure_encoded(int H, int W, int num_samples) {
+    DeviceScope g(dev_);
+    H_ = H; W_ = W; ns_ = num_samples;
+    if (!h_meta_) {
+      hip_check(hipHostMalloc(&h_meta_, meta_bytes_ ? meta_bytes_ : 224 * 4, hipHostMallocDefault), "hipHostMalloc");
+      hip_check(hipHostMalloc(&h_coef_, coef_cap_ ? coef_cap_ : 2, hipHostMallocDefault), "hipHostMalloc");
+      host_.push_back(h_meta_);
+      host_.push_back(h_coef_);
+    }
+  }
+
+  int submit_encoded(py::bytes color, py::bytes depth) {
+    char *cp = nullptr, *dp = nullptr;
+    Py_ssize_t cn = 0, dn = 0;
+    if (PyBytes_AsStringAndSize(color.ptr(), &cp, &cn) != 0 || PyBytes_AsStringAndSize(depth.ptr(), &dp, &dn) != 0)
+      throw py::error_already_set();
+    if (!h_meta_ || !h_coef_ || !exec_[2] || !exec_[3]) throw std::runtime_error("FrameRunner: configure_encoded first");
+    py::gil_scoped_release nogil;
+    t0_ = std::chrono::steady_clock::now();
+    const uint8_t* c = (const uint8_t*)cp;
+    const uint8_t* d = (const uint8_t*)dp;
+    // headers first: nothing is launched unless both halves are native frames of this pipeline's size
+    int hi[24];
+    const long nco = rdp_jpeg_info(c, (long)cn, hi);
+    if (nco == -1) return kCorrupt;
+    if (nco <= 0) return kNotNative;
+    int pw = 0, ph = 0, bd = 0;
+    if (rdp_png_info(d, (long)dn, &pw, &ph, &bd) != 0 || bd != 16) return kNotNative;
+    if (hi[0] != W_ || hi[1] != H_ || pw != W_ || ph != H_) return kSize;
+    if ((size_t)nco * 2 > coef_cap_ || meta_bytes_ < 224 * 4) return kNotNative;
+    int rc[2] = {0, 0};
+    std::string err;
+    DeviceScope g(dev_);
+    rdp::host_pool().parallel_for(2, [&](int k) {
+      try {
+        work_half(k, c, (long)cn, d, (long)dn, hi, nco, rc);
+      } catch (const std::exception& e) {  // never out of a pool thread
+        rc[k] = -1;
+        err = e.what();
+      }
+    });
+    if (rc[0] < 0 || rc[1] < 0) {
+      (void)hipStreamSynchronize(s_);
+      throw std::runtime_error("submit_encoded: " + err);
+    }
+    if (rc[0]) {  // nothing of the frame was launched
+      return rc[0];
+    }
+    if (rc[1]) {  // the colour half is in flight: drain it, report the frame
+      hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
+      return rc[1];
+    }
+    launch_depth_half();
+    return kOk;
+  }
+
+  void work_half(int k, const uint8_t* c, long cn, const uint8_t* d, long dn, const int* hi, long nco, int* rc) {
+    {
+      if (k == 0) {  // colour: entropy decode, then the network half on the frame stream
+        int* meta = (int*)h_meta_;
+        rdp_jpeg_meta(hi, meta);
+        uint16_t qt[3 * 64];
+        if (rdp_jpeg_decode(c, cn, (int16_t*)h_coef_, nco, qt, 1) != 0) { rc[0] = kCorrupt; return; }
+        for (int i = 0; i < 3 * 64; ++i) meta[32 + i] = qt[i];
+        DeviceScope gk(dev_);
+        hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
+        hip_check(hipMemcpyAsync(d_meta_, h_meta_, meta_bytes_, hipMemcpyHostToDevice, s_), "H2D meta");
+        hip_check(hipMemcpyAsync(d_coef_, h_coef_, (size_t)nco * 2, hipMemcpyHostToDevice, s_), "H2D coefs");
+        hip_check(hipGraphLaunch(exec_[2], s_), "hipGraphLaunch");
+      } else {  // depth: 16-bit PNG straight into the pinned staging buffer
+        if (rdp_png_decode(d, dn, (uint8_t*)h_depth_, (long)depth_bytes_, 1) != 0) rc[1] = kCorrupt;
+      }
+    }
+  }
+
+  // (payload bytes, mean, max, coverage %, status code, gpu ms); status code 4 = the fit needs the host
+  // (the caller finishes that frame from the device edge buffers)
+  py::tuple collect_encoded(int level, int bands) {
+    float gpu_ms = 0.f;
+    double mean = 0, maxc = 0, cov = 0;
+    int st = 0;
+    std::string out;
+    {
+      py::gil_scoped_release nogil;
+      DeviceScope g(dev_);
+      hip_check(hipEventSynchronize(ev1_), "hipEventSynchronize");
+      hip_check(hipEventElapsedTime(&gpu_ms, ev0_, ev1_), "hipEventElapsedTime");
+      const double* r = (const double*)h_res_;
+      st = (int)r[0];
+      const double count = r[8 + 3 * ns_];
+      cov = 100.0 * count / ((double)H_ * W_);
+      if (st != 4) {
+        static const char* names[4] = {"ok", "too_few_points", "too_few_edge_points", "fit_failed"};
+        const std::string status = (st >= 0 && st < 4) ? names[st] : "fit_failed";
+        if (st == 0) { mean = r[4]; maxc = r[5]; }
+        const float proc =
+            std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0_).count();
+        out = encode_wire(mean, maxc, st == 0 ? r + 8 : nullptr, st == 0 ? (size_t)ns_ : 0, status,
+                          (const uint8_t*)h_mask_, H_, W_, (float)cov, proc, level, bands);
+      }
+    }
+    return py::make_tuple(py::bytes(out), mean, maxc, cov, st, gpu_ms);
   }
 
   // a frame whose depth half never came (its decode failed): drain the colour half
@@ -192,6 +321,9 @@ class FrameRunner {
 
   bool recorded_ = false;
   bool depth_stream_ = true;
+  int H_ = 0, W_ = 0, ns_ = 0;
+  void *h_meta_ = nullptr, *h_coef_ = nullptr;
+  std::chrono::steady_clock::time_point t0_;
   int dev_;
   hipStream_t s_;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr, evd_ = nullptr;
@@ -255,33 +387,44 @@ py::bytes encode_response(double mean, double maxc, py::object points, const std
   std::string out;
   {
     py::gil_scoped_release nogil;
-    std::string png;
-    if (h > 0 && w > 0) {
-      for (auto& v : img) v = v ? 255 : 0;
-      png.resize((size_t)rdp_png_encode_bound(w, h, 1, bands));
-      const long n = rdp_png_encode_gray(img.data(), w, h, 1, level, bands, (uint8_t*)&png[0], (long)png.size());
-      if (n < 0) throw std::runtime_error("mask PNG encode failed");
-      png.resize((size_t)n);
-    }
-    out.reserve(png.size() + status.size() + pts.size() * 10 + 64);
-    put_fixed64(out, 1, mean);
-    put_fixed64(out, 2, maxc);
-    std::string sub;
-    for (size_t i = 0; i + 3 <= pts.size(); i += 3) {
-      sub.clear();
-      put_fixed64(sub, 1, pts[i]);
-      put_fixed64(sub, 2, pts[i + 1]);
-      put_fixed64(sub, 3, pts[i + 2]);
-      put_varint(out, 3 << 3 | 2);  // repeated Point3D: always present, even when empty
-      put_varint(out, sub.size());
-      out += sub;
-    }
-    put_bytes(out, 4, status.data(), status.size());
-    put_bytes(out, 5, png.data(), png.size());
-    put_fixed32(out, 6, coverage);
-    put_fixed32(out, 7, proc_ms);
+    out = encode_wire(mean, maxc, pts.data(), pts.size() / 3, status, h > 0 && w > 0 ? img.data() : nullptr, h, w,
+                      coverage, proc_ms, level, bands);
   }
   return py::bytes(out);
+}
+
+// AnalysisResponse wire bytes (no Python objects: callable without the GIL). mask01: HxW u8 {0, 1}
+// (PNG-encoded as 0 / 255) or nullptr; pts: npts x 3 doubles.
+std::string encode_wire(double mean, double maxc, const double* pts, size_t npts, const std::string& status,
+                        const uint8_t* mask01, int h, int w, float coverage, float proc_ms, int level, int bands) {
+  std::string png;
+  if (mask01 && h > 0 && w > 0) {
+    std::vector<uint8_t> img((size_t)h * w);
+    for (size_t i = 0; i < img.size(); ++i) img[i] = mask01[i] ? 255 : 0;
+    png.resize((size_t)rdp_png_encode_bound(w, h, 1, bands));
+    const long n = rdp_png_encode_gray(img.data(), w, h, 1, level, bands, (uint8_t*)&png[0], (long)png.size());
+    if (n < 0) throw std::runtime_error("mask PNG encode failed");
+    png.resize((size_t)n);
+  }
+  std::string out;
+  out.reserve(png.size() + status.size() + npts * 30 + 64);
+  put_fixed64(out, 1, mean);
+  put_fixed64(out, 2, maxc);
+  std::string sub;
+  for (size_t i = 0; i < npts; ++i) {
+    sub.clear();
+    put_fixed64(sub, 1, pts[3 * i]);
+    put_fixed64(sub, 2, pts[3 * i + 1]);
+    put_fixed64(sub, 3, pts[3 * i + 2]);
+    put_varint(out, 3 << 3 | 2);  // repeated Point3D: always present, even when empty
+    put_varint(out, sub.size());
+    out += sub;
+  }
+  put_bytes(out, 4, status.data(), status.size());
+  put_bytes(out, 5, png.data(), png.size());
+  put_fixed32(out, 6, coverage);
+  put_fixed32(out, 7, proc_ms);
+  return out;
 }
 
 }  // namespace
@@ -297,6 +440,10 @@ void register_serve_runtime(py::module_& m) {
       .def("submit_array", &FrameRunner::submit_array)
       .def("submit_jpeg", &FrameRunner::submit_jpeg)
       .def("submit_depth", &FrameRunner::submit_depth)
+      .def("configure_encoded", &FrameRunner::configure_encoded, py::arg("H"), py::arg("W"), py::arg("num_samples"))
+      .def("submit_encoded", &FrameRunner::submit_encoded, py::arg("color"), py::arg("depth"),
+           "0 launched, 1 not a native frame, 2 other frame size, 3 corrupt (nothing in flight)")
+      .def("collect_encoded", &FrameRunner::collect_encoded, py::arg("level") = 1, py::arg("bands") = 4)
       .def("abort", &FrameRunner::abort)
       .def("wait", &FrameRunner::wait);
   m.def("encode_response", &encode_response, py::arg("mean"), py::arg("max"), py::arg("points"), py::arg("status"),

@@ -81,6 +81,16 @@ class FrameResult:
     points: Optional[np.ndarray] = None  # spline points [n, 3] float64 (device fits; the server encodes them)
 
 
+@dataclass
+class WireResult:
+    """A frame served end to end natively: its AnalysisResponse wire bytes plus the metrics-log fields."""
+    payload: bytes
+    mean_curvature: float
+    max_curvature: float
+    coverage: float
+    gpu_ms: float
+
+
 SRC_BGR, SRC_RGB, SRC_JPEG = 0, 1, 2  # colour sources of a network graph
 GEO, GEO_SLOT = "geo", 3  # the geometry graph (FrameRunner slot 3)
 
@@ -192,6 +202,10 @@ class FramePipeline:
                 self._capture(SRC_JPEG)
         else:
             self.refresh_weights()
+        # whole encoded requests natively (FrameRunner.submit_encoded): JPEG pipelines with a runner
+        self.encoded = bool(graph and jpeg and self.runner is not None)
+        if self.encoded:
+            self.runner.configure_encoded(H, W, self.cfg.num_samples)
 
     # ---------------------------------------------------------------- device program
     # A frame is two captured graphs on the pipeline's stream: the network graph of its colour source
@@ -334,6 +348,29 @@ class FramePipeline:
                         self.h_res.copy_(self.geo.res, non_blocking=True)
                     self.ev1.record(s)
         self._pending_src = None
+
+    def submit_encoded(self, color: bytes, depth: bytes) -> int:
+        """A request's colour JPEG + 16-bit depth PNG bytes, decoded and launched natively without the
+        interpreter lock (csrc/serve_runtime.cpp). 0: in flight (``collect_encoded``); 1 / 2: not a
+        frame this path takes (other JPEG kinds, other sizes, 8-bit depth), 3: corrupt -- nothing in
+        flight, the caller decodes it itself."""
+        if not self.encoded:
+            return 1
+        with trace.range("serve.frame.submit_encoded"):
+            return self.runner.submit_encoded(color, depth)
+
+    def collect_encoded(self):
+        """WireResult of the frame ``submit_encoded`` launched, or a FrameResult when its spline fit
+        must finish on the host (the device's capacity was exceeded: rare)."""
+        with trace.range("serve.frame.collect_encoded"):
+            payload, mean, maxc, cov, st, gpu_ms = self.runner.collect_encoded(1, 4)
+        if st == 4:
+            from ..geometry.curvature import coverage_from_device
+            h_res = self.h_res.numpy()
+            res = self.geo.finish_device(h_res)
+            cov = 100.0 * coverage_from_device(h_res, self.cfg) / (self.H * self.W)
+            return FrameResult(self.h_mask.numpy().copy(), cov, res, {"gpu_ms": gpu_ms})
+        return WireResult(payload, mean, maxc, cov, gpu_ms)
 
     def abort(self):
         """Drop a frame whose depth half will not come (its decode failed)."""
@@ -632,10 +669,40 @@ class EngineSession:
         self.inflight.append((tag, p, q))
         return out
 
-    def _collect_one(self):
-        tag, p, q = self.inflight.popleft()
+    def submit_encoded(self, color: bytes, depth: bytes, tag=None):
+        """A request's encoded colour / depth bytes straight to a pipeline of the pool's configured size
+        (FramePipeline.submit_encoded: decode + launch natively, no interpreter lock). Returns
+        (collected, code): the frames it had to collect, and 0 when this frame is in flight -- else
+        nothing of it is (1 / 2 / 3: decode it and ``submit`` instead)."""
+        out = []
+        while len(self.inflight) >= self.depth:
+            out.append(self._collect_one())
+        q = self.pool._get(self.replica, *self.pool.home_size)
         try:
-            return tag, p.collect()
+            p = q.get_nowait()
+        except queue.Empty:
+            while self.inflight:
+                out.append(self._collect_one())
+            p = q.get()
+        try:
+            code = p.submit_encoded(color, depth) if getattr(p, "encoded", False) else 1
+        except BaseException as e:
+            q.put(p)
+            if not isinstance(e, Exception):
+                raise
+            out += self.drain()
+            out.append((tag, e))
+            return out, 0
+        if code != 0:
+            q.put(p)
+            return out, code
+        self.inflight.append((tag, p, q, True))
+        return out, 0
+
+    def _collect_one(self):
+        tag, p, q, *enc = self.inflight.popleft()
+        try:
+            return tag, (p.collect_encoded() if enc else p.collect())
         except Exception as e:  # a failed frame must not take the pipeline with it
             return tag, e
         finally:
@@ -654,7 +721,7 @@ class EngineSession:
         """Give every pipeline this session holds back to its pool without building results (a stream
         that ended early: client cancel, transport error, abort). Idempotent."""
         while self.inflight:
-            _, p, q = self.inflight.popleft()
+            _, p, q, *_enc = self.inflight.popleft()
             try:
                 p.wait_idle()
             except Exception:  # the pipeline goes back either way

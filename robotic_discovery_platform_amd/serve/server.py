@@ -35,7 +35,7 @@ from ..data.image_io import decode_image, encode_png
 from ..data.jpeg import decode_coefs
 from ..proto import vision as pb
 from ..utils import trace
-from .engine import EnginePool, _is_native
+from .engine import EnginePool, WireResult, _is_native
 
 log = logging.getLogger(__name__)
 
@@ -147,6 +147,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         # the pixel stage runs in the frame graph (data/jpeg.py)
         self._gpu_jpeg = bool(getattr(engine, "jpeg", False))
         self._pin = bool(getattr(engine, "gpu", False))  # pinned coefficient buffers: GPU engines only
+        # whole frames natively (EngineSession.submit_encoded): the request bytes go to a pipeline that
+        # decodes, launches, waits and encodes the response without the interpreter lock; this thread
+        # only moves bytes. Frames that path declines take the decode path below.
+        self._encoded = self._gpu_jpeg and self._pin and hasattr(engine, "home_size")
         try:
             from ..ops import native
             self._encode = getattr(native(build_if_missing=False), "encode_response", None)
@@ -194,6 +198,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     cb, db = req.color_image.data, req.depth_image.data
                     if self.faults is not None:
                         cb, db = self.faults.corrupt_request(i, cb, db)
+                    if self._encoded:  # decoded natively by the pipeline (or on demand, see the handler)
+                        if not put((t, cb, db, None)):
+                            return
+                        continue
                     fc = self._pool.submit(self._decode_color, cb)
                     fd = self._pool.submit(self._decode_depth, db)
                     if not put((t, fc, fd, None)):
@@ -212,6 +220,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                 if item[3] is not None:
                     raise item[3]
                 t, fc, fd, _ = item
+                if isinstance(fc, bytes):  # encoded frame: (colour bytes, depth bytes)
+                    yield t, fc, fd, None, lambda: q.qsize() > 0
+                    continue
                 try:
                     color, err = fc.result(), None
                 except Exception as e:
@@ -239,9 +250,22 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
 
     def _log(self, r):
         if self.metrics is not None and r is not None:
-            c = r.curvature
-            self.metrics.write(c.mean_curvature, c.max_curvature, r.coverage)
+            if isinstance(r, WireResult):
+                self.metrics.write(r.mean_curvature, r.max_curvature, r.coverage)
+            else:
+                c = r.curvature
+                self.metrics.write(c.mean_curvature, c.max_curvature, r.coverage)
         self.frames += 1
+
+    def _wire_ready(self, r: "WireResult", t):
+        """A natively served frame: the response bytes exist already; bookkeeping only."""
+        t_read, t_start = t
+        now = time.perf_counter()
+        with self._stats_lock:
+            self.queue_ms.append((t_start - t_read) * 1e3)
+            self.proc_ms.append((now - t_start) * 1e3)
+        self.stage_ms["gpu"].append(r.gpu_ms)
+        return r.payload, r, now
 
     def _respond_timed(self, r, t):
         t0 = time.perf_counter()
@@ -322,7 +346,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                         raise r
                     self.frame_failures += 1
                     log.warning("frame failed (%s: %s): degraded response", type(r).__name__, r)
-                inflight.append(self._pool.submit(self._respond_timed, r, times.pop(tag)))
+                if isinstance(r, WireResult):
+                    inflight.append(_Ready(self._wire_ready(r, times.pop(tag))))
+                else:
+                    inflight.append(self._pool.submit(self._respond_timed, r, times.pop(tag)))
 
         def ready(force: bool):
             while inflight and (force or inflight[0].done() or len(inflight) > self.prefetch):
@@ -336,7 +363,22 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             for i, (t_read, color, depth, err, more) in enumerate(frames):
                 t_start = time.perf_counter()
                 times[i] = (t_read, t_start)
-                if err is not None:
+                if isinstance(color, bytes):  # encoded frame: natively decoded + launched by a pipeline
+                    with trace.range("serve.rpc.frame"):
+                        done, code = sess.submit_encoded(color, depth, tag=i)
+                        encode(done)
+                        if code != 0:  # a frame that path declines: decode here, then the array path
+                            try:
+                                c, d = self._decode_color(color), self._decode_depth(depth)
+                            except Exception as e:
+                                encode(sess.drain())
+                                encode([(i, e)])
+                            else:
+                                encode(sess.submit(c, d, tag=i, rgb=True))
+                        self.stage_ms["submit"].append((time.perf_counter() - t_start) * 1e3)
+                    if not more():
+                        encode(sess.drain())
+                elif err is not None:
                     encode(sess.drain())  # keep request order: older frames first
                     encode([(i, err)])
                 else:
@@ -360,6 +402,20 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             # error, abort), the session's in-flight pipelines go back to the pool and the reader stops
             sess.close()
             frames.close()
+
+
+class _Ready:
+    """A response that needs no more work, in the handler's queue of pending futures."""
+    __slots__ = ("_v",)
+
+    def __init__(self, v):
+        self._v = v
+
+    def done(self) -> bool:
+        return True
+
+    def result(self):
+        return self._v
 
 
 class ModelWatcher(threading.Thread):

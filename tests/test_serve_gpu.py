@@ -346,3 +346,66 @@ def test_session_split_submit_and_failed_depth_half():
     for k in (0, 3):
         assert np.array_equal(res[k].mask, ref.mask) and res[k].coverage == ref.coverage
         assert res[k].curvature.mean_curvature == ref.curvature.mean_curvature
+
+
+class _Ctx:
+    def set_code(self, c):
+        self.code = c
+
+    def set_details(self, d):
+        self.details = d
+
+
+def test_encoded_fast_path_matches_decode_path(tmp_path):
+    """The native whole-frame path (request bytes -> pipeline decode, launch, wait, response encode
+    without the interpreter lock) answers every frame exactly as the decode path does -- every field
+    but proc_time_ms; frames it declines (progressive JPEG, another frame size, 8-bit depth) and corrupt
+    ones take the decode path in the same stream, in order."""
+    from robotic_discovery_platform_amd.data.image_io import encode_jpeg, encode_png
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K, make_scene
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.proto import vision as pb
+    from robotic_discovery_platform_amd.serve.engine import EnginePool
+    from robotic_discovery_platform_amd.serve.server import MetricsLog, VisionAnalysisService
+    torch.manual_seed(0)
+    nat = UNetNative(3, 1, device=torch.device("cuda")).eval()
+    with torch.no_grad():
+        nat.store.view("outc.conv.bias").fill_(0.0)
+    reqs = []
+    for seed in (2, 5, 7, 9):
+        sc = make_scene(seed)
+        reqs.append(pb.AnalysisRequest(color_image=pb.Image(data=encode_jpeg(sc.color, 92, restart_rows=1)),
+                                       depth_image=pb.Image(data=encode_png(sc.depth, 1, bands=8))))
+    sc = make_scene(3)
+    prog = _jpeg_bytes(np.ascontiguousarray(sc.color[..., ::-1]), quality=90, progressive=True)
+    reqs.insert(1, pb.AnalysisRequest(color_image=pb.Image(data=prog), depth_image=pb.Image(data=encode_png(sc.depth))))
+    small = make_scene(4)
+    reqs.insert(3, pb.AnalysisRequest(color_image=pb.Image(data=encode_jpeg(small.color[::2, ::2].copy(), 92)),
+                                      depth_image=pb.Image(data=encode_png(small.depth[::2, ::2].copy()))))
+    reqs.insert(4, pb.AnalysisRequest(color_image=pb.Image(data=encode_jpeg(sc.color, 92)),
+                                      depth_image=pb.Image(data=encode_png((sc.depth // 256).astype(np.uint8)))))
+    reqs.append(pb.AnalysisRequest(color_image=pb.Image(data=b"\xff\xd8\xff\xdb"), depth_image=pb.Image(data=b"x")))
+    out = {}
+    for mode in ("encoded", "decode"):
+        pool = EnginePool(nat, DEFAULT_K, 0.001, n=2, graph=True, rgb=True, jpeg=True)
+        svc = VisionAnalysisService(pool, MetricsLog(str(tmp_path / f"{mode}.csv")))
+        assert svc._encoded
+        if mode == "decode":
+            svc._encoded = False
+        resp = list(svc.AnalyzeActuatorPerformance(iter(reqs), _Ctx()))
+        svc.close()
+        out[mode] = [pb.AnalysisResponse.FromString(r if isinstance(r, bytes) else r.SerializeToString())
+                     for r in resp]
+        if mode == "encoded":  # the native path served the plain frames
+            assert len(svc.stage_ms["decode_color"]) < len(reqs)
+    a, b = out["encoded"], out["decode"]
+    assert len(a) == len(b) == len(reqs)
+    for x, y in zip(a, b):
+        assert x.proc_time_ms > 0 or x.status.startswith("error")
+        x.proc_time_ms = y.proc_time_ms = 0.0
+        assert x == y
+    assert a[-1].status.startswith("error") and a[0].status == "ok" and len(a[0].spline_points) == 100
+    # the metrics log gets the same (mean, max, coverage) rows, timestamps aside
+    ra = [r.split(",")[1:] for r in open(tmp_path / "encoded.csv").read().splitlines()[1:]]
+    rb = [r.split(",")[1:] for r in open(tmp_path / "decode.csv").read().splitlines()[1:]]
+    assert ra == rb and len(ra) == len(reqs) - 1  # the corrupt frame logs no row
