@@ -295,8 +295,10 @@ def measure_e2e_procs(model, frames: int = 200, warmup: int = 20, procs: int = 2
         for p in servers:
             so, _ = p.communicate("", timeout=120)
             stats.append(json.loads(so.strip().splitlines()[-1]))
-        for k in ("decode_color", "decode_depth", "gpu", "respond"):
-            out[f"e2e_stage_{k}_p50_ms" + sfx] = round(float(np.median([st[f"{k}_p50_ms"] for st in stats])), 3)
+        for k in ("submit", "decode_color", "decode_depth", "gpu", "respond"):
+            v = float(np.median([st[f"{k}_p50_ms"] for st in stats]))
+            if v == v:  # stages a path does not have (native frames: no separate decode / respond) stay out
+                out[f"e2e_stage_{k}_p50_ms" + sfx] = round(v, 3)
         _progress(f"e2e procs: {out}")
     finally:
         for p in servers:

@@ -370,7 +370,7 @@ def test_encoded_fast_path_matches_decode_path(tmp_path):
     torch.manual_seed(0)
     nat = UNetNative(3, 1, device=torch.device("cuda")).eval()
     with torch.no_grad():
-        nat.store.view("outc.conv.bias").fill_(0.0)
+        nat.store.view("outc.conv.bias").fill_(4.0)  # mask ~ everything: fits run on the edge points
     reqs = []
     for seed in (2, 5, 7, 9):
         sc = make_scene(seed)
@@ -403,8 +403,11 @@ def test_encoded_fast_path_matches_decode_path(tmp_path):
     for x, y in zip(a, b):
         assert x.proc_time_ms > 0 or x.status.startswith("error")
         x.proc_time_ms = y.proc_time_ms = 0.0
+        if x.status.startswith("error"):  # the message names a Python object address
+            x.status, y.status = x.status.split(" <")[0], y.status.split(" <")[0]
         assert x == y
-    assert a[-1].status.startswith("error") and a[0].status == "ok" and len(a[0].spline_points) == 100
+    assert a[-1].status.startswith("error")
+    assert sum(r.status == "ok" and len(r.spline_points) == 100 for r in a) >= 3
     # the metrics log gets the same (mean, max, coverage) rows, timestamps aside
     ra = [r.split(",")[1:] for r in open(tmp_path / "encoded.csv").read().splitlines()[1:]]
     rb = [r.split(",")[1:] for r in open(tmp_path / "decode.csv").read().splitlines()[1:]]
