@@ -827,16 +827,21 @@ class UNetExecutor:
         return self._on_side(lambda: fn(self.slab))
 
     @contextlib.contextmanager
-    def comm_stream(self):
-        """Make the current stream one ordered after EVERY gradient issued so far -- the main stream's
-        (BN, head, bias gradients) and the wgrad side stream's (conv weight gradients) -- for the DDP
-        bucket all-reduces (parallel.ddp.FlatBucketer ``launch_ctx``): the side stream after a fork
-        from the main stream. Without a side stream the current stream already is."""
+    def comm_stream(self, producer=None):
+        """Make the current stream one ordered after EVERY gradient issued so far, for the DDP bucket
+        all-reduces (parallel.ddp.FlatBucketer ``launch_ctx``): the wgrad side stream (conv weight
+        gradients), after a fork from the main stream (BN, head, bias gradients) -- skipped when the
+        bucket was completed on the side stream (``producer``): every main-stream gradient of it was
+        issued before the completing weight gradient's own fork. Without a side stream the current
+        stream already is ordered.
+        (Measured, forced DDP at world 1: a dedicated collective stream waiting on side + main instead
+        cost 6.5 % at bs 64 and 7 % at bs 4 -- 20.96 vs 19.69 ms, 2.66 vs 2.49 ms -- and more with 8
+        hardware queues, 23.3 / 5.5 ms; profiles/ddp_world1.md.)"""
         if self.side is None:
             yield
             return
         cur = torch.cuda.current_stream()
-        if cur != self.side:
+        if cur != self.side and (producer is None or producer != self.side):
             _stream_wait(self.side, cur)
         with torch.cuda.stream(self.side):
             yield

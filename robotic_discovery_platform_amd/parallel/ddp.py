@@ -15,8 +15,8 @@ Design (MI355X-first):
     The native executor produces gradients on two streams (BN / head gradients on the main stream,
     conv weight gradients on the wgrad side stream), so a bucket may only be issued from a stream
     that is ordered after EVERY producer of its gradients. ``launch_ctx`` supplies that stream
-    (the executor's: the side stream after a fork from main, ``UNetExecutor.comm_stream``); the
-    bf16 narrowing copy runs there too. :class:`StreamOrderChecker` verifies it with vector clocks.
+    (the executor's wgrad side stream, forked from the main stream where needed:
+    ``UNetExecutor.comm_stream``); the bf16 narrowing copy runs there too. :class:`StreamOrderChecker` verifies it with vector clocks.
   * A parameter of at least half a bucket that would overflow the open bucket starts a new one, so
     the small decoder layers whose gradients are final first (outc, up4 .. up1.conv.3, 12.5 MB) go
     out before the 18.9 MB up1.conv.0 gradient exists.
@@ -120,8 +120,10 @@ class FlatBucketer:
         self.pending = [len(p) for p in self.bucket_params]
         self.handles = []
 
-    def _launch(self, b: int):
-        with (self.launch_ctx() if self.launch_ctx is not None else contextlib.nullcontext()):
+    def _launch(self, b: int, producer=None):
+        """Issue bucket ``b``; ``producer``: the stream of the gradient that completed it (launch_ctx may
+        use it to skip a wait)."""
+        with (self.launch_ctx(producer) if self.launch_ctx is not None else contextlib.nullcontext()):
             if self.checker is not None:
                 self.checker.check_launch(self.bucket_params[b], torch.cuda.current_stream())
             lo, hi = self.buckets[b]
@@ -151,9 +153,9 @@ class FlatBucketer:
             self.pending[b] -= 1
             if self.pending[b] == 0:
                 if self.host_call is not None:
-                    self.host_call(lambda b=b: self._launch(b))
+                    self.host_call(lambda b=b, s=stream: self._launch(b, s))
                 else:
-                    self._launch(b)
+                    self._launch(b, stream)
 
     def finish(self):
         """Every bucket issued; the caller's stream is ordered after the reductions. With native issue

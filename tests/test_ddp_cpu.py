@@ -228,7 +228,7 @@ def _hook_sequence_launches(bilinear: bool, bucket_mb: float):
         off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
     b = FlatBucketer(torch.zeros(off), ranges, bucket_mb)
     launches, hooks = [], []
-    b._launch = lambda k: launches.append((k, len(hooks)))
+    b._launch = lambda k, s=None: launches.append((k, len(hooks)))
     specs = unet_conv_specs(4, 64, 3, bilinear)
     ups = [] if bilinear else [UpTSpec(f"up{i}.up", 64 * 2 ** (5 - i), 64 * 2 ** (4 - i)) for i in range(1, 5)]
     b.reset()
@@ -269,8 +269,9 @@ def test_bucket_big_param_starts_new_bucket():
 def _simulate_issue(bilinear: bool, ordered: bool):
     """The native executor's two-stream protocol on fake stream ids, checked by StreamOrderChecker:
     BN / head gradients on the main stream, each conv / ConvTranspose weight gradient on the side
-    stream after a fork from main; buckets issued either on the comm stream (side after a fork from
-    main: ``UNetExecutor.comm_stream``) or, unordered, on the stream the hook runs on (main)."""
+    stream after a fork from main; buckets issued either on the side stream (forked from main unless side
+    completed the bucket: ``UNetExecutor.comm_stream``) or, unordered, on the stream the hook runs on
+    (main)."""
     from robotic_discovery_platform_amd.models.unet import (ALIGN, BNHook, ConvSpec, UpTSpec, backward_hook_order,
                                                              unet_conv_specs)
     from robotic_discovery_platform_amd.models.unet_ref import UNetRef
@@ -285,9 +286,10 @@ def _simulate_issue(bilinear: bool, ordered: bool):
     b = FlatBucketer(torch.zeros(off), ranges, 16.0)
     b.checker = ck
 
-    def launch(k):
-        if ordered:
-            ck.wait(SIDE, MAIN)
+    def launch(k, producer=None):
+        if ordered:  # UNetExecutor.comm_stream: on side, forked from main unless side completed the bucket
+            if producer != SIDE:
+                ck.wait(SIDE, MAIN)
             ck.check_launch(b.bucket_params[k], SIDE)
         else:
             ck.check_launch(b.bucket_params[k], MAIN)

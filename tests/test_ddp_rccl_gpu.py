@@ -155,7 +155,7 @@ def _order_worker(rank, port, out):
         hooks, launches = [], []
         hook0, launch0 = tr._hook, tr.bucketer._launch
         tr._hook = lambda sp, st=None: (hooks.append(sp.name), hook0(sp, st))
-        tr.bucketer._launch = lambda b: (launches.append((b, len(hooks))), launch0(b))
+        tr.bucketer._launch = lambda b, s=None: (launches.append((b, len(hooks))), launch0(b, s))
         x, t = _data(2)
         tr.set_batch(x.to(dev), t.to(dev))
         tr.step()
