@@ -593,7 +593,10 @@ class UNetExecutor:
             self.colsum_ws = torch.zeros(1024 * max(4 * us.cout for us in self.m.up_specs), dtype=torch.float32,
                                          device=dev)
         maxc = max(L.spec.cout for L in self.layers)
-        self.bn_partial = torch.zeros(1024 * 2 * maxc, dtype=torch.float32, device=dev)
+        # (also the fused head's BN-backward partials: 128 floats per head block -- the larger need for
+        # shallow / narrow models at large batch)
+        self.bn_partial = torch.zeros(max(1024 * 2 * maxc, C.head_partial_blocks(self.M) * 128), dtype=torch.float32,
+                                      device=dev)
 
     # ------------------------------------------------------------------ data
     def set_input(self, x: torch.Tensor, target: Optional[torch.Tensor] = None):
