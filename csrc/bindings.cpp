@@ -57,6 +57,12 @@ int rdp_upsample2_fwd(const void*, int, void*, int, int, int, int, int, int, int
                       hipStream_t);
 int rdp_upsample2_bwd(const void*, int, void*, int, int, int, int, int, int, int, int, int, const void*, int,
                       const float*, float*, int, hipStream_t);
+int rdp_conv_upT_fwd(const void*, long, int, int, const void*, long, int, void*, long, int, const float*, int, int, int, int,
+                     int, int, int, int, hipStream_t);
+int rdp_conv_upT_dgrad(const void*, long, int, int, int, int, int, int, const void*, long, int, void*, long, int, int,
+                       int, int, int, hipStream_t);
+int rdp_conv_wgrad_upT(const void*, long, int, int, int, int, int, int, const void*, long, int, int, int, int, int,
+                       float*, long, float*, int, int, hipStream_t);
 int rdp_upT_shuffle(const void*, int, const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_upT_unshuffle(const void*, int, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int rdp_colsum_bf16(const void*, int, long, int, int, float*, float*, int, hipStream_t);
@@ -788,6 +794,51 @@ void upT_shuffle(torch::Tensor yT, torch::Tensor bias, torch::Tensor u, int oy, 
                               o.C, st)) == 0, "upT_shuffle");
 }
 
+// ConvTranspose2d(2, s2) + bias written straight into u at (oy, ox) by the ping-pong GEMM's epilogue
+// (w = the [4C][Cin] forward weight). Returns 0, or -1 when that kernel does not take the shape: the
+// caller then runs conv_fwd into yT + upT_shuffle. u's border outside the window is not written.
+int conv_upT_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor bias, torch::Tensor u, int oy, int ox) {
+  Act a = act(x, "x"), o = act(u, "u");
+  check_f32(bias, "bias");
+  TORCH_CHECK(w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2 && w.size(0) == 4 * o.C &&
+                  w.size(1) >= a.C, "conv_upT_fwd: w must be bf16 [4C][>= Cin]");
+  TORCH_CHECK(a.N == o.N && bias.numel() == o.C, "conv_upT_fwd shapes");
+  TORCH_CHECK(oy >= 0 && ox >= 0 && 2 * a.H + oy <= o.H && 2 * a.W + ox <= o.W, "conv_upT_fwd placement");
+  const long xb = ((long)a.N * a.H * a.W - 1) * a.pitch * 2 + (long)a.C * 2;
+  const long ub = ((long)o.N * o.H * o.W - 1) * o.pitch * 2 + (long)o.C * 2;
+  return RDP_PLAN(rdp_conv_upT_fwd(a.ptr, xb, a.C, a.pitch, w.data_ptr(), w.numel() * 2, (int)w.size(1), o.ptr, ub,
+                                   o.pitch, bias.data_ptr<float>(), a.N, a.H, a.W, o.H, o.W, oy, ox, o.C, st));
+}
+
+// ConvTranspose2d(2, s2) input gradient dx [N,h,w,Cin] read straight from du (its 4 sub-pixels per
+// pixel; wd = the [Cin][4C] dgrad weight) on the ping-pong kernel. Returns 0, or -1 (nothing
+// launched) where that kernel does not take the shape: the caller unshuffles and runs the GEMM.
+int conv_upT_dgrad(torch::Tensor du, torch::Tensor wd, torch::Tensor dx, int oy, int ox) {
+  Act d = act(du, "du"), o = act(dx, "dx");
+  TORCH_CHECK(wd.scalar_type() == torch::kBFloat16 && wd.is_contiguous() && wd.dim() == 2 && wd.size(0) == o.C &&
+                  wd.size(1) >= 4 * d.C, "conv_upT_dgrad: wd must be bf16 [Cin][>= 4C]");
+  TORCH_CHECK(d.N == o.N && oy >= 0 && ox >= 0 && 2 * o.H + oy <= d.H && 2 * o.W + ox <= d.W, "conv_upT_dgrad placement");
+  const long db = ((long)d.N * d.H * d.W - 1) * d.pitch * 2 + (long)d.C * 2;
+  const long ob = ((long)o.N * o.H * o.W - 1) * o.pitch * 2 + (long)o.C * 2;
+  return RDP_PLAN(rdp_conv_upT_dgrad(d.ptr, db, d.C, d.pitch, d.H, d.W, oy, ox, wd.data_ptr(), wd.numel() * 2,
+                                     (int)wd.size(1), o.ptr, ob, o.C, o.pitch, o.N, o.H, o.W, st));
+}
+
+// ConvTranspose2d(2, s2) weight gradient out [Cin][4C] (+)= from du (4 sub-pixels per pixel of x) and
+// its input x [N,h,w,Cin]. Returns the split count (< 0: shape not taken, nothing launched).
+int conv_wgrad_upT(torch::Tensor du, torch::Tensor x, int oy, int ox, torch::Tensor slab, torch::Tensor out,
+                   int accumulate, int splits) {
+  Act d = act(du, "du"), a = act(x, "x");
+  check_f32(slab, "slab");
+  check_f32(out, "out");
+  TORCH_CHECK(out.numel() == (long)a.C * 4 * d.C, "conv_wgrad_upT out numel");
+  TORCH_CHECK(d.N == a.N && oy >= 0 && ox >= 0 && 2 * a.H + oy <= d.H && 2 * a.W + ox <= d.W, "conv_wgrad_upT placement");
+  const long db = ((long)d.N * d.H * d.W - 1) * d.pitch * 2 + (long)d.C * 2;
+  const long xb = ((long)a.N * a.H * a.W - 1) * a.pitch * 2 + (long)a.C * 2;
+  return RDP_PLAN(rdp_conv_wgrad_upT(d.ptr, db, d.C, d.pitch, d.H, d.W, oy, ox, a.ptr, xb, a.C, a.pitch, a.N, a.H, a.W,
+                                     slab.data_ptr<float>(), slab.numel(), out.data_ptr<float>(), accumulate, splits, st));
+}
+
 void upT_unshuffle(torch::Tensor du, torch::Tensor dyT, int oy, int ox) {
   Act d = act(du, "du"), y = act(dyT, "dyT");
   TORCH_CHECK(y.N == d.N && y.C == 4 * d.C, "upT_unshuffle shapes");
@@ -800,7 +851,7 @@ void upT_unshuffle(torch::Tensor du, torch::Tensor dyT, int oy, int ox) {
 void colsum_bf16(torch::Tensor x, int groups, torch::Tensor partial, torch::Tensor out, int accumulate) {
   Act a = act(x, "x");
   check_f32(partial, "partial"); check_f32(out, "out");
-  TORCH_CHECK(partial.numel() >= 1024L * a.C && out.numel() * groups == a.C, "colsum_bf16 sizes");
+  TORCH_CHECK(out.numel() * groups == a.C && partial.numel() >= 1024L * a.C + 64L * out.numel(), "colsum_bf16 sizes");
   TORCH_CHECK(RDP_PLAN(rdp_colsum_bf16(a.ptr, a.pitch, (long)a.N * a.H * a.W, a.C, groups, partial.data_ptr<float>(),
                               out.data_ptr<float>(), accumulate, st)) == 0,
               "colsum_bf16: channels must be a power of two in [8, 2048]");
@@ -1289,6 +1340,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("upsample2_fwd", on_device(&upsample2_fwd), py::arg("x"), py::arg("out"), py::arg("oy"), py::arg("ox"),
         py::arg("coef") = py::none());
   m.def("upT_shuffle", on_device(&upT_shuffle));
+  m.def("conv_upT_fwd", on_device(&conv_upT_fwd));
+  m.def("conv_upT_dgrad", on_device(&conv_upT_dgrad));
+  m.def("conv_wgrad_upT", on_device(&conv_wgrad_upT));
   m.def("upT_unshuffle", on_device(&upT_unshuffle));
   m.def("colsum_bf16", on_device(&colsum_bf16));
   m.def("upsample2_bwd", on_device(&upsample2_bwd), py::arg("dout"), py::arg("dx"), py::arg("oy"), py::arg("ox"),

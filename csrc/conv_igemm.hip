@@ -60,6 +60,11 @@ struct ConvArgs {
   float urh, urw;
   int tilesN, ntiles;
   uint32_t fhw_m, fhw_s, fw_m, fw_s;  // magic division by H*W and by W
+  // ConvTranspose2d(k=2, s=2) output written in place (ping-pong epilogue, rdp_conv_upT_fwd): GEMM
+  // column n = sub * 2^tlc + c of low-res pixel (img, h, w) goes to y1 pixel (img, 2h + sub/2 + toy,
+  // 2w + sub%2 + tox) of a [N][tH2][tW2] map, channel c, + ubias[c]. tlc = 0: plain output.
+  const float* ubias = nullptr;
+  int tlc = 0, tH2 = 0, tW2 = 0, toy = 0, tox = 0;
 };
 
 // tap (0..8) -> (dr, ds) without division: dr + 1 = (tap * 11) >> 5
@@ -376,7 +381,11 @@ __global__ __launch_bounds__(64 * NWV, 2) void conv_igemm_kernel(const ConvArgs 
 // cout halves of the weight fragments stay in registers (HOLDB: no re-read in phase 3); BN = 128
 // runs a 3-stage K ring (NST). (A 512 x 64 form and a BN-backward reduction in the dgrad epilogue
 // were measured slower: profiles/dead_ends.md.)
-template <int BN, bool SPLIT = false>
+// UT: ConvTranspose2d sub-pixel output (ConvArgs tlc / ubias; no stats, no split); UTR: the
+// ConvTranspose2d input gradient, the A operand read at the 4 sub-pixels of the output gradient
+// (taps = 4, ConvArgs tH2 / tW2 / toy / tox) -- their own instantiations, so the plain kernels'
+// scalar registers are untouched.
+template <int BN, bool SPLIT = false, bool UT = false, bool UTR = false>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
   // 256-pixel tile, wave (wm, wn) = 128 pixels x BN/4 couts
   constexpr int NST = BN == 128 ? 3 : 2;
@@ -430,9 +439,17 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
       const int m = tm * BM + (wave * NROW + r) * 8 + (lane >> 3);
       const bool valid = m < a.M;
       const uint32_t mm = valid ? (uint32_t)m : 0u;
-      const uint32_t hw = mm - ((__umulhi(mm, a.fhw_m) + mm) >> a.fhw_s) * (uint32_t)(a.H * a.W);
+      const uint32_t img = (__umulhi(mm, a.fhw_m) + mm) >> a.fhw_s;
+      const uint32_t hw = mm - img * (uint32_t)(a.H * a.W);
       const uint32_t h = (__umulhi(hw, a.fw_m) + hw) >> a.fw_s;
       const uint32_t w = hw - h * (uint32_t)a.W;
+      if constexpr (UTR) {  // the (2h + toy, 2w + tox) pixel of the output-gradient map; 4 valid taps
+        const uint32_t px = (img * (uint32_t)a.tH2 + 2u * h + (uint32_t)a.toy) * (uint32_t)a.tW2 + 2u * w + (uint32_t)a.tox;
+        nmask[r] = valid ? ~0xfu : ~0u;
+        pb1[r] = (px * (uint32_t)a.pitch1 + (uint32_t)gch * 8u) * 2u;
+        pb2[r] = pb1[r];
+        continue;
+      }
       const uint32_t rok = (h > 0 ? 1u : 0u) | 2u | (h + 1 < (uint32_t)a.H ? 4u : 0u);
       const uint32_t cok = (w > 0 ? 1u : 0u) | 2u | (w + 1 < (uint32_t)a.W ? 4u : 0u);
       uint32_t msk = 0;
@@ -454,9 +471,9 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
     const int c0 = icc * 64;
     const bool s2 = c0 >= a.C1;
     const int pitch = s2 ? a.pitch2 : a.pitch1;
-    const int tap_lin = a.taps == 9 ? tap_dr(itap) * a.W + tap_ds(itap) : 0;
+    const int tap_lin = UTR ? (itap >> 1) * a.tW2 + (itap & 1) : a.taps == 9 ? tap_dr(itap) * a.W + tap_ds(itap) : 0;
     const int soff = (tap_lin * pitch + (s2 ? c0 - a.C1 : c0)) * 2;
-    const int bit = a.taps == 9 ? itap : 0;
+    const int bit = UTR || a.taps == 9 ? itap : 0;
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
       const uint32_t bad = __builtin_amdgcn_ubfe(nmask[r], (uint32_t)bit, 1u);
@@ -476,6 +493,13 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
 
   const int srow = wm;
   float* const sst = (float*)(smem + ST_OFF) + srow * 2 * BN;  // this wave (row)'s statistics words
+  // UT: the bias in the (unused) statistics words, read by the epilogue with LDS loads -- a global load
+  // there would wait (vmcnt) for the in-flight DMA stages too. 2^tlc <= 4 BN floats (host-checked).
+  const float* const sbias = (const float*)(smem + ST_OFF);
+  if constexpr (UT) {
+    for (int c = (int)threadIdx.x * 4; c < (1 << a.tlc); c += 512 * 4)
+      *(float4*)(smem + ST_OFF + c * 4) = *(const float4*)(a.ubias + c);
+  }
   if (a.stats && (lane & 15) == 0) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -546,6 +570,9 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
       const bool d2 = nb >= a.Cy1;  // wave-uniform: Cy1 % 32 == 0 (host-checked), one SRD per store
       const int nn = d2 ? n - a.Cy1 : n;
       const int yp = d2 ? a.ypitch2 : a.ypitch1;
+      // UT: sub-pixel of this cout pair (wave-uniform: 2^tlc >= 64) and its offset from the (2h, 2w) pixel
+      const int sub = UT ? nb >> a.tlc : 0, cmask = UT ? (1 << a.tlc) - 1 : 0;
+      const int subo = UT ? ((sub >> 1) * a.tW2 + (sub & 1)) * yp + (n & cmask) : 0;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int m = m0 + wpx + i * 16 + (lane & 15);
@@ -562,6 +589,9 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
             if (a.erelu) {
               o[0] = fmaxf(o[0], 0.f); o[1] = fmaxf(o[1], 0.f); o[2] = fmaxf(o[2], 0.f); o[3] = fmaxf(o[3], 0.f);
             }
+          } else if (UT) {
+            const float4 b = *(const float4*)(sbias + ((nb + h * 16 + 4 * gq) & cmask));
+            o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w;
           }
           v[h].x = pack2bf(o[0], o[1]);
           v[h].y = pack2bf(o[2], o[3]);
@@ -577,7 +607,20 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const ConvArgs a) {
         }
         const auto rxs = __builtin_amdgcn_permlane16_swap(v[0].x, v[1].x, false, false);
         const auto rys = __builtin_amdgcn_permlane16_swap(v[0].y, v[1].y, false, false);
-        const uint32_t off = m < a.M ? (uint32_t)(m * yp + nn) * 2u : RDP_OOB;
+        uint32_t pix = (uint32_t)m * (uint32_t)yp + (uint32_t)nn;
+        if constexpr (UT) {  // low-res pixel (img, h, w) -> the (2h + toy, 2w + tox) pixel of the output map
+          // W % 16 == 0: the 16 pixels of fragment row i lie in one image row, so the division runs once
+          // on the (wave-uniform) first pixel; else per lane
+          const bool row16 = (a.W & 15) == 0;
+          const uint32_t mm = row16 ? (uint32_t)(m0 + wpx + i * 16) : (uint32_t)m;
+          const uint32_t img = (__umulhi(mm, a.fhw_m) + mm) >> a.fhw_s;
+          const uint32_t hw = mm - img * (uint32_t)(a.H * a.W);
+          const uint32_t hh = (__umulhi(hw, a.fw_m) + hw) >> a.fw_s;
+          const uint32_t ww = hw - hh * (uint32_t)a.W + (row16 ? (uint32_t)(lane & 15) : 0u);
+          pix = ((img * (uint32_t)a.tH2 + 2u * hh + (uint32_t)a.toy) * (uint32_t)a.tW2 + 2u * ww + (uint32_t)a.tox) *
+                    (uint32_t)yp + (uint32_t)subo;
+        }
+        const uint32_t off = m < a.M ? pix * 2u : RDP_OOB;
         bstore16(d2 ? ry2 : ry1, off, make_uint4(rxs[0], rys[0], rxs[1], rys[1]));
       }
     }
@@ -701,12 +744,81 @@ static int launch_pp(ConvArgs a, hipStream_t s, int ksplit = 1, int* pooled = nu
   a.ksplit = 1;
   a.pool = nullptr;
   a.up = nullptr;
+  if (a.tlc || a.taps == 4) {  // ConvTranspose2d output (rdp_conv_upT_fwd) / input gradient (rdp_conv_upT_dgrad)
+    if (a.stats || a.escale || a.y2) return -1;
+    const int grid = a.ntiles < 256 ? a.ntiles : 256;
+    if (a.tlc) hipLaunchKernelGGL((conv_pp_kernel<BN, false, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv_pp_kernel<BN, false, false, true>), dim3(grid), dim3(512), 0, s, a);
+    return 0;
+  }
   // one persistent block per CU (512 blocks or one block per tile, which let the dispatcher balance
   // the tiles around the concurrent wgrads, measured 0.8 % / 1.7 % slower: profiles/dead_ends.md)
   const int grid = a.ntiles < 256 ? a.ntiles : 256;
   if (a.stats && grid % a.tilesN) return -1;
   hipLaunchKernelGGL((conv_pp_kernel<BN>), dim3(grid), dim3(512), 0, s, a);
   return grid / a.tilesN * 2;
+}
+
+// ConvTranspose2d(k=2, s=2) + bias straight into its (padded) output map u [N][H2][W2][upitch]: the
+// 1x1 GEMM yT[px][sub * C + c] = sum_ci x[px][ci] Wt[sub * C + c][ci] on the ping-pong kernel with the
+// sub-pixel scatter + bias in its epilogue (no yT round trip and no upT_shuffle pass). u's border
+// outside the 2h x 2w window at (oy, ox) is not written (the caller zeroes it once). Returns 0, or -1
+// where the ping-pong grid would not fill the chip / the shape does not fit (the caller then runs the
+// GEMM + upT_shuffle).
+extern "C" int rdp_conv_upT_fwd(const void* x, long xbytes, int Cin, int pitch, const void* w, long wbytes, int ldw,
+                                void* u, long ubytes, int upitch, const float* bias, int N, int h, int wd, int H2,
+                                int W2, int oy, int ox, int C, hipStream_t s) {
+  // (C <= 512: the bias fits the kernel's 4 BN statistics words at BN = 128)
+  if (C < 64 || C > 512 || (C & (C - 1)) || Cin % 64 || ldw < Cin || upitch % 8 || oy < 0 || ox < 0 ||
+      2 * h + oy > H2 || 2 * wd + ox > W2)
+    return -1;
+  if (xbytes >= (1l << 31) || ubytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+  ConvArgs a;
+  a.x1 = (const u16*)x; a.x2 = nullptr; a.xbytes1 = (uint32_t)xbytes; a.xbytes2 = 0;
+  a.C1 = Cin; a.C2 = 0; a.pitch1 = pitch; a.pitch2 = pitch;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y1 = (u16*)u; a.y2 = nullptr; a.ybytes1 = (uint32_t)ubytes; a.ybytes2 = 0;
+  a.Cout = 4 * C; a.Cy1 = a.Cout; a.ypitch1 = upitch; a.ypitch2 = upitch; a.stats = nullptr;
+  a.escale = nullptr; a.eshift = nullptr; a.erelu = 0;
+  a.N = N; a.H = h; a.W = wd; a.M = N * h * wd;
+  a.taps = 1; a.packed = 0; a.cpt = Cin / 64; a.nks = a.cpt;
+  a.ksplit = 1; a.kslab = nullptr; a.pool = nullptr; a.up = nullptr;
+  const FastDiv fhw = make_fastdiv((uint32_t)(h * wd)), fw = make_fastdiv((uint32_t)wd);
+  a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;
+  a.ubias = bias; a.tH2 = H2; a.tW2 = W2; a.toy = oy; a.tox = ox;
+  a.tlc = 0;
+  while ((1 << a.tlc) < C) ++a.tlc;
+  if (a.Cout % 256 == 0 && (long)(a.M + 255) / 256 * (a.Cout / 256) >= 256) return launch_pp<256>(a, s) >= 0 ? 0 : -1;
+  if (Cin >= 128 && (long)(a.M + 255) / 256 * (a.Cout / 128) >= 256) return launch_pp<128>(a, s) >= 0 ? 0 : -1;
+  return -1;
+}
+
+// ConvTranspose2d(k=2, s=2) input gradient straight from the output gradient du [N][H2][W2][C] (the
+// window 2h x 2w at (oy, ox)): dx[px][ci] = sum_(sub, c) du[sub-pixel sub of px][c] Wd[ci][sub * C + c]
+// on the ping-pong kernel, its A operand DMA'd from the 4 sub-pixels as 4 "taps" (no unshuffled copy
+// of du). wd = the [Cin][4C] dgrad weight. Returns 0, or -1 where the ping-pong grid would not fill
+// the chip / the shape does not fit (the caller unshuffles and runs the 1x1 GEMM).
+extern "C" int rdp_conv_upT_dgrad(const void* du, long dubytes, int C, int dupitch, int H2, int W2, int oy, int ox,
+                                  const void* wd, long wbytes, int ldw, void* dx, long dxbytes, int Cin, int dxpitch,
+                                  int N, int h, int wdt, hipStream_t s) {
+  if (C % 64 || Cin % 128 || ldw < 4 * C || oy < 0 || ox < 0 || 2 * h + oy > H2 || 2 * wdt + ox > W2) return -1;
+  if (dubytes >= (1l << 31) || dxbytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
+  ConvArgs a;
+  a.x1 = (const u16*)du; a.x2 = nullptr; a.xbytes1 = (uint32_t)dubytes; a.xbytes2 = 0;
+  a.C1 = C; a.C2 = 0; a.pitch1 = dupitch; a.pitch2 = dupitch;
+  a.w = (const u16*)wd; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y1 = (u16*)dx; a.y2 = nullptr; a.ybytes1 = (uint32_t)dxbytes; a.ybytes2 = 0;
+  a.Cout = Cin; a.Cy1 = Cin; a.ypitch1 = dxpitch; a.ypitch2 = dxpitch; a.stats = nullptr;
+  a.escale = nullptr; a.eshift = nullptr; a.erelu = 0;
+  a.N = N; a.H = h; a.W = wdt; a.M = N * h * wdt;
+  a.taps = 4; a.packed = 0; a.cpt = C / 64; a.nks = 4 * a.cpt;
+  a.ksplit = 1; a.kslab = nullptr; a.pool = nullptr; a.up = nullptr;
+  const FastDiv fhw = make_fastdiv((uint32_t)(h * wdt)), fw = make_fastdiv((uint32_t)wdt);
+  a.fhw_m = fhw.m; a.fhw_s = fhw.s; a.fw_m = fw.m; a.fw_s = fw.s;
+  a.tH2 = H2; a.tW2 = W2; a.toy = oy; a.tox = ox;
+  if (Cin % 256 == 0 && (long)(a.M + 255) / 256 * (Cin / 256) >= 256) return launch_pp<256>(a, s) >= 0 ? 0 : -1;
+  if ((long)(a.M + 255) / 256 * (Cin / 128) >= 256) return launch_pp<128>(a, s) >= 0 ? 0 : -1;
+  return -1;
 }
 
 extern "C" int rdp_conv_ring(const void* x, long xbytes, int C, int pitch, const void* w, long wbytes, int ldw,

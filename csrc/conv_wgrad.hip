@@ -42,6 +42,10 @@ struct WgradArgs {
   int colTiles, coutTiles, splits;
   int pix_per_split;
   uint32_t fw_m, fw_s, fh_m, fh_s;  // fast div by W and by H
+  // UTR (ConvTranspose2d(2, s2) weight gradient, rdp_conv_wgrad_upT): x1 = the output gradient du
+  // [N][uH2][uW2][C1], read at the 4 sub-pixels (2h + tap/2 + uoy, 2w + tap%2 + uox) of low-res
+  // pixel (h, w) -- the "taps" -- instead of an unshuffled [N][h][w][4 C1] copy
+  int uH2 = 0, uW2 = 0, uoy = 0, uox = 0;
 };
 
 RDP_DEV int swz(int p) { return (((p >> 1) & 1) << 1) | (((p >> 3) & 1) << 2); }
@@ -50,7 +54,7 @@ RDP_DEV uint32_t fdiv2(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n,
 
 // BKP = 64 pixels per K step, double-buffered; 8 waves: waves 2s, 2s+1 split x-subtile s into two
 // 32-column halves (twice the waves per SIMD of a 4-wave block, same LDS footprint).
-template <bool PACKED>
+template <bool PACKED, bool UTR = false>
 __global__ __launch_bounds__(512, 2) void conv_wgrad_kernel(const WgradArgs a) {
   constexpr bool TILE_FAST = true;
   constexpr int BKP = 64, STAGES = 2, NWV = 8;
@@ -93,8 +97,8 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_kernel(const WgradArgs a) {
     } else {
       const int tap = kc / a.Cin;
       const int cin0 = kc - tap * a.Cin;
-      s_dr[sub] = a.taps == 9 ? tap / 3 - 1 : 0;
-      s_ds[sub] = a.taps == 9 ? tap % 3 - 1 : 0;
+      s_dr[sub] = UTR ? tap >> 1 : a.taps == 9 ? tap / 3 - 1 : 0;
+      s_ds[sub] = UTR ? tap & 1 : a.taps == 9 ? tap % 3 - 1 : 0;
       s_src[sub] = cin0 >= a.C1;
       s_ch[sub] = s_src[sub] ? cin0 - a.C1 : cin0;
     }
@@ -129,6 +133,12 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_kernel(const WgradArgs a) {
           const int hh = h + dr, ww = w + ds;
           const bool ok = mv & (bool)s_ok[sub] & (tap < 9) & inb(hh, a.H) & inb(ww, a.W);
           const uint32_t off = ok ? (uint32_t)((m + dr * a.W + ds) * a.pitch1) * 2u : RDP_OOB;
+          dma16_async(rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
+        } else if constexpr (UTR) {  // sub-pixel (dr, ds) of the (2h + uoy, 2w + uox) pixel of du
+          ch = s_ch[sub] + g * 8;
+          const int img = (int)fdiv2(q, a.fh_m, a.fh_s);
+          const int px = (img * a.uH2 + 2 * h + a.uoy + dr) * a.uW2 + 2 * w + a.uox + ds;
+          const uint32_t off = mv & (bool)s_ok[sub] ? (uint32_t)(px * a.pitch1 + ch) * 2u : RDP_OOB;
           dma16_async(rx1, (lds_void*)(buf + sub * SUB + s * 1024), off);
         } else {
           ch = s_ch[sub] + g * 8;
@@ -747,6 +757,41 @@ extern "C" int rdp_conv_wgrad(const void* x1, const void* x2, long xbytes1, long
   else hipLaunchKernelGGL((conv_wgrad_kernel<false>), dim3(nblk), dim3(512), 0, s, a);
   rdp_wgrad_reduce(slab, out, a.splits, Cout, a.ncols_pad, taps, packed ? 8 : a.Cin, packed ? cin_real : a.Cin,
                    accumulate, s);
+  return a.splits;
+}
+
+// ConvTranspose2d(k=2, s=2) weight gradient straight from its output gradient du [N][H2][W2][C] (the
+// window 2h x 2w at (oy, ox)) and its input x [N][h][w][Cin]: out[ci][(sub, c)] (+)= sum_px
+// x[px][ci] du[sub-pixel sub of px][c] -- the generic kernel's role-swapped GEMM (columns = the 4
+// sub-pixels x C, "couts" = Cin) reading du at the sub-pixels instead of an unshuffled copy.
+// Returns the split count, or < 0 if the shape does not fit.
+extern "C" int rdp_conv_wgrad_upT(const void* du, long dubytes, int C, int dupitch, int H2, int W2, int oy, int ox,
+                                  const void* x, long xbytes, int Cin, int xpitch, int N, int h, int w, float* slab,
+                                  long slab_elems, float* out, int accumulate, int splits, hipStream_t s) {
+  if (C % 64 || Cin % 64 || oy < 0 || ox < 0 || 2 * h + oy > H2 || 2 * w + ox > W2) return -1;
+  if (dubytes >= (1l << 31) || xbytes >= (1l << 31)) return -1;
+  WgradArgs a;
+  a.x1 = (const u16*)du; a.x2 = nullptr; a.xbytes1 = (uint32_t)dubytes; a.xbytes2 = 0;
+  a.C1 = C; a.C2 = 0; a.pitch1 = dupitch; a.pitch2 = dupitch;
+  a.dy = (const u16*)x; a.dybytes = (uint32_t)xbytes; a.dypitch = xpitch;
+  a.slab = slab; a.H = h; a.W = w; a.M = N * h * w; a.Cout = Cin;
+  a.taps = 4; a.packed = 0; a.Cin = C; a.ncols = 4 * C;
+  a.uH2 = H2; a.uW2 = W2; a.uoy = oy; a.uox = ox;
+  a.colTiles = (a.ncols + 255) / 256;
+  a.ncols_pad = a.colTiles * 256;
+  a.coutTiles = Cin / 64;
+  if (splits < 1) splits = 1;
+  int pps = (a.M + splits - 1) / splits;
+  pps = (pps + 63) / 64 * 64;
+  a.pix_per_split = pps;
+  a.splits = (a.M + pps - 1) / pps;
+  if ((long)a.splits * a.Cout * a.ncols_pad > slab_elems) return -2;
+  if ((long)a.splits * a.Cout * a.ncols_pad * 4l >= (1l << 31)) return -3;
+  FastDiv fw = make_fastdiv(w), fh = make_fastdiv(h);
+  a.fw_m = fw.m; a.fw_s = fw.s; a.fh_m = fh.m; a.fh_s = fh.s;
+  const int nblk = a.colTiles * a.coutTiles * a.splits;
+  hipLaunchKernelGGL((conv_wgrad_kernel<false, true>), dim3(nblk), dim3(512), 0, s, a);
+  rdp_wgrad_reduce(slab, out, a.splits, Cin, a.ncols_pad, 4, C, C, accumulate, s);
   return a.splits;
 }
 

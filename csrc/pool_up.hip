@@ -537,29 +537,44 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const u16* __restrict_
     partial[(long)blockIdx.x * K + cc] = s;
   }
 }
-// Stage 2: one block per 64 channels; its 16 waves stride over the (block, group) partial rows with
-// coalesced 256 B row reads, fp64 accumulation, then a fixed-order LDS fold (deterministic). A single
-// thread per channel walking all nblk*groups rows serially was latency-bound (1.4 ms at nblk 1024, K 2048).
-__global__ __launch_bounds__(1024) void colsum_fold_kernel(const float* __restrict__ partial, int nblk, int K,
-                                                           int groups, float* __restrict__ out, int accumulate) {
-  __shared__ double sfold[16][64];
+// Stage 2a: the (block, group) partial rows folded in FOLD_RB row chunks: block (channel block of 64,
+// chunk) = 4 waves striding over the chunk's rows (coalesced 256 B row reads, 4 loads in flight per
+// lane, fp64), fixed-order LDS fold -> part2[chunk][c]. Stage 2b sums the chunks in order
+// (deterministic). One block per 64 channels walking every row took 83 us per call at nblk 1024
+// (bs 64, transposed decoder): latency-bound.
+constexpr int FOLD_RB = 32;
+__global__ __launch_bounds__(256) void colsum_fold_kernel(const float* __restrict__ partial, int nblk, int K, int groups,
+                                                          double* __restrict__ part2) {
+  __shared__ double sfold[4][64];
   const int C = K / groups;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
-  double s = 0.0;
+  const long rows = (long)nblk * groups;
+  const long r0 = rows * blockIdx.y / FOLD_RB, r1 = rows * (blockIdx.y + 1) / FOLD_RB;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (c < C) {
-    const long rows = (long)nblk * groups;
-#pragma unroll 4
-    for (long q = ty; q < rows; q += 16) s += partial[(q / groups) * K + (q % groups) * C + c];
+    long q = r0 + ty;
+    for (; q + 12 < r1; q += 16) {
+      const float v0 = partial[(q / groups) * K + (q % groups) * C + c];
+      const float v1 = partial[((q + 4) / groups) * K + ((q + 4) % groups) * C + c];
+      const float v2 = partial[((q + 8) / groups) * K + ((q + 8) % groups) * C + c];
+      const float v3 = partial[((q + 12) / groups) * K + ((q + 12) % groups) * C + c];
+      s0 += v0; s1 += v1; s2 += v2; s3 += v3;
+    }
+    for (; q < r1; q += 4) s0 += partial[(q / groups) * K + (q % groups) * C + c];
   }
-  sfold[ty][tx] = s;
+  sfold[ty][tx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (ty == 0 && c < C) {
-    double t = 0.0;
+  if (ty == 0 && c < C) part2[(long)blockIdx.y * C + c] = ((sfold[0][tx] + sfold[1][tx]) + sfold[2][tx]) + sfold[3][tx];
+}
+__global__ __launch_bounds__(256) void colsum_fold2_kernel(const double* __restrict__ part2, int C, float* __restrict__ out,
+                                                           int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double t = 0.0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += sfold[k][tx];
-    out[c] = accumulate ? out[c] + (float)t : (float)t;
-  }
+  for (int k = 0; k < FOLD_RB; ++k) t += part2[(long)k * C + c];
+  out[c] = accumulate ? out[c] + (float)t : (float)t;
 }
 
 
@@ -655,7 +670,7 @@ int rdp_upT_unshuffle(const void* du, int dpitch, void* dyT, int ypitch, int N, 
                      (const u16*)du, dpitch, (u16*)dyT, ypitch, g);
   return 0;
 }
-// partial must hold >= 1024 * K floats
+// partial must hold >= 1024 * K + 2 * FOLD_RB * K / groups floats
 int rdp_colsum_bf16(const void* x, int pitch, long M, int K, int groups, float* partial, float* out, int accumulate,
                     hipStream_t s) {
   if (K < 8 || K > 2048 || (K & (K - 1)) || K % groups || pitch % 8) return -1;
@@ -664,7 +679,9 @@ int rdp_colsum_bf16(const void* x, int pitch, long M, int K, int groups, float* 
   hipLaunchKernelGGL(colsum_bf16_kernel, dim3(nblk), dim3(256), (size_t)rpb * K * sizeof(float), s, (const u16*)x,
                      pitch, M, K, partial);
   const int C = K / groups;
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, partial, nblk, K, groups, out, accumulate);
+  double* part2 = (double*)(partial + 1024L * K);  // 8-B aligned: K is a power of two >= 8
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((C + 63) / 64, FOLD_RB), dim3(256), 0, s, partial, nblk, K, groups, part2);
+  hipLaunchKernelGGL(colsum_fold2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, (const double*)part2, C, out, accumulate);
   return 0;
 }
 }

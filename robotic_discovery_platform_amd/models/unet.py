@@ -590,7 +590,7 @@ class UNetExecutor:
                                                             int(L0.spec.packed), L0.splits),
                                          dtype=torch.float32, device=dev)
         if self.m.up_specs:
-            self.colsum_ws = torch.zeros(1024 * max(4 * us.cout for us in self.m.up_specs), dtype=torch.float32,
+            self.colsum_ws = torch.zeros((1024 * 4 + 64) * max(us.cout for us in self.m.up_specs), dtype=torch.float32,
                                          device=dev)
         maxc = max(L.spec.cout for L in self.layers)
         # (also the fused head's BN-backward partials: 128 floats per head block -- the larger need for
@@ -704,9 +704,13 @@ class UNetExecutor:
                 C.upsample2_fwd(low, u, oy, ox)
             else:
                 us = self.m.up_specs[i - 1]
-                C.conv_fwd(low, None, self.m.upT_fwd_weight(us), 1, 0, self.yTs[i - 1], None, None, 0, None, 0,
-                           self.kws)
-                C.upT_shuffle(self.yTs[i - 1], self.m.store.view(us.name + ".bias"), u, oy, ox)
+                bias = self.m.store.view(us.name + ".bias")
+                # the sub-pixel scatter + bias in the ping-pong GEMM's epilogue where that kernel takes the
+                # shape (u's zero border is never written); else the GEMM into yT + the shuffle pass
+                if C.conv_upT_fwd(low, self.m.upT_fwd_weight(us), bias, u, oy, ox) != 0:
+                    C.conv_fwd(low, None, self.m.upT_fwd_weight(us), 1, 0, self.yTs[i - 1], None, None, 0, None, 0,
+                               self.kws)
+                    C.upT_shuffle(self.yTs[i - 1], bias, u, oy, ox)
             la, lb = self.up_layers[i - 1]
             self._conv_bn_relu(C, la)
             last = i == D
@@ -971,13 +975,29 @@ class UNetExecutor:
             else:
                 us = self.m.up_specs[i - 1]
                 dyT = self.dyTs[i - 1]
-                C.upT_unshuffle(du, dyT, oy, ox)
-                C.colsum_bf16(dyT, 4, self.colsum_ws, st.flat_slice(us.name + ".bias", st.grad), 0)
-                self._on_wgrad_stream(lambda slab, dyT=dyT, xa=low_layer.a, us=us, ns=self.upT_splits[i - 1]:
-                                      C.conv_wgrad(dyT, None, xa, 1, 0, 4 * us.cout, slab,
-                                                   st.flat_slice(us.name + ".weight", st.grad), 0, ns, 0))
-                C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
-                           self.kws)
+                bgrad = st.flat_slice(us.name + ".bias", st.grad)
+                wgrad = st.flat_slice(us.name + ".weight", st.grad)
+                ns = self.upT_splits[i - 1]
+                exact = du.shape[1] == 2 * dyT.shape[1] and du.shape[2] == 2 * dyT.shape[2]  # no F.pad border
+                if exact:
+                    # bias / weight / input gradients read du's 2x2 sub-pixels in place (no unshuffled copy):
+                    # bias = column sums of du, weight = the role-swapped GEMM over the sub-pixels (wgrad
+                    # stream), input = the ping-pong GEMM with the sub-pixels as 4 taps where it takes the
+                    # shape (else the unshuffle + 1x1 GEMM)
+                    C.colsum_bf16(du, 1, self.colsum_ws, bgrad, 0)
+                    self._on_wgrad_stream(lambda slab, du=du, xa=low_layer.a, ns=ns, g=wgrad:
+                                          C.conv_wgrad_upT(du, xa, 0, 0, slab, g, 0, ns))
+                    if C.conv_upT_dgrad(du, self.m.upT_dgrad_weight(us), low_layer.da, 0, 0) != 0:
+                        C.upT_unshuffle(du, dyT, oy, ox)
+                        C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None,
+                                   0, self.kws)
+                else:
+                    C.upT_unshuffle(du, dyT, oy, ox)
+                    C.colsum_bf16(dyT, 4, self.colsum_ws, bgrad, 0)
+                    self._on_wgrad_stream(lambda slab, dyT=dyT, xa=low_layer.a, us=us, ns=ns, g=wgrad:
+                                          C.conv_wgrad(dyT, None, xa, 1, 0, 4 * us.cout, slab, g, 0, ns, 0))
+                    C.conv_fwd(dyT, None, self.m.upT_dgrad_weight(us), 1, 0, low_layer.da, None, None, 0, None, 0,
+                               self.kws)
                 if grad_hook is not None:  # bias (main) + weight (side, forked after the bias)
                     grad_hook(us, self.side if self.side is not None else torch.cuda.current_stream())
         for i in range(D, 0, -1):

@@ -572,7 +572,7 @@ def test_conv_transpose2x2(C, N, h, w, Cin, Cout, H2, W2):
     dyT = torch.empty_like(yT)
     C.upT_unshuffle(nhwc(du), dyT, oy, ox)
     db = torch.zeros(Cout, device=dev)
-    C.colsum_bf16(dyT, 4, torch.zeros(1024 * 4 * Cout, device=dev), db, 0)
+    C.colsum_bf16(dyT, 4, torch.zeros((1024 * 4 + 64) * Cout, device=dev), db, 0)
     assert torch.allclose(db, br.grad, rtol=1e-3, atol=1e-2)
     M = N * h * w
     splits = max(1, M // 64)
@@ -583,6 +583,81 @@ def test_conv_transpose2x2(C, N, h, w, Cin, Cout, H2, W2):
     dx = torch.empty(N, h, w, Cin, dtype=torch.bfloat16, device=dev)
     C.conv_fwd(dyT, None, wphys, 1, 0, dx, None, None, 0, None, 0)
     assert relerr(nchw(dx), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout,H2,W2", [(4, 64, 64, 512, 256, 128, 128), (2, 128, 128, 128, 64, 256, 256),
+                                                 (4, 64, 64, 256, 256, 129, 130)])
+def test_conv_upT_fwd_fused(C, N, h, w, Cin, Cout, H2, W2):
+    """ConvTranspose2d(k=2, s=2) + bias with the sub-pixel scatter in the ping-pong GEMM epilogue (both
+    tile widths, padded placement) vs torch fp32 and vs the unfused GEMM + upT_shuffle."""
+    torch.manual_seed(7)
+    dev = "cuda"
+    x = bf(torch.randn(N, Cin, h, w, device=dev))
+    W = bf(torch.randn(Cin, Cout, 2, 2, device=dev) / math.sqrt(Cin))
+    b = torch.randn(Cout, device=dev)
+    oy, ox = (H2 - 2 * h) // 2, (W2 - 2 * w) // 2
+    ref = F.pad(F.conv_transpose2d(x.float(), W.float(), b, stride=2), [ox, W2 - 2 * w - ox, oy, H2 - 2 * h - oy])
+    wt = W.permute(0, 2, 3, 1).reshape(Cin, 4 * Cout).t().contiguous()  # [(dh, dw, co)][ci]
+    u = torch.zeros(N, H2, W2, Cout, dtype=torch.bfloat16, device=dev)
+    assert C.conv_upT_fwd(nhwc(x), wt, b, u, oy, ox) == 0
+    torch.cuda.synchronize()
+    assert relerr(nchw(u), ref) < 1e-2
+    yT = torch.empty(N, h, w, 4 * Cout, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(nhwc(x), None, wt, 1, 0, yT, None, None, 0, None, 0)
+    u2 = torch.zeros_like(u)
+    C.upT_shuffle(yT, b, u2, oy, ox)
+    # one rounding of (acc + bias): within half a bf16 ulp of the fp32 result everywhere (the unfused path
+    # rounds twice), and never further from it overall than the unfused path
+    r = nhwc(ref).float()
+    assert float(((u.float() - r).abs() - r.abs() * 2 ** -8).max()) < 1e-3
+    assert relerr(nchw(u), ref) <= relerr(nchw(u2), ref) * 1.01
+    # a grid that would not fill the chip declines (the caller runs GEMM + shuffle)
+    assert C.conv_upT_fwd(nhwc(x[:1, :, :8, :8].contiguous()), wt, b, torch.zeros(1, 16, 16, Cout, dtype=torch.bfloat16,
+                                                                                   device=dev), 0, 0) == -1
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(8, 64, 64, 512, 256), (4, 128, 128, 128, 64), (8, 64, 64, 256, 128),
+                                           (2, 8, 8, 256, 128)])
+def test_conv_upT_backward_in_place(C, N, h, w, Cin, Cout):
+    """ConvTranspose2d(k=2, s=2) backward read straight from du's 2x2 sub-pixels: input gradient on the
+    ping-pong kernel with 4 sub-pixel taps (both tile widths; a grid too small to fill the chip
+    declines), weight gradient on the generic wgrad kernel, bias as column sums -- vs torch fp32, and
+    the input gradient bitwise vs unshuffle + 1x1 GEMM."""
+    torch.manual_seed(8)
+    dev = "cuda"
+    x = bf(torch.randn(N, Cin, h, w, device=dev))
+    W = bf(torch.randn(Cin, Cout, 2, 2, device=dev) / math.sqrt(Cin))
+    b = torch.randn(Cout, device=dev)
+    xr = x.float().requires_grad_(True)
+    Wr = W.float().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    du = bf(torch.randn(N, Cout, 2 * h, 2 * w, device=dev))
+    F.conv_transpose2d(xr, Wr, br, stride=2).backward(du.float())
+    wd = W.permute(0, 2, 3, 1).reshape(Cin, 4 * Cout).contiguous()  # [ci][(dh, dw, co)]
+    dun = nhwc(du)
+    dx = torch.zeros(N, h, w, Cin, dtype=torch.bfloat16, device=dev)
+    r = C.conv_upT_dgrad(dun, wd, dx, 0, 0)
+    tiles = -(-N * h * w // 256) * (Cin // 128)
+    assert r == (0 if tiles >= 256 else -1)
+    dyT = torch.empty(N, h, w, 4 * Cout, dtype=torch.bfloat16, device=dev)
+    C.upT_unshuffle(dun, dyT, 0, 0)
+    dx2 = torch.empty_like(dx)
+    C.conv_fwd(dyT, None, wd, 1, 0, dx2, None, None, 4 if Cin % 256 == 0 and tiles >= 512 else 5, None, 0)
+    if r == 0:
+        assert relerr(nchw(dx), xr.grad) < 1e-2
+        assert torch.equal(dx, dx2)  # same kernel, same K order: only the A operand's addresses differ
+    M = N * h * w
+    splits = max(1, min(512, M // 2048))
+    slab = torch.zeros(C.wgrad_slab_elems(N, h, w, 4 * Cout, Cin, 1, 0, splits), device=dev)
+    gw = torch.zeros(Cin * 4 * Cout, device=dev)
+    assert C.conv_wgrad_upT(dun, nhwc(x), 0, 0, slab, gw, 0, splits) > 0
+    assert relerr(gw.view(Cin, 2, 2, Cout).permute(0, 3, 1, 2), Wr.grad) < 1e-2
+    gw2 = torch.zeros_like(gw)
+    C.conv_wgrad(dyT, None, nhwc(x), 1, 0, 4 * Cout, slab, gw2, 0, splits, 0)
+    assert torch.equal(gw, gw2)
+    db = torch.zeros(Cout, device=dev)
+    C.colsum_bf16(dun, 1, torch.zeros((1024 * 4 + 64) * Cout, device=dev), db, 0)
+    assert torch.allclose(db, br.grad, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(1, 16, 16, 512, 0, 512), (1, 8, 8, 256, 256, 256),
