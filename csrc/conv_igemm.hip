@@ -1170,8 +1170,7 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
     const int pref = bm_pref % 1000;
     const long ring_pairs = W % 64 == 0 ? (long)N * (W / 64) * H / 2 : 0;
     const bool two = C1 == 64 && C2 == 64 && x2 != nullptr, one = C1 == 128 && C2 == 0 && x2 == nullptr;
-    static const bool ring2_auto = getenv("RDP_RING2") == nullptr || atoi(getenv("RDP_RING2")) != 0;  // A/B
-    if ((pref == 14 || (pref == 0 && ring2_auto && ring_pairs >= 256)) && taps == 9 && !packed && Cout == 64 && (two || one) &&
+    if ((pref == 14 || (pref == 0 && ring_pairs >= 256)) && taps == 9 && !packed && Cout == 64 && (two || one) &&
         y2 == nullptr && !(pool && pooled) && !(up && pooled)) {
       const void* s1 = two ? x2 : (const void*)((const u16*)x1 + 64);
       const long b1 = two ? xbytes2 : xbytes1 - 128;
