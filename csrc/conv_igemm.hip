@@ -67,6 +67,12 @@ struct ConvArgs {
   int tlc = 0, tH2 = 0, tW2 = 0, toy = 0, tox = 0;
 };
 
+// 128 -> 128 convs as two two-source-ring launches where the ring grid is at least this large. Measured
+// (scripts/conv_microbench.py --shapes 2, one MI355X): 128^2 128 -> 128 at bs 64 330.5 vs 368.9 us for the
+// 256 x 128 ping-pong kernel, but 106.8 vs 98.5 at bs 16 and 45.8 vs 28.3 at bs 4 (each launch reads the
+// whole input); bs-64 step 19.43 / 19.55 vs 19.47 / 19.61 ms (interleaved).
+constexpr long RING2_X2_PAIRS = 4096;
+
 // tap (0..8) -> (dr, ds) without division: dr + 1 = (tap * 11) >> 5
 RDP_DEV int tap_dr(int tap) { return ((tap * 11) >> 5) - 1; }
 RDP_DEV int tap_ds(int tap) { return tap - 3 * ((tap * 11) >> 5) - 1; }
@@ -833,7 +839,7 @@ extern "C" int rdp_conv_halo_tiles(int N, int H, int W, int C1, int C2, int Cout
 extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const void* x1, long xbytes1, int pitch1,
                               const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, float* stats,
                               int N, int H, int W, const float* escale, const float* eshift, int erelu, int max_blocks,
-                              hipStream_t s);
+                              int cout_total, int co0, hipStream_t s);
 extern "C" int rdp_conv_first(const void* x, long xbytes, int pitch, const void* w, long wbytes, void* y, long ybytes,
                               int ypitch, float* stats, int N, int H, int W, const float* escale, const float* eshift,
                               int erelu, hipStream_t s);
@@ -1165,18 +1171,27 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
     }
   }
   // two-source row ring (conv_ring.hip conv_ring2_kernel): 128 input channels (two 64-channel sources,
-  // or one 128-channel tensor as its two halves) -> 64, 3x3, one destination; 14 = force
+  // or one 128-channel tensor as its two halves) -> 64, 3x3, one destination; 14 = force. 15 = force
+  // (auto: RING2_X2_PAIRS) 128 -> 128 as two launches over the output-channel halves (each reads the input).
   {
     const int pref = bm_pref % 1000;
     const long ring_pairs = W % 64 == 0 ? (long)N * (W / 64) * H / 2 : 0;
     const bool two = C1 == 64 && C2 == 64 && x2 != nullptr, one = C1 == 128 && C2 == 0 && x2 == nullptr;
-    if ((pref == 14 || (pref == 0 && ring_pairs >= 256)) && taps == 9 && !packed && Cout == 64 && (two || one) &&
-        y2 == nullptr && !(pool && pooled) && !(up && pooled)) {
+    const bool c64 = Cout == 64 && (pref == 14 || (pref == 0 && ring_pairs >= 256));
+    const bool c128 = Cout == 128 && (pref == 15 || (pref == 0 && ring_pairs >= RING2_X2_PAIRS));
+    if ((c64 || c128) && taps == 9 && !packed && (two || one) && y2 == nullptr && !(pool && pooled) &&
+        !(up && pooled)) {
       const void* s1 = two ? x2 : (const void*)((const u16*)x1 + 64);
       const long b1 = two ? xbytes2 : xbytes1 - 128;
-      const int r = rdp_conv_ring2(x1, xbytes1, pitch1, s1, b1, two ? pitch2 : pitch1, w, wbytes, ldw, y1, ybytes1,
-                                   ypitch1, stats, N, H, W, escale, eshift, erelu, 256, s);
-      if (r >= 0 || pref == 14) return r;
+      int r = -1;
+      for (int co0 = 0; co0 < Cout; co0 += 64) {
+        const long yoff = (long)co0 * 2;
+        r = rdp_conv_ring2(x1, xbytes1, pitch1, s1, b1, two ? pitch2 : pitch1, (const u16*)w + (long)co0 * ldw,
+                           wbytes - (long)co0 * ldw * 2, ldw, (u16*)y1 + co0, ybytes1 - yoff, ypitch1, stats, N, H, W,
+                           escale ? escale + co0 : nullptr, eshift ? eshift + co0 : nullptr, erelu, 256, Cout, co0, s);
+        if (r < 0) break;
+      }
+      if (r >= 0 || pref == 14 || pref == 15) return r;
     }
   }
   {

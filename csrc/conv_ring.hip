@@ -714,7 +714,8 @@ struct Ring2Args {
   u16* y;
   uint32_t ybytes;
   int ypitch;
-  float* stats;  // [gridDim.x * 4][2][64] partial (sum, sumsq) or nullptr
+  float* stats;  // [gridDim.x * 4][2][scout] partial (sum, sumsq) at channels co0 .. co0 + 63, or nullptr
+  int scout, co0;
   const float* escale;
   const float* eshift;
   int erelu;
@@ -942,24 +943,26 @@ __global__ __launch_bounds__(512, 2) void conv_ring2_kernel(const Ring2Args a) {
         s2[j][r] = row16_sum(s2[j][r]);
       }
     if ((lane & 15) == 0) {
-      float* row = a.stats + (size_t)(blockIdx.x * 4 + orow * 2 + kh) * 2 * 64;
+      float* row = a.stats + (size_t)(blockIdx.x * 4 + orow * 2 + kh) * 2 * a.scout + a.co0;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = 32 * cg + 16 * j + 4 * gq;
         *(float4*)(row + c) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
-        *(float4*)(row + 64 + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+        *(float4*)(row + a.scout + c) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
       }
     }
   }
 }
 
 // Two-source row ring (see conv_ring2_kernel): x0 / x1 = the two 64-channel sources (for one
-// 128-channel tensor: its two halves), 64 outputs, 3x3, W % 64 == 0, even H. Returns the stats rows
-// written (grid * 4), or -1 when not applicable.
+// 128-channel tensor: its two halves), 64 outputs, 3x3, W % 64 == 0, even H. cout_total / co0: the
+// launch computes output channels co0 .. co0 + 63 of a cout_total-channel conv (w, y, escale / eshift
+// already offset by the caller; the stats rows are [rows][2][cout_total], this launch's 64 columns
+// at co0). Returns the stats rows written (grid * 4), or -1 when not applicable.
 extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const void* x1, long xbytes1, int pitch1,
                               const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, float* stats,
                               int N, int H, int W, const float* escale, const float* eshift, int erelu, int max_blocks,
-                              hipStream_t s) {
+                              int cout_total, int co0, hipStream_t s) {
   if (W % 64 || H % 2 || ldw < 1152 || ypitch % 8 || pitch0 % 8 || pitch1 % 8) return -1;
   if (xbytes0 >= (1l << 31) || xbytes1 >= (1l << 31) || ybytes >= (1l << 31) || wbytes >= (1l << 31)) return -1;
   if ((escale == nullptr) != (eshift == nullptr)) return -1;
@@ -969,6 +972,8 @@ extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const vo
   a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
   a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
   a.stats = stats; a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  if (cout_total < 64 || co0 < 0 || co0 + 64 > cout_total) return -1;
+  a.scout = cout_total; a.co0 = co0;
   a.H = H; a.W = W; a.WS = W / 64;
   a.nrows = N * a.WS * H;
   a.npairs = a.nrows / 2;

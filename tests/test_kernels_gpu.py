@@ -1062,6 +1062,43 @@ def test_conv_ring2_128_to_64(C, N, H, W, form):
     assert relerr(nchw(ye), torch.relu(ref * sc[None, :, None, None] + sh[None, :, None, None])) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,form", [(2, 8, 128, "one"), (1, 6, 64, "concat")])
+def test_conv_ring2_128_to_128_halves(C, N, H, W, form):
+    """128 -> 128 as two two-source-ring launches over the output-channel halves (bm_pref 15): output,
+    BN partial rows ([rows][2][128], each launch filling its 64 columns) and the eval epilogue vs torch
+    fp32; each half bitwise equal to the 128 -> 64 ring on that half's weights."""
+    torch.manual_seed(17)
+    dev = "cuda"
+    if form == "concat":
+        x1, x2 = bf(torch.randn(N, H, W, 64, device=dev)), bf(torch.randn(N, H, W, 64, device=dev))
+        xin = torch.cat([x1, x2], -1)
+    else:
+        x1, x2 = bf(torch.randn(N, H, W, 128, device=dev)), None
+        xin = x1
+    w = bf(torch.randn(128, 128, 3, 3, device=dev) / 34)
+    wk = ohwi(w).contiguous()
+    ref = F.conv2d(nchw(xin).float(), w.float(), padding=1)
+    rows = C.conv_stats_rows(N * H * W, 128, 0)
+    y = torch.empty(N, H, W, 128, dtype=torch.bfloat16, device=dev)
+    stats = torch.zeros(rows * 2 * 128, device=dev)
+    r = C.conv_fwd(x1, x2, wk, 9, 0, y, None, stats, 15, None, 0)
+    assert 0 < r <= rows
+    assert relerr(nchw(y), ref) < 1e-2
+    yq = nchw(y).float()
+    st = stats.view(rows, 2, 128)[:r].sum(0)
+    assert torch.allclose(st[0], yq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[1], (yq * yq).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    for h in range(2):
+        yh = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=dev)
+        C.conv_fwd(x1, x2, wk[64 * h:64 * h + 64].contiguous(), 9, 0, yh, None, None, 14, None, 0)
+        assert torch.equal(yh, y[..., 64 * h:64 * h + 64])
+    sc, sh = torch.rand(128, device=dev) + 0.5, torch.randn(128, device=dev) * 0.1
+    aff = torch.cat([torch.zeros(128, device=dev), torch.ones(128, device=dev), sc, sh])
+    ye = torch.empty(N, H, W, 128, dtype=torch.bfloat16, device=dev)
+    C.conv_fwd(x1, x2, wk, 9, 0, ye, None, None, 15, aff, 1)
+    assert relerr(nchw(ye), torch.relu(ref * sc[None, :, None, None] + sh[None, :, None, None])) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,split", [(2, 4, 64, False), (1, 6, 128, True), (2, 2, 64, True)])
 def test_conv_ring_cout128(C, N, H, W, split):
     """Row-ring kernel with 128 outputs (down1 conv0 forward; up4 conv0 dgrad into the two halves of
