@@ -1,5 +1,7 @@
 #!/bin/bash
-# Hardware counters for the conv kernels (PMC run: kernel-trace only, no sys/runtime trace).
+# Hardware counters (PMC run: kernel-trace only, no sys/runtime trace), one counter set per line of
+# scripts/$PMC_FILE; the profiled program is scripts/conv_microbench.py $MB_ARGS, or $PMC_PROG (a repo-relative
+# python script) with $MB_ARGS.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/pmc
 export RDP_NO_BUILD=1
@@ -10,6 +12,6 @@ i=0
 while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $line -d $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i -o pmc --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/conv_microbench.py ${MB_ARGS} > $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i.log 2>&1 || { echo "set $i failed"; tail -5 $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i.log; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $line -d $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i -o pmc --output-format csv -- python3 $GRAFT_REPO_ROOT/${PMC_PROG:-scripts/conv_microbench.py} ${MB_ARGS} > $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i.log 2>&1 || { echo "set $i failed"; tail -5 $GRAFT_REPO_ROOT/gpurun_out/pmc/set$i.log; }
 done < $GRAFT_REPO_ROOT/scripts/${PMC_FILE:-pmc_sets.txt}
 echo done
