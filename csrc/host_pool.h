@@ -5,6 +5,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -89,9 +90,17 @@ class HostPool {
   bool stop_ = false;
 };
 
-// one pool per process (inline: a single instance across the translation units of the library)
+// one pool per process (inline: a single instance across the translation units of the library);
+// RDP_HOST_THREADS sets its size (default: half the visible CPUs, at most 8)
+inline int host_pool_threads() {
+  if (const char* e = std::getenv("RDP_HOST_THREADS")) {
+    const int n = std::atoi(e);
+    if (n >= 0 && n <= 256) return n;
+  }
+  return (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2));
+}
 inline HostPool& host_pool() {
-  static HostPool p((int)std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2)));
+  static HostPool p(host_pool_threads());
   return p;
 }
 
