@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--conv-only", action="store_true", help="print only the conv times (A/B of conv settings)")
     a = ap.parse_args()
     C = native()
     dev = "cuda"
@@ -54,8 +55,11 @@ def main():
         torch.cuda.synchronize()
         tg, tc = [], []
         for _ in range(a.rounds):
-            tg.append(timed(gemm, a.reps))
+            tg.append(timed(gemm, a.reps) if not a.conv_only else 1.0)
             tc.append(timed(conv, a.reps))
+        if a.conv_only:
+            print(f"{N}x{H}x{H} {Cin}->{Cout}: conv {statistics.median(tc) * 1e3:.1f} us", flush=True)
+            continue
         flops = 2.0 * M * Cout * K
         g, c = statistics.median(tg), statistics.median(tc)
         print(json.dumps({"shape": f"{N}x{H}x{H} {Cin}->{Cout}", "M": M, "N": Cout, "K": K,
