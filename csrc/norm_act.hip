@@ -161,25 +161,29 @@ RDP_DEV void ld8(const float* p, float* f) {
 #define APX 4
 __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const u16* __restrict__ y, int ypitch,
                                                             u16* __restrict__ out, int opitch,
-                                                            const float* __restrict__ coef, int M, int C, int relu) {
+                                                            const float* __restrict__ coef, int M, int C, int relu,
+                                                            int chunk) {
   const int CG = C >> 3, RPB = 256 / CG;  // C is a power of two in [8, 2048]
   const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
   const int c = g * 8;
   float ss[8], hh[8];
   ld8(coef + 2 * C + c, ss);
   ld8(coef + 3 * C + c, hh);
-  const int stride = gridDim.x * RPB;
-  for (int p0 = blockIdx.x * RPB + r; p0 < M; p0 += stride * APX) {
+  // chunk > 0: block b walks pixels [b * chunk, (b + 1) * chunk) contiguously (RPB * APX per step)
+  const int stride = chunk ? RPB : gridDim.x * RPB;
+  const int pbeg = chunk ? blockIdx.x * chunk : blockIdx.x * RPB;
+  const int pend = chunk ? min(M, pbeg + chunk) : M;
+  for (int p0 = pbeg + r; p0 < pend; p0 += stride * APX) {
     uint4 v[APX];
 #pragma unroll
     for (int u = 0; u < APX; ++u) {
       const int p = p0 + u * stride;
-      if (p < M) v[u] = *(const uint4*)(y + (size_t)p * ypitch + c);
+      if (p < pend) v[u] = *(const uint4*)(y + (size_t)p * ypitch + c);
     }
 #pragma unroll
     for (int u = 0; u < APX; ++u) {
       const int p = p0 + u * stride;
-      if (p < M) {
+      if (p < pend) {
         float f[8];
         unpack8(v[u], f);
 #pragma unroll
@@ -281,20 +285,22 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(const u16* __res
                                                                 const float* __restrict__ coef,
                                                                 const float* __restrict__ coef2,
                                                                 u16* __restrict__ dy, int dypitch, int M, int C,
-                                                                int relu) {
+                                                                int relu, int chunk) {
   const int CG = C >> 3, RPB = 256 / CG;
   const int g = threadIdx.x & (CG - 1), r = threadIdx.x / CG;
   const int c = g * 8;
   float ss[8], hh[8], A[8], B[8], K[8];
   ld8(coef + 2 * C + c, ss); ld8(coef + 3 * C + c, hh);
   ld8(coef2 + c, A); ld8(coef2 + C + c, B); ld8(coef2 + 2 * C + c, K);
-  const int stride = gridDim.x * RPB;
-  for (int p0 = blockIdx.x * RPB + r; p0 < M; p0 += stride * APX) {
+  const int stride = chunk ? RPB : gridDim.x * RPB;  // (see bn_relu_apply_kernel)
+  const int pbeg = chunk ? blockIdx.x * chunk : blockIdx.x * RPB;
+  const int pend = chunk ? min(M, pbeg + chunk) : M;
+  for (int p0 = pbeg + r; p0 < pend; p0 += stride * APX) {
     uint4 vd[APX], vy[APX];
 #pragma unroll
     for (int u = 0; u < APX; ++u) {
       const int p = p0 + u * stride;
-      if (p < M) {
+      if (p < pend) {
         vd[u] = *(const uint4*)(da + (size_t)p * dapitch + c);
         vy[u] = *(const uint4*)(y + (size_t)p * ypitch + c);
       }
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(const u16* __res
 #pragma unroll
     for (int u = 0; u < APX; ++u) {
       const int p = p0 + u * stride;
-      if (p < M) {
+      if (p < pend) {
         float fd[8], fy[8], o[8];
         unpack8(vd[u], fd);
         unpack8(vy[u], fy);
@@ -323,6 +329,14 @@ static int grid_px(long M, int C) {  // blocks for the pixel-walking elementwise
   const long rpb = 256 / (C / 8);
   const long g = (M + rpb * APX - 1) / (rpb * APX);
   return (int)std::max<long>(1, std::min<long>(g, 2048));
+}
+// Contiguous per-block pixel chunks for the streaming BN apply passes: each block walks its own range
+// (RPB * APX pixels per step) instead of a grid stride that keeps ~2,048 x APX far-apart streams open.
+// Measured (scripts/pass_bench.py, bs 64): apply 256^2 x 64 256 -> 204 us (4.2 -> 5.3 TB/s), backward
+// apply 383 -> 305 us, 128^2 x 128 182 -> 155 us; step 19.32 / 19.31 -> 19.22 / 19.21 ms (interleaved).
+static int px_chunk(long M, int C, int grid) {
+  const long step = (long)(256 / (C / 8)) * APX;
+  return (int)(((M + grid - 1) / grid + step - 1) / step * step);
 }
 
 extern "C" {
@@ -345,8 +359,9 @@ int rdp_bn_eval_coef(int C, const float* gamma, const float* beta, const float* 
 int rdp_bn_relu_apply(const void* y, int ypitch, void* out, int opitch, const float* coef, int M, int C, int relu,
                       hipStream_t s) {
   if (!pow2_channels(C) || ypitch % 8 || opitch % 8) return -1;
-  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(grid_px(M, C)), dim3(256), 0, s, (const u16*)y, ypitch, (u16*)out,
-                     opitch, coef, M, C, relu);
+  const int grid = grid_px(M, C);
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(grid), dim3(256), 0, s, (const u16*)y, ypitch, (u16*)out,
+                     opitch, coef, M, C, relu, px_chunk(M, C, grid));
   return 0;
 }
 
@@ -374,8 +389,9 @@ int rdp_bn_bwd_finalize(const float* partial, int T, int C, long count, const fl
 int rdp_bn_relu_bwd_apply(const void* da, int dapitch, const void* y, int ypitch, const float* coef,
                           const float* coef2, void* dy, int dypitch, int M, int C, int relu, hipStream_t s) {
   if (!pow2_channels(C) || dapitch % 8 || ypitch % 8 || dypitch % 8) return -1;
-  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3(grid_px(M, C)), dim3(256), 0, s, (const u16*)da, dapitch,
-                     (const u16*)y, ypitch, coef, coef2, (u16*)dy, dypitch, M, C, relu);
+  const int grid = grid_px(M, C);
+  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3(grid), dim3(256), 0, s, (const u16*)da, dapitch,
+                     (const u16*)y, ypitch, coef, coef2, (u16*)dy, dypitch, M, C, relu, px_chunk(M, C, grid));
   return 0;
 }
 
