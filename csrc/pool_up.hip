@@ -301,9 +301,10 @@ RDP_DEV void bn_relu8(float* v, const float* sc, const float* sh) {
   for (int k = 0; k < 8; ++k) v[k] = bf2f(f2bf(fmaxf(fmaf(v[k], sc[k], sh[k]), 0.f)));
 }
 
-__global__ __launch_bounds__(256) void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch,
-                                                            u16* __restrict__ out, int opitch, UpGeom g, int lcg,
-                                                            int nchunk, const float* __restrict__ coef) {
+// R = 1 (too few rows for bands, e.g. batch-1 serving): one output row per work item, 4 taps per output.
+__global__ __launch_bounds__(256) void upsample2_fwd_taps_kernel(const u16* __restrict__ x, int xpitch,
+                                                                 u16* __restrict__ out, int opitch, UpGeom g, int lcg,
+                                                                 int nchunk, const float* __restrict__ coef) {
   const int CG = 1 << lcg;
   const int items = g.N * g.Hout * nchunk;
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
@@ -342,6 +343,85 @@ __global__ __launch_bounds__(256) void upsample2_fwd_kernel(const u16* __restric
   }
 }
 
+// One work item = a band of R output rows x 256 (pixel, 8-channel group) columns; each thread walks
+// its column down the band. The interpolation is evaluated in PyTorch's order, horizontal blend of each
+// source row first, h = hx*x[y][x0] + lx*x[y][x1], then o = hy*h[y0] + ly*h[y1]: the source-row
+// blends are kept in registers while the row pair slides down (y0/y1 advance by at most one per
+// output row), so a band of R rows loads ~R/2+1 source-row pairs instead of 4 taps per output.
+RDP_DEV void up_hrow(const u16* __restrict__ x, long rowbase, int x0, int x1, int xpitch, int c, float hx,
+                     float lx, const float* __restrict__ coef, int C, float* h) {
+  float a[8], b[8];
+  unpack8f(*(const uint4*)(x + (rowbase + x0) * xpitch + c), a);
+  unpack8f(*(const uint4*)(x + (rowbase + x1) * xpitch + c), b);
+  if (coef) {
+    float sc[8], sh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { sc[k] = coef[2 * C + c + k]; sh[k] = coef[3 * C + c + k]; }
+    bn_relu8(a, sc, sh); bn_relu8(b, sc, sh);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = hx * a[k] + lx * b[k];
+}
+
+__global__ __launch_bounds__(256) void upsample2_fwd_kernel(const u16* __restrict__ x, int xpitch,
+                                                            u16* __restrict__ out, int opitch, UpGeom g, int lcg,
+                                                            int nchunk, int R, const float* __restrict__ coef) {
+  const int CG = 1 << lcg;
+  const int nband = (g.Hout + R - 1) / R;
+  const int items = g.N * nband * nchunk;
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int band = it / nchunk, q = it - band * nchunk;
+    const int n = band / nband, Yb = (band - n * nband) * R;
+    const int t = q * 256 + threadIdx.x;
+    const int X = t >> lcg, c = (t & (CG - 1)) * 8;
+    if (X >= g.Wout) continue;
+    const int ux = X - g.ox;
+    const bool xin = ux >= 0 && ux < 2 * g.win;
+    int x0 = 0, x1 = 0;
+    float lx = 0.f;
+    if (xin) up_src(ux, g.win, g.rw, x0, x1, lx);
+    const float hx = 1.f - lx;
+    const long base = (long)n * g.hin;
+    float h0[8], h1[8];
+    int r0 = -1, r1 = -1;  // source rows held in h0 / h1
+    const int Ye = min(Yb + R, g.Hout);
+    for (int Y = Yb; Y < Ye; ++Y) {
+      const int uy = Y - g.oy;
+      float o[8];
+      if (!xin || uy < 0 || uy >= 2 * g.hin) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = 0.f;
+      } else {
+        int y0, y1;
+        float ly;
+        up_src(uy, g.hin, g.rh, y0, y1, ly);
+        if (y0 != r0) {
+          if (y0 == r1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h0[k] = h1[k];
+          } else {
+            up_hrow(x, (base + y0) * g.win, x0, x1, xpitch, c, hx, lx, coef, g.C, h0);
+          }
+          r0 = y0;
+        }
+        if (y1 != r1) {
+          if (y1 == r0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h1[k] = h0[k];
+          } else {
+            up_hrow(x, (base + y1) * g.win, x0, x1, xpitch, c, hx, lx, coef, g.C, h1);
+          }
+          r1 = y1;
+        }
+        const float hy = 1.f - ly;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = hy * h0[k] + ly * h1[k];
+      }
+      *(uint4*)(out + (((long)n * g.Hout + Y) * g.Wout + X) * opitch + c) = pack8f(o);
+    }
+  }
+}
+
 RDP_DEV float up_weight(int u, int in, float r, int i) {
   int i0, i1;
   float l1;
@@ -351,17 +431,35 @@ RDP_DEV float up_weight(int u, int in, float r, int i) {
 
 // dx[n][i][j] = sum_{uy,ux} w(uy,i) w(ux,j) dout[n][uy+oy][ux+ox]. With r = (in-1)/(2in-1) < 1/2,
 // a nonzero w(u,i) needs floor(u*r) in {i-1, i}, which holds only for u in [2i-1, 2i+2]: a fixed
-// 4x4 window. All 16 taps are loaded unconditionally (clamped address, weight 0 when the tap is
-// outside the image or the window) so the loads issue back to back; the row weights are
-// block-uniform. Taps are summed in ascending (uy, ux) order like a plain gather.
+// 4x4 window, evaluated separably: h(uy) = sum_ux w(ux,j) dout[uy][ux] (4 taps, clamped address,
+// weight 0 outside the image), dx = sum_uy w(uy,i) h(uy) in ascending uy. One work item = a band of R
+// input-gradient rows x 256 (pixel, 8-channel group) columns; walking down the band, rows 2i+1, 2i+2
+// of i are rows 2i'-1, 2i' of i' = i+1, so each row after the first loads 2 new h rows (8 taps)
+// instead of 16.
 // BNR: the consumer's training-BN backward reduction of g = bf16(dx) * relu'(y*scale+shift) is
 // accumulated on the fly (bn_relu_bwd_reduce layout, one partial row per block), so dx is never
 // re-read for it.
+RDP_DEV void up_hsum(const u16* __restrict__ dout, long ro, const int* xo, const float* wx, int dpitch, int c,
+                     float* h) {
+  uint4 v[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) v[b] = *(const uint4*)(dout + (ro + xo[b]) * dpitch + c);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = 0.f;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    float d[8];
+    unpack8f(v[b], d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = fmaf(wx[b], d[k], h[k]);
+  }
+}
+
 template <bool BNR>
 __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const u16* __restrict__ dout, int dpitch,
                                                             u16* __restrict__ dx, int xpitch, UpGeom g, int lcg,
-                                                            int nchunk, const u16* __restrict__ y, int ypitch,
-                                                            const float* __restrict__ coef,
+                                                            int nchunk, int R, const u16* __restrict__ y,
+                                                            int ypitch, const float* __restrict__ coef,
                                                             float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // BNR: [256 / CG][C][2]
   const int CG = 1 << lcg;
@@ -379,56 +477,64 @@ __global__ __launch_bounds__(256) void upsample2_bwd_kernel(const u16* __restric
       hh[k] = coef[3 * g.C + c + k];
     }
   }
-  const int items = g.N * g.hin * nchunk;
+  const int nband = (g.hin + R - 1) / R;
+  const int items = g.N * nband * nchunk;
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
-    const int row = it / nchunk, q = it - row * nchunk;
-    const int n = row / g.hin, i = row - n * g.hin;
+    const int band = it / nchunk, q = it - band * nchunk;
+    const int n = band / nband, ib = (band - n * nband) * R, ie = min(ib + R, g.hin);
     const int j = (q * 256 + threadIdx.x) >> lcg;
     if (j >= g.win) continue;
-    float wy[4], wx[4];
-    long ro[4];
+    float wx[4];
     int xo[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int uy = 2 * i - 1 + t, ux = 2 * j - 1 + t;
-      const int Y = uy + g.oy, X = ux + g.ox;
-      const bool oky = uy >= 0 && uy < uh && Y >= 0 && Y < g.Hout;
+      const int ux = 2 * j - 1 + t, X = ux + g.ox;
       const bool okx = ux >= 0 && ux < uw && X >= 0 && X < g.Wout;
-      wy[t] = oky ? up_weight(uy, g.hin, g.rh, i) : 0.f;
       wx[t] = okx ? up_weight(ux, g.win, g.rw, j) : 0.f;
-      ro[t] = ((long)n * g.Hout + (oky ? Y : 0)) * g.Wout;
       xo[t] = okx ? X : 0;
     }
-    uint4 v[4][4];
+    auto rowoff = [&](int uy) {
+      const int Y = uy + g.oy;
+      const bool oky = uy >= 0 && uy < uh && Y >= 0 && Y < g.Hout;
+      return ((long)n * g.Hout + (oky ? Y : 0)) * g.Wout;
+    };
+    float h0[8], h1[8], h2[8], h3[8];  // h(2i-1) .. h(2i+2)
+    up_hsum(dout, rowoff(2 * ib - 1), xo, wx, dpitch, c, h2);
+    up_hsum(dout, rowoff(2 * ib), xo, wx, dpitch, c, h3);
+    for (int i = ib; i < ie; ++i) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int k = 0; k < 8; ++k) { h0[k] = h2[k]; h1[k] = h3[k]; }
+      up_hsum(dout, rowoff(2 * i + 1), xo, wx, dpitch, c, h2);
+      up_hsum(dout, rowoff(2 * i + 2), xo, wx, dpitch, c, h3);
+      float wy[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) v[a][b] = *(const uint4*)(dout + (ro[a] + xo[b]) * dpitch + c);
-    float acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const float w = wy[a] * wx[b];
-        float d[8];
-        unpack8f(v[a][b], d);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, d[k], acc[k]);
+      for (int t = 0; t < 4; ++t) {
+        const int uy = 2 * i - 1 + t, Y = uy + g.oy;
+        const bool oky = uy >= 0 && uy < uh && Y >= 0 && Y < g.Hout;
+        wy[t] = oky ? up_weight(uy, g.hin, g.rh, i) : 0.f;
       }
-    const long p = (long)row * g.win + j;
-    const uint4 o = pack8f(acc);
-    *(uint4*)(dx + p * xpitch + c) = o;
-    if (BNR) {
-      float fg[8], fy[8];
-      unpack8f(o, fg);
-      unpack8f(*(const uint4*)(y + p * ypitch + c), fy);
+      float acc[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float gg = fmaf(fy[k], ss[k], hh[k]) > 0.f ? fg[k] : 0.f;
-        sg[k] += gg;
-        sgx[k] += gg * (fy[k] - mean[k]) * inv[k];
+        acc[k] = wy[0] * h0[k];
+        acc[k] = fmaf(wy[1], h1[k], acc[k]);
+        acc[k] = fmaf(wy[2], h2[k], acc[k]);
+        acc[k] = fmaf(wy[3], h3[k], acc[k]);
+      }
+      const int row = n * g.hin + i;
+      const long p = (long)row * g.win + j;
+      const uint4 o = pack8f(acc);
+      *(uint4*)(dx + p * xpitch + c) = o;
+      if (BNR) {
+        float fg[8], fy[8];
+        unpack8f(o, fg);
+        unpack8f(*(const uint4*)(y + p * ypitch + c), fy);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gg = fmaf(fy[k], ss[k], hh[k]) > 0.f ? fg[k] : 0.f;
+          sg[k] += gg;
+          sgx[k] += gg * (fy[k] - mean[k]) * inv[k];
+        }
       }
     }
   }
@@ -628,9 +734,18 @@ int rdp_upsample2_fwd(const void* x, int xpitch, void* out, int opitch, int N, i
   if (!pow2c(C) || xpitch % 8 || opitch % 8) return -1;
   UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
   const int lcg = ilog2(C / 8), nchunk = (int)(((long)Wout * (C / 8) + 255) / 256);
-  const long items = (long)N * Hout * nchunk;
-  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3((int)std::min<long>(items, 8192)), dim3(256), 0, s, (const u16*)x,
-                     xpitch, (u16*)out, opitch, g, lcg, nchunk, coef);
+  // band height 8 (128^2 -> 256^2 x 64, bs 64: 196 us with 4 taps per output -> 132 us; 16 rows 139 us),
+  // shortened while fewer than 4096 work items (16 waves per CU) would be in flight
+  int R = 8;
+  while (R > 1 && (long)N * ((Hout + R - 1) / R) * nchunk < 4096) R >>= 1;
+  const long items = (long)N * ((Hout + R - 1) / R) * nchunk;
+  if (R == 1) {
+    hipLaunchKernelGGL(upsample2_fwd_taps_kernel, dim3((int)std::min<long>(items, 8192)), dim3(256), 0, s,
+                       (const u16*)x, xpitch, (u16*)out, opitch, g, lcg, nchunk, coef);
+    return 0;
+  }
+  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3((int)std::min<long>(items, 32768)), dim3(256), 0, s, (const u16*)x,
+                     xpitch, (u16*)out, opitch, g, lcg, nchunk, R, coef);
   return 0;
 }
 // y/coef/partial given: fused BN-backward reduction of dx's consumer BN; returns the partial rows
@@ -641,16 +756,20 @@ int rdp_upsample2_bwd(const void* dout, int dpitch, void* dx, int xpitch, int N,
   if (!pow2c(C) || dpitch % 8 || xpitch % 8 || (y && ypitch % 8)) return -1;
   UpGeom g{N, hin, win, Hout, Wout, oy, ox, C, ac_scale(hin, 2 * hin), ac_scale(win, 2 * win)};
   const int lcg = ilog2(C / 8), nchunk = (int)(((long)win * (C / 8) + 255) / 256);
-  const long items = (long)N * hin * nchunk;
+  // band height 4 (256^2 -> 128^2 x 64 + BN reduce, bs 64: 198 us unbanded -> 165 us; 2 rows 171, 8 rows
+  // 175), shortened while fewer than 4096 work items would be in flight
+  int R = 4;
+  while (R > 1 && (long)N * ((hin + R - 1) / R) * nchunk < 4096) R >>= 1;
+  const long items = (long)N * ((hin + R - 1) / R) * nchunk;
   if (y) {
     const int grid = (int)std::max<long>(1, std::min<long>(items, max_blocks));
     const size_t lds = (size_t)(256 / (C / 8)) * C * 2 * sizeof(float);
     hipLaunchKernelGGL(upsample2_bwd_kernel<true>, dim3(grid), dim3(256), lds, s, (const u16*)dout, dpitch, (u16*)dx,
-                       xpitch, g, lcg, nchunk, (const u16*)y, ypitch, coef, partial);
+                       xpitch, g, lcg, nchunk, R, (const u16*)y, ypitch, coef, partial);
     return grid;
   }
   hipLaunchKernelGGL(upsample2_bwd_kernel<false>, dim3((int)std::min<long>(items, 8192)), dim3(256), 0, s,
-                     (const u16*)dout, dpitch, (u16*)dx, xpitch, g, lcg, nchunk, (const u16*)nullptr, 0,
+                     (const u16*)dout, dpitch, (u16*)dx, xpitch, g, lcg, nchunk, R, (const u16*)nullptr, 0,
                      (const float*)nullptr, (float*)nullptr);
   return 0;
 }
