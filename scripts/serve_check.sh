@@ -9,7 +9,7 @@ if [ -z "$NOTESTS" ]; then
 fi
 if [ -n "$AB" ]; then
   for r in 1 2; do for e in $AB; do
-    env $e timeout -k 10 400 python -m robotic_discovery_platform_amd.serve.bench_serve --frames 400 --warmup 40 --e2e ${E2E:-0} --multi 1 > gpurun_out/sab.json 2> gpurun_out/sab.err || { tail -20 gpurun_out/sab.err; exit 1; }
+    env ${e//,/ } timeout -k 10 400 python -m robotic_discovery_platform_amd.serve.bench_serve --frames 400 --warmup 40 --e2e ${E2E:-0} --multi 1 > gpurun_out/sab.json 2> gpurun_out/sab.err || { tail -20 gpurun_out/sab.err; exit 1; }
     python -c "
 import json;d=json.loads(open('gpurun_out/sab.json').read().splitlines()[-1])
 print('$e r$r', {k: d[k] for k in sorted(d) if k.startswith('serve_') and isinstance(d[k], (int, float)) and not k.endswith('p99_ms')})"
