@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Standalone rate of the memory-bound passes of the training step at their bs-64 shapes (the layers
 where they are largest): BN apply (+ pool), BN backward reduce / apply, maxpool backward + BN reduce,
-bilinear x2 upsample forward / backward (+ BN reduce). Median of interleaved rounds; GB/s = the bytes
+bilinear x2 upsample forward / backward (+ BN reduce), the training head forward / BN-backward apply. Median of interleaved rounds; GB/s = the bytes
 each pass must move (tensor reads + writes) / time.
 
 usage: python scripts/pass_bench.py [--batch 64] [--rounds 5]
@@ -76,6 +76,27 @@ def main():
             (f"upsample2_bwd + BN reduce {2 * h}^2 -> {h}^2 x {Cc}", 4 * El + 2 * El,
              lambda u=u, dx=dx, ylow=ylow, cf=cf, part=part: C.upsample2_bwd(u, dx, 0, 0, ylow, cf, part)),
         ]
+    # the training head (last conv's BN + ReLU, 1x1 conv, BCE partials and the backward partials from
+    # the same read of y; head_fwd GRAD) and its BN-backward apply (y read again, dy written)
+    H, Cc = 256, 64
+    M = N * H * H
+    y = t(H, H, Cc)
+    cf = coef(Cc)
+    wt, b = torch.randn(64, device=dev) * 0.1, torch.randn(1, device=dev) * 0.1
+    tg = (torch.rand(M, device=dev) > 0.5).float()
+    nb = C.head_partial_blocks(M)
+    lg, part = torch.zeros(M, device=dev), torch.zeros(nb * 65, device=dev)
+    sums, loss = torch.zeros(4, device=dev), torch.zeros(2, device=dev)
+    gp, bp = torch.zeros(nb * 65, device=dev), torch.zeros(nb * 128, device=dev)
+    c2 = torch.randn(3 * Cc, device=dev)
+    dyh = t(H, H, Cc)
+    E = M * Cc * 2
+    cases += [
+        (f"head_fwd (BN, grad partials) {H}^2 x {Cc}", E + 8 * M,
+         lambda: C.head_fwd(y, wt, b, tg, lg, part, sums, loss, 0.0, 1.0, cf, gp, bp, 1.0)),
+        (f"head_bn_bwd_apply {H}^2 x {Cc}", 2 * E + 8 * M,
+         lambda: C.head_bn_bwd_apply(y, wt, lg, tg, sums, cf, c2, dyh, 0.0, 1.0, 1.0)),
+    ]
     for name, nbytes, fn in cases:
         fn()
     torch.cuda.synchronize()
