@@ -492,6 +492,52 @@ def test_upsample_fwd_bwd(C, hin, win, H2, W2):
     assert torch.equal(fused, ref_out)
 
 
+@pytest.mark.parametrize("N,hin,win,H2,W2", [(16, 128, 128, 256, 256), (32, 128, 128, 256, 256),
+                                              (96, 61, 64, 125, 130)])
+def test_upsample_banded_large(C, N, hin, win, H2, W2):
+    """Batches large enough for the banded upsample kernels (forward bands of 4-8 output rows, backward
+    bands of 2-4 input-gradient rows; the small shapes above take the one-row forms): forward and
+    backward against F.interpolate (align_corners) + centred pad / autograd, and the BN-fused forms
+    identical to the unfused ones."""
+    torch.manual_seed(17)
+    dev = "cuda"
+    Ch = 64
+    x = bf(torch.randn(N, hin, win, Ch, device=dev))
+    xr = nchw(x).float().requires_grad_(True)
+    up = F.interpolate(xr, scale_factor=2, mode="bilinear", align_corners=True)
+    dY, dX = H2 - up.shape[2], W2 - up.shape[3]
+    ref = F.pad(up, [dX // 2, dX - dX // 2, dY // 2, dY - dY // 2])
+    out = torch.empty(N, H2, W2, Ch, dtype=torch.bfloat16, device=dev)
+    C.upsample2_fwd(x, out, dY // 2, dX // 2)
+    assert relerr(nchw(out), ref) < 1e-2
+    g = bf(torch.randn_like(ref))
+    ref.backward(g.float())
+    del ref, up
+    dx = torch.empty_like(x)
+    C.upsample2_bwd(nhwc(g), dx, dY // 2, dX // 2)
+    assert relerr(nchw(dx), xr.grad) < 1e-2
+    y = bf(torch.randn(N, hin, win, Ch, device=dev) * 2 + 0.3)
+    mean, inv = torch.randn(Ch, device=dev) * 0.1, torch.rand(Ch, device=dev) + 0.5
+    gamma, beta = torch.randn(Ch, device=dev), torch.randn(Ch, device=dev) * 0.2
+    ss = gamma * inv
+    coef = torch.cat([mean, inv, ss, beta - mean * ss]).contiguous()
+    part = torch.zeros(4096 * 2 * Ch, device=dev)
+    dx2 = torch.empty_like(x)
+    T = C.upsample2_bwd(nhwc(g), dx2, dY // 2, dX // 2, y, coef, part)
+    assert 1 <= T <= 4096 and torch.equal(dx2, dx)
+    got = part[:T * 2 * Ch].view(T, 2, Ch).double().sum(0)
+    gg = dx.float() * ((y.float() * ss + (beta - mean * ss)) > 0)
+    exact = torch.stack([gg.sum((0, 1, 2)), (gg * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
+    assert torch.allclose(got, exact, rtol=1e-3, atol=1e-2)
+    a = torch.empty_like(y)
+    C.bn_relu_apply(y, a, coef, 1)
+    ref_out = torch.empty_like(out)
+    C.upsample2_fwd(a, ref_out, dY // 2, dX // 2)
+    fused = torch.empty_like(out)
+    C.upsample2_fwd(y, fused, dY // 2, dX // 2, coef)
+    assert torch.equal(fused, ref_out)
+
+
 @pytest.mark.parametrize("dice_w", [0.0, 1.0])
 def test_head_loss(C, dice_w):
     torch.manual_seed(8)
