@@ -1,10 +1,18 @@
 #!/usr/bin/env python3
 """Headline benchmark: U-Net train imgs/sec at 256x256 (BASELINE.json metric, config 2/3).
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched under
-torch.distributed.run, one rank per GPU. W untimed warm-up steps, then exactly K timed steps
-bracketed by barrier + device sync on both sides; the time is the MAX over ranks; rank 0 prints one
-JSON line. ``value`` is the whole-job aggregate (images/s over all ranks).
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``. Both launch forms run N ranks,
+one per GPU:
+  * under a launcher (``torch.distributed.run --nproc-per-node N ... bench.py --gpus N``): every rank
+    reads RANK / LOCAL_RANK / WORLD_SIZE from the env; a WORLD_SIZE different from ``--gpus`` is an
+    error (exit 2), never a silent 1-GPU run;
+  * directly (``python bench.py --gpus N``, no WORLD_SIZE in the env, N > 1): this process touches no
+    GPU -- it starts ``torch.distributed.run`` with N ranks as a child process (never exec),
+    its rank 0 prints the JSON line to the inherited stdout, and the parent exits with the child's
+    return code (torchrun's: non-zero if any rank failed).
+W untimed warm-up steps, then exactly K timed steps bracketed by barrier + device sync on both
+sides; the time is the MAX over ranks; rank 0 prints one JSON line. ``value`` is the whole-job
+aggregate (images/s over all ranks).
 
 The step is the full reference training step (``scripts/train_segmenter.py:156-165``): forward,
 BCEWithLogits loss, backward, Adam(lr=1e-4) -- on random-init weights of the reference
@@ -62,6 +70,34 @@ def parse():
     p.add_argument("--serve", type=int, default=-1,
                    help="also measure e2e serving FPS / p50 latency (default: on for single-GPU runs)")
     return p.parse_args()
+
+
+def self_launch(args) -> "int | None":
+    """``--gpus N`` without a launcher: start N ranks as a child ``torch.distributed.run`` job and
+    return its exit code. Returns None when this process is (or should act as) the rank itself.
+    Nothing here initialises the GPU (``device_count`` does not on this ROCm image)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks; "
+                  f"pass --gpus {env_world} (or launch {args.gpus} ranks)", file=sys.stderr, flush=True)
+            sys.exit(2)
+        return None
+    if args.gpus <= 1:
+        return None
+    shared = os.environ.get("RDP_DIST_BACKEND") == "gloo"  # test mode: ranks may share one GPU
+    if args.impl == "native" and not shared:
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) are visible", file=sys.stderr, flush=True)
+            sys.exit(2)
+    import subprocess
+    from robotic_discovery_platform_amd.utils.launch import _free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def setup_dist(args):
@@ -214,6 +250,9 @@ class _Progress:
 
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     rank, world, dev = setup_dist(args)
     step = make_eager_step(args, dev, world) if args.impl == "eager" else make_native_step(args, dev, world)
     tr = getattr(step, "trainer", None)

@@ -212,19 +212,19 @@ class FrameRunner {
     if (hi[0] != W_ || hi[1] != H_ || pw != W_ || ph != H_) return kSize;
     if ((size_t)nco * 2 > coef_cap_ || meta_bytes_ < 224 * 4) return kNotNative;
     int rc[2] = {0, 0};
-    std::string err;
+    std::string err[2];  // one per half: both halves may throw concurrently
     DeviceScope g(dev_);
     rdp::host_pool().parallel_for(2, [&](int k) {
       try {
         work_half(k, c, (long)cn, d, (long)dn, hi, nco, rc);
       } catch (const std::exception& e) {  // never out of a pool thread
         rc[k] = -1;
-        err = e.what();
+        err[k] = e.what();
       }
     });
     if (rc[0] < 0 || rc[1] < 0) {
       (void)hipStreamSynchronize(s_);
-      throw std::runtime_error("submit_encoded: " + err);
+      throw std::runtime_error("submit_encoded: " + (rc[0] < 0 ? err[0] : err[1]));
     }
     if (rc[0]) {  // nothing of the frame was launched
       return rc[0];

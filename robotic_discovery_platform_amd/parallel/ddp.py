@@ -123,6 +123,9 @@ class FlatBucketer:
     def _launch(self, b: int, producer=None):
         """Issue bucket ``b``; ``producer``: the stream of the gradient that completed it (launch_ctx may
         use it to skip a wait)."""
+        # issued exactly once per step: a launch-plan replay re-runs this recorded call after reset()
+        # without going through mark_ready, and finish() must not issue the bucket a second time
+        self.pending[b] = 0
         with (self.launch_ctx(producer) if self.launch_ctx is not None else contextlib.nullcontext()):
             if self.checker is not None:
                 self.checker.check_launch(self.bucket_params[b], torch.cuda.current_stream())

@@ -36,3 +36,19 @@ def test_bench_two_ranks_json_contract(sync_bn):
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
     assert d["config"]["sync_bn"] is bool(sync_bn)
     assert d["value"] > 0 and abs(d["value"] - 4 * 1000.0 / d["ms_per_step"]) / d["value"] < 0.02
+
+
+def test_plain_bench_gpus2_self_launches():
+    """The driver's form ``python bench.py --gpus N`` (no launcher): bench.py starts the N ranks
+    itself, from a parent that never touches the GPU (native implementation, gloo sharing one GPU)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RDP_DIST_BACKEND="gloo", RDP_NO_BUILD="1")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2",
+           "--size", "64"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    assert d["config"]["impl"] == "native"

@@ -72,6 +72,45 @@ def test_flat_bucketer_allreduce(tmp_path):
     assert json.load(open(out))["nbuckets"] > 1
 
 
+def _replay_worker(rank, world, comm, out):
+    """The launch-plan protocol of NativeTrainer (train/engine.py): the recorded step keeps every bucket
+    launch (and finish) as host call points; a replay resets the bucketer and re-runs those calls
+    WITHOUT mark_ready. Each bucket must still be reduced exactly once per step."""
+    from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer
+    sizes = [5, 300, 17, 1024, 64, 3, 700]
+    ranges, off = [], 0
+    for i, n in enumerate(sizes):
+        ranges.append((f"p{i}", off, off + n))
+        off += n
+    g = torch.zeros(off)
+    b = FlatBucketer(g, ranges, bucket_mb=1200 * 4 / 2 ** 20,
+                     comm_dtype=torch.bfloat16 if comm == "bf16" else None)
+    recorded = []
+    b.host_call = lambda fn: (recorded.append(fn), fn())
+    calls = []
+    for step in range(4):
+        g.copy_(torch.arange(off, dtype=torch.float32) % 7 * (rank + 1))
+        b.reset()
+        if step == 0:  # recording
+            for n, _, _ in reversed(ranges):
+                b.mark_ready([n])
+            b.host_call(b.finish)
+        else:  # replay: the recorded host calls, in order
+            for fn in list(recorded):
+                fn()
+        exp = torch.arange(off, dtype=torch.float32) % 7 * sum(r + 1 for r in range(world))
+        calls.append(bool(torch.equal(g, exp)))
+    if rank == 0:
+        json.dump({"ok": calls}, open(out, "w"))
+
+
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_flat_bucketer_plan_replay_reduces_once(tmp_path, comm):
+    out = str(tmp_path / "r.json")
+    _run(_replay_worker, 2, comm, out)
+    assert json.load(open(out))["ok"] == [True] * 4
+
+
 def _bucketer_bf16_worker(rank, world, out):
     """bf16 comm mirror: buckets are narrowed to bf16, summed over the ranks, widened back."""
     from robotic_discovery_platform_amd.parallel.ddp import FlatBucketer
