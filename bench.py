@@ -319,6 +319,8 @@ def main():
                 "sync_bn": bool(args.sync_bn) and world > 1 and args.impl == "native",
                 "hipgraph": used_graph,
                 "grad_comm": args.grad_comm if (world > 1 or args.ddp_force) else None,
+                "ddp_stream": getattr(tr, "ddp_stream", None),
+                "ddp_emulate": os.environ.get("RDP_DDP_EMULATE") or None,
             },
             "baseline_note": "vs_baseline = value / 2.14 img/s (BASELINE.md: reference bs4 fp32 on CPU; "
                              "no published GPU number exists)",

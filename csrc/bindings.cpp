@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <link.h>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -78,6 +80,7 @@ int rdp_head_mask(const void*, int, const float*, const float*, float, void*, in
 int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float, float, float, float, float, int*, int,
              hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
+int rdp_comm_emulate(double, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
 int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
@@ -297,10 +300,12 @@ void plan_free(int id) {
 typedef int (*NcclAllReduceFn)(const void*, void*, size_t, int, int, void*, hipStream_t);
 typedef int (*NcclAsyncErrFn)(void*, int*);
 typedef const char* (*NcclErrStrFn)(int);
+typedef int (*NcclAbortFn)(void*);
 struct RcclApi {
   NcclAllReduceFn all_reduce = nullptr;
   NcclAsyncErrFn async_err = nullptr;
   NcclErrStrFn err_str = nullptr;
+  NcclAbortFn abort = nullptr;
   std::string path;
 } g_rccl;
 
@@ -322,17 +327,31 @@ std::string comm_bind() {
   g_rccl.all_reduce = (NcclAllReduceFn)dlsym(h, "ncclAllReduce");
   g_rccl.async_err = (NcclAsyncErrFn)dlsym(h, "ncclCommGetAsyncError");
   g_rccl.err_str = (NcclErrStrFn)dlsym(h, "ncclGetErrorString");
-  TORCH_CHECK(g_rccl.all_reduce && g_rccl.async_err && g_rccl.err_str, "comm_bind: RCCL symbols in ", path);
+  g_rccl.abort = (NcclAbortFn)dlsym(h, "ncclCommAbort");
+  TORCH_CHECK(g_rccl.all_reduce && g_rccl.async_err && g_rccl.err_str && g_rccl.abort, "comm_bind: RCCL symbols in ",
+              path);
   g_rccl.path = path;
   return path;
 }
 
 long rccl_check(int r, void* comm) {
   constexpr int kInProgress = 7;  // ncclInProgress: a non-blocking communicator is still enqueuing
+  // bounded: the communicators are created blocking (parallel/ddp.py), so this loop should never
+  // spin; if one does, fail after RDP_DIST_TIMEOUT_S instead of hanging the issuing thread
+  static const double limit_s = [] {
+    const char* v = std::getenv("RDP_DIST_TIMEOUT_S");
+    return v ? std::atof(v) : 600.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
   while (r == kInProgress) {
     int e = 0;
     g_rccl.async_err(comm, &e);
     r = e;
+    if (r == kInProgress &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+      g_rccl.abort(comm);
+      TORCH_CHECK(false, "ncclAllReduce: still in progress after ", limit_s, " s; communicator aborted");
+    }
   }
   TORCH_CHECK(r == 0, "ncclAllReduce: ", g_rccl.err_str(r));
   return 0;
@@ -349,6 +368,32 @@ void comm_all_reduce(torch::Tensor buf, long comm) {
   void* const c = (void*)comm;
   const NcclAllReduceFn fn = g_rccl.all_reduce;
   RDP_PLAN(rccl_check(fn(p, p, n, dt, /*ncclSum*/ 0, c, st), c));
+}
+
+// ncclCommGetAsyncError of `comm` (0 = healthy) and its message: polled by the host watchdog
+// (parallel/watchdog.py) while natively issued collectives are outstanding -- they have no
+// ProcessGroupNCCL work objects, so c10d's own watchdog never sees them.
+py::tuple comm_async_error(long comm) {
+  TORCH_CHECK(g_rccl.async_err != nullptr && comm != 0, "comm_async_error: call comm_bind() first");
+  int e = 0;
+  const int r = g_rccl.async_err((void*)comm, &e);
+  const int code = r != 0 ? r : e;
+  return py::make_tuple(code, std::string(code ? g_rccl.err_str(code) : ""));
+}
+
+// ncclCommAbort: unblocks every kernel of the communicator still waiting on a dead peer (the watchdog's
+// last step before it exits the process)
+int comm_abort(long comm) {
+  TORCH_CHECK(g_rccl.abort != nullptr && comm != 0, "comm_abort: call comm_bind() first");
+  py::gil_scoped_release nogil;
+  return g_rccl.abort((void*)comm);
+}
+
+// RDP_DDP_EMULATE: the modelled all-reduce (`us` microseconds, `blocks` resident workgroups) on the current
+// stream in place of ncclAllReduce (csrc/comm.hip), recorded into plans like the real call
+void comm_emulate(double us, int blocks) {
+  TORCH_CHECK(us >= 0 && blocks >= 1 && blocks <= 4096, "comm_emulate: bad duration / block count");
+  RDP_PLAN(rdp_comm_emulate(us, blocks, st));
 }
 
 struct Act {
@@ -1305,6 +1350,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_bind", &comm_bind, "resolve RCCL from the library torch loaded; returns its path");
   m.def("comm_all_reduce", on_device(&comm_all_reduce), py::arg("buf"), py::arg("comm"),
         "in-place SUM all-reduce over an RCCL communicator on the current stream (recorded in plans)");
+  m.def("comm_async_error", &comm_async_error, py::arg("comm"), "(code, message) of ncclCommGetAsyncError");
+  m.def("comm_abort", &comm_abort, py::arg("comm"), "ncclCommAbort");
+  m.def("comm_emulate", &comm_emulate, py::arg("us"), py::arg("blocks"),
+        "modelled collective on the current stream (RDP_DDP_EMULATE; recorded in plans)");
   m.def("plan_mark", &plan_mark, "record a host call point (replay calls host_call(tag) there)");
   m.def("plan_pause", &plan_pause);
   m.def("plan_resume", &plan_resume);

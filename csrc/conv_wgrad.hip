@@ -26,6 +26,7 @@
 #include "common.h"
 #include <algorithm>
 #include <stdlib.h>
+#include <string.h>
 
 struct WgradArgs {
   const u16* x1;
@@ -655,14 +656,25 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
   }
 }
 
+// RDP_ABLATE (profiling only, wrong results): "wgsum" skips the level-1 group sums, "wgred" both levels
+static int ablate_flags() {
+  static const int f = [] {
+    const char* v = getenv("RDP_ABLATE");
+    if (!v) return 0;
+    return (strstr(v, "wgsum") ? 1 : 0) | (strstr(v, "wgred") ? 2 : 0);
+  }();
+  return f;
+}
+
 extern "C" void rdp_wgrad_reduce(float* slab, float* out, int splits, int Cout, int ncols_pad, int taps, int cin_pad,
                                  int cin_real, int accumulate, hipStream_t s) {
+  if (ablate_flags() & 2) return;
   const long E = (long)Cout * ncols_pad;  // multiple of 4 (Cout % 64 == 0)
   const long chunks = (E / 4 + 255) / 256;
   // ~1000 level-1 blocks, at most 32 group rows for level 2; few splits (deep layers) need no level 1
   int G = (int)std::min<long>(std::min<long>(splits, 32), std::max<long>(1, (1024 + chunks - 1) / chunks));
   if (splits <= 8) G = splits;
-  if (G < splits) hipLaunchKernelGGL(wgrad_group_sum_kernel, dim3((unsigned)chunks, G), dim3(256), 0, s, slab, E, splits, G);
+  if (G < splits && !(ablate_flags() & 1)) hipLaunchKernelGGL(wgrad_group_sum_kernel, dim3((unsigned)chunks, G), dim3(256), 0, s, slab, E, splits, G);
   const long total = (long)Cout * taps * cin_real;
   if (cin_real % 4 == 0 && cin_pad % 4 == 0) {
     const int rb = (int)std::min<long>((total / 4 + 255) / 256, 4096);

@@ -331,9 +331,35 @@ class UNetNative(nn.Module):
         return cache[key]
 
 
+class _Ablated:
+    """``RDP_ABLATE=<binding>[,<binding>...]`` -- PROFILING ONLY, results are wrong: the listed kernel
+    bindings become no-ops in the executor (e.g. ``bn_relu_bwd_reduce``, ``bn_relu_bwd_apply``,
+    ``bn_relu_apply``, ``conv_wgrad``), and ``wgsum`` / ``wgred`` drop the weight-gradient slab
+    reductions inside ``conv_wgrad`` (csrc/conv_wgrad.hip). The step time without a kernel class bounds
+    what fusing or speeding it up can gain (profiles/step_ablation.md)."""
+    RET = {"bn_relu_bwd_reduce": 1, "conv_wgrad": 1, "wgrad_first_bn": 0, "conv_dgrad_bnred": 0}
+
+    def __init__(self, C, names):
+        self._C, self._names = C, frozenset(names)
+
+    def __getattr__(self, n):
+        if n in self._names:
+            return lambda *a, **k: self.RET.get(n)
+        return getattr(self._C, n)
+
+
+_ABLATED = None
+
+
 def _native():
     from ..ops import native
-    return native()
+    global _ABLATED
+    spec = os.environ.get("RDP_ABLATE", "")
+    if not spec:
+        return native()
+    if _ABLATED is None:
+        _ABLATED = _Ablated(native(), [n for n in spec.split(",") if n and n not in ("wgsum", "wgred")])
+    return _ABLATED
 
 
 @dataclass
@@ -858,6 +884,29 @@ class UNetExecutor:
         has no work handles to wait on: stream order is the dependency)."""
         if self.side is not None:
             _stream_wait(torch.cuda.current_stream(), self.side)
+
+    @contextlib.contextmanager
+    def comm_stream_dedicated(self, producer=None):
+        """A collective stream of its own (``RDP_DDP_STREAM=dedicated``): it waits for the wgrad side
+        stream (every conv weight gradient issued so far) and, unless the bucket was completed there, for
+        the current stream too (BN / head / bias gradients); the weight gradients issued after it keep
+        running beside the collective instead of queueing behind it on the side stream."""
+        if self.side is None:
+            yield
+            return
+        if getattr(self, "comm_side", None) is None:
+            self.comm_side = torch.cuda.Stream(self.dev)
+        cur = torch.cuda.current_stream()
+        _stream_wait(self.comm_side, self.side)
+        if cur != self.side and (producer is None or producer != self.side):
+            _stream_wait(self.comm_side, cur)
+        with torch.cuda.stream(self.comm_side):
+            yield
+
+    def join_comm_dedicated(self):
+        """Order the current stream after the collectives of :meth:`comm_stream_dedicated`."""
+        if getattr(self, "comm_side", None) is not None:
+            _stream_wait(torch.cuda.current_stream(), self.comm_side)
 
     def _on_side(self, fn):
         """Run ``fn`` on the wgrad side stream after everything issued so far on the main stream

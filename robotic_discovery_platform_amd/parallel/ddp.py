@@ -30,6 +30,14 @@ Design (MI355X-first):
     stream order is the dependency, no per-bucket ProcessGroupNCCL work objects, events or waits,
     and the launch is recorded into the step's launch plan like a kernel. ``RDP_DDP_COMM=torch``
     issues through torch.distributed instead (gloo always does).
+  * Issue stream at world > 1 (``RDP_DDP_STREAM``): ``side`` enqueues each collective on the wgrad side
+    stream itself (every later weight gradient then waits for it), ``dedicated`` on a collective stream
+    of its own that waits for the side stream (and the main stream where the bucket needs it), so the
+    remaining weight gradients run beside the collective. The default per world size comes from the
+    emulated A/B in ``profiles/ddp_emulated.md``: ``RDP_DDP_EMULATE=<n>:<GB/s>[:<blocks>[:<alpha_us>]]``
+    replaces each native all-reduce by a resident spin of the modelled ring time
+    2 (n - 1) / n x bytes / bw + alpha on ``blocks`` CUs (``csrc/comm.hip``), so a one-GPU box measures
+    what an n-rank collective does to the step.
   * ``comm_dtype=torch.bfloat16`` (SURVEY.md §7.4 option): each ready bucket is cast into a bf16
     mirror of the gradient buffer on the producing stream and all-reduced there (half the xGMI bytes:
     34.5 MB instead of 69 MB per step for the bilinear U-Net); ``finish()`` widens the reduced sums
@@ -44,6 +52,30 @@ import torch
 import torch.distributed as dist
 
 
+def emulate_spec(spec: Optional[str] = None) -> Optional[Tuple[int, float, int, float]]:
+    """Parse ``RDP_DDP_EMULATE`` = ``<n>:<GB/s>[:<blocks>[:<alpha_us>]]`` -> (n, GB/s, blocks, alpha_us), or
+    None. ``blocks`` resident workgroups (default 16, RCCL's channel count order on xGMI), ``alpha_us``
+    the fixed latency of one ring all-reduce (default 15 us: 2 (n - 1) hops of ~1 us)."""
+    import os
+    spec = os.environ.get("RDP_DDP_EMULATE", "") if spec is None else spec
+    if not spec:
+        return None
+    parts = spec.split(":")
+    if len(parts) < 2:
+        raise ValueError(f"RDP_DDP_EMULATE must be <n>:<GB/s>[:<blocks>[:<alpha_us>]], got {spec!r}")
+    n, bw = int(parts[0]), float(parts[1])
+    blocks = int(parts[2]) if len(parts) > 2 and parts[2] else 16
+    alpha = float(parts[3]) if len(parts) > 3 and parts[3] else 15.0
+    if n < 2 or bw <= 0 or not 1 <= blocks <= 4096 or alpha < 0:
+        raise ValueError(f"RDP_DDP_EMULATE out of range: {spec!r}")
+    return n, bw, blocks, alpha
+
+
+def ring_allreduce_us(nbytes: int, n: int, gbps: float, alpha_us: float) -> float:
+    """Modelled time of one ring all-reduce of ``nbytes`` over ``n`` ranks at ``gbps`` per-rank bus rate."""
+    return alpha_us + 2.0 * (n - 1) / n * nbytes / (gbps * 1e3)
+
+
 def dist_info() -> Tuple[int, int]:
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -56,8 +88,11 @@ class FlatBucketer:
     def __init__(self, grad_flat: torch.Tensor, param_ranges: Sequence[Tuple[str, int, int]],
                  bucket_mb: float = 16.0, group=None, comm_dtype: Optional[torch.dtype] = None,
                  launch_ctx: Optional[Callable[[], ContextManager]] = None, native_comm: Optional[int] = None,
-                 join: Optional[Callable[[], None]] = None):
+                 join: Optional[Callable[[], None]] = None,
+                 emulate: Optional[Tuple[int, float, int, float]] = None):
         self.grad = grad_flat
+        # (n, GB/s, blocks, alpha_us): a modelled collective instead of ncclAllReduce (native issue only)
+        self.emulate = emulate
         # RCCL communicator (ncclComm_t as int) for native issue, and the callable that orders the
         # caller's stream after the issuing stream once every bucket is out (native mode has no handles)
         self.native_comm = native_comm
@@ -137,7 +172,11 @@ class FlatBucketer:
                 if self.comm is not None:
                     buf = self.comm[lo:hi]
                     C.cast_bf16(self.grad[lo:hi], buf)  # narrowing cast, ordered after every producer
-                C.comm_all_reduce(buf, self.native_comm)
+                if self.emulate is not None:
+                    n, bw, blocks, alpha = self.emulate
+                    C.comm_emulate(ring_allreduce_us(buf.numel() * buf.element_size(), n, bw, alpha), blocks)
+                else:
+                    C.comm_all_reduce(buf, self.native_comm)
                 self.handles.append((b, None))
                 return
             if self.comm is not None:

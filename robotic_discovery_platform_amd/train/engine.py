@@ -45,7 +45,7 @@ import torch.nn as nn
 
 from ..models.unet import NativeAdam, UNetNative
 from ..models.unet_ref import UNetRef
-from ..parallel.ddp import FlatBucketer, broadcast_module_state, dist_info, native_comm_group
+from ..parallel.ddp import FlatBucketer, broadcast_module_state, dist_info, emulate_spec, native_comm_group
 from ..utils import trace
 
 
@@ -62,6 +62,7 @@ class NativeTrainer:
         self.opt = NativeAdam(model, lr=lr)
         self.rank, self.world = dist_info()
         self.bucketer = None
+        self.watchdog = None
         # DDP machinery (broadcast, bucketer, side-stream hooks, gscale) also at world == 1 when forced
         # (RDP_DDP_FORCE=1): exercises the RCCL path on a single GPU (all_reduce over one rank)
         if ddp_force is None:
@@ -81,12 +82,23 @@ class NativeTrainer:
             # buckets are issued from a stream ordered after both gradient streams (main: BN / head,
             # side: conv weights), never from whichever stream a hook happens to run on
             group, comm_ptr, join = None, None, None
+            launch_ctx = self.ex.comm_stream
+            emu = emulate_spec()
+            self.ddp_stream = None
             if self._native_comm_wanted(model):
                 group, comm_ptr = native_comm_group(model.store.device)
-                join = self.ex.join_comm
+                self.ddp_stream = self.ddp_stream_mode(emu[0] if emu else self.world)
+                if self.ddp_stream == "dedicated":
+                    launch_ctx, join = self.ex.comm_stream_dedicated, self.ex.join_comm_dedicated
+                else:
+                    join = self.ex.join_comm
+                if self.world > 1 or os.environ.get("RDP_COMM_WATCHDOG") == "1":
+                    self.watchdog = self._make_watchdog(comm_ptr)
+            elif emu is not None:
+                raise ValueError("RDP_DDP_EMULATE needs native RCCL issue (nccl backend, RDP_DDP_COMM=native)")
             self.bucketer = FlatBucketer(st.grad, ranges, bucket_mb, group=group,
                                          comm_dtype=torch.bfloat16 if grad_comm == "bf16" else None,
-                                         launch_ctx=self.ex.comm_stream, native_comm=comm_ptr, join=join)
+                                         launch_ctx=launch_ctx, native_comm=comm_ptr, join=join, emulate=emu)
             self.ex.set_sync_bn(enabled=sync_bn)
         if graph == "auto":
             graph = batch * h * w <= self.GRAPH_AUTO_MAX_PIXELS
@@ -105,12 +117,44 @@ class NativeTrainer:
         self.steps = 0
 
     def __del__(self):
+        if getattr(self, "watchdog", None) is not None:
+            self.watchdog.close()
         if getattr(self, "plan_id", None) is not None:
             try:
                 from ..ops import native
                 native(build_if_missing=False).plan_free(self.plan_id)
             except Exception:  # interpreter teardown
                 pass
+
+    # Issue stream of the natively issued bucket all-reduces by (emulated) world size, from the A/B in
+    # profiles/ddp_emulated.md (RDP_DDP_EMULATE on one MI355X); RDP_DDP_STREAM=side|dedicated overrides.
+    # World 1 (forced DDP): RCCL launches nothing, an extra stream wait would only cost (ddp_world1.md).
+    DDP_STREAM_BY_WORLD = {1: "side"}
+    DDP_STREAM_DEFAULT = "dedicated"
+
+    @classmethod
+    def ddp_stream_mode(cls, world: int) -> str:
+        mode = os.environ.get("RDP_DDP_STREAM", "auto")
+        if mode not in ("auto", "side", "dedicated"):
+            raise ValueError(f"RDP_DDP_STREAM must be auto, side or dedicated, got {mode!r}")
+        if mode != "auto":
+            return mode
+        return cls.DDP_STREAM_BY_WORLD.get(int(world), cls.DDP_STREAM_DEFAULT)
+
+    def _make_watchdog(self, comm_ptr: int):
+        """Host watchdog over the natively issued collectives (parallel/watchdog.py): they bypass
+        ProcessGroupNCCL's work objects, so its timeout would not see a dead peer."""
+        from ..ops import native
+        from ..parallel.watchdog import CommWatchdog
+        C = native(build_if_missing=False)
+        return CommWatchdog(poll=lambda: tuple(C.comm_async_error(comm_ptr)), abort=lambda: C.comm_abort(comm_ptr),
+                            rank=self.rank)
+
+    def _arm_watchdog(self):
+        if self.watchdog is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.watchdog.arm(ev)
 
     @staticmethod
     def _native_comm_wanted(model) -> bool:
@@ -208,6 +252,7 @@ class NativeTrainer:
                 self.plan_id = C.plan_end()
                 self._plan_version = version
             self.steps += 1
+            self._arm_watchdog()
             return self.ex.loss
         if self.use_graph:
             if self.graph is None:
@@ -227,6 +272,7 @@ class NativeTrainer:
         else:
             self._step_body()
         self.steps += 1
+        self._arm_watchdog()
         return self.ex.loss
 
     def eval_loss(self) -> torch.Tensor:

@@ -1,11 +1,13 @@
 #!/bin/bash
 # GPU check: GPU tests (TESTS=..., default all), then the default bench; AB="ENV=v1 ENV=v2" adds an
 # interleaved step A/B of those settings (E1=a,E2=b sets several; 2 rounds, bs 64 and bs 4; ABARGS: extra bench.py arguments,
-# ABBATCH: batch sizes).
+# ABBATCH: batch sizes; SKIPTESTS=1: no pytest; NOBENCH=1: no default bench).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export RDP_NO_BUILD=1
-timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
+if [ -z "$SKIPTESTS" ]; then
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+fi
 if [ -n "$AB" ]; then
   for r in 1 2; do for b in ${ABBATCH:-64 4}; do for e in $AB; do
     st=$([ $b = 4 ] && echo 200 || echo 25)

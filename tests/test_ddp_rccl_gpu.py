@@ -36,9 +36,10 @@ def _data(n=4, hw=64, seed=5):
 STEPS = 5  # a launch plan is recorded at the third step and replayed from the fourth
 
 
-def _worker(rank, port, comm, out, plan=True, issue="native"):
+def _worker(rank, port, comm, out, plan=True, issue="native", extra_env=None):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", RDP_DDP_COMM=issue)
+    os.environ.update(extra_env or {})
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
@@ -64,6 +65,14 @@ def _worker(rank, port, comm, out, plan=True, issue="native"):
             g = tr.bucketer.comm if issue == "native" and comm == "bf16" else nat.store.grad
             grads.append(g.float().clone())
         torch.cuda.synchronize()
+        env = extra_env or {}
+        if "RDP_DDP_STREAM" in env:
+            assert tr.ddp_stream == env["RDP_DDP_STREAM"]
+        if env.get("RDP_COMM_WATCHDOG") == "1":  # armed every step, healthy: nothing pending after the sync
+            import time
+            assert tr.watchdog is not None
+            time.sleep(1.5)
+            assert tr.watchdog.failed is None and tr.watchdog.pending() == 0
         if plan and issue == "torch":  # the all-reduces ran as host call points of the replayed plan
             assert tr.plan_id is not None and len(tr._plan_calls) == len(tr.bucketer.buckets) + 1
         if plan and issue == "native":  # the all-reduces are recorded launches: no host call points
@@ -103,8 +112,26 @@ def test_rccl_world1_ddp_step_matches_plain_step(tmp_path, comm, plan, issue):
     """DDP step under nccl at world 1 == the plain step, bit for bit: eager or launch-plan replay, with
     the bucket all-reduces issued natively (ncclAllReduce on the stream, recorded in the plan) or
     through torch.distributed (plan host call points)."""
+    _check_world1(tmp_path, comm, plan, issue, None)
+
+
+@pytest.mark.parametrize("comm,env", [
+    ("fp32", {"RDP_DDP_STREAM": "dedicated", "RDP_COMM_WATCHDOG": "1"}),
+    ("bf16", {"RDP_DDP_STREAM": "dedicated"}),
+    ("fp32", {"RDP_DDP_STREAM": "side", "RDP_DDP_EMULATE": "8:150:16"}),
+    ("bf16", {"RDP_DDP_STREAM": "dedicated", "RDP_DDP_EMULATE": "8:300:32"}),
+])
+def test_rccl_world1_issue_streams_and_emulation(tmp_path, comm, env):
+    """The world > 1 issue options at world 1: the dedicated collective stream, the host watchdog, and the
+    emulated collective (a resident spin in place of each all-reduce, RDP_DDP_EMULATE) -- every variant
+    must still equal the plain step bit for bit (the gradients it reads are ordered after every
+    producer; a 1-rank sum is the identity)."""
+    _check_world1(tmp_path, comm, True, "native", env)
+
+
+def _check_world1(tmp_path, comm, plan, issue, env):
     out = str(tmp_path / f"ddp_{comm}.pt")
-    mp.spawn(_worker, args=(_free_port(), comm, out, plan, issue), nprocs=1, join=True)
+    mp.spawn(_worker, args=(_free_port(), comm, out, plan, issue, env), nprocs=1, join=True)
     got = torch.load(out, weights_only=True)
     flat, grads = _plain(comm)
     for i, (a, b) in enumerate(zip(got["grads"], grads)):
