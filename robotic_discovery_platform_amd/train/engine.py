@@ -129,8 +129,10 @@ class NativeTrainer:
     # Issue stream of the natively issued bucket all-reduces by (emulated) world size, from the A/B in
     # profiles/ddp_emulated.md (RDP_DDP_EMULATE on one MI355X); RDP_DDP_STREAM=side|dedicated overrides.
     # World 1 (forced DDP): RCCL launches nothing, an extra stream wait would only cost (ddp_world1.md).
+    # Measured: the side stream wins at every emulated point (n = 8 at 150 GB/s x 16 CUs and 300 GB/s x 32
+    # CUs; bs 64: 20.34 / 20.04 ms vs 22.33 / 21.96 ms dedicated; bs 4: 3.26 / 2.87 vs 3.62 / 3.21 ms).
     DDP_STREAM_BY_WORLD = {1: "side"}
-    DDP_STREAM_DEFAULT = "dedicated"
+    DDP_STREAM_DEFAULT = "side"
 
     @classmethod
     def ddp_stream_mode(cls, world: int) -> str:
