@@ -341,6 +341,21 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
   const int cf = wave & 3, cg = wave >> 2;
   const int ca = 2 * cf + (tpp >> 1);  // 16-B chunk of this lane's A fragment row (input channels)
   typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  // LDS fragment offsets, hoisted: the swizzle reads pixel-row bits 1 and 3 only, so the half step's
+  // 32-row offset (hf) is a constant 4 KB -- one set of lane offsets serves both halves (immediates)
+  const int q0 = 8 * tg + tq;
+  int offB[2][4], offA[2][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 2 * i + (tpp >> 1);
+    offB[0][i] = q0 * 128 + 8 * (tpp & 1) + 16 * (c ^ swz(q0));
+    offB[1][i] = (q0 + 4) * 128 + 8 * (tpp & 1) + 16 * (c ^ swz(q0 + 4));
+  }
+#pragma unroll
+  for (int sh = 0; sh < 3; ++sh) {
+    offA[0][sh] = (q0 + sh) * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(q0 + sh));
+    offA[1][sh] = (q0 + sh + 4) * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(q0 + sh + 4));
+  }
 
 #pragma unroll
   for (int st = 0; st < STAGES - 1; ++st)
@@ -354,18 +369,13 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
     const char* db = cur + 3 * XREG + cg * DSUB;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      const int p0 = 32 * hf + 8 * tg + tq;
       bf16x8 fb[4];
-      {
-        const int sw0 = swz(p0), sw1 = swz(p0 + 4);
-        const int ro0 = p0 * 128 + 8 * (tpp & 1), ro1 = ro0 + 4 * 128;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = 2 * i + (tpp >> 1);
-          const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro0 + 16 * (c ^ sw0)));
-          const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(db + ro1 + 16 * (c ^ sw1)));
-          fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
+      for (int i = 0; i < 4; ++i) {
+        const char* dbi = db + hf * 4096;
+        const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(dbi + offB[0][i]));
+        const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(dbi + offB[1][i]));
+        fb[i] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
       // multi-row segments (W < 64): window pixel p + ds of tap ds = -1 / +1 crosses into the
       // neighbouring image row where w = 0 / W - 1; zero those dY pixels for that tap. This lane
@@ -382,18 +392,16 @@ __global__ __launch_bounds__(BN * 4, 2) void conv_wgrad_halo_kernel(const WgradH
           if (MULTIROW && sh == 0) fbs[i][0] = mL ? (short)0 : fb[i][0];
           if (MULTIROW && sh == 2) fbs[i][7] = mR ? (short)0 : fb[i][7];
         }
-        const int pa = p0 + sh, pb = p0 + sh + 4;
-        const int oa = pa * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pa));
-        const int ob = pb * 128 + 8 * (tpp & 1) + 16 * (ca ^ swz(pb));
 #pragma unroll
         for (int r = 0; r < 3; ++r) {  // dr + 1: input row region
-          const char* xb = cur + r * XREG;
-          const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + oa));
-          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + ob));
+          const char* xb = cur + r * XREG + hf * 4096;
+          const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + offA[0][sh]));
+          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(xb + offA[1][sh]));
           const bf16x8 fa = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
           const int tap = r * 3 + sh;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbs[i], acc[tap][i], 0, 0, 0);
+          for (int i = 0; i < 4; ++i)
+            acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbs[i], acc[tap][i], 0, 0, 0);
         }
       }
     }
