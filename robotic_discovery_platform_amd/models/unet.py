@@ -211,11 +211,17 @@ class UNetNative(nn.Module):
         return mod._buffers[leaf]
 
     def _join_wprep(self):
-        """Order the current stream after a dgrad re-layout still running on a training executor's side
-        stream (NativeAdam.step with ``side``) before the masters / derived buffers are touched here."""
+        """Order the current stream after the work NativeAdam.step left on a training executor's side
+        stream (the dgrad re-layout; with the overlapped update also Adam's group B, i.e. most masters,
+        the bf16 shadow and the step counter) before the masters / derived buffers are touched here."""
         pend = self.__dict__.pop("_wprep_pending", None)
         if pend is not None:
             _stream_wait(torch.cuda.current_stream(), pend)
+
+    def state_dict(self, *args, **kwargs):
+        # the masters of the Adam update's group B may still be written on the side stream
+        self._join_wprep()
+        return super().state_dict(*args, **kwargs)
 
     def load_state_dict(self, sd, strict: bool = True):  # keep flat-buffer views intact
         self._join_wprep()
@@ -289,6 +295,24 @@ class UNetNative(nn.Module):
         self._segs_fwd, self._nseg_fwd = table(fwd)
         self._segs_bwd, self._nseg_bwd = table(bwd)
         self._wblk_fwd, self._wblk_bwd = blocks(fwd), blocks(bwd)
+        # Adam split for the overlap with the next forward (NativeAdam.step with a side stream): group A =
+        # the parameters of the first two DoubleConvs (inc, down1; ~1.5 % of the U-Net), updated on the
+        # main stream; group B = the rest, on the side stream, which the next forward joins just before the
+        # first layer that reads them (UNetExecutor._wait_layer). The derived forward layouts split the
+        # same way: the packed first layer (A) and the transposed decoder's ConvTranspose2d weights (B).
+        self._adam_split = 0
+        if len(self.specs) > 4:
+            split = st.offsets[self.specs[4].name + ".weight"]
+            names_a = [n for n in st.names if st.offsets[n] < split]
+            own_a = {sp.name for sp in self.specs[:4]}
+            if all(n.rsplit(".", 1)[0] in own_a or any(n.startswith(sp.bn + ".") for sp in self.specs[:4])
+                   for n in names_a):
+                self._adam_split = split
+        fwd_a = [s for i, s in enumerate(segs) if i < n_conv and self.specs[i].packed and i < 4]
+        fwd_b = [s for s in fwd if s not in fwd_a]
+        self._segs_fwd_a, self._nseg_fwd_a = table(fwd_a)
+        self._segs_fwd_b, self._nseg_fwd_b = table(fwd_b + bwd)
+        self._wblk_fwd_a, self._wblk_fwd_b = blocks(fwd_a), blocks(fwd_b + bwd)
         self.refresh_weights()
 
     def refresh_weights(self):
@@ -477,6 +501,8 @@ class UNetExecutor:
             self.up_layers.append((la, lb))
             low = lb.a
         self.final = low
+        # overlapped Adam (NativeAdam.step): join the side stream before the first layer of group B
+        self._wait_layer = self.layers[4] if model._adam_split and len(self.layers) > 4 else None
         # BN + ReLU of the first layer of the full-resolution DoubleConvs (inc, up4) applied by the
         # consumer conv instead of a separate pass (training; the forward and the weight-gradient
         # row-ring kernels stage the pre-BN rows and form the activation in LDS)
@@ -650,6 +676,8 @@ class UNetExecutor:
         F.pad of Up.forward); returns True when it was produced."""
         sp = L.spec
         m = self.m
+        if L is self._wait_layer:  # the first layer whose parameters the side stream's Adam group B updates
+            m._join_wprep()
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
             # with ``pool`` / ``up``: MaxPool2d(2) / the upsample too (fused into the split-K reduce or
@@ -685,6 +713,7 @@ class UNetExecutor:
     def prepare_eval(self):
         C = _native()
         m = self.m
+        m._join_wprep()  # reads every layer's BN parameters and running statistics
         for L in self.layers:
             sp = L.spec
             C.bn_eval_coef(m.store.view(sp.bn + ".weight"), m.store.view(sp.bn + ".bias"),
@@ -1104,6 +1133,10 @@ class NativeAdam:
         self.m = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
 
+    # Overlap the update with the next forward (RDP_ADAM_OVERLAP, default on; needs ``side`` and a model
+    # whose parameter layout splits, UNetNative._adam_split)
+    OVERLAP = os.environ.get("RDP_ADAM_OVERLAP", "1") != "0"
+
     def step(self, gscale: float = 1.0, side: Optional["torch.cuda.Stream"] = None,
              grad: Optional[torch.Tensor] = None):
         """``grad``: the gradients to apply (default the store's fp32 grad; the DDP bf16 all-reduce buffer
@@ -1114,7 +1147,27 @@ class NativeAdam:
         C = _native()
         st = self.m.store
         m = self.m
-        C.adam(st.flat, st.grad if grad is None else grad, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr,
+        g = st.grad if grad is None else grad
+        split = m._adam_split
+        if side is not None and self.OVERLAP and 0 < split < st.numel and m._nseg_bwd > 0:
+            # group A (inc, down1) on the main stream, then the rest of the update and every derived layout
+            # but the packed first layer on the side stream: the next forward runs its first two
+            # DoubleConvs meanwhile and joins the side stream before down2 (UNetExecutor._wait_layer); the
+            # step counter advances once, after both groups read it. Per element the same arithmetic as
+            # the single launch, so the result is bitwise the same.
+            a, b = slice(0, split), slice(split, st.numel)
+            C.adam(st.flat[a], g[a], st.exp_avg[a], st.exp_avg_sq[a], st.shadow[a], self.lr, self.betas[0],
+                   self.betas[1], self.eps, self.wd, gscale, st.step, False)
+            if m._nseg_fwd_a:
+                C.wprep(st.flat, m.derived, m._segs_fwd_a, m._nseg_fwd_a, None, m._wblk_fwd_a)
+            _stream_wait(side, torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                C.adam(st.flat[b], g[b], st.exp_avg[b], st.exp_avg_sq[b], st.shadow[b], self.lr, self.betas[0],
+                       self.betas[1], self.eps, self.wd, gscale, st.step, False)
+                C.wprep(st.flat, m.derived, m._segs_fwd_b, m._nseg_fwd_b, st.step, m._wblk_fwd_b)
+            m.__dict__["_wprep_pending"] = side
+            return
+        C.adam(st.flat, g, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr,
                self.betas[0], self.betas[1], self.eps,
                self.wd, gscale, st.step, False)
         if side is None or m._nseg_bwd == 0:
@@ -1132,11 +1185,13 @@ class NativeAdam:
 
     def state_dict(self):
         st = self.m.store
+        self.m._join_wprep()
         return {"step": st.step.clone(), "exp_avg": st.exp_avg.clone(), "exp_avg_sq": st.exp_avg_sq.clone(),
                 "lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.wd}
 
     def load_state_dict(self, sd):
         st = self.m.store
+        self.m._join_wprep()
         with torch.no_grad():
             st.step.copy_(sd["step"])
             st.exp_avg.copy_(sd["exp_avg"])

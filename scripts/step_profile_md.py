@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Markdown summary of training steps from a rocprofv3 kernel trace (steps delimited by adam_kernel):
+"""Markdown summary of training steps from a rocprofv3 kernel trace (steps delimited by the starts of
+the first layer's conv_first_kernel; the optimizer may end a step on two streams):
 wall / per-queue busy / union busy per step, per-queue kernel totals of one step, and the main
 queue's kernel sequence with the idle gap before each launch.
 
@@ -24,9 +25,9 @@ def union(iv):
 
 def main(path, title, sequence):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    ends = [int(r["End_Timestamp"]) for r in rows if "adam_kernel" in r["Kernel_Name"]]
+    ends = [int(r["Start_Timestamp"]) for r in rows if "conv_first_kernel" in r["Kernel_Name"]]
     print(f"# {title}\n")
-    print(f"Source: rocprofv3 --kernel-trace (`{path.split('/')[-1]}`); steps end at the Adam kernel.\n")
+    print(f"Source: rocprofv3 --kernel-trace (`{path.split('/')[-1]}`); a step starts at the first layer's conv.\n")
     print("## Per step (us)\n")
     print("| step | wall | union busy | " + " | ".join(f"queue {q} busy" for q in sorted({r['Queue_Id'] for r in rows})) + " | kernels |")
     qs = sorted({r["Queue_Id"] for r in rows})
@@ -34,7 +35,7 @@ def main(path, title, sequence):
     steps = []
     for k in range(1, len(ends)):
         lo, hi = ends[k - 1], ends[k]
-        st = [r for r in rows if lo < int(r["Start_Timestamp"]) <= hi]
+        st = [r for r in rows if lo <= int(r["Start_Timestamp"]) < hi]
         steps.append(st)
         busy = {q: sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in st if r["Queue_Id"] == q) / 1e3
                 for q in qs}
@@ -56,13 +57,12 @@ def main(path, title, sequence):
         for n, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
             print(f"| `{n}` | {c} | {t:.1f} | {t / c:.1f} |")
         print()
-    if sequence:
-        main_q = max(qs, key=lambda q: sum(1 for r in st if r["Queue_Id"] == q))
-        print(f"## Main queue ({main_q}) sequence of one step\n\n```\n start us   gap us  dur us     grid kernel")
+    for qq in (qs if sequence else []):
+        print(f"## Queue {qq} sequence of one step\n\n```\n start us   gap us  dur us     grid kernel")
         t0 = int(st[0]["Start_Timestamp"])
         prev = None
         for r in st:
-            if r["Queue_Id"] != main_q:
+            if r["Queue_Id"] != qq:
                 continue
             s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
             gap = (s - prev) / 1e3 if prev else 0.0

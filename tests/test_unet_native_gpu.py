@@ -179,6 +179,51 @@ def test_plan_rerecords_after_load_state_dict():
     assert torch.equal(got[0][0], want[0])
 
 
+@pytest.mark.parametrize("plan", [False, True])
+def test_overlapped_adam_matches_single_launch_under_stall(plan):
+    """NativeAdam's overlapped update (group A on the main stream, group B + re-layouts on the side stream,
+    joined by the next forward before down2) is bitwise the single-launch update over several steps; with
+    a ~2 ms spin in front of every side-stream Adam launch (eager steps), a forward that read group B's
+    weights too early would diverge."""
+    from robotic_discovery_platform_amd.models.unet import NativeAdam, UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.ops import native
+    from robotic_discovery_platform_amd.train.engine import NativeTrainer
+    torch.manual_seed(8)
+    dev = torch.device("cuda")
+    ref = UNetRef(3, 1)
+    x = torch.rand(2, 3, 64, 64, device=dev)
+    y = (torch.rand(2, 1, 64, 64, device=dev) > 0.5).float()
+    C = native()
+    orig = C.adam
+
+    def slow(*a, **k):
+        if torch.cuda.current_stream() != torch.cuda.default_stream():
+            torch.cuda._sleep(5_000_000)
+        return orig(*a, **k)
+    states = []
+    for overlap in (True, False):
+        NativeAdam.OVERLAP = overlap
+        try:
+            if overlap and not plan:
+                C.adam = slow
+            nat = UNetNative(3, 1, device=dev, init_from=ref)
+            tr = NativeTrainer(nat, 2, 64, 64, lr=1e-3, plan=plan)
+            assert nat._adam_split > 0 and tr._wprep_side() is not None
+            tr.set_batch(x, y)
+            losses = [tr.step().clone() for _ in range(5)]
+            torch.cuda.synchronize()
+            states.append((nat.store.flat.clone(), nat.store.shadow.clone(), nat.derived.clone(),
+                           nat.store.exp_avg_sq.clone(), int(nat.store.step.item()), torch.stack(losses)))
+        finally:
+            NativeAdam.OVERLAP = True
+            C.adam = orig
+    a, b = states
+    assert a[4] == b[4] == 5
+    for u, v in zip(a[:4] + a[5:], b[:4] + b[5:]):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("bilinear", [True, False])
 def test_side_stream_wprep_matches_inline(bilinear):
     """NativeTrainer rebuilds the dgrad weight layouts on the wgrad side stream after Adam (overlapping
