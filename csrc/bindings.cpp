@@ -78,7 +78,7 @@ int rdp_head_bn_bwd_apply(const void*, int, const float*, const float*, const fl
                           const float*, void*, int, int, float, float, float, hipStream_t);
 int rdp_head_mask(const void*, int, const float*, const float*, float, void*, int, hipStream_t);
 int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float, float, float, float, float, int*, int,
-             hipStream_t);
+             int, hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_comm_emulate(double, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
@@ -153,7 +153,8 @@ auto on_device(R (*fn)(A...)) {
 // the mark's tag at the same position in the launch sequence, so the collectives keep their place
 // between the recorded kernels.
 struct PlanOp {
-  int kind;        // 0: launch, 1: waiter waits for everything issued so far on waitee, 2: host call
+  int kind;        // 0: launch, 1: waiter waits for everything issued so far on waitee, 2: host call,
+                   // 3: record a runtime-owned event on s, 4: s waits for that event's last record
   hipStream_t s;   // launch stream / waiter
   hipStream_t s2;  // waitee
   hipEvent_t ev;
@@ -218,6 +219,33 @@ void stream_wait(long waiter, long waitee) {
   if (g_rec) g_rec->ops.push_back(PlanOp{1, w, e, ev, nullptr});
 }
 
+// Named cross-stream points (runtime-owned events, recorded into plans): event_record marks "everything
+// issued so far on this stream", stream_wait_event makes another stream wait for the LAST such mark --
+// a dependency on a point in the middle of a stream's work (NativeAdam's overlapped update: the next
+// forward waits for the update, not for the weight re-layouts queued behind it).
+std::vector<hipEvent_t> g_events;
+
+int event_create() {
+  hipEvent_t e;
+  TORCH_CHECK(hipEventCreateWithFlags(&e, wait_event_flags()) == hipSuccess, "event_create");
+  g_events.push_back(e);
+  return (int)g_events.size() - 1;
+}
+
+void event_record(int id, long stream) {
+  TORCH_CHECK(id >= 0 && id < (int)g_events.size(), "event_record: bad event id");
+  const hipStream_t s = (hipStream_t)stream;
+  TORCH_CHECK(hipEventRecord(g_events[id], s) == hipSuccess, "event_record");
+  if (g_rec) g_rec->ops.push_back(PlanOp{3, s, nullptr, g_events[id], nullptr});
+}
+
+void stream_wait_event(long stream, int id) {
+  TORCH_CHECK(id >= 0 && id < (int)g_events.size(), "stream_wait_event: bad event id");
+  const hipStream_t s = (hipStream_t)stream;
+  TORCH_CHECK(hipStreamWaitEvent(s, g_events[id], 0) == hipSuccess, "stream_wait_event");
+  if (g_rec) g_rec->ops.push_back(PlanOp{4, s, nullptr, g_events[id], nullptr});
+}
+
 void plan_begin() {
   TORCH_CHECK(g_rec == nullptr && g_paused == nullptr, "plan_begin: already recording");
   g_plans.emplace_back(new Plan());
@@ -236,7 +264,7 @@ void plan_abort() {
     g_paused = nullptr;
   }
   if (g_rec) {
-    for (auto& op : g_rec->ops) if (op.ev) hipEventDestroy(op.ev);
+    for (auto& op : g_rec->ops) if (op.ev && op.kind == 1) hipEventDestroy(op.ev);
     g_rec->ops.clear();
     g_rec = nullptr;
   }
@@ -272,6 +300,10 @@ void plan_replay(int id, py::object host_call) {
     } else if (op.kind == 1) {
       hipEventRecord(op.ev, op.s2);
       hipStreamWaitEvent(op.s, op.ev, 0);
+    } else if (op.kind == 3) {
+      hipEventRecord(op.ev, op.s);
+    } else if (op.kind == 4) {
+      hipStreamWaitEvent(op.s, op.ev, 0);
     } else {
       TORCH_CHECK(!host_call.is_none(), "plan_replay: the plan has host call points, pass a callback");
       host_call(op.tag);
@@ -286,7 +318,7 @@ int plan_size(int id) {
 
 void plan_free(int id) {
   if (id < 0 || id >= (int)g_plans.size() || !g_plans[id]) return;
-  for (auto& op : g_plans[id]->ops) if (op.ev) hipEventDestroy(op.ev);
+  for (auto& op : g_plans[id]->ops) if (op.ev && op.kind == 1) hipEventDestroy(op.ev);
   g_plans[id].reset();
 }
 
@@ -1019,7 +1051,8 @@ void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_t
 }
 
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
-          double lr, double b1, double b2, double eps, double wd, double gscale, torch::Tensor step, bool inc) {
+          double lr, double b1, double b2, double eps, double wd, double gscale, torch::Tensor step, bool inc,
+          int max_blocks) {
   check_f32(p, "p"); check_f32(m, "m"); check_f32(v, "v");
   const bool gbf = g.scalar_type() == torch::kBFloat16;  // bf16 gradients (the DDP bf16 all-reduce buffer)
   if (!gbf) check_f32(g, "g");
@@ -1034,7 +1067,7 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c1
   const void* gp = g.data_ptr();
   TORCH_CHECK(RDP_PLAN(rdp_adam(p.data_ptr<float>(), gp, gbf ? 1 : 0, m.data_ptr<float>(), v.data_ptr<float>(), sh, p.numel(),
                        (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)gscale,
-                       (int*)step.data_ptr(), inc ? 1 : 0, st)) == 0, "adam: numel must be a multiple of 4");
+                       (int*)step.data_ptr(), inc ? 1 : 0, max_blocks, st)) == 0, "adam: numel must be a multiple of 4");
 }
 
 void cast_bf16(torch::Tensor p, torch::Tensor out) {
@@ -1342,6 +1375,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_serve_runtime(m);
   m.doc() = "rdp MI355X (gfx950) HIP kernels";
   m.def("stream_wait", &stream_wait, "waiter stream waits for the work issued so far on waitee (recorded in plans)");
+  m.def("event_create", &event_create, "runtime-owned cross-stream event (id)");
+  m.def("event_record", &event_record, py::arg("id"), py::arg("stream"), "record event id on stream (recorded in plans)");
+  m.def("stream_wait_event", &stream_wait_event, py::arg("stream"), py::arg("id"),
+        "stream waits for the last record of event id (recorded in plans)");
   m.def("plan_begin", &plan_begin);
   m.def("plan_end", &plan_end);
   m.def("plan_abort", &plan_abort);
@@ -1410,7 +1447,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_head_mask", on_device(&conv_head_mask));
   m.def("adam", on_device(&adam), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
-        py::arg("inc") = true);
+        py::arg("inc") = true, py::arg("max_blocks") = 0);
   m.def("cast_bf16", on_device(&cast_bf16));
   m.def("wprep", on_device(&wprep), py::arg("master"), py::arg("out"), py::arg("segs"), py::arg("nseg"),
         py::arg("step") = py::none(), py::arg("blocks") = 0);

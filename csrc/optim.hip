@@ -118,11 +118,14 @@ __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ ma
 extern "C" {
 // inc = 0: the caller advances the step counter later on this stream (rdp_wprep with step)
 // g_bf16: g is bf16 (u16) instead of fp32
+// max_blocks > 0 caps the grid (grid-stride loop): the overlapped update on the side stream leaves CUs to
+// the next forward's first layers
 int rdp_adam(float* p, const void* g, int g_bf16, float* m, float* v, void* shadow, long n, float lr, float b1,
-             float b2, float eps, float wd, float gscale, int* step, int inc, hipStream_t s) {
+             float b2, float eps, float wd, float gscale, int* step, int inc, int max_blocks, hipStream_t s) {
   if (n % 4) return -1;
   const long n4 = n / 4;
-  const int grid = (int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 8192));
+  int grid = (int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 8192));
+  if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
   if (g_bf16)
     hipLaunchKernelGGL(adam_kernel<u16>, dim3(grid), dim3(256), 0, s, p, (const u16*)g, m, v, (u16*)shadow, n, lr, b1,
                        b2, eps, wd, gscale, step);

@@ -215,8 +215,15 @@ class UNetNative(nn.Module):
         stream (the dgrad re-layout; with the overlapped update also Adam's group B, i.e. most masters,
         the bf16 shadow and the step counter) before the masters / derived buffers are touched here."""
         pend = self.__dict__.pop("_wprep_pending", None)
+        self.__dict__.pop("_adam_ev_pending", None)
         if pend is not None:
             _stream_wait(torch.cuda.current_stream(), pend)
+
+    def _join_adam(self):
+        """Order the current stream after the side stream's Adam group B only (not the re-layouts queued
+        behind it): the next forward's join before its first group-B layer."""
+        if self.__dict__.pop("_adam_ev_pending", False):
+            _native().stream_wait_event(torch.cuda.current_stream().cuda_stream, self._adam_ev)
 
     def state_dict(self, *args, **kwargs):
         # the masters of the Adam update's group B may still be written on the side stream
@@ -311,8 +318,8 @@ class UNetNative(nn.Module):
         fwd_a = [s for i, s in enumerate(segs) if i < n_conv and self.specs[i].packed and i < 4]
         fwd_b = [s for s in fwd if s not in fwd_a]
         self._segs_fwd_a, self._nseg_fwd_a = table(fwd_a)
-        self._segs_fwd_b, self._nseg_fwd_b = table(fwd_b + bwd)
-        self._wblk_fwd_a, self._wblk_fwd_b = blocks(fwd_a), blocks(fwd_b + bwd)
+        self._segs_fwd_b, self._nseg_fwd_b = table(fwd_b)
+        self._wblk_fwd_a, self._wblk_fwd_b = blocks(fwd_a), blocks(fwd_b)
         self.refresh_weights()
 
     def refresh_weights(self):
@@ -677,7 +684,7 @@ class UNetExecutor:
         sp = L.spec
         m = self.m
         if L is self._wait_layer:  # the first layer whose parameters the side stream's Adam group B updates
-            m._join_wprep()
+            m._join_adam()
         w = m.fwd_weight(sp)
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
             # with ``pool`` / ``up``: MaxPool2d(2) / the upsample too (fused into the split-K reduce or
@@ -1136,6 +1143,10 @@ class NativeAdam:
     # Overlap the update with the next forward (RDP_ADAM_OVERLAP, default on; needs ``side`` and a model
     # whose parameter layout splits, UNetNative._adam_split)
     OVERLAP = os.environ.get("RDP_ADAM_OVERLAP", "1") != "0"
+    # grid cap of the side-stream group (0: full grid)
+    # (measured: 256 blocks 19.00 / 19.10 ms bs 64 and 2.392 / 2.387 ms bs 4 vs 19.10 / 19.12 and 2.405 / 2.394
+    # with the full grid, vs 19.10 / 19.28 and 2.400 / 2.391 without the overlap; one box, interleaved)
+    SIDE_BLOCKS = int(os.environ.get("RDP_ADAM_SIDE_BLOCKS", "256"))
 
     def step(self, gscale: float = 1.0, side: Optional["torch.cuda.Stream"] = None,
              grad: Optional[torch.Tensor] = None):
@@ -1160,12 +1171,20 @@ class NativeAdam:
                    self.betas[1], self.eps, self.wd, gscale, st.step, False)
             if m._nseg_fwd_a:
                 C.wprep(st.flat, m.derived, m._segs_fwd_a, m._nseg_fwd_a, None, m._wblk_fwd_a)
+            if m.__dict__.get("_adam_ev") is None:
+                m.__dict__["_adam_ev"] = C.event_create()
             _stream_wait(side, torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 C.adam(st.flat[b], g[b], st.exp_avg[b], st.exp_avg_sq[b], st.shadow[b], self.lr, self.betas[0],
-                       self.betas[1], self.eps, self.wd, gscale, st.step, False)
-                C.wprep(st.flat, m.derived, m._segs_fwd_b, m._nseg_fwd_b, st.step, m._wblk_fwd_b)
+                       self.betas[1], self.eps, self.wd, gscale, st.step, False, self.SIDE_BLOCKS)
+                if m._nseg_fwd_b:  # the transposed decoder's ConvTranspose2d forward layouts
+                    C.wprep(st.flat, m.derived, m._segs_fwd_b, m._nseg_fwd_b, None, m._wblk_fwd_b)
+                C.event_record(m._adam_ev, side.cuda_stream)  # the next forward's join point
+                # dgrad layouts, read only by the next backward (+ the step counter advance, after both
+                # groups read it)
+                C.wprep(st.flat, m.derived, m._segs_bwd, m._nseg_bwd, st.step, m._wblk_bwd)
             m.__dict__["_wprep_pending"] = side
+            m.__dict__["_adam_ev_pending"] = True
             return
         C.adam(st.flat, g, st.exp_avg, st.exp_avg_sq, st.shadow, self.lr,
                self.betas[0], self.betas[1], self.eps,
