@@ -82,6 +82,7 @@ int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_comm_emulate(double, int, hipStream_t);
 int rdp_batch_copy(const void*, int, int, int, void*, long, hipStream_t);
+int rdp_rows_fold(float*, int, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
 int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
@@ -401,6 +402,14 @@ void comm_all_reduce(torch::Tensor buf, long comm) {
   void* const c = (void*)comm;
   const NcclAllReduceFn fn = g_rccl.all_reduce;
   RDP_PLAN(rccl_check(fn(p, p, n, dt, /*ncclSum*/ 0, c, st), c));
+}
+
+// SyncBN: fold buf's [rows][width] fp32 partial rows into row 0 (fp64 sums), recorded in plans
+void rows_fold(torch::Tensor buf, int rows, int width) {
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == torch::kFloat && buf.is_contiguous() &&
+              (long)rows * width <= buf.numel() && rows >= 1 && width >= 1, "rows_fold: fp32 buffer of rows x width");
+  float* p = buf.data_ptr<float>();
+  RDP_PLAN(rdp_rows_fold(p, rows, width, st));
 }
 
 // ncclCommGetAsyncError of `comm` (0 = healthy) and its message: polled by the host watchdog
@@ -1406,6 +1415,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_bind", &comm_bind, "resolve RCCL from the library torch loaded; returns its path");
   m.def("comm_all_reduce", on_device(&comm_all_reduce), py::arg("buf"), py::arg("comm"),
         "in-place SUM all-reduce over an RCCL communicator on the current stream (recorded in plans)");
+  m.def("rows_fold", on_device(&rows_fold), py::arg("buf"), py::arg("rows"), py::arg("width"));
   m.def("comm_async_error", &comm_async_error, py::arg("comm"), "(code, message) of ncclCommGetAsyncError");
   m.def("comm_abort", &comm_abort, py::arg("comm"), "ncclCommAbort");
   m.def("comm_emulate", &comm_emulate, py::arg("us"), py::arg("blocks"),

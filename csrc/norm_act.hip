@@ -35,6 +35,21 @@ __global__ void colsum_kernel(const float* __restrict__ in, int T, int K, int rp
   if (ty == 0 && col < K) out[(size_t)blockIdx.y * K + col] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
+// SyncBatchNorm: fold a layer's [T][K] partial rows into row 0 in place (fp64 accumulation, one thread
+// per column), so one K-float all-reduce per layer carries the rank's sums (models/unet.py _sync_rows)
+__global__ void rows_fold_kernel(float* __restrict__ buf, int T, int K) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= K) return;
+  double a = 0.0, b = 0.0;
+  int r = 0;
+  for (; r + 1 < T; r += 2) {
+    a += (double)buf[(size_t)r * K + col];
+    b += (double)buf[(size_t)(r + 1) * K + col];
+  }
+  if (r < T) a += (double)buf[(size_t)r * K + col];
+  buf[col] = (float)(a + b);
+}
+
 #define FIN_DIRECT_ROWS 2048
 #define FIN_RG 16  // row groups per finalize block (blockDim = 64 * FIN_RG)
 
@@ -347,6 +362,12 @@ int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* g
   stats = shrink_rows(stats, T, 2 * C, ws, T, s);
   hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3((C + 63) / 64), dim3(64 * FIN_RG), 0, s, stats, T, C, (double)count, gamma,
                      beta, rmean, rvar, nbt, momentum, eps, coef);
+  return 0;
+}
+
+int rdp_rows_fold(float* buf, int T, int K, hipStream_t s) {
+  if (T < 1 || K < 1) return -1;
+  hipLaunchKernelGGL(rows_fold_kernel, dim3((K + 255) / 256), dim3(256), 0, s, buf, T, K);
   return 0;
 }
 

@@ -553,6 +553,9 @@ class UNetExecutor:
         # layer, forward and backward) and finalized with the global pixel count.
         self.sync_group = None
         self.sync_world = 1
+        self.sync_comm = None  # native RCCL communicator of the statistics all-reduces (set_sync_bn)
+        self.sync_emulate = None
+        self._sync_on = False
         self.red_ws = torch.zeros(64 * 2 * max(L.spec.cout for L in self.layers), dtype=torch.float32, device=dev)
         # split-K workspace (fp32 partial tiles) for the convs whose tile grid alone underfills the
         # chip (deep layers at small batch, e.g. serving at N=1); shared: convs run in sequence
@@ -706,7 +709,7 @@ class UNetExecutor:
         b = m.store.view(sp.bn + ".bias")
         if self.training:
             M = L.y.shape[0] * L.y.shape[1] * L.y.shape[2]
-            if self.sync_world > 1:
+            if self._sync_on:
                 rows, M = self._sync_rows(self.stats, rows, sp.cout, (L.y.shape[1], L.y.shape[2]))
             C.bn_finalize(self.stats, rows, M, g, b, m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"),
                           m.buf(sp.bn + ".num_batches_tracked"), 0.1, 1e-5, L.coef, self.red_ws)
@@ -827,7 +830,7 @@ class UNetExecutor:
         # the reduction already ran inside the pool/head backward that produced L.da (fused), or runs now
         T = L.bwd_rows if L.bwd_rows else C.bn_relu_bwd_reduce(L.da, L.y, L.coef, 1, self.bn_partial)
         L.bwd_rows = 0
-        if self.sync_world > 1:
+        if self._sync_on:
             # gamma/beta gradients stay local (DDP averages them like any weight); the input-gradient
             # coefficients use the globally reduced sums, as torch.nn.SyncBatchNorm does
             C.bn_bwd_finalize(self.bn_partial, T, M, st.view(sp.bn + ".weight"), L.coef,
@@ -865,6 +868,15 @@ class UNetExecutor:
                     group = dist.new_group()
                     self.m.__dict__["_sync_bn_group"] = group
             self.sync_group, self.sync_world = group, dist.get_world_size(group)
+            # nccl on GPUs: the per-layer statistics all-reduces issued natively on the main stream over a
+            # communicator of their own (parallel.ddp.native_comm_group "syncbn"), folded by a kernel --
+            # every step of it a recorded launch, so SyncBN keeps the launch plan
+            self.sync_comm = None
+            if (group is self.m.__dict__.get("_sync_bn_group") and dist.get_backend(group) == "nccl"
+                    and self.dev.type == "cuda" and os.environ.get("RDP_DDP_COMM", "native") == "native"):
+                from ..parallel.ddp import emulate_spec, native_comm_group
+                self.sync_comm = native_comm_group(self.dev, "syncbn")[1]
+                self.sync_emulate = emulate_spec()
             shp = torch.tensor([self.N, self.H, self.W], dtype=torch.int64)
             if dist.get_backend(group) != "gloo":
                 shp = shp.to(self.dev)
@@ -881,12 +893,26 @@ class UNetExecutor:
                 self._sync_m[(h, w)] = tot
         else:
             self.sync_group, self.sync_world = None, 1
+            self.sync_comm = None
+        # statistics shared across ranks (also at world 1 under RDP_DDP_EMULATE: the modelled collectives)
+        self._sync_on = self.sync_world > 1 or (self.sync_comm is not None and self.sync_emulate is not None)
 
     def _sync_rows(self, buf: torch.Tensor, rows: int, c: int, hw: Tuple[int, int]) -> Tuple[int, int]:
         """Fold ``rows`` partial [2][C] rows of ``buf`` into row 0 (fp64 sum), all-reduce it over the
         sync group and return (1, global pixel count at spatial size ``hw``): the row count the
         finalize kernels then read and the pixels the reduced sums cover."""
         import torch.distributed as dist
+        if getattr(self, "sync_comm", None) is not None:  # native: fold kernel + ncclAllReduce on this stream
+            C = _native()
+            C.rows_fold(buf, rows, 2 * c)
+            emu = getattr(self, "sync_emulate", None)
+            if emu is not None:  # RDP_DDP_EMULATE: the modelled collective instead (one-GPU A/B)
+                from ..parallel.ddp import ring_allreduce_us
+                n, bw, blocks, alpha = emu
+                C.comm_emulate(ring_allreduce_us(8 * c, n, bw, alpha), 1)
+            else:
+                C.comm_all_reduce(buf[: 2 * c], self.sync_comm)
+            return 1, self._sync_m[hw]
         tot = buf[: rows * 2 * c].view(rows, 2 * c).sum(0, dtype=torch.float64)
         if dist.get_backend(self.sync_group) == "gloo":  # host round trip (gloo tests: ranks share a GPU)
             tot = tot.cpu()

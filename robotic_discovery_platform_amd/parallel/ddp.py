@@ -277,16 +277,19 @@ class StreamOrderChecker:
             unet._STREAM_OBSERVERS.remove(self)
 
 
-_GRAD_GROUPS: Dict[int, object] = {}
+_GRAD_GROUPS: Dict[Tuple[int, str], object] = {}
 
 
-def native_comm_group(device: torch.device):
-    """(process group, ncclComm_t as int) for natively issued gradient all-reduces on ``device``: a
-    dedicated nccl group (created once per device; collective -- every rank calls this in the same
-    order) with BLOCKING communicators (eager-init groups default to non-blocking ones, whose calls
-    may return ncclInProgress), initialised by one all-reduce before its communicator is taken."""
+def native_comm_group(device: torch.device, tag: str = "grad"):
+    """(process group, ncclComm_t as int) for natively issued all-reduces on ``device``: a dedicated
+    nccl group per (device, ``tag``) -- "grad" for the gradient buckets (wgrad side stream), "syncbn" for
+    the SyncBatchNorm statistics (main stream: a communicator of its own, so the two streams never
+    interleave operations of one communicator in a rank-dependent order) -- created once (collective:
+    every rank calls this in the same order) with BLOCKING communicators (eager-init groups default to
+    non-blocking ones, whose calls may return ncclInProgress), initialised by one all-reduce before its
+    communicator is taken."""
     from torch._C._distributed_c10d import ProcessGroupNCCL
-    key = device.index or 0
+    key = (device.index or 0, tag)
     if key not in _GRAD_GROUPS:
         opts = ProcessGroupNCCL.Options()
         opts.config.blocking = 1

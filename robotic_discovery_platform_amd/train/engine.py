@@ -106,8 +106,10 @@ class NativeTrainer:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         if plan == "auto":
             plan = os.environ.get("RDP_PLAN", "1") != "0"
-        # SyncBN's statistics all-reduces sit inside the executor's kernel sequence: no plan with it
-        self.use_plan = (bool(plan) and not (self.ddp and sync_bn) and not self.use_graph
+        # SyncBN's statistics all-reduces sit inside the executor's kernel sequence: a plan holds them only
+        # when they are native launches (nccl: fold kernel + ncclAllReduce, UNetExecutor._sync_rows)
+        sync_py = self.ddp and sync_bn and self.ex.sync_comm is None
+        self.use_plan = (bool(plan) and not sync_py and not self.use_graph
                          and torch.cuda.is_available() and model.store.device.type == "cuda")
         self.plan_id: Optional[int] = None
         self._plan_calls: list = []  # host call points of the recorded plan (DDP collectives), by tag

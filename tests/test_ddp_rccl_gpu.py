@@ -209,3 +209,45 @@ def test_rccl_bucket_launch_order(tmp_path):
         names = r["buckets"][b]
         done_at = max(i for i, h in enumerate(hooks) if any(p.startswith(h + ".") for p in names)) + 1
         assert n_fired == done_at
+
+
+def _syncbn_worker(rank, port, out, emulate):
+    """Native SyncBN (fold kernel + ncclAllReduce on the main stream, own communicator) at world 1 under
+    nccl, in launch-plan mode; at world 1 (or with the emulated collective) the shared statistics equal the
+    local ones, so the step must match the plain step up to the fp64 fold order."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      RDP_DDP_COMM="native")
+    if emulate:
+        os.environ["RDP_DDP_EMULATE"] = "8:150:16"
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from robotic_discovery_platform_amd.models.unet import UNetNative
+        from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+        from robotic_discovery_platform_amd.train.engine import NativeTrainer
+        torch.manual_seed(7)
+        nat = UNetNative(3, 1, device=dev, init_from=UNetRef(3, 1))
+        tr = NativeTrainer(nat, 4, 64, 64, lr=1e-3, graph=False, bucket_mb=4.0, ddp_force=True, sync_bn=True,
+                           plan=True)
+        assert tr.ex.sync_comm is not None and tr.use_plan
+        assert tr.ex._sync_on == emulate  # world 1: statistics shared only when emulating the collective
+        x, t = _data()
+        tr.set_batch(x.to(dev), t.to(dev))
+        for _ in range(STEPS):
+            tr.step()
+        torch.cuda.synchronize()
+        assert tr.plan_id is not None and tr._plan_calls == []  # every collective a recorded launch
+        torch.save({"flat": nat.store.flat.cpu()}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("emulate", [False, True])
+def test_syncbn_native_plan_world1(tmp_path, emulate):
+    out = str(tmp_path / "sbn.pt")
+    mp.spawn(_syncbn_worker, args=(_free_port(), out, emulate), nprocs=1, join=True)
+    got = torch.load(out, weights_only=True)
+    flat, _ = _plain("fp32")
+    assert torch.allclose(got["flat"], flat, atol=2e-5, rtol=0), float((got["flat"] - flat).abs().max())
