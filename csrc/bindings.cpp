@@ -81,7 +81,6 @@ int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float
              int, hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_comm_emulate(double, int, hipStream_t);
-int rdp_batch_copy(const void*, int, int, int, void*, long, hipStream_t);
 int rdp_rows_fold(float*, int, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
 int rdp_wseg_size();
@@ -1369,24 +1368,6 @@ void preprocess(torch::Tensor bgr, torch::Tensor ystart, torch::Tensor ysize, to
                  rgb, o.ptr, unplanned_stream());
 }
 
-// batched serving network: gather the members' [1,S,S,8] inputs into x ([N,S,S,8]) / scatter the [N*S*S] masks
-// back to the members (device table: N, inputs, masks; csrc/serve_kernels.hip)
-void batch_gather(torch::Tensor table, int B, torch::Tensor x) {
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kInt64 && table.numel() >= 1 + 2 * B, "table int64 [1+2B]");
-  Act a = act(x, "x");
-  TORCH_CHECK(a.N <= B && a.pitch == a.C, "x: contiguous [N<=B,S,S,C]");
-  const long per = (long)a.H * a.W * a.C * 2;
-  TORCH_CHECK(rdp_batch_copy(table.data_ptr(), B, a.N, 0, a.ptr, per, unplanned_stream()) == 0, "batch_gather");
-}
-
-void batch_scatter(torch::Tensor table, int B, torch::Tensor masks, int N) {
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kInt64 && table.numel() >= 1 + 2 * B, "table int64 [1+2B]");
-  TORCH_CHECK(masks.is_cuda() && masks.scalar_type() == torch::kUInt8 && masks.is_contiguous() && N >= 1 && N <= B &&
-              masks.numel() % N == 0, "masks: u8 [N*S*S]");
-  TORCH_CHECK(rdp_batch_copy(table.data_ptr(), B, N, 1, masks.data_ptr(), masks.numel() / N, unplanned_stream()) == 0,
-              "batch_scatter");
-}
-
 void mask_upsample(torch::Tensor m, torch::Tensor out, torch::Tensor count) {
   TORCH_CHECK(m.is_cuda() && m.scalar_type() == torch::kUInt8 && m.dim() == 2 && m.is_contiguous(), "m");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kUInt8 && out.dim() == 2 && out.is_contiguous(), "out");
@@ -1504,8 +1485,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("area_maxtap", &rdp_area_maxtap);
   m.def("geo_spline_res_len", &rdp_geo_spline_res_len);
   m.def("geo_work_ints", &geo_work_ints);
-  m.def("batch_gather", on_device(&batch_gather), py::arg("table"), py::arg("B"), py::arg("x"));
-  m.def("batch_scatter", on_device(&batch_scatter), py::arg("table"), py::arg("B"), py::arg("masks"), py::arg("N"));
   m.def("preprocess", on_device(&preprocess), py::arg("bgr"), py::arg("ystart"), py::arg("ysize"), py::arg("yw"),
         py::arg("xstart"), py::arg("xsize"), py::arg("xw"), py::arg("out"), py::arg("rgb") = 0);
   m.def("mask_upsample", on_device(&mask_upsample));

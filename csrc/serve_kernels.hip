@@ -9,7 +9,6 @@
 // mask_upsample: replaces (sigmoid(logits) > 0.5) -> cv2.resize(INTER_NEAREST) -> count_nonzero
 //   (server.py:124-125,133): u8 {0,1} mask at the camera resolution + coverage count (atomics).
 #include "common.h"
-#include <algorithm>
 
 #define AA_MAXTAP 16
 
@@ -260,29 +259,4 @@ int rdp_jpeg_gpu(const void* coefs, const int* geo, const int* qt, void* planes,
                      (uint8_t*)rgb);
   return 0;
 }
-}
-
-// ---- batched serving network (serve/engine.py BatchEngine, csrc/serve_runtime.cpp BatchNet) -----------
-// Frames of concurrent streams that wait for the GPU are run as ONE network launch of N frames. Each
-// frame's colour stage writes its own N = 1 input buffer and its geometry reads its own 256 x 256 mask;
-// the batched network graph starts by gathering the members' inputs into its [N] input and ends by
-// scattering its [N] masks back, both through a device table the host fills per launch:
-//   table[0] = N, table[1 + i] = member i's input (bytes each), table[1 + B + i] = member i's mask.
-__global__ __launch_bounds__(256) void batch_copy_kernel(const uint64_t* __restrict__ table, int B, int scatter,
-                                                         uint8_t* __restrict__ base, long bytes) {
-  const int i = blockIdx.y;
-  if (i >= (int)table[0]) return;
-  const long n16 = bytes >> 4;
-  uint4* dst = (uint4*)(scatter ? (uint8_t*)table[1 + B + i] : base + (long)i * bytes);
-  const uint4* src = (const uint4*)(scatter ? base + (long)i * bytes : (const uint8_t*)table[1 + i]);
-  for (long k = blockIdx.x * 256l + threadIdx.x; k < n16; k += (long)gridDim.x * 256) dst[k] = src[k];
-}
-
-extern "C" int rdp_batch_copy(const void* table, int B, int N, int scatter, void* base, long bytes, hipStream_t s) {
-  if (N < 1 || N > B || bytes % 16) return -1;
-  const long n16 = bytes / 16;
-  const int gx = (int)std::min<long>((n16 + 255) / 256, 256);
-  hipLaunchKernelGGL(batch_copy_kernel, dim3(gx, N), dim3(256), 0, s, (const uint64_t*)table, B, scatter,
-                     (uint8_t*)base, bytes);
-  return 0;
 }

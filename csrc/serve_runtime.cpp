@@ -22,15 +22,10 @@
 #include <pybind11/pybind11.h>
 
 #include <chrono>
-#include <condition_variable>
 #include <cstdint>
-#include <deque>
-#include <mutex>
-#include <thread>
 #include <cstring>
 #include <stdexcept>
 #include <string>
-#include <memory>
 #include <vector>
 
 #include "host_pool.h"
@@ -68,141 +63,6 @@ inline void* P(uintptr_t v) { return reinterpret_cast<void*>(v); }
 std::string encode_wire(double mean, double maxc, const double* pts, size_t npts, const std::string& status,
                         const uint8_t* mask01, int h, int w, float coverage, float proc_ms, int level, int bands);
 
-// ---- batched network across concurrent streams --------------------------------------------------------
-// Concurrent streams' frames each used to run their own N = 1 network graph; at N = 1 the network is
-// latency-bound (0.38 ms on one MI355X) and two frames cost almost two networks. BatchNet runs frames that
-// would otherwise QUEUE for the GPU as one network launch of N frames instead (0.48 ms at N = 2, 0.70 at
-// N = 4: scripts/serve_batch_probe.py). Policy (continuous batching, no waiting on an idle GPU):
-//   * a frame whose colour half finds no network in flight runs its own N = 1 network graph on its own
-//     stream, exactly as without batching (single-stream latency unchanged);
-//   * otherwise its colour stage (JPEG pixel stage + preprocess into its own input) runs on its stream and
-//     the frame joins the forming batch; the batch is launched on the network stream -- by whichever
-//     member thread sees it first -- as soon as it is full or fewer than 2 networks are in flight (one
-//     running, at most one queued behind it), so the GPU never idles between networks;
-//   * the network graph of N gathers the members' inputs and scatters their masks back (device table,
-//     csrc/serve_kernels.hip); each member's geometry half then waits for that launch's event.
-// Every wait is on a network already launched (which waits only on launched colour stages): no deadlock.
-class BatchNet {
- public:
-  BatchNet(int device, uintptr_t stream, int max_batch, uintptr_t d_table)
-      : dev_(device), ns_((hipStream_t)stream), B_(max_batch), d_table_((uint64_t*)d_table) {
-    if (B_ < 2 || B_ > 16) throw std::invalid_argument("max_batch must be 2..16");
-    DeviceScope g(dev_);
-    for (int k = 0; k < kRing; ++k) {
-      hip_check(hipHostMalloc((void**)&h_table_[k], (1 + 2 * B_) * sizeof(uint64_t), hipHostMallocDefault),
-                "hipHostMalloc");
-      hip_check(hipEventCreateWithFlags(&tcopy_[k], hipEventDisableTiming), "hipEventCreate");
-      hip_check(hipEventCreateWithFlags(&net_[k], hipEventDisableTiming | hipEventDisableSystemFence),
-                "hipEventCreate");
-    }
-    exec_.assign(B_ + 1, nullptr);
-    sizes_.assign(B_ + 1, 0);
-  }
-  ~BatchNet() {
-    for (int k = 0; k < kRing; ++k) {
-      (void)hipHostFree(h_table_[k]);
-      (void)hipEventDestroy(tcopy_[k]);
-      (void)hipEventDestroy(net_[k]);
-    }
-  }
-  void set_graph(int n, uintptr_t exec) {
-    if (n < 1 || n > B_) throw std::invalid_argument("batch size");
-    exec_[n] = (hipGraphExec_t)exec;
-  }
-  int max_batch() const { return B_; }
-  // launches per batch size so far (tests / bench report)
-  std::vector<long> sizes() {
-    std::lock_guard<std::mutex> lk(mu_);
-    return sizes_;
-  }
-
-  // true when no network (batched or a solo frame's) is in flight
-  bool idle() {
-    std::lock_guard<std::mutex> lk(mu_);
-    prune_locked();
-    return inflight_.empty() && !forming_;
-  }
-  // a solo frame's network was launched; `ev` (recorded after it on the frame's stream) marks its end
-  void note_solo(hipEvent_t ev) {
-    std::lock_guard<std::mutex> lk(mu_);
-    inflight_.push_back(ev);
-    sizes_[0] += 1;
-  }
-  // the calling frame's colour stage is enqueued (`ecol` recorded after it); returns the event of the
-  // network launch that includes the frame (its geometry waits for it). Blocks until that launch.
-  hipEvent_t join(hipEvent_t ecol, void* input, void* mask) {
-    std::unique_lock<std::mutex> lk(mu_);
-    if (!forming_) {
-      forming_ = std::make_shared<Batch>();
-    }
-    std::shared_ptr<Batch> b = forming_;
-    const int slot = b->n++;
-    b->ecol[slot] = ecol;
-    b->in[slot] = (uint64_t)input;
-    b->out[slot] = (uint64_t)mask;
-    for (;;) {
-      if (b->launched) return b->ev;
-      prune_locked();
-      if (b->n == B_ || inflight_.size() < 2) {
-        launch_locked(*b);
-        return b->ev;
-      }
-      lk.unlock();
-      std::this_thread::sleep_for(std::chrono::microseconds(10));
-      lk.lock();
-    }
-  }
-
- private:
-  static constexpr int kRing = 32;
-  static constexpr int kMaxB = 16;
-  struct Batch {
-    int n = 0;
-    bool launched = false;
-    hipEvent_t ev = nullptr;
-    hipEvent_t ecol[kMaxB];
-    uint64_t in[kMaxB], out[kMaxB];
-  };
-  void prune_locked() {
-    while (!inflight_.empty() && hipEventQuery(inflight_.front()) == hipSuccess) inflight_.pop_front();
-  }
-  void launch_locked(Batch& b) {
-    DeviceScope g(dev_);
-    if (!exec_[b.n]) throw std::runtime_error("BatchNet: no graph for batch size " + std::to_string(b.n));
-    const int k = (int)(launches_++ % kRing);
-    hip_check(hipEventSynchronize(tcopy_[k]), "hipEventSynchronize");  // ring slot's last copy is done
-    uint64_t* t = h_table_[k];
-    t[0] = (uint64_t)b.n;
-    for (int i = 0; i < B_; ++i) {
-      t[1 + i] = i < b.n ? b.in[i] : 0;
-      t[1 + B_ + i] = i < b.n ? b.out[i] : 0;
-    }
-    hip_check(hipMemcpyAsync(d_table_, t, (1 + 2 * B_) * sizeof(uint64_t), hipMemcpyHostToDevice, ns_), "H2D table");
-    hip_check(hipEventRecord(tcopy_[k], ns_), "hipEventRecord");
-    for (int i = 0; i < b.n; ++i) hip_check(hipStreamWaitEvent(ns_, b.ecol[i], 0), "hipStreamWaitEvent");
-    hip_check(hipGraphLaunch(exec_[b.n], ns_), "hipGraphLaunch");
-    hip_check(hipEventRecord(net_[k], ns_), "hipEventRecord");
-    b.ev = net_[k];
-    b.launched = true;
-    inflight_.push_back(net_[k]);
-    sizes_[b.n] += 1;
-    forming_.reset();
-  }
-
-  int dev_;
-  hipStream_t ns_;
-  int B_;
-  uint64_t* d_table_;
-  uint64_t* h_table_[kRing] = {};
-  hipEvent_t tcopy_[kRing] = {}, net_[kRing] = {};
-  std::vector<hipGraphExec_t> exec_;
-  std::vector<long> sizes_;  // [0] = solo frames, [n] = batched launches of n frames
-  std::deque<hipEvent_t> inflight_;
-  std::shared_ptr<Batch> forming_;
-  long launches_ = 0;
-  std::mutex mu_;
-};
-
 class FrameRunner {
  public:
   FrameRunner(int device, uintptr_t stream) : dev_(device), s_((hipStream_t)stream) {
@@ -213,30 +73,19 @@ class FrameRunner {
     // for it (a GPU-side dependency only: no system-scope fence)
     hip_check(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking), "hipStreamCreate");
     hip_check(hipEventCreateWithFlags(&evd_, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate");
-    hip_check(hipEventCreateWithFlags(&ecol_, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate");
-    hip_check(hipEventCreateWithFlags(&esolo_, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate");
   }
   ~FrameRunner() {
     (void)hipEventDestroy(ev0_);
     (void)hipEventDestroy(ev1_);
     (void)hipEventDestroy(evd_);
-    (void)hipEventDestroy(ecol_);
-    (void)hipEventDestroy(esolo_);
     (void)hipStreamDestroy(cs_);
     for (void* p : host_) (void)hipHostFree(p);
   }
   // graph execs, owned by the pipeline's torch CUDAGraphs (kept alive there): slots 0..2 = the network
-  // graph of colour source 0 BGR / 1 RGB / 2 JPEG coefficients, slot 3 = the geometry graph, slots 4..6 =
-  // the colour stage alone of source 0..2 (batched frames: the network runs in a BatchNet launch)
+  // graph of colour source 0 BGR / 1 RGB / 2 JPEG coefficients, slot 3 = the geometry graph
   void set_graph(int slot, uintptr_t exec) {
-    if (slot < 0 || slot > 6) throw std::invalid_argument("slot");
+    if (slot < 0 || slot > 3) throw std::invalid_argument("slot");
     exec_[slot] = (hipGraphExec_t)exec;
-  }
-  // batch this pipeline's frames with other streams' (input: its N = 1 network input, mask: its 256^2 mask)
-  void set_batch(BatchNet* b, uintptr_t input, uintptr_t mask) {
-    batch_ = b;
-    b_in_ = P(input);
-    b_mask_ = P(mask);
   }
   // Measured (same box, 2 rounds): the copy stream vs the depth H2D in order on the frame stream --
   // engine GPU p50 0.515-0.524 vs 0.536 ms, pipelined 3,025-3,105 vs 2,837-2,926 FPS, e2e 4 streams in
@@ -279,26 +128,7 @@ class FrameRunner {
     std::memcpy(h_color_, cp, color_bytes_);  // host staging: the caller's "submit" stage, not device time
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
     hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
-    launch_network(src);
-  }
-
-  // the network half of source `src` after its colour H2D: its own N = 1 network graph, or -- when
-  // another network is in flight -- the colour stage alone and a place in the next BatchNet launch
-  void launch_network(int src) {
-    if (batch_ && exec_[4 + src] && !batch_->idle()) {
-      hip_check(hipGraphLaunch(exec_[4 + src], s_), "hipGraphLaunch");
-      hip_check(hipEventRecord(ecol_, s_), "hipEventRecord");
-      hipEvent_t net = batch_->join(ecol_, b_in_, b_mask_);
-      hip_check(hipStreamWaitEvent(s_, net, 0), "hipStreamWaitEvent");
-      batched_ = true;
-      return;
-    }
     hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
-    batched_ = false;
-    if (batch_) {
-      hip_check(hipEventRecord(esolo_, s_), "hipEventRecord");
-      batch_->note_solo(esolo_);
-    }
   }
 
   // colour half, from an entropy-decoded JPEG (data/jpeg.py JpegCoefs: pinned meta + coefficient
@@ -311,7 +141,7 @@ class FrameRunner {
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
     hip_check(hipMemcpyAsync(d_meta_, P(meta), meta_bytes, hipMemcpyHostToDevice, s_), "H2D meta");
     hip_check(hipMemcpyAsync(d_coef_, P(coefs), coef_bytes, hipMemcpyHostToDevice, s_), "H2D coefs");
-    launch_network(2);
+    hip_check(hipGraphLaunch(exec_[2], s_), "hipGraphLaunch");
   }
 
   // depth half (HxW 16-bit): H2D, the geometry graph, the result read-back and the frame's end event
@@ -419,7 +249,7 @@ class FrameRunner {
         hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
         hip_check(hipMemcpyAsync(d_meta_, h_meta_, meta_bytes_, hipMemcpyHostToDevice, s_), "H2D meta");
         hip_check(hipMemcpyAsync(d_coef_, h_coef_, (size_t)nco * 2, hipMemcpyHostToDevice, s_), "H2D coefs");
-        launch_network(2);
+        hip_check(hipGraphLaunch(exec_[2], s_), "hipGraphLaunch");
       } else {  // depth: 16-bit PNG straight into the pinned staging buffer
         if (rdp_png_decode(d, dn, (uint8_t*)h_depth_, (long)depth_bytes_, 1) != 0) rc[1] = kCorrupt;
       }
@@ -463,8 +293,6 @@ class FrameRunner {
     hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
   }
 
-  bool last_batched() const { return batched_; }
-
   // block until the frame's results are on the host; returns its device time (ms, event to event)
   float wait() {
     if (!recorded_) return 0.f;  // nothing submitted yet
@@ -493,10 +321,6 @@ class FrameRunner {
 
   bool recorded_ = false;
   bool depth_stream_ = true;
-  bool batched_ = false;  // the last frame's network ran in a BatchNet launch
-  BatchNet* batch_ = nullptr;
-  void *b_in_ = nullptr, *b_mask_ = nullptr;
-  hipEvent_t ecol_ = nullptr, esolo_ = nullptr;
   int H_ = 0, W_ = 0, ns_ = 0;
   void *h_meta_ = nullptr, *h_coef_ = nullptr;
   std::chrono::steady_clock::time_point t0_;
@@ -505,7 +329,7 @@ class FrameRunner {
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr, evd_ = nullptr;
   hipStream_t cs_ = nullptr;
   std::vector<void*> host_;
-  hipGraphExec_t exec_[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipGraphExec_t exec_[4] = {nullptr, nullptr, nullptr, nullptr};
   void *d_color_ = nullptr, *h_color_ = nullptr, *d_depth_ = nullptr, *h_depth_ = nullptr;
   void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
   void *d_res_ = nullptr, *h_res_ = nullptr;
@@ -606,22 +430,9 @@ std::string encode_wire(double mean, double maxc, const double* pts, size_t npts
 }  // namespace
 
 void register_serve_runtime(py::module_& m) {
-  py::class_<BatchNet>(m, "BatchNet")
-      .def(py::init<int, uintptr_t, int, uintptr_t>(), py::arg("device"), py::arg("stream"), py::arg("max_batch"),
-           py::arg("table"))
-      .def("set_graph", &BatchNet::set_graph)
-      .def("max_batch", &BatchNet::max_batch)
-      .def("sizes", &BatchNet::sizes, "[solo frames, launches of 1 frame, of 2, ...]")
-      .def("idle", [](BatchNet& b) {
-        py::gil_scoped_release nogil;
-        return b.idle();
-      });
   py::class_<FrameRunner>(m, "FrameRunner")
       .def(py::init<int, uintptr_t>(), py::arg("device"), py::arg("stream"))
       .def("set_graph", &FrameRunner::set_graph)
-      .def("set_batch", &FrameRunner::set_batch, py::arg("batch"), py::arg("input"), py::arg("mask"),
-           py::keep_alive<1, 2>())
-      .def("last_batched", &FrameRunner::last_batched)
       .def("set_buffers", &FrameRunner::set_buffers)
       .def("alloc_host", &FrameRunner::alloc_host)
       .def("set_depth_stream", [](FrameRunner& r, bool on) { r.depth_stream(on); },

@@ -88,9 +88,6 @@ class ServeConfig:
     graph: bool = True
     devices: str = ""  # comma-separated GPU indices for per-GPU replicas ("" = current device only; "all")
     replicas_per_device: int = 2  # independent stream pipelines (hipGraph + buffers) per GPU
-    # frames of concurrent streams that would queue for the GPU run as one network launch of up to this
-    # many frames (serve/engine.py BatchEngine); 1 = every frame its own N = 1 network
-    max_batch: int = 4
     frame_errors: str = "degrade"  # "degrade": bad frame -> error status, stream goes on; "abort": reference
     gpu_jpeg: bool = True  # baseline JPEGs: native entropy decode on the host, pixel stage in the frame graph
     workers: int = 1  # server processes sharing the port (SO_REUSEPORT): one interpreter lock each

@@ -121,8 +121,7 @@ class FramePipeline:
 
     def __init__(self, model, K: np.ndarray, depth_scale: float, H: int = 480, W: int = 640, size: int = 256,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 device: Optional[torch.device] = None, rgb: bool = False, jpeg: bool = False,
-                 batch: Optional["BatchEngine"] = None):
+                 device: Optional[torch.device] = None, rgb: bool = False, jpeg: bool = False):
         from ..models.unet import UNetNative
         if not isinstance(model, UNetNative):
             raise TypeError("FramePipeline needs the native UNet (UNetNative); use CpuFramePipeline otherwise")
@@ -132,9 +131,9 @@ class FramePipeline:
         # everything below (buffers, stream, graph capture) belongs to the model's GPU, whatever device
         # the calling thread has current
         with torch.cuda.device(dev):
-            self._init(model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb, jpeg, batch)
+            self._init(model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb, jpeg)
 
-    def _init(self, model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb, jpeg, batch):
+    def _init(self, model, K, depth_scale, H, W, size, threshold, graph, geo_cfg, dev, rgb, jpeg):
         from ..models.unet import UNetExecutor
         from ..ops import native
         self.C = native()
@@ -193,11 +192,6 @@ class FramePipeline:
                           self.mask.data_ptr(), self.h_mask.data_ptr(), 0,
                           self.geo.res.data_ptr(), self.h_res.data_ptr(), 0)
             self.runner = r
-        # frames of concurrent streams that would queue for the GPU share one network launch (BatchEngine):
-        # this pipeline's colour stage alone is captured too, and its input / mask are the batch members'
-        self.batch = batch if (batch is not None and self.runner is not None and batch.size == size) else None
-        if self.batch is not None:
-            self.runner.set_batch(self.batch.native, self.ex.x_in.data_ptr(), self.m256.data_ptr())
         # the graphs for the sources this pipeline will be fed (the gRPC server: JPEG coefficients, or
         # RGB arrays for streams the native decoder does not take) are captured here, at build time --
         # for the configured frame size when the server starts; a pipeline for another frame size is
@@ -232,14 +226,6 @@ class FramePipeline:
         ex.forward(head=False, refresh_eval=False,
                    mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
                               self.thr_logit, self.m256))
-
-    def _color_program(self, src: int = 0):
-        """The colour stage alone (JPEG pixel stage, preprocess into this pipeline's network input): a
-        batched frame's network runs in its BatchEngine launch."""
-        C, ex = self.C, self.ex
-        if src == SRC_JPEG:
-            C.jpeg_to_rgb(self.d_coef, self.d_meta[:32], self.d_meta[32:], self.d_planes, self.d_color)
-        C.preprocess(self.d_color, *self.tab, ex.x_in, int(src != SRC_BGR))
 
     def _geo_program(self):
         zc = self.zero_copy
@@ -280,15 +266,12 @@ class FramePipeline:
                 program()
         self.graphs[key] = g
         if self.runner is not None:
-            slot = GEO_SLOT if key == GEO else (4 + key[1] if isinstance(key, tuple) else key)
-            self.runner.set_graph(slot, g.raw_cuda_graph_exec())
+            self.runner.set_graph(GEO_SLOT if key == GEO else key, g.raw_cuda_graph_exec())
 
     def _capture(self, src: int):
         if not self.graphs:
             self.refresh_weights()
         self._capture_one(src, lambda: self._net_program(src))
-        if self.batch is not None:
-            self._capture_one(("color", src), lambda: self._color_program(src))
         if GEO not in self.graphs:
             self._capture_one(GEO, self._geo_program)
 
@@ -511,71 +494,6 @@ def replicate_model(model, device: torch.device):
     return copy.deepcopy(model).to(device).eval()
 
 
-class BatchEngine:
-    """One replica's batched network for frames of concurrent streams (``csrc/serve_runtime.cpp`` BatchNet).
-
-    At N = 1 the network is latency-bound: 0.38 ms per launch on one MI355X, vs 0.48 ms for 2 frames and
-    0.70 ms for 4 (``scripts/serve_batch_probe.py``). A frame that finds a network already in flight does
-    not start a second one beside it: its colour stage writes its pipeline's own input, and the frames
-    gathered meanwhile run as ONE launch of this engine's network graph for their count N (gather inputs
-    -> U-Net with BN folded -> fused head + threshold -> scatter masks), on this engine's stream. A frame
-    that finds the GPU free runs its pipeline's own N = 1 graph as before, so one stream's latency is
-    unchanged. Weights are the replica's (shared, updated in place on hot reload; ``refresh_weights``
-    recomputes the BN-fold coefficients of every batch size)."""
-
-    def __init__(self, model, device: torch.device, size: int = 256, threshold: float = 0.5, max_batch: int = 4):
-        from ..models.unet import UNetExecutor
-        from ..ops import native
-        self.C = C = native()
-        self.model, self.dev, self.size, self.B = model, device, size, int(max_batch)
-        self.thr_logit = _logit(threshold)
-        with torch.cuda.device(device):
-            self.stream = torch.cuda.Stream(device)
-            self.table = torch.zeros(1 + 2 * self.B, dtype=torch.int64, device=device)
-            self.ex = {n: UNetExecutor(model, n, size, size, False, "bce", 1.0) for n in range(1, self.B + 1)}
-            self.masks = {n: torch.empty(n * size * size, dtype=torch.uint8, device=device) for n in self.ex}
-            self.native = C.BatchNet(device.index, self.stream.cuda_stream, self.B, self.table.data_ptr())
-            self.graphs = {}
-            self.refresh_weights()
-            for n in self.ex:
-                self._capture(n)
-
-    def _program(self, n: int):
-        C, ex, m = self.C, self.ex[n], self.model
-        C.batch_gather(self.table, self.B, ex.x_in)
-        ex.forward(head=False, refresh_eval=False,
-                   mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
-                              self.thr_logit, self.masks[n]))
-        C.batch_scatter(self.table, self.B, self.masks[n], n)
-
-    def _capture(self, n: int):
-        with torch.cuda.device(self.dev):
-            # warm-up with a table of n valid members that point at this engine's own buffers
-            x = self.ex[n].x_in
-            per = x[0].numel() * x.element_size()
-            t = [n] + [x.data_ptr() + i * per for i in range(n)] + [0] * (self.B - n) \
-                + [self.masks[n].data_ptr() + i * self.size * self.size for i in range(n)] + [0] * (self.B - n)
-            with torch.cuda.stream(self.stream):
-                self.table.copy_(torch.tensor(t, dtype=torch.int64))
-                self._program(n)
-            self.stream.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
-                self._program(n)
-        self.graphs[n] = g
-        self.native.set_graph(n, g.raw_cuda_graph_exec())
-
-    def refresh_weights(self):
-        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
-            for ex in self.ex.values():
-                ex.prepare_eval()
-        self.stream.synchronize()
-
-    def sizes(self) -> list:
-        """[frames that ran their own N = 1 network, launches of 1 frame, of 2 frames, ...]"""
-        return list(self.native.sizes())
-
-
 class EnginePool:
     """Per-frame pipelines for the server's streams, with one model replica per GPU.
 
@@ -595,8 +513,7 @@ class EnginePool:
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 devices=None, rgb: bool = False, jpeg: bool = False, max_sizes: int = 3,
-                 max_batch: Optional[int] = None):
+                 devices=None, rgb: bool = False, jpeg: bool = False, max_sizes: int = 3):
         self.model = model
         self.home_size = (H, W)
         self.max_sizes = max(0, max_sizes)
@@ -611,14 +528,6 @@ class EnginePool:
         self.devices = devs
         self.replicas = [model if devs[i] == home and i == 0 else replicate_model(model, devs[i])
                          for i in range(len(devs))]
-        # cross-stream batching of the network (BatchEngine): one per replica, for GPU graph pipelines
-        # that more than one stream may feed (RDP_SERVE_MAX_BATCH: max frames per launch, 1 = off)
-        if max_batch is None:
-            max_batch = int(os.environ.get("RDP_SERVE_MAX_BATCH", "4"))
-        self.batches = [None] * len(self.replicas)
-        if self.gpu and graph and max_batch > 1 and self.n > 1:
-            self.batches = [BatchEngine(m, d, size=size, threshold=threshold, max_batch=max_batch)
-                            for m, d in zip(self.replicas, devs)]
         self._pools: "collections.OrderedDict" = collections.OrderedDict()  # (r, H, W) -> Queue, LRU order
         self._mk_lock = threading.Lock()
         self._rr = 0
@@ -630,7 +539,7 @@ class EnginePool:
         m = self.replicas[r]
         if self.gpu:
             return FramePipeline(m, H=H, W=W, graph=self.graph, device=self.devices[r], rgb=self.rgb,
-                                 jpeg=self.jpeg, batch=self.batches[r], **self.args)
+                                 jpeg=self.jpeg, **self.args)
         return CpuFramePipeline(m, H=H, W=W, **self.args)
 
     def _get(self, r: int, H, W) -> "queue.Queue":
@@ -684,17 +593,11 @@ class EnginePool:
                 if hasattr(m, "refresh_weights"):
                     m.refresh_weights()
 
-    def refresh_weights(self, pipelines):
+    @staticmethod
+    def refresh_weights(pipelines):
         """After the shared weights changed (inside ``exclusive()``): refresh derived state."""
         for p in pipelines:
             p.refresh_weights()
-        for b in self.batches:
-            if b is not None:
-                b.refresh_weights()
-
-    def batch_sizes(self) -> list:
-        """Per replica: [solo frames, batched launches of 1, 2, ... frames] (None without batching)."""
-        return [b.sizes() if b is not None else None for b in self.batches]
 
     def process(self, color_bgr: np.ndarray, depth: np.ndarray) -> FrameResult:
         """One frame, synchronously, on the next replica."""

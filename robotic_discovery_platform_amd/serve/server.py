@@ -480,7 +480,7 @@ def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_s
     metrics = MetricsLog(cfg.metrics_log)
     engine = EnginePool(model, K, ds, n=pool_size or cfg.replicas_per_device, threshold=cfg.mask_threshold,
                         graph=cfg.graph, size=cfg.model_img_size, devices=devices, rgb=True,
-                        jpeg=cfg.gpu_jpeg and _is_native(model), max_batch=cfg.max_batch)
+                        jpeg=cfg.gpu_jpeg and _is_native(model))
     service = VisionAnalysisService(engine, metrics, frame_errors=cfg.frame_errors, faults=faults)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.max_workers))
     pb.add_VisionAnalysisServiceServicer_to_server(service, server)
