@@ -328,6 +328,8 @@ def main():
         out.update(extra)
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
+        from robotic_discovery_platform_amd.parallel.watchdog import close_all
+        close_all()  # the comm watchdog polls communicators of the groups destroyed next
         dist.destroy_process_group()
     return bool(serve) and rank == 0
 

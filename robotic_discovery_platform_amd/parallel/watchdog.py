@@ -32,6 +32,15 @@ from typing import Callable, Deque, Optional, Tuple
 
 EXIT_CODE = 75  # distinct from a crash (1) / injected fault (17) in merged launcher logs
 
+_LIVE: "list[CommWatchdog]" = []
+
+
+def close_all() -> None:
+    """Stop every watchdog of this process: call before destroying the process groups whose
+    communicators they poll (utils/launch.py shutdown_distributed, bench.py)."""
+    while _LIVE:
+        _LIVE.pop().close()
+
 
 def _default_fail(msg: str) -> None:
     sys.stderr.write(msg + "\n")
@@ -57,6 +66,7 @@ class CommWatchdog:
         self.failed: Optional[str] = None
         self._thread = threading.Thread(target=self._run, name="rdp-comm-watchdog", daemon=True)
         self._thread.start()
+        _LIVE.append(self)
 
     def arm(self, event) -> None:
         """Watch ``event`` (anything with ``query() -> bool``: done). Called once per step from the
@@ -74,7 +84,11 @@ class CommWatchdog:
     def close(self) -> None:
         self._stop.set()
         self._wake.set()
+        with self._lock:  # a poll in progress finishes before the caller may free the communicator
+            pass
         self._thread.join(timeout=5.0)
+        if self in _LIVE:
+            _LIVE.remove(self)
 
     def _fail(self, why: str) -> None:
         self.failed = why
@@ -91,12 +105,14 @@ class CommWatchdog:
         if self.failed is not None:
             return False
         with self._lock:
+            if self._stop.is_set():
+                return True
             while self._armed and self._armed[0][1].query():
                 self._armed.popleft()
             oldest = self._armed[0] if self._armed else None
-        if oldest is None:
-            return True
-        code, text = self.poll()
+            if oldest is None:
+                return True
+            code, text = self.poll()  # under the lock: close() waits for a poll in progress
         if code:
             self._fail(f"collective failed with RCCL error {code}: {text}")
             return False

@@ -58,6 +58,8 @@ def _free_port() -> int:
 
 
 def shutdown_distributed() -> None:
+    from ..parallel.watchdog import close_all
+    close_all()  # they poll communicators of the groups destroyed here
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
 
