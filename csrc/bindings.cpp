@@ -81,7 +81,8 @@ int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float
              int, hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_comm_emulate(double, int, hipStream_t);
-int rdp_rows_fold(float*, int, int, hipStream_t);
+int rdp_rows_fold(const float*, int, int, double*, hipStream_t);
+int rdp_rows_hilo(const double*, float*, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
 int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
@@ -394,8 +395,11 @@ long rccl_check(int r, void* comm) {
 void comm_all_reduce(torch::Tensor buf, long comm) {
   TORCH_CHECK(g_rccl.all_reduce != nullptr, "comm_all_reduce: call comm_bind() first");
   TORCH_CHECK(buf.is_cuda() && buf.is_contiguous(), "comm_all_reduce: contiguous device tensor");
-  const int dt = buf.scalar_type() == torch::kFloat ? 7 : buf.scalar_type() == torch::kBFloat16 ? 9 : -1;
-  TORCH_CHECK(dt >= 0 && comm != 0, "comm_all_reduce: fp32 / bf16 buffer and a communicator");
+  const int dt = buf.scalar_type() == torch::kFloat      ? 7
+                 : buf.scalar_type() == torch::kBFloat16 ? 9
+                 : buf.scalar_type() == torch::kDouble   ? 8
+                                                         : -1;
+  TORCH_CHECK(dt >= 0 && comm != 0, "comm_all_reduce: fp32 / bf16 / fp64 buffer and a communicator");
   void* const p = buf.data_ptr();
   const size_t n = (size_t)buf.numel();
   void* const c = (void*)comm;
@@ -403,12 +407,26 @@ void comm_all_reduce(torch::Tensor buf, long comm) {
   RDP_PLAN(rccl_check(fn(p, p, n, dt, /*ncclSum*/ 0, c, st), c));
 }
 
-// SyncBN: fold buf's [rows][width] fp32 partial rows into row 0 (fp64 sums), recorded in plans
-void rows_fold(torch::Tensor buf, int rows, int width) {
+// SyncBN: fold buf's [rows][width] fp32 partial rows into `out` (width fp64 sums) / write fp64 sums back as
+// hi + lo fp32 rows; both recorded in plans
+void rows_fold(torch::Tensor buf, int rows, int width, torch::Tensor out) {
   TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == torch::kFloat && buf.is_contiguous() &&
               (long)rows * width <= buf.numel() && rows >= 1 && width >= 1, "rows_fold: fp32 buffer of rows x width");
-  float* p = buf.data_ptr<float>();
-  RDP_PLAN(rdp_rows_fold(p, rows, width, st));
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kDouble && out.is_contiguous() && out.numel() >= width,
+              "rows_fold: fp64 out");
+  const float* p = buf.data_ptr<float>();
+  double* o = out.data_ptr<double>();
+  RDP_PLAN(rdp_rows_fold(p, rows, width, o, st));
+}
+
+void rows_hilo(torch::Tensor in, torch::Tensor buf, int width) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == torch::kDouble && in.is_contiguous() && in.numel() >= width,
+              "rows_hilo: fp64 sums");
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == torch::kFloat && buf.is_contiguous() && buf.numel() >= 2l * width,
+              "rows_hilo: fp32 buffer of 2 rows");
+  const double* i = in.data_ptr<double>();
+  float* b = buf.data_ptr<float>();
+  RDP_PLAN(rdp_rows_hilo(i, b, width, st));
 }
 
 // ncclCommGetAsyncError of `comm` (0 = healthy) and its message: polled by the host watchdog
@@ -1396,7 +1414,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_bind", &comm_bind, "resolve RCCL from the library torch loaded; returns its path");
   m.def("comm_all_reduce", on_device(&comm_all_reduce), py::arg("buf"), py::arg("comm"),
         "in-place SUM all-reduce over an RCCL communicator on the current stream (recorded in plans)");
-  m.def("rows_fold", on_device(&rows_fold), py::arg("buf"), py::arg("rows"), py::arg("width"));
+  m.def("rows_fold", on_device(&rows_fold), py::arg("buf"), py::arg("rows"), py::arg("width"), py::arg("out"));
+  m.def("rows_hilo", on_device(&rows_hilo), py::arg("sums"), py::arg("buf"), py::arg("width"));
   m.def("comm_async_error", &comm_async_error, py::arg("comm"), "(code, message) of ncclCommGetAsyncError");
   m.def("comm_abort", &comm_abort, py::arg("comm"), "ncclCommAbort");
   m.def("comm_emulate", &comm_emulate, py::arg("us"), py::arg("blocks"),

@@ -35,10 +35,11 @@ __global__ void colsum_kernel(const float* __restrict__ in, int T, int K, int rp
   if (ty == 0 && col < K) out[(size_t)blockIdx.y * K + col] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
-// SyncBatchNorm: fold a layer's [T][K] partial rows into row 0 in place (fp64 sums), so one K-float
-// all-reduce per layer carries the rank's sums (models/unet.py _sync_rows). 64 columns x 16 row groups per
-// block, 4 loads in flight per thread (one thread per column walked T rows serially: ~150 us per fold).
-__global__ __launch_bounds__(1024) void rows_fold_kernel(float* __restrict__ buf, int T, int K) {
+// SyncBatchNorm: fold a layer's [T][K] partial rows into K fp64 sums, so one fp64 all-reduce per layer
+// carries the rank's statistics (models/unet.py _sync_rows). 64 columns x 16 row groups per block, 4
+// loads in flight per thread (one thread per column walked T rows serially: ~150 us per fold).
+__global__ __launch_bounds__(1024) void rows_fold_kernel(const float* __restrict__ buf, int T, int K,
+                                                         double* __restrict__ out) {
   __shared__ double red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + tx;
@@ -54,12 +55,24 @@ __global__ __launch_bounds__(1024) void rows_fold_kernel(float* __restrict__ buf
     for (; r < T; r += 16) a0 += (double)buf[(size_t)r * K + col];
   }
   red[ty][tx] = (a0 + a1) + (a2 + a3);
-  __syncthreads();  // every read of this block's columns is done before row 0 is overwritten
+  __syncthreads();
   if (ty == 0 && col < K) {
     double t = 0.0;
     for (int g = 0; g < 16; ++g) t += red[g][tx];
-    buf[col] = (float)t;
+    out[col] = t;
   }
+}
+
+// the (all-reduced) fp64 sums back as TWO fp32 rows, hi = fp32(sum) and lo = fp32(sum - hi), which the
+// finalize kernels add in fp64: the statistics keep ~48 bits instead of fp32's 24 -- E[x^2] - mean^2
+// cancels, and one fp32 rounding of the sums moved a small U-Net's bf16 gradients by tens of percent
+__global__ void rows_hilo_kernel(const double* __restrict__ in, float* __restrict__ buf, int K) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= K) return;
+  const double v = in[col];
+  const float hi = (float)v;
+  buf[col] = hi;
+  buf[K + col] = (float)(v - (double)hi);
 }
 
 #define FIN_DIRECT_ROWS 2048
@@ -377,9 +390,15 @@ int rdp_bn_finalize(const float* stats, int T, int C, long count, const float* g
   return 0;
 }
 
-int rdp_rows_fold(float* buf, int T, int K, hipStream_t s) {
+int rdp_rows_fold(const float* buf, int T, int K, double* out, hipStream_t s) {
   if (T < 1 || K < 1) return -1;
-  hipLaunchKernelGGL(rows_fold_kernel, dim3((K + 63) / 64), dim3(1024), 0, s, buf, T, K);
+  hipLaunchKernelGGL(rows_fold_kernel, dim3((K + 63) / 64), dim3(1024), 0, s, buf, T, K, out);
+  return 0;
+}
+
+int rdp_rows_hilo(const double* in, float* buf, int K, hipStream_t s) {
+  if (K < 1) return -1;
+  hipLaunchKernelGGL(rows_hilo_kernel, dim3((K + 255) / 256), dim3(256), 0, s, in, buf, K);
   return 0;
 }
 

@@ -877,6 +877,8 @@ class UNetExecutor:
                 from ..parallel.ddp import emulate_spec, native_comm_group
                 self.sync_comm = native_comm_group(self.dev, "syncbn")[1]
                 self.sync_emulate = emulate_spec()
+            self.sync_ws64 = torch.zeros(2 * max(L.spec.cout for L in self.layers), dtype=torch.float64,
+                                         device=self.dev)
             shp = torch.tensor([self.N, self.H, self.W], dtype=torch.int64)
             if dist.get_backend(group) != "gloo":
                 shp = shp.to(self.dev)
@@ -902,23 +904,31 @@ class UNetExecutor:
         sync group and return (1, global pixel count at spatial size ``hw``): the row count the
         finalize kernels then read and the pixels the reduced sums cover."""
         import torch.distributed as dist
+        # the global sums travel in fp64 and come back as two fp32 rows (hi, lo) that the finalize kernels
+        # add in fp64 (one fp32 rounding of the sums is enough to move small layers' bf16 gradients by tens
+        # of percent through E[x^2] - mean^2)
+        ws = self.sync_ws64
         if getattr(self, "sync_comm", None) is not None:  # native: fold kernel + ncclAllReduce on this stream
             C = _native()
-            C.rows_fold(buf, rows, 2 * c)
+            C.rows_fold(buf, rows, 2 * c, ws)
             emu = getattr(self, "sync_emulate", None)
             if emu is not None:  # RDP_DDP_EMULATE: the modelled collective instead (one-GPU A/B)
                 from ..parallel.ddp import ring_allreduce_us
                 n, bw, blocks, alpha = emu
-                C.comm_emulate(ring_allreduce_us(8 * c, n, bw, alpha), 1)
+                C.comm_emulate(ring_allreduce_us(16 * c, n, bw, alpha), 1)
             else:
-                C.comm_all_reduce(buf[: 2 * c], self.sync_comm)
-            return 1, self._sync_m[hw]
+                C.comm_all_reduce(ws[: 2 * c], self.sync_comm)
+            C.rows_hilo(ws, buf, 2 * c)
+            return 2, self._sync_m[hw]
         tot = buf[: rows * 2 * c].view(rows, 2 * c).sum(0, dtype=torch.float64)
         if dist.get_backend(self.sync_group) == "gloo":  # host round trip (gloo tests: ranks share a GPU)
             tot = tot.cpu()
         dist.all_reduce(tot, group=self.sync_group)
-        buf[: 2 * c].copy_(tot)
-        return 1, self._sync_m[hw]
+        tot = tot.to(buf.device)
+        hi = tot.float()
+        buf[: 2 * c].copy_(hi)
+        buf[2 * c: 4 * c].copy_((tot - hi.double()).float())
+        return 2, self._sync_m[hw]
 
     def _on_wgrad_stream(self, fn):
         """Run ``fn(slab)`` (a weight gradient) on the side stream with its slab. (Several side streams,
