@@ -154,7 +154,8 @@ def _syncbn_rows_worker(rank, world):
     from robotic_discovery_platform_amd.models.unet import UNetExecutor
     C, T = 8, 5
     # set_sync_bn: rank r runs batch r + 1 (unequal), 8x8 input, two levels
-    ex = SimpleNamespace(m=SimpleNamespace(), N=rank + 1, H=8, W=8, sizes=[(8, 8), (4, 4)], dev="cpu")
+    ex = SimpleNamespace(m=SimpleNamespace(), N=rank + 1, H=8, W=8, sizes=[(8, 8), (4, 4)], dev="cpu",
+                         layers=[SimpleNamespace(spec=SimpleNamespace(cout=C))])
     UNetExecutor.set_sync_bn(ex)
     assert ex.sync_world == world and ex.sync_group is not None
     nsum = sum(r + 1 for r in range(world))
@@ -165,9 +166,11 @@ def _syncbn_rows_worker(rank, world):
     buf = torch.zeros(64 * 2 * C)
     rows = torch.arange(T * 2 * C, dtype=torch.float32).view(T, 2 * C) * (rank + 1)
     buf[: T * 2 * C] = rows.reshape(-1)
-    assert UNetExecutor._sync_rows(ex, buf, T, C, (4, 4)) == (1, 16 * nsum)
-    exp = rows.sum(0) / (rank + 1) * nsum
-    assert torch.equal(buf[: 2 * C], exp)
+    # the global fp64 sums come back as two rows, hi + lo (the finalize kernels add them in fp64)
+    assert UNetExecutor._sync_rows(ex, buf, T, C, (4, 4)) == (2, 16 * nsum)
+    exp = rows.double().sum(0) / (rank + 1) * nsum
+    got = buf[: 2 * C].double() + buf[2 * C: 4 * C].double()
+    assert torch.equal(got, exp)
     UNetExecutor.set_sync_bn(ex, enabled=False)
     assert ex.sync_world == 1 and ex.sync_group is None
 
