@@ -316,7 +316,8 @@ def main():
                 "impl": args.impl,
                 "optimizer": "Adam(lr=1e-4)",
                 "loss": args.loss,
-                "sync_bn": bool(args.sync_bn) and world > 1 and args.impl == "native",
+                # statistics actually shared (world > 1, or the emulated collective of RDP_DDP_EMULATE)
+                "sync_bn": bool(getattr(getattr(tr, "ex", None), "_sync_on", False)),
                 "hipgraph": used_graph,
                 "grad_comm": args.grad_comm if (world > 1 or args.ddp_force) else None,
                 "ddp_stream": getattr(tr, "ddp_stream", None),
