@@ -836,6 +836,21 @@ extern "C" int rdp_conv_ring_pool(const void* x, long xbytes, int C, int pitch, 
                                   const float* escale, const float* eshift, int erelu, void* pool, int ppitch,
                                   hipStream_t s);
 extern "C" int rdp_conv_halo_tiles(int N, int H, int W, int C1, int C2, int Cout, int taps, int packed);
+extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
+                                int pitch2, const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, int N,
+                                int H, int W, int Cout, const float* escale, const float* eshift, int erelu, void* pool,
+                                long pbytes, int ppitch, hipStream_t s);
+
+// Eval convs on small maps run on the row-band kernel (csrc/conv_rowband.hip) where it takes the shape:
+// RDP_ROWBAND=0 turns the auto choice off (A/B); bm_pref 16 forces it.
+static bool rowband_auto(int N, int H, int W, int Cin, int Cout) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("RDP_ROWBAND");
+    on = e ? atoi(e) : 0;
+  }
+  return on != 0 && (long)N * H * W <= 4096 && W <= 64 && Cin >= 128 && Cout >= 64;
+}
 extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const void* x1, long xbytes1, int pitch1,
                               const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, float* stats,
                               int N, int H, int W, const float* escale, const float* eshift, int erelu, int max_blocks,
@@ -1145,6 +1160,23 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
       const int r = rdp_conv_first(x1, xbytes1, pitch1, w, wbytes, y1, ybytes1, ypitch1, stats, N, H, W, escale, eshift,
                                    erelu, s);
       if (r >= 0 || pref == 13) return r;
+    }
+  }
+  // eval (BN folded, one destination) on small maps: the row-band kernel, MaxPool2d fused (16 = force)
+  {
+    const int pref = bm_pref % 1000;
+    if (escale && eshift && !stats && !y2 && taps == 9 && !packed &&
+        (pref == 16 || (pref == 0 && rowband_auto(N, H, W, C1 + C2, Cout)))) {
+      const bool wp = pool && pooled && H % 2 == 0 && W % 2 == 0;
+      const long pbytes = wp ? ((long)N * (H / 2) * (W / 2) - 1) * ppitch * 2 + (long)Cout * 2 : 0;
+      const int r = rdp_conv_rowband(x1, x2, xbytes1, xbytes2, C1, C2, pitch1, pitch2, w, wbytes, ldw, y1, ybytes1,
+                                     ypitch1, N, H, W, Cout, escale, eshift, erelu, wp ? pool : nullptr, pbytes,
+                                     ppitch, s);
+      if (r >= 0) {
+        if (r == 1) *pooled = 1;
+        return 0;
+      }
+      if (pref == 16) return -1;
     }
   }
   // bm_pref % 1000: 0 = auto, 1 = force the halo-tile kernel, 6 = force the row-ring kernel,

@@ -1,0 +1,260 @@
+// Row-band convolution for small eval feature maps (serving at N = 1..4: the 64^2 .. 16^2 levels),
+// NHWC bf16, 3x3, BN folded into the epilogue + ReLU, optional fused MaxPool2d(2).
+//
+// Replaces, at these sizes, the implicit GEMM + split-K slab + reduce launch pair
+// (csrc/conv_igemm.hip) for the eval U-Net the reference serves
+// (/root/reference/services/vision_analysis/server.py:121-125 -> pkg/segmentation_model.py:31,34).
+//
+// Why a different structure: at N = 1 a deep conv has M = 256 .. 4096 pixels and K = 9 x 256 .. 9 x 1024.
+// The LDS-staged GEMM tile needs split-K to fill 256 CUs, then pays a per-K-step block barrier on a
+// two-deep DMA pipeline (~0.75 us per step at 1 block / CU), an fp32 slab round trip and a second
+// launch. Here a block owns R image rows x 32 output channels with the WHOLE K, split over its 8 waves
+// by input channel (wave w: channels [w Cin / 8, (w + 1) Cin / 8) of all 9 taps). Both MFMA operands are
+// read straight from global memory into registers -- a 16x16x32 bf16 fragment row is 8 consecutive
+// channels, i.e. 16 contiguous bytes of NHWC activations or OHWI weights -- so a wave issues its loads
+// G k-steps ahead with no barrier and no LDS until the end, where the 8 partial tiles are summed in LDS
+// (fixed wave order: deterministic) and the epilogue (scale, shift, ReLU, bf16, optional 2x2 max) writes
+// the rows. No slab, no second launch.
+//
+// Block -> tile: consecutive logical ids (one XCD after xcd_remap) are consecutive row bands of ONE
+// 32-channel output slice, so that slice's weights (32 x 9 Cin bf16) are fetched into that XCD's L2
+// once and re-read there by every band.
+#include "common.h"
+#include <stdlib.h>
+
+struct RowbandArgs {
+  const u16* x1;
+  const u16* x2;
+  uint32_t xbytes1, xbytes2;
+  int C1, C2, pitch1, pitch2;
+  const u16* w;
+  uint32_t wbytes;
+  int ldw;
+  u16* y;
+  uint32_t ybytes;
+  int ypitch;
+  u16* pool;  // MaxPool2d(2) of y, [N][H/2][W/2] (R == 2), or nullptr
+  uint32_t pbytes;
+  int ppitch;
+  const float* escale;
+  const float* eshift;
+  int erelu;
+  int N, H, W, Cout;
+  int wshift;  // log2(W)
+  int R;       // image rows per block
+  int bands;   // H / R
+  int cshift;  // log2(Cin / 32): k-step -> tap
+  int T;       // k-steps = 9 * Cin / 32
+};
+
+// tap (0..8) -> (dr, ds) without division
+RDP_DEV int rb_dr(int tap) { return ((tap * 11) >> 5) - 1; }
+RDP_DEV int rb_ds(int tap) { return tap - 3 * ((tap * 11) >> 5) - 1; }
+
+template <int NF, int NPG>
+struct RbFrag {
+  bf16x8 A[NF];   // weights: cout row (lane & 15) of fragment f, channels 8 (lane >> 4) .. +7
+  bf16x8 B[NPG];  // pixels: pixel (lane & 15) of group g, channels 8 (lane >> 4) .. +7
+};
+
+// NWV = 8: two blocks per CU (<= 128 VGPRs), 16: one block per CU with K split twice as finely
+template <int NF, int NPG, int G, int NWV>
+__global__ __launch_bounds__(NWV * 64, 4) void conv_rowband_kernel(const RowbandArgs a) {
+  constexpr int NC = NF * 16, PB = NPG * 16;
+  __shared__ f32x4 red[NWV][NF * NPG][64];
+  __shared__ uint2 ytile[PB][NC / 4];  // bf16 output tile for the fused pool
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = a.N * a.bands;
+  const int ct = (int)lid / nb, band = (int)lid - ct * nb;
+  const int img = band / a.bands, h0 = (band - img * a.bands) * a.R;
+  const int cout0 = ct * NC;
+
+  const auto rx1 = make_rsrc(a.x1, a.xbytes1);
+  const auto rx2 = make_rsrc(a.x2 ? a.x2 : a.x1, a.x2 ? a.xbytes2 : 0u);
+  const auto rw = make_rsrc(a.w, a.wbytes);
+
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  uint32_t wrow[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) wrow[f] = (uint32_t)((cout0 + 16 * f + lr) * a.ldw + lk) * 2u;
+  int ph[NPG], pw[NPG];
+#pragma unroll
+  for (int g = 0; g < NPG; ++g) {
+    const int p = 16 * g + lr;
+    ph[g] = h0 + (p >> a.wshift);
+    pw[g] = p & (a.W - 1);
+  }
+  const int ks0 = wave * a.T / NWV, ks1 = (wave + 1) * a.T / NWV;
+
+  typedef RbFrag<NF, NPG> Frag;
+  auto load = [&](int ks, Frag& fr) {
+    const bool live = ks < ks1;
+    const int tap = ks >> a.cshift;
+    const int cbase = (ks - (tap << a.cshift)) << 5;  // first channel of the k-step (wave-uniform)
+    const int dr = rb_dr(tap), ds = rb_ds(tap);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const uint32_t off = live ? wrow[f] + (uint32_t)ks * 64u : RDP_OOB;
+      fr.A[f] = __builtin_bit_cast(bf16x8, bload16(rw, off));
+    }
+    const bool s2 = cbase >= a.C1;
+    const int pitch = s2 ? a.pitch2 : a.pitch1;
+    const int ch = (s2 ? cbase - a.C1 : cbase) + lk;
+#pragma unroll
+    for (int g = 0; g < NPG; ++g) {
+      const int hh = ph[g] + dr, ww = pw[g] + ds;
+      const bool ok = live & inb(hh, a.H) & inb(ww, a.W);
+      const uint32_t off = ok ? (uint32_t)((((img * a.H + hh) << a.wshift) + ww) * pitch + ch) * 2u : RDP_OOB;
+      fr.B[g] = __builtin_bit_cast(bf16x8, bload16(s2 ? rx2 : rx1, off));
+    }
+  };
+
+  f32x4 acc[NF][NPG];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int g = 0; g < NPG; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto comp = [&](const Frag* fr) {
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int g = 0; g < NPG; ++g)
+          acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i].A[f], fr[i].B[g], acc[f][g], 0, 0, 0);
+  };
+  auto load_g = [&](int k, Frag* fr) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) load(k + i, fr[i]);
+  };
+
+  // two register buffers of G k-steps: the next group's loads are in flight while this one computes
+  Frag fa[G], fb[G];
+  int k = ks0;
+  if (k < ks1) {
+    load_g(k, fa);
+    while (true) {
+      if (k + G < ks1) load_g(k + G, fb);
+      comp(fa);
+      k += G;
+      if (k >= ks1) break;
+      if (k + G < ks1) load_g(k + G, fa);
+      comp(fb);
+      k += G;
+      if (k >= ks1) break;
+    }
+  }
+
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int g = 0; g < NPG; ++g) red[wave][f * NPG + g][lane] = acc[f][g];
+  __syncthreads();
+
+  const auto ry = make_rsrc(a.y, a.ybytes);
+  for (int u = threadIdx.x; u < NF * NPG * 64; u += NWV * 64) {
+    const int q = u >> 6, l = u & 63;
+    f32x4 v = red[0][q][l];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) v += red[w][q][l];
+    const int f = q / NPG, g = q - f * NPG;
+    const int cl = 16 * f + 4 * (l >> 4);  // first of this lane's 4 output channels (within the tile)
+    const int c = cout0 + cl;
+    const float4 sc = *(const float4*)(a.escale + c), sh = *(const float4*)(a.eshift + c);
+    float o[4] = {fmaf(v[0], sc.x, sh.x), fmaf(v[1], sc.y, sh.y), fmaf(v[2], sc.z, sh.z), fmaf(v[3], sc.w, sh.w)};
+    if (a.erelu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+    }
+    const uint2 pk = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+    const int p = 16 * g + (l & 15);
+    const int m = ((img * a.H + h0 + (p >> a.wshift)) << a.wshift) + (p & (a.W - 1));
+    bstore8(ry, (uint32_t)(m * a.ypitch + c) * 2u, pk);
+    if (a.pool) ytile[p][cl >> 2] = pk;
+  }
+  if (!a.pool) return;  // block-uniform
+  __syncthreads();
+  // 2 x 2 max of the block's two rows: W / 2 pooled pixels x NC / 4 channel quads
+  const auto rp = make_rsrc(a.pool, a.pbytes);
+  const int Wo = a.W >> 1;
+  for (int u = threadIdx.x; u < Wo * (NC / 4); u += NWV * 64) {
+    const int wo = u / (NC / 4), cq = u - wo * (NC / 4);
+    const int p00 = 2 * wo, p10 = a.W + 2 * wo;
+    const uint2 q[4] = {ytile[p00][cq], ytile[p00 + 1][cq], ytile[p10][cq], ytile[p10 + 1][cq]};
+    float mx[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t wd = e < 2 ? q[0].x : q[0].y;
+      mx[e] = __uint_as_float((e & 1) ? (wd & 0xffff0000u) : (wd << 16));
+    }
+#pragma unroll
+    for (int t = 1; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t wd = e < 2 ? q[t].x : q[t].y;
+        mx[e] = fmaxf(mx[e], __uint_as_float((e & 1) ? (wd & 0xffff0000u) : (wd << 16)));
+      }
+    const int mo = (img * (a.H >> 1) + (h0 >> 1)) * Wo + wo;
+    bstore8(rp, (uint32_t)(mo * a.ppitch + cout0 + 4 * cq) * 2u, make_uint2(pack2bf(mx[0], mx[1]), pack2bf(mx[2], mx[3])));
+  }
+}
+
+static int ilog2_exact(long v) {
+  int s = 0;
+  while ((1L << s) < v) ++s;
+  return (1L << s) == v ? s : -1;
+}
+
+// Returns 1 if it also wrote the pool, 0 if not, < 0 (nothing launched) when the shape does not fit.
+extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
+                                int pitch2, const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, int N,
+                                int H, int W, int Cout, const float* escale, const float* eshift, int erelu, void* pool,
+                                long pbytes, int ppitch, hipStream_t s) {
+  const int Cin = C1 + C2;
+  const int cs = ilog2_exact(Cin / 32), ws = ilog2_exact(W);
+  if (C1 % 32 || C2 % 32 || Cin < 64 || Cin % 32 || cs < 0 || ws < 4 || W > 64 || Cout % 32) return -1;
+  if (!escale || !eshift || ldw < 9 * Cin || (C2 && !x2)) return -1;
+  if (pitch1 % 8 || (C2 && pitch2 % 8) || ypitch % 4) return -1;
+  if (xbytes1 >= (1L << 31) || xbytes2 >= (1L << 31) || wbytes >= (1L << 31) || ybytes >= (1L << 31) ||
+      pbytes >= (1L << 31))
+    return -1;
+  // the pool needs two rows per block: only where that block is <= 64 pixels (else the caller pools)
+  const bool pl = pool != nullptr && H % 2 == 0 && ppitch % 4 == 0 && 2 * W <= 64;
+  const int R = pl ? 2 : 1;
+  const int PB = R * W;
+  RowbandArgs a;
+  a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
+  a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
+  a.C1 = C1; a.C2 = C2; a.pitch1 = pitch1; a.pitch2 = pitch2;
+  a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+  a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+  a.pool = pl ? (u16*)pool : nullptr; a.pbytes = pl ? (uint32_t)pbytes : 0u; a.ppitch = ppitch;
+  a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+  a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.wshift = ws;
+  a.R = R; a.bands = H / R; a.cshift = cs; a.T = 9 * Cin / 32;
+  const int grid = N * a.bands * (Cout / 32);
+  // a grid of <= 256 blocks leaves the second block slot of every CU empty: split K over 16 waves instead
+  // (RDP_ROWBAND_WAVES=8 / 16 forces one form)
+  static const int force_w = [] {
+    const char* e = getenv("RDP_ROWBAND_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const bool w16 = force_w == 16 || (force_w != 8 && grid <= 256);
+  const dim3 blk(w16 ? 1024 : 512);
+  if (PB == 16) {
+    if (w16) hipLaunchKernelGGL((conv_rowband_kernel<2, 1, 4, 16>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((conv_rowband_kernel<2, 1, 4, 8>), dim3(grid), blk, 0, s, a);
+  } else if (PB == 32) {
+    if (w16) hipLaunchKernelGGL((conv_rowband_kernel<2, 2, 2, 16>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((conv_rowband_kernel<2, 2, 2, 8>), dim3(grid), blk, 0, s, a);
+  } else if (PB == 64) {
+    if (w16) hipLaunchKernelGGL((conv_rowband_kernel<2, 4, 1, 16>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((conv_rowband_kernel<2, 4, 1, 8>), dim3(grid), blk, 0, s, a);
+  } else {
+    return -1;
+  }
+  return pl ? 1 : 0;
+}

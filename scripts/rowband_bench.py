@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Serving-size eval convs (BN folded + ReLU, N = 1): the row-band kernel (bm_pref 16,
+csrc/conv_rowband.hip) against the split-K implicit GEMM + reduce launch pair (bm_pref 2: the 8-wave
+128 x 128 kernel the auto dispatch otherwise picks at these shapes).
+
+Each variant runs `--reps` convs back to back inside one captured hipGraph (kernel boundaries included,
+as in the serving frame's graph); device time per conv = replay time / reps, median over interleaved
+rounds. usage: python scripts/rowband_bench.py [--batch 1] [--reps 20] [--rounds 7]
+"""
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from robotic_discovery_platform_amd.ops import native  # noqa: E402
+
+# (name, H, C1, C2, Cout, fused output): the U-Net levels at <= 64^2 of a 256^2 frame
+SHAPES = [("down2.conv1", 64, 128, 0, 256, None), ("down2.conv2", 64, 256, 0, 256, "pool"),
+          ("down3.conv1", 32, 256, 0, 512, None), ("down3.conv2", 32, 512, 0, 512, "pool"),
+          ("down4.conv1", 16, 512, 0, 512, None), ("down4.conv2", 16, 512, 0, 512, "up"),
+          ("up1.conv1", 32, 512, 512, 512, None), ("up1.conv2", 32, 512, 0, 256, "up"),
+          ("up2.conv1", 64, 256, 256, 256, None), ("up2.conv2", 64, 256, 0, 128, "up")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--variants", default="2,16")
+    a = ap.parse_args()
+    C = native()
+    dev = torch.device("cuda")
+    N = a.batch
+    variants = [int(v) for v in a.variants.split(",")]
+    total = {v: 0.0 for v in variants}
+    s = torch.cuda.Stream()
+    for (name, H, C1, C2, Co, fuse) in SHAPES:
+        torch.manual_seed(0)
+        x1 = torch.randn(N, H, H, C1, device=dev).to(torch.bfloat16)
+        x2 = torch.randn(N, H, H, C2, device=dev).to(torch.bfloat16) if C2 else None
+        Cin = C1 + C2
+        w = (torch.randn(Co, 9 * Cin, device=dev) / math.sqrt(9 * Cin)).to(torch.bfloat16)
+        coef = torch.zeros(4 * Co, device=dev)
+        C.bn_eval_coef(torch.rand(Co, device=dev) + 0.5, torch.randn(Co, device=dev) * 0.1,
+                       torch.zeros(Co, device=dev), torch.ones(Co, device=dev), 1e-5, coef)
+        y = torch.empty(N, H, H, Co, dtype=torch.bfloat16, device=dev)
+        pool = torch.empty(N, H // 2, H // 2, Co, dtype=torch.bfloat16, device=dev) if fuse == "pool" else None
+        up = torch.empty(N, 2 * H, 2 * H, Co, dtype=torch.bfloat16, device=dev) if fuse == "up" else None
+        n_ws = max(C.conv_ws_elems(N, H, H, C1, C2, Co, 9, 0, v) for v in variants)
+        ws = torch.zeros(max(n_ws, 1), device=dev)
+        graphs = {}
+        for v in variants:
+            def run(v=v):
+                C.conv_fwd(x1, x2, w, 9, 0, y, None, None, v, coef, 1, ws, pool, up, 0, 0)
+            with torch.cuda.stream(s):
+                run()
+            s.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(a.reps):
+                    run()
+            graphs[v] = g
+        times = {v: [] for v in variants}
+        for _ in range(a.rounds):
+            for v in variants:
+                graphs[v].replay()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                graphs[v].replay()
+                e1.record()
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1) * 1000.0 / a.reps)
+        row = {"layer": name, "H": H, "cin": Cin, "cout": Co, "fused": fuse}
+        for v in variants:
+            t = statistics.median(times[v])
+            row[f"us_v{v}"] = round(t, 2)
+            total[v] += t
+        print(json.dumps(row), flush=True)
+    print(json.dumps({"total_us": {f"v{v}": round(t, 1) for v, t in total.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1356,3 +1356,44 @@ torch.save({"y": y.cpu(), "s": st[: r * 256].view(r, 2, 128).sum(0).cpu(), "g": 
     assert torch.allclose(outs[0]["s"], outs[1]["s"], rtol=1e-4, atol=1e-2)
     assert relerr(outs[1]["g"], outs[0]["g"]) < 1e-5
 
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pool", [
+    (1, 32, 32, 256, 0, 512, False), (1, 32, 32, 512, 0, 512, True), (1, 16, 16, 512, 0, 512, False),
+    (1, 16, 16, 512, 0, 512, True), (1, 32, 32, 512, 512, 512, False), (1, 32, 32, 512, 0, 256, False),
+    (1, 64, 64, 128, 0, 256, False), (1, 64, 64, 256, 0, 256, True), (2, 16, 16, 256, 256, 128, True),
+    (1, 64, 64, 256, 256, 256, False), (3, 16, 32, 64, 64, 96, False)])
+def test_conv_rowband_eval(C, N, H, W, C1, C2, Cout, pool):
+    """Row-band eval conv (bm_pref 16; auto on small maps): BN fold + ReLU, concat input, fused
+    MaxPool2d(2) -- vs fp32 torch, vs the split-K implicit GEMM (bm_pref 128) at bf16 rounding, and the
+    pool bitwise the 2x2 max of the output."""
+    torch.manual_seed(12)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wk = ohwi(w).contiguous()
+    g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    a = torch.full((N, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    p = torch.full((N, H // 2, W // 2, Cout), float("nan"), dtype=torch.bfloat16, device=dev) if pool else None
+    C.conv_fwd(x1, x2, wk, 9, 0, a, None, None, 16, coef, 1, None, p)
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.relu(F.batch_norm(F.conv2d(xin, w.float(), padding=1), rm, rv, g, b, False, 0.0, 1e-5))
+    assert not torch.isnan(a.float()).any()
+    assert relerr(nchw(a), ref) < 1e-2
+    if Cout % 128 == 0:
+        n_ws = C.conv_ws_elems(N, H, W, C1, C2, Cout, 9, 0, 128)
+        ws = torch.zeros(max(n_ws, 1), device=dev)
+        a2 = torch.empty_like(a)
+        C.conv_fwd(x1, x2, wk, 9, 0, a2, None, None, 128, coef, 1, ws)
+        d = (a.float() - a2.float()).abs()
+        assert (d <= 2 ** -6 * a2.float().abs() + 1e-2).all(), d.max()
+    if pool:
+        assert torch.equal(p, F.max_pool2d(nchw(a).float(), 2).to(torch.bfloat16).permute(0, 2, 3, 1))
+    # deterministic: a second launch is bitwise identical
+    a3 = torch.empty_like(a)
+    C.conv_fwd(x1, x2, wk, 9, 0, a3, None, None, 16, coef, 1)
+    assert torch.equal(a, a3)
