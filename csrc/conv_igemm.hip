@@ -841,15 +841,22 @@ extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, lo
                                 int H, int W, int Cout, const float* escale, const float* eshift, int erelu, void* pool,
                                 long pbytes, int ppitch, hipStream_t s);
 
-// Eval convs on small maps run on the row-band kernel (csrc/conv_rowband.hip) where it takes the shape:
-// RDP_ROWBAND=0 turns the auto choice off (A/B); bm_pref 16 forces it.
-static bool rowband_auto(int N, int H, int W, int Cin, int Cout) {
+extern "C" long rdp_conv_rowband_bytes(int N, int H, int W, int Cin, int Cout, int pool);
+
+// Eval convs on small maps run on the row-band kernel (csrc/conv_rowband.hip) where its operand traffic
+// model says it wins (<= 160 MB; a pool it cannot fuse would cost a separate launch): RDP_ROWBAND=0 turns
+// the auto choice off (A/B); bm_pref 16 forces it.
+static bool rowband_auto(int N, int H, int W, int Cin, int Cout, bool pool) {
   static int on = -1;
   if (on < 0) {
     const char* e = getenv("RDP_ROWBAND");
-    on = e ? atoi(e) : 0;
+    on = e ? atoi(e) : 1;
   }
-  return on != 0 && (long)N * H * W <= 4096 && W <= 64 && Cin >= 128 && Cout >= 64;
+  if (on == 0 || (long)N * H * W > 4096 || W > 64 || Cin < 128 || Cout < 64) return false;
+  if (pool && !(H % 2 == 0 && 2 * W <= 64)) return false;
+  // (the estimate without the pool's two-row blocks: with or without a pool the same kernel runs, so the
+  // two calls give bitwise the same activations)
+  return rdp_conv_rowband_bytes(N, H, W, Cin, Cout, 0) <= 160000000L;
 }
 extern "C" int rdp_conv_ring2(const void* x0, long xbytes0, int pitch0, const void* x1, long xbytes1, int pitch1,
                               const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, float* stats,
@@ -1166,7 +1173,7 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   {
     const int pref = bm_pref % 1000;
     if (escale && eshift && !stats && !y2 && taps == 9 && !packed &&
-        (pref == 16 || (pref == 0 && rowband_auto(N, H, W, C1 + C2, Cout)))) {
+        (pref == 16 || (pref == 0 && rowband_auto(N, H, W, C1 + C2, Cout, pool && pooled)))) {
       const bool wp = pool && pooled && H % 2 == 0 && W % 2 == 0;
       const long pbytes = wp ? ((long)N * (H / 2) * (W / 2) - 1) * ppitch * 2 + (long)Cout * 2 : 0;
       const int r = rdp_conv_rowband(x1, x2, xbytes1, xbytes2, C1, C2, pitch1, pitch2, w, wbytes, ldw, y1, ybytes1,

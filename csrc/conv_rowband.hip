@@ -20,7 +20,6 @@
 // 32-channel output slice, so that slice's weights (32 x 9 Cin bf16) are fetched into that XCD's L2
 // once and re-read there by every band.
 #include "common.h"
-#include <stdlib.h>
 
 struct RowbandArgs {
   const u16* x1;
@@ -57,10 +56,12 @@ struct RbFrag {
   bf16x8 B[NPG];  // pixels: pixel (lane & 15) of group g, channels 8 (lane >> 4) .. +7
 };
 
-// NWV = 8: two blocks per CU (<= 128 VGPRs), 16: one block per CU with K split twice as finely
-template <int NF, int NPG, int G, int NWV>
-__global__ __launch_bounds__(NWV * 64, 4) void conv_rowband_kernel(const RowbandArgs a) {
-  constexpr int NC = NF * 16, PB = NPG * 16;
+// Two blocks per CU (<= 128 VGPRs: G k-steps of operands per register buffer). (16-wave blocks, K split
+// twice as finely, and 8-wave blocks at one per CU with deeper register buffers measured the same:
+// scripts/rowband_bench.py -- the kernel is bound by the L2 -> CU operand bytes, not by load latency.)
+template <int NF, int NPG, int G>
+__global__ __launch_bounds__(512, 4) void conv_rowband_kernel(const RowbandArgs a) {
+  constexpr int NWV = 8, NC = NF * 16, PB = NPG * 16;
   __shared__ f32x4 red[NWV][NF * NPG][64];
   __shared__ uint2 ytile[PB][NC / 4];  // bf16 output tile for the fused pool
 
@@ -202,6 +203,17 @@ __global__ __launch_bounds__(NWV * 64, 4) void conv_rowband_kernel(const Rowband
   }
 }
 
+// Operand bytes the kernel moves from L2 (every block re-reads its weight slice; every activation is read
+// once per tap and per 32-channel output slice). Measured (scripts/rowband_bench.py, N = 1, MI355X) the
+// kernel runs at ~8-9 TB/s of these bytes: it beats the split-K implicit GEMM + reduce pair at <= ~150 MB
+// (17-25 % faster on the 64^2 128 -> 256, 32^2 256 -> 512, 16^2 512 -> 512, 32^2 512 -> 256 and
+// 64^2 256 -> 128 layers) and loses from ~225 MB up (32^2 1024 -> 512: 64 vs 27 us).
+extern "C" long rdp_conv_rowband_bytes(int N, int H, int W, int Cin, int Cout, int pool) {
+  const int R = pool && H % 2 == 0 && 2 * W <= 64 ? 2 : 1;
+  const long wb = (long)Cout * 9 * Cin * 2, xb = (long)N * H * W * Cin * 2;
+  return wb * ((long)N * H / R) + xb * 9 * (Cout / 32);
+}
+
 static int ilog2_exact(long v) {
   int s = 0;
   while ((1L << s) < v) ++s;
@@ -236,25 +248,9 @@ extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, lo
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.wshift = ws;
   a.R = R; a.bands = H / R; a.cshift = cs; a.T = 9 * Cin / 32;
   const int grid = N * a.bands * (Cout / 32);
-  // a grid of <= 256 blocks leaves the second block slot of every CU empty: split K over 16 waves instead
-  // (RDP_ROWBAND_WAVES=8 / 16 forces one form)
-  static const int force_w = [] {
-    const char* e = getenv("RDP_ROWBAND_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  const bool w16 = force_w == 16 || (force_w != 8 && grid <= 256);
-  const dim3 blk(w16 ? 1024 : 512);
-  if (PB == 16) {
-    if (w16) hipLaunchKernelGGL((conv_rowband_kernel<2, 1, 4, 16>), dim3(grid), blk, 0, s, a);
-    else hipLaunchKernelGGL((conv_rowband_kernel<2, 1, 4, 8>), dim3(grid), blk, 0, s, a);
-  } else if (PB == 32) {
-    if (w16) hipLaunchKernelGGL((conv_rowband_kernel<2, 2, 2, 16>), dim3(grid), blk, 0, s, a);
-    else hipLaunchKernelGGL((conv_rowband_kernel<2, 2, 2, 8>), dim3(grid), blk, 0, s, a);
-  } else if (PB == 64) {
-    if (w16) hipLaunchKernelGGL((conv_rowband_kernel<2, 4, 1, 16>), dim3(grid), blk, 0, s, a);
-    else hipLaunchKernelGGL((conv_rowband_kernel<2, 4, 1, 8>), dim3(grid), blk, 0, s, a);
-  } else {
-    return -1;
-  }
+  if (PB == 16) hipLaunchKernelGGL((conv_rowband_kernel<2, 1, 4>), dim3(grid), dim3(512), 0, s, a);
+  else if (PB == 32) hipLaunchKernelGGL((conv_rowband_kernel<2, 2, 2>), dim3(grid), dim3(512), 0, s, a);
+  else if (PB == 64) hipLaunchKernelGGL((conv_rowband_kernel<2, 4, 1>), dim3(grid), dim3(512), 0, s, a);
+  else return -1;
   return pl ? 1 : 0;
 }
