@@ -16,11 +16,15 @@
 #include <functional>
 #include <memory>
 #include <vector>
+#include <array>
 
 extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
                    float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
+int rdp_conv_rowband_chain(int, const void*, long, int, int, const void* const*, const long*, const int*, void* const*,
+                           const long*, const int*, const int*, const float* const*, const float* const*, int, int, int,
+                           int*, int*, hipStream_t);
 int rdp_conv_ring_ex(const void*, long, int, int, const void*, long, int, void*, long, int, void*, long, int, int, int,
                      float*, int, int, int, const float*, const float*, int, int, const void*, int, const float*,
                      const float*, const float*, void*, long, int, hipStream_t);
@@ -1070,6 +1074,39 @@ bool conv_head_mask(torch::Tensor x, torch::Tensor w, torch::Tensor coef, torch:
   return r == 0;
 }
 
+// Persistent row-band chain (csrc/conv_rowband.hip): layer 0 reads x, layer l > 0 layer l - 1's output;
+// eval BN fold + ReLU per layer (coef = [mean|invstd|scale|shift]). cnt: int32 >= 1 + nl * N * H, err: int32.
+bool conv_rowband_chain(torch::Tensor x, std::vector<torch::Tensor> ws, std::vector<torch::Tensor> ys,
+                        std::vector<torch::Tensor> coefs, torch::Tensor cnt, torch::Tensor err) {
+  const int nl = (int)ws.size();
+  TORCH_CHECK(nl >= 1 && nl <= 4 && (int)ys.size() == nl && (int)coefs.size() == nl, "1..4 layers");
+  Act a = act(x, "x");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == torch::kInt32 && cnt.numel() >= 1 + (long)nl * a.N * a.H, "cnt");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == torch::kInt32 && err.numel() >= 1, "err");
+  std::array<const void*, 4> wp{};
+  std::array<void*, 4> yp{};
+  std::array<long, 4> wb{}, yb{};
+  std::array<int, 4> ldw{}, ypit{}, co{};
+  std::array<const float*, 4> sc{}, sh{};
+  for (int l = 0; l < nl; ++l) {
+    TORCH_CHECK(ws[l].is_cuda() && ws[l].scalar_type() == torch::kBFloat16 && ws[l].is_contiguous() && ws[l].dim() == 2,
+                "w: bf16 [Cout][K]");
+    Act o = act(ys[l], "y");
+    TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && o.C == ws[l].size(0), "y shape");
+    check_f32(coefs[l], "coef");
+    TORCH_CHECK(coefs[l].numel() >= 4l * o.C, "coef size");
+    wp[l] = ws[l].data_ptr(); wb[l] = ws[l].numel() * 2; ldw[l] = (int)ws[l].size(1);
+    yp[l] = o.ptr; yb[l] = o.bytes; ypit[l] = o.pitch; co[l] = o.C;
+    sc[l] = coefs[l].data_ptr<float>() + 2 * o.C; sh[l] = coefs[l].data_ptr<float>() + 3 * o.C;
+  }
+  int* const cp = cnt.data_ptr<int>();
+  int* const ep = err.data_ptr<int>();
+  const int r = RDP_PLAN(rdp_conv_rowband_chain(nl, a.ptr, a.bytes, a.C, a.pitch, wp.data(), wb.data(), ldw.data(),
+                                                yp.data(), yb.data(), ypit.data(), co.data(), sc.data(), sh.data(),
+                                                a.N, a.H, a.W, cp, ep, st));
+  return r == 0;
+}
+
 void head_mask(torch::Tensor a, torch::Tensor w, torch::Tensor b, double logit_thr, torch::Tensor mask) {
   Act x = act(a, "a");
   TORCH_CHECK(mask.scalar_type() == torch::kUInt8 && mask.numel() == (long)x.N * x.H * x.W, "mask u8 numel");
@@ -1474,6 +1511,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_bn_bwd_apply", on_device(&head_bn_bwd_apply));
   m.def("head_mask", on_device(&head_mask));
   m.def("conv_head_mask", on_device(&conv_head_mask));
+  m.def("conv_rowband_chain", on_device(&conv_rowband_chain));
   m.def("adam", on_device(&adam), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
         py::arg("inc") = true, py::arg("max_blocks") = 0);

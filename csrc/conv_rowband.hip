@@ -20,6 +20,8 @@
 // 32-channel output slice, so that slice's weights (32 x 9 Cin bf16) are fetched into that XCD's L2
 // once and re-read there by every band.
 #include "common.h"
+#include <algorithm>
+#include <stdlib.h>
 
 struct RowbandArgs {
   const u16* x1;
@@ -56,18 +58,21 @@ struct RbFrag {
   bf16x8 B[NPG];  // pixels: pixel (lane & 15) of group g, channels 8 (lane >> 4) .. +7
 };
 
-// Two blocks per CU (<= 128 VGPRs: G k-steps of operands per register buffer). (16-wave blocks, K split
-// twice as finely, and 8-wave blocks at one per CU with deeper register buffers measured the same:
-// scripts/rowband_bench.py -- the kernel is bound by the L2 -> CU operand bytes, not by load latency.)
-template <int NF, int NPG, int G>
-__global__ __launch_bounds__(512, 4) void conv_rowband_kernel(const RowbandArgs a) {
-  constexpr int NWV = 8, NC = NF * 16, PB = NPG * 16;
-  __shared__ f32x4 red[NWV][NF * NPG][64];
-  __shared__ uint2 ytile[PB][NC / 4];  // bf16 output tile for the fused pool
+template <int NF, int NPG>
+struct RbSmem {
+  f32x4 red[8][NF * NPG][64];   // the 8 waves' partial tiles
+  uint2 ytile[NPG * 16][NF * 4];  // bf16 output tile for the fused pool
+};
 
+// One tile (row band x 32-channel slice, logical id lid) of layer a; the caller's LDS. WT: write-through
+// (sc1) output stores, for an in-launch consumer on another XCD (the chain)
+template <int NF, int NPG, int G, bool WT = false>
+RDP_DEV void rowband_tile(const RowbandArgs& a, uint32_t lid, RbSmem<NF, NPG>& sm) {
+  constexpr int NWV = 8, NC = NF * 16;
+  auto& red = sm.red;
+  auto& ytile = sm.ytile;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
   const int nb = a.N * a.bands;
   const int ct = (int)lid / nb, band = (int)lid - ct * nb;
   const int img = band / a.bands, h0 = (band - img * a.bands) * a.R;
@@ -173,7 +178,8 @@ __global__ __launch_bounds__(512, 4) void conv_rowband_kernel(const RowbandArgs 
     const uint2 pk = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
     const int p = 16 * g + (l & 15);
     const int m = ((img * a.H + h0 + (p >> a.wshift)) << a.wshift) + (p & (a.W - 1));
-    bstore8(ry, (uint32_t)(m * a.ypitch + c) * 2u, pk);
+    __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<const __attribute__((ext_vector_type(2))) uint32_t*>(&pk), ry,
+                                          (uint32_t)(m * a.ypitch + c) * 2u, 0, WT ? 16 : 0);
     if (a.pool) ytile[p][cl >> 2] = pk;
   }
   if (!a.pool) return;  // block-uniform
@@ -200,6 +206,99 @@ __global__ __launch_bounds__(512, 4) void conv_rowband_kernel(const RowbandArgs 
       }
     const int mo = (img * (a.H >> 1) + (h0 >> 1)) * Wo + wo;
     bstore8(rp, (uint32_t)(mo * a.ppitch + cout0 + 4 * cq) * 2u, make_uint2(pack2bf(mx[0], mx[1]), pack2bf(mx[2], mx[3])));
+  }
+}
+
+// Two blocks per CU (<= 128 VGPRs: G k-steps of operands per register buffer). (16-wave blocks, K split
+// twice as finely, and 8-wave blocks at one per CU with deeper register buffers measured the same:
+// scripts/rowband_bench.py -- the kernel is bound by the L2 -> CU operand bytes, not by load latency.)
+template <int NF, int NPG, int G>
+__global__ __launch_bounds__(512, 4) void conv_rowband_kernel(const RowbandArgs a) {
+  __shared__ RbSmem<NF, NPG> sm;
+  rowband_tile<NF, NPG, G>(a, xcd_remap(blockIdx.x, gridDim.x), sm);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent chain of row-band layers of one map size (layer l + 1's input = layer l's output) in ONE
+// launch with row-level readiness counters instead of kernel boundaries (measured
+// against the per-layer launches by scripts/rowband_bench.py --chain, profiles/dead_ends.md).
+// Work items are dealt by a ticket counter in layer order, so an item only ever waits for items with
+// smaller tickets, which are already running: no residency assumption, no deadlock. Hand-off
+// (cdna_hip_programming.md Guideline 16): the producer's write-through (sc1) stores -> every wave
+// vmcnt(0) -> block barrier -> relaxed agent add on each of its rows' counters (a plain-store + agent
+// release form measured slower still: the release writes back the whole XCD L2);
+// the consumer: one lane polls the counters of its input rows (relaxed agent loads + s_sleep, bounded:
+// on timeout it flags *err and goes on, so a bug cannot hang the GPU) -> agent acquire fence ->
+// vmcnt(0) -> block barrier -> plain loads. cnt[0] = ticket, cnt[1 + l * rows + r] = slices of row r of
+// layer l written; zeroed by the host before every launch.
+struct RowbandChainArgs {
+  RowbandArgs L[4];
+  int nl;
+  int start[5];  // first ticket of each layer
+  int nct[4];    // 32-channel slices per layer (a row is complete at nct)
+  int rows;      // N * H
+  int* cnt;
+  int* err;
+  int spin_limit;  // polls per row before the wait gives up (RDP_CHAIN_SPINS)
+};
+
+// Every branch around a block barrier is wave-uniform: the ticket, the polls and the counter adds are
+// issued by ALL lanes of wave 0 (the other lanes add 0; the compiler's atomic combining leaves one add per
+// wave instruction) under `wave == 0`, a scalar branch. (A first form with `threadIdx.x == 0` regions
+// inside the ticket loop was compiled into a divergent loop whose lanes 1..63 kept re-running the old
+// ticket with the other waves while lane 0 waited for them: a hang.)
+template <int NF, int NPG, int G>
+__global__ __launch_bounds__(512, 4) void conv_rowband_chain_kernel(const RowbandChainArgs c) {
+  __shared__ RbSmem<NF, NPG> sm;
+  __shared__ int s_ticket;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int one = lane == 0 ? 1 : 0;
+  const int total = c.start[c.nl];
+  while (true) {
+    if (wave == 0) {
+      const int v = __hip_atomic_fetch_add(c.cnt, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ticket = __builtin_amdgcn_readfirstlane(v);  // lane 0's value: the ticket
+    }
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(s_ticket);
+    if (t >= total) break;
+    int l = 0;
+    while (l + 1 < c.nl && t >= c.start[l + 1]) ++l;
+    l = __builtin_amdgcn_readfirstlane(l);
+    const RowbandArgs& a = c.L[l];  // uniform index into the kernel arguments: scalar loads
+    const int lid = t - c.start[l];
+    const int nb = a.N * a.bands;
+    const int band = lid - (lid / nb) * nb;
+    const int img = band / a.bands, h0 = (band - img * a.bands) * a.R;
+    if (l > 0) {  // input rows h0 - 1 .. h0 + R of layer l - 1 complete
+      if (wave == 0) {
+        const int r0 = max(h0 - 1, 0), r1 = min(h0 + a.R, a.H - 1);
+        const int* rc = c.cnt + 1 + (l - 1) * c.rows + img * a.H;
+        for (int r = r0; r <= r1; ++r) {
+          for (int spins = 0;; ++spins) {
+            const int v = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(rc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (v >= c.nct[l - 1]) break;
+            if (spins >= c.spin_limit) {
+              __hip_atomic_store(c.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+    rowband_tile<NF, NPG, G, true>(a, (uint32_t)lid, sm);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its write-through stores landed
+    __syncthreads();
+    if (wave == 0) {
+      int* rc = c.cnt + 1 + l * c.rows + img * a.H + h0;
+      for (int r = 0; r < a.R; ++r) __hip_atomic_fetch_add(rc + r, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -253,4 +352,53 @@ extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, lo
   else if (PB == 64) hipLaunchKernelGGL((conv_rowband_kernel<2, 4, 1>), dim3(grid), dim3(512), 0, s, a);
   else return -1;
   return pl ? 1 : 0;
+}
+
+// The chain launch: layer 0 reads x (C0 channels), layer l > 0 reads layer l - 1's output; every layer is
+// an eval conv (BN folded + ReLU) on the same N x H x W map. cnt: >= 1 + nl * N * H ints, err: 1 int.
+// Returns 0, or < 0 (nothing launched) when a layer does not fit the row-band kernel.
+extern "C" int rdp_conv_rowband_chain(int nl, const void* x, long xbytes, int C0, int xpitch, const void* const* w,
+                                      const long* wbytes, const int* ldw, void* const* y, const long* ybytes,
+                                      const int* ypitch, const int* cout, const float* const* escale,
+                                      const float* const* eshift, int N, int H, int W, int* cnt, int* err,
+                                      hipStream_t s) {
+  if (nl < 1 || nl > 4) return -1;
+  const int ws = ilog2_exact(W);
+  if (ws < 4 || W != 16) return -1;  // one tile shape (16-pixel rows) for the whole chain
+  RowbandChainArgs c;
+  c.nl = nl;
+  c.rows = N * H;
+  c.cnt = cnt;
+  c.err = err;
+  static const int spins = [] {
+    const char* e = getenv("RDP_CHAIN_SPINS");
+    return e ? atoi(e) : (1 << 20);
+  }();
+  c.spin_limit = spins;
+  c.start[0] = 0;
+  int cin = C0;
+  for (int l = 0; l < nl; ++l) {
+    const int cs = ilog2_exact(cin / 32);
+    if (cin % 32 || cin < 64 || cs < 0 || cout[l] % 32 || ldw[l] < 9 * cin || ypitch[l] % 4) return -1;
+    RowbandArgs& a = c.L[l];
+    a.x1 = (const u16*)(l == 0 ? x : y[l - 1]);
+    a.x2 = nullptr;
+    a.xbytes1 = (uint32_t)(l == 0 ? xbytes : ybytes[l - 1]);
+    a.xbytes2 = 0;
+    a.C1 = cin; a.C2 = 0; a.pitch1 = l == 0 ? xpitch : ypitch[l - 1]; a.pitch2 = 0;
+    a.w = (const u16*)w[l]; a.wbytes = (uint32_t)wbytes[l]; a.ldw = ldw[l];
+    a.y = (u16*)y[l]; a.ybytes = (uint32_t)ybytes[l]; a.ypitch = ypitch[l];
+    a.pool = nullptr; a.pbytes = 0; a.ppitch = 0;
+    a.escale = escale[l]; a.eshift = eshift[l]; a.erelu = 1;
+    a.N = N; a.H = H; a.W = W; a.Cout = cout[l]; a.wshift = ws;
+    a.R = 1; a.bands = H; a.cshift = cs; a.T = 9 * cin / 32;
+    c.nct[l] = cout[l] / 32;
+    c.start[l + 1] = c.start[l] + N * H * c.nct[l];
+    cin = cout[l];
+  }
+  for (int l = nl; l < 4; ++l) c.L[l] = c.L[0];
+  const int grid = std::min(c.start[nl], 512);
+  if (hipMemsetAsync(cnt, 0, (size_t)(1 + nl * c.rows) * sizeof(int), s) != hipSuccess) return -2;
+  hipLaunchKernelGGL((conv_rowband_chain_kernel<2, 1, 3>), dim3(grid), dim3(512), 0, s, c);
+  return 0;
 }

@@ -27,14 +27,82 @@ SHAPES = [("down2.conv1", 64, 128, 0, 256, None), ("down2.conv2", 64, 256, 0, 25
           ("up2.conv1", 64, 256, 256, 256, None), ("up2.conv2", 64, 256, 0, 128, "up")]
 
 
+def chain_bench(C, a):
+    """--chain: the 16^2 level (down4 conv1 -> conv2, 512 -> 512 -> 512) as two row-band launches vs one
+    persistent chain launch (conv_rowband_chain: row readiness counters, no kernel boundary) vs the split-K
+    pair; outputs of the chain bitwise those of the launches."""
+    dev = torch.device("cuda")
+    N, H, Cs = a.batch, 16, [512, 512, 512]
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, Cs[0], device=dev).to(torch.bfloat16)
+    ws, coefs, ys, ys2 = [], [], [], []
+    for l in range(a.chain_layers):
+        ci, co = Cs[min(l, 2)], Cs[min(l + 1, 2)]
+        ws.append((torch.randn(co, 9 * ci, device=dev) / math.sqrt(9 * ci)).to(torch.bfloat16))
+        cf = torch.zeros(4 * co, device=dev)
+        C.bn_eval_coef(torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev) * 0.1, torch.zeros(co, device=dev),
+                       torch.ones(co, device=dev), 1e-5, cf)
+        coefs.append(cf)
+        ys.append(torch.empty(N, H, H, co, dtype=torch.bfloat16, device=dev))
+        ys2.append(torch.empty(N, H, H, co, dtype=torch.bfloat16, device=dev))
+    cnt = torch.zeros(1 + len(ws) * N * H, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    kws = torch.zeros(max(max(C.conv_ws_elems(N, H, H, 512, 0, 512, 9, 0, 2), 1), 1), device=dev)
+
+    def per_layer(pref):
+        inp = x
+        for w, y, cf in zip(ws, ys2, coefs):
+            C.conv_fwd(inp, None, w, 9, 0, y, None, None, pref, cf, 1, kws)
+            inp = y
+
+    def chain():
+        assert C.conv_rowband_chain(x, ws, ys, coefs, cnt, err)
+
+    s = torch.cuda.Stream()
+    runs = {"rowband_launches": lambda: per_layer(16), "chain": chain, "splitk_pairs": lambda: per_layer(2)}
+    graphs = {}
+    for k, fn in runs.items():
+        with torch.cuda.stream(s):
+            fn()
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(a.reps):
+                fn()
+        graphs[k] = g
+    per_layer(16)
+    chain()
+    torch.cuda.synchronize()
+    same = all(torch.equal(p, q) for p, q in zip(ys, ys2))
+    times = {k: [] for k in runs}
+    for _ in range(a.rounds):
+        for k, g in graphs.items():
+            g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) * 1000.0 / a.reps)
+    print(json.dumps({"chain_layers": len(ws), "N": N, "map": f"{H}x{H}", "bitwise_equal": same,
+                      "err": int(err.item()), **{f"us_{k}": round(statistics.median(v), 2) for k, v in times.items()}}),
+          flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--chain", type=int, default=0, help="also time the persistent chain of the 16^2 level")
+    ap.add_argument("--chain-layers", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--variants", default="2,16")
     a = ap.parse_args()
     C = native()
+    if a.chain:
+        chain_bench(C, a)
+        return
     dev = torch.device("cuda")
     N = a.batch
     variants = [int(v) for v in a.variants.split(",")]

@@ -1397,3 +1397,36 @@ def test_conv_rowband_eval(C, N, H, W, C1, C2, Cout, pool):
     a3 = torch.empty_like(a)
     C.conv_fwd(x1, x2, wk, 9, 0, a3, None, None, 16, coef, 1)
     assert torch.equal(a, a3)
+
+
+@pytest.mark.parametrize("N,nl", [(1, 2), (2, 3), (1, 4)])
+def test_conv_rowband_chain(C, N, nl):
+    """Persistent row-band chain (one launch, row readiness counters) == the same layers as separate
+    row-band launches, bitwise; no bounded wait timed out."""
+    torch.manual_seed(13)
+    dev = "cuda"
+    H = 16
+    chans = [256, 512, 256, 512, 256][: nl + 1]
+    x = bf(torch.randn(N, H, H, chans[0], device=dev))
+    ws, coefs, ys, refs = [], [], [], []
+    for l in range(nl):
+        ci, co = chans[l], chans[l + 1]
+        ws.append(bf(torch.randn(co, 9 * ci, device=dev) / math.sqrt(9 * ci)))
+        cf = torch.zeros(4 * co, device=dev)
+        C.bn_eval_coef(torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev) * 0.1,
+                       torch.randn(co, device=dev) * 0.1, torch.rand(co, device=dev) + 0.5, 1e-5, cf)
+        coefs.append(cf)
+        ys.append(torch.full((N, H, H, co), float("nan"), dtype=torch.bfloat16, device=dev))
+        refs.append(torch.empty(N, H, H, co, dtype=torch.bfloat16, device=dev))
+    inp = x
+    for w, r, cf in zip(ws, refs, coefs):
+        C.conv_fwd(inp, None, w, 9, 0, r, None, None, 16, cf, 1)
+        inp = r
+    cnt = torch.full((1 + nl * N * H,), 7, dtype=torch.int32, device=dev)  # poisoned: the launch zeroes it
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        assert C.conv_rowband_chain(x, ws, ys, coefs, cnt, err)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        for y, r in zip(ys, refs):
+            assert torch.equal(y, r)
