@@ -22,6 +22,9 @@ extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
                    float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
+int rdp_conv_rowband_ex(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, long, int,
+                        int, int, int, int, const float*, const float*, int, void*, long, int, int, hipStream_t);
+int rdp_conv_rowband_frag_auto(int, int, int, int, int);
 int rdp_conv_rowband_chain(int, const void*, long, int, int, const void* const*, const long*, const int*, void* const*,
                            const long*, const int*, const int*, const float* const*, const float* const*, int, int, int,
                            int*, int*, hipStream_t);
@@ -527,7 +530,8 @@ int conv_stats_rows(long M, int Cout, int bm_pref) {
 int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, int taps, int packed,
              torch::Tensor y1, c10::optional<torch::Tensor> y2, c10::optional<torch::Tensor> stats, int bm_pref,
              c10::optional<torch::Tensor> affine, int relu, c10::optional<torch::Tensor> ws,
-             c10::optional<torch::Tensor> pool, c10::optional<torch::Tensor> up, int up_oy, int up_ox) {
+             c10::optional<torch::Tensor> pool, c10::optional<torch::Tensor> up, int up_oy, int up_ox,
+             c10::optional<torch::Tensor> wfrag) {
   Act a1 = act(x1, "x1"), a2;
   if (x2) {
     a2 = act(*x2, "x2");
@@ -604,10 +608,26 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     const bool want_fused = pool || up;
     // the fused pool / upsample result flag: a heap cell owned by the launch (kept alive in a plan)
     auto pooled = std::make_shared<int>(0);
-    const int r = RDP_PLAN(rdp_conv_igemm(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wp, wb, (int)ldw, py1, py2, by1,
-                                          by2, o1.C, o1.pitch, yp2, spc, nn, a1.H, a1.W, Cout, taps, packed, bm_pref, esc,
-                                          esh, relu, wsp, wsn, ppo, ppit, want_fused ? pooled.get() : nullptr, pup, upit,
-                                          uH, uW, up_oy, up_ox, st));
+    // eval with the fragment-major weight copy (wfrag): the row-band kernel wherever its traffic model picks it
+    const bool frag = wfrag && esc && !sp && !y2 && taps == 9 && !packed && bm_pref == 0 &&
+                      rdp_conv_rowband_frag_auto(nn, a1.H, a1.W, a1.C + C2, Cout);
+    int r;
+    if (frag) {
+      void* const wfp = wfrag->data_ptr();
+      const long wfb = wfrag->numel() * 2;
+      const long pbytes = pool ? ((long)nn * po.H * po.W - 1) * ppit * 2 + (long)po.C * 2 : 0;
+      const int rb = RDP_PLAN(rdp_conv_rowband_ex(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wfp, wfb, 0, py1, by1,
+                                                  o1.pitch, nn, a1.H, a1.W, Cout, esc, esh, relu, ppo, pbytes, ppit, 1,
+                                                  st));
+      TORCH_CHECK(rb >= 0, "conv_fwd: row-band kernel rejected a shape its model picked");
+      *pooled = rb == 1 ? 1 : 0;
+      r = 0;
+    } else {
+      r = RDP_PLAN(rdp_conv_igemm(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wp, wb, (int)ldw, py1, py2, by1, by2, o1.C,
+                                  o1.pitch, yp2, spc, nn, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu, wsp,
+                                  wsn, ppo, ppit, want_fused ? pooled.get() : nullptr, pup, upit, uH, uW, up_oy, up_ox,
+                                  st));
+    }
     TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", C2, ", Cout=", Cout, ")");
     const int oN = nn, oH = o1.H, oW = o1.W, oC = o1.C, op1 = o1.pitch;
     if (pool && !*pooled)
@@ -1074,6 +1094,34 @@ bool conv_head_mask(torch::Tensor x, torch::Tensor w, torch::Tensor coef, torch:
   return r == 0;
 }
 
+// Row-band eval conv called directly (csrc/conv_rowband.hip), with OHWI weights (wfrag = 0) or their
+// fragment-major copy (wfrag = 1: [Cout/16][9 Cin/32][64 lanes][8], rowband_frag_weights in Python).
+// Returns 1 when the pool was written, 0 when not, < 0 when the kernel does not take the shape.
+int conv_rowband(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w, torch::Tensor y,
+                 torch::Tensor coef, c10::optional<torch::Tensor> pool, int wfrag) {
+  Act a1 = act(x1, "x1"), a2;
+  if (x2) a2 = act(*x2, "x2");
+  Act o = act(y, "y");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous(), "w: bf16 contiguous");
+  check_f32(coef, "coef");
+  TORCH_CHECK(coef.numel() >= 4l * o.C, "coef size");
+  Act po;
+  if (pool) po = act(*pool, "pool");
+  const int ldw = wfrag ? 0 : (int)w.size(1);
+  void* const px2 = x2 ? a2.ptr : nullptr;
+  const long bx2 = x2 ? a2.bytes : 0;
+  const int C2 = x2 ? a2.C : 0, p2 = x2 ? a2.pitch : 0;
+  void* const pp = pool ? po.ptr : nullptr;
+  const long pb = pool ? po.bytes : 0;
+  const int ppit = pool ? po.pitch : 0;
+  const float* sc = coef.data_ptr<float>() + 2 * o.C;
+  const float* sh = coef.data_ptr<float>() + 3 * o.C;
+  void* const wp = w.data_ptr();
+  const long wb = w.numel() * 2;
+  return (int)RDP_PLAN(rdp_conv_rowband_ex(a1.ptr, px2, a1.bytes, bx2, a1.C, C2, a1.pitch, p2, wp, wb, ldw, o.ptr, o.bytes,
+                                           o.pitch, a1.N, a1.H, a1.W, o.C, sc, sh, 1, pp, pb, ppit, wfrag, st));
+}
+
 // Persistent row-band chain (csrc/conv_rowband.hip): layer 0 reads x, layer l > 0 layer l - 1's output;
 // eval BN fold + ReLU per layer (coef = [mean|invstd|scale|shift]). cnt: int32 >= 1 + nl * N * H, err: int32.
 bool conv_rowband_chain(torch::Tensor x, std::vector<torch::Tensor> ws, std::vector<torch::Tensor> ys,
@@ -1465,7 +1513,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", on_device(&conv_fwd), py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("taps"), py::arg("packed"),
         py::arg("y1"), py::arg("y2"), py::arg("stats"), py::arg("bm_pref"), py::arg("affine"), py::arg("relu"),
         py::arg("ws") = py::none(), py::arg("pool") = py::none(), py::arg("up") = py::none(),
-        py::arg("up_oy") = 0, py::arg("up_ox") = 0);
+        py::arg("up_oy") = 0, py::arg("up_ox") = 0, py::arg("wfrag") = py::none());
   m.def("conv_ws_elems", [](int N, int H, int W, int C1, int C2, int Cout, int taps, int packed, int bm_pref) {
     return rdp_conv_ws_elems(N, H, W, C1, C2, Cout, taps, packed, bm_pref);
   });
@@ -1512,6 +1560,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_mask", on_device(&head_mask));
   m.def("conv_head_mask", on_device(&conv_head_mask));
   m.def("conv_rowband_chain", on_device(&conv_rowband_chain));
+  m.def("conv_rowband", on_device(&conv_rowband));
   m.def("adam", on_device(&adam), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
         py::arg("inc") = true, py::arg("max_blocks") = 0);

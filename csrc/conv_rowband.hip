@@ -46,6 +46,7 @@ struct RowbandArgs {
   int bands;   // H / R
   int cshift;  // log2(Cin / 32): k-step -> tap
   int T;       // k-steps = 9 * Cin / 32
+  int wfrag;   // 1: w is fragment-major (rdp_rowband_frag_weights): one k-step of 16 couts = 1 KiB contiguous
 };
 
 // tap (0..8) -> (dr, ds) without division
@@ -85,7 +86,10 @@ RDP_DEV void rowband_tile(const RowbandArgs& a, uint32_t lid, RbSmem<NF, NPG>& s
   const int lr = lane & 15, lk = 8 * (lane >> 4);
   uint32_t wrow[NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) wrow[f] = (uint32_t)((cout0 + 16 * f + lr) * a.ldw + lk) * 2u;
+  for (int f = 0; f < NF; ++f)
+    wrow[f] = a.wfrag ? (uint32_t)((cout0 / 16 + f) * a.T) * 1024u + (uint32_t)lane * 16u
+                      : (uint32_t)((cout0 + 16 * f + lr) * a.ldw + lk) * 2u;
+  const uint32_t wstep = a.wfrag ? 1024u : 64u;  // bytes per k-step
   int ph[NPG], pw[NPG];
 #pragma unroll
   for (int g = 0; g < NPG; ++g) {
@@ -103,7 +107,7 @@ RDP_DEV void rowband_tile(const RowbandArgs& a, uint32_t lid, RbSmem<NF, NPG>& s
     const int dr = rb_dr(tap), ds = rb_ds(tap);
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const uint32_t off = live ? wrow[f] + (uint32_t)ks * 64u : RDP_OOB;
+      const uint32_t off = live ? wrow[f] + (uint32_t)ks * wstep : RDP_OOB;
       fr.A[f] = __builtin_bit_cast(bf16x8, bload16(rw, off));
     }
     const bool s2 = cbase >= a.C1;
@@ -313,6 +317,21 @@ extern "C" long rdp_conv_rowband_bytes(int N, int H, int W, int Cin, int Cout, i
   return wb * ((long)N * H / R) + xb * 9 * (Cout / 32);
 }
 
+// With the fragment-major weight copy (1 KiB contiguous per MFMA fragment: 8 full lines per load instead of
+// 16 half lines) a weight byte costs about half an activation byte (scripts/rowband_bench.py variant 17:
+// 16^2 512 -> 512 8.8 vs 14.6 us on OHWI weights, 32^2 256 -> 512 13.2 vs 18.9). The eval dispatch
+// (bindings conv_fwd with wfrag) takes the row-band kernel up to 250 MB of weighted operand bytes: every
+// <= 64^2 layer of the U-Net but the two long-K decoder convs (32^2 1024 -> 512, 64^2 512 -> 256).
+extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int Cin, int Cout) {
+  static const int on = [] {
+    const char* e = getenv("RDP_ROWBAND");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || (long)N * H * W > 4096 || W > 64 || W < 16 || Cin < 128 || Cout < 64 || Cout % 32) return 0;
+  const long wb = (long)Cout * 9 * Cin * 2, xb = (long)N * H * W * Cin * 2;
+  return wb * ((long)N * H) / 2 + xb * 9 * (Cout / 32) <= 250000000L;
+}
+
 static int ilog2_exact(long v) {
   int s = 0;
   while ((1L << s) < v) ++s;
@@ -320,14 +339,28 @@ static int ilog2_exact(long v) {
 }
 
 // Returns 1 if it also wrote the pool, 0 if not, < 0 (nothing launched) when the shape does not fit.
+// wfrag: w is the fragment-major copy of the OHWI weights (rdp_rowband_frag_weights) instead of OHWI.
+extern "C" int rdp_conv_rowband_ex(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2,
+                                   int pitch1, int pitch2, const void* w, long wbytes, int ldw, void* y, long ybytes,
+                                   int ypitch, int N, int H, int W, int Cout, const float* escale, const float* eshift,
+                                   int erelu, void* pool, long pbytes, int ppitch, int wfrag, hipStream_t s);
 extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2, int pitch1,
                                 int pitch2, const void* w, long wbytes, int ldw, void* y, long ybytes, int ypitch, int N,
                                 int H, int W, int Cout, const float* escale, const float* eshift, int erelu, void* pool,
                                 long pbytes, int ppitch, hipStream_t s) {
+  return rdp_conv_rowband_ex(x1, x2, xbytes1, xbytes2, C1, C2, pitch1, pitch2, w, wbytes, ldw, y, ybytes, ypitch, N, H,
+                             W, Cout, escale, eshift, erelu, pool, pbytes, ppitch, 0, s);
+}
+
+extern "C" int rdp_conv_rowband_ex(const void* x1, const void* x2, long xbytes1, long xbytes2, int C1, int C2,
+                                   int pitch1, int pitch2, const void* w, long wbytes, int ldw, void* y, long ybytes,
+                                   int ypitch, int N, int H, int W, int Cout, const float* escale, const float* eshift,
+                                   int erelu, void* pool, long pbytes, int ppitch, int wfrag, hipStream_t s) {
   const int Cin = C1 + C2;
   const int cs = ilog2_exact(Cin / 32), ws = ilog2_exact(W);
   if (C1 % 32 || C2 % 32 || Cin < 64 || Cin % 32 || cs < 0 || ws < 4 || W > 64 || Cout % 32) return -1;
-  if (!escale || !eshift || ldw < 9 * Cin || (C2 && !x2)) return -1;
+  if (!escale || !eshift || (!wfrag && ldw < 9 * Cin) || (wfrag && wbytes < (long)Cout * 9 * Cin * 2) || (C2 && !x2))
+    return -1;
   if (pitch1 % 8 || (C2 && pitch2 % 8) || ypitch % 4) return -1;
   if (xbytes1 >= (1L << 31) || xbytes2 >= (1L << 31) || wbytes >= (1L << 31) || ybytes >= (1L << 31) ||
       pbytes >= (1L << 31))
@@ -345,7 +378,7 @@ extern "C" int rdp_conv_rowband(const void* x1, const void* x2, long xbytes1, lo
   a.pool = pl ? (u16*)pool : nullptr; a.pbytes = pl ? (uint32_t)pbytes : 0u; a.ppitch = ppitch;
   a.escale = escale; a.eshift = eshift; a.erelu = erelu;
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.wshift = ws;
-  a.R = R; a.bands = H / R; a.cshift = cs; a.T = 9 * Cin / 32;
+  a.R = R; a.bands = H / R; a.cshift = cs; a.T = 9 * Cin / 32; a.wfrag = wfrag;
   const int grid = N * a.bands * (Cout / 32);
   if (PB == 16) hipLaunchKernelGGL((conv_rowband_kernel<2, 1, 4>), dim3(grid), dim3(512), 0, s, a);
   else if (PB == 32) hipLaunchKernelGGL((conv_rowband_kernel<2, 2, 2>), dim3(grid), dim3(512), 0, s, a);
@@ -391,7 +424,7 @@ extern "C" int rdp_conv_rowband_chain(int nl, const void* x, long xbytes, int C0
     a.pool = nullptr; a.pbytes = 0; a.ppitch = 0;
     a.escale = escale[l]; a.eshift = eshift[l]; a.erelu = 1;
     a.N = N; a.H = H; a.W = W; a.Cout = cout[l]; a.wshift = ws;
-    a.R = 1; a.bands = H; a.cshift = cs; a.T = 9 * cin / 32;
+    a.R = 1; a.bands = H; a.cshift = cs; a.T = 9 * cin / 32; a.wfrag = 0;
     c.nct[l] = cout[l] / 32;
     c.start[l + 1] = c.start[l] + N * H * c.nct[l];
     cin = cout[l];

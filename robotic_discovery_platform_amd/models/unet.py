@@ -335,6 +335,23 @@ class UNetNative(nn.Module):
             return self.derived[o:o + n].view(sp.cout, 128)
         return self.store.flat_slice(sp.name + ".weight", self.store.shadow).view(sp.cout, sp.taps * sp.cin)
 
+    def eval_frag_weight(self, sp: ConvSpec) -> Optional[torch.Tensor]:
+        """The fragment-major copy of ``sp``'s forward weights for the row-band eval conv, or None
+        (built by the eval executor's prepare_eval for its small-map layers)."""
+        return self.__dict__.get("_wfrag", {}).get(sp.name)
+
+    def refresh_eval_frag(self, specs) -> None:
+        """(Re)build the fragment-major eval weights of ``specs`` in place (stable pointers for captured
+        graphs): after a weight change, like the BN eval coefficients."""
+        d = self.__dict__.setdefault("_wfrag", {})
+        for sp in specs:
+            src = rowband_frag_weights(self.fwd_weight(sp))
+            buf = d.get(sp.name)
+            if buf is None or buf.shape != src.shape:
+                d[sp.name] = src
+            else:
+                buf.copy_(src)
+
     def dgrad_weight(self, sp: ConvSpec) -> torch.Tensor:
         o, n = self._dw[sp.name]
         return self.derived[o:o + n].view(sp.cin, sp.taps * sp.cout)
@@ -385,6 +402,14 @@ class _Ablated:
 
 _ABLATED = None
 
+
+
+def rowband_frag_weights(w: torch.Tensor) -> torch.Tensor:
+    """OHWI [Cout][9 Cin] bf16 -> the row-band eval conv's fragment-major layout
+    [Cout/16][9 Cin/32][64 lanes][8] (lane = 16 * 8-channel group + output row): every MFMA A fragment
+    is one contiguous KiB, 8 full cache lines per load instead of 16 half lines (csrc/conv_rowband.hip)."""
+    co, k = w.shape
+    return w.view(co // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(co, k)
 
 def _native():
     from ..ops import native
@@ -692,13 +717,15 @@ class UNetExecutor:
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
             # with ``pool`` / ``up``: MaxPool2d(2) / the upsample too (fused into the split-K reduce or
             # the row-ring epilogue where those run, else separate launches)
+            wf = m.eval_frag_weight(sp)
             if up is not None:
                 oy = (up.shape[1] - 2 * L.a.shape[1]) // 2
                 ox = (up.shape[2] - 2 * L.a.shape[2]) // 2
                 C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, None, up,
-                           oy, ox)
+                           oy, ox, wf)
                 return True
-            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool)
+            C.conv_fwd(L.x1, L.x2, w, sp.taps, int(sp.packed), L.a, None, None, 0, L.coef, 1, self.kws, pool, None, 0, 0,
+                       wf)
             return pool is not None
         if L.bnin is not None:  # the producer's BN + ReLU applied by this conv (row-ring BNIN)
             rows = C.conv_fwd_bnin(L.bnin.y, w, L.y, self.stats, L.bnin.coef, L.bnin.a)
@@ -728,6 +755,16 @@ class UNetExecutor:
             sp = L.spec
             C.bn_eval_coef(m.store.view(sp.bn + ".weight"), m.store.view(sp.bn + ".bias"),
                            m.buf(sp.bn + ".running_mean"), m.buf(sp.bn + ".running_var"), 1e-5, L.coef)
+        # the row-band eval conv's fragment-major weights for the small-map 3x3 layers (csrc/conv_rowband.hip;
+        # conv_fwd picks the kernel per layer from its traffic model)
+        if self.dev.type == "cuda":
+            m.refresh_eval_frag([L.spec for L in self.layers if self._rowband_candidate(L)])
+
+    def _rowband_candidate(self, L: "_Layer") -> bool:
+        sp = L.spec
+        n, h, w, _ = L.x1.shape
+        return (not sp.packed and sp.taps == 9 and sp.cout % 32 == 0 and n * h * w <= 4096 and w <= 64
+                and (sp.taps * sp.cin) % 32 == 0)
 
     def forward(self, head: bool = True, refresh_eval: bool = True, mask_head: Optional[tuple] = None):
         """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead).

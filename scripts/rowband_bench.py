@@ -27,6 +27,13 @@ SHAPES = [("down2.conv1", 64, 128, 0, 256, None), ("down2.conv2", 64, 256, 0, 25
           ("up2.conv1", 64, 256, 256, 256, None), ("up2.conv2", 64, 256, 0, 128, "up")]
 
 
+def frag_weights(w):
+    """OHWI [Cout][9 Cin] -> the row-band kernel's fragment-major layout [Cout/16][9 Cin/32][64 lanes][8]
+    (lane = 16 * (8-channel group) + row): every MFMA A fragment is 1 KiB contiguous."""
+    co, k = w.shape
+    return w.view(co // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(co, k)
+
+
 def chain_bench(C, a):
     """--chain: the 16^2 level (down4 conv1 -> conv2, 512 -> 512 -> 512) as two row-band launches vs one
     persistent chain launch (conv_rowband_chain: row readiness counters, no kernel boundary) vs the split-K
@@ -120,11 +127,16 @@ def main():
         y = torch.empty(N, H, H, Co, dtype=torch.bfloat16, device=dev)
         pool = torch.empty(N, H // 2, H // 2, Co, dtype=torch.bfloat16, device=dev) if fuse == "pool" else None
         up = torch.empty(N, 2 * H, 2 * H, Co, dtype=torch.bfloat16, device=dev) if fuse == "up" else None
-        n_ws = max(C.conv_ws_elems(N, H, H, C1, C2, Co, 9, 0, v) for v in variants)
+        n_ws = max(C.conv_ws_elems(N, H, H, C1, C2, Co, 9, 0, v) for v in variants if v != 17)
         ws = torch.zeros(max(n_ws, 1), device=dev)
         graphs = {}
+        wf = frag_weights(w)
         for v in variants:
             def run(v=v):
+                if v == 17:  # the row-band kernel on fragment-major weights
+                    if C.conv_rowband(x1, x2, wf, y, coef, pool, 1) < 0:
+                        raise RuntimeError("conv_rowband: shape not taken")
+                    return
                 C.conv_fwd(x1, x2, w, 9, 0, y, None, None, v, coef, 1, ws, pool, up, 0, 0)
             with torch.cuda.stream(s):
                 run()

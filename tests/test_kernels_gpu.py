@@ -1430,3 +1430,27 @@ def test_conv_rowband_chain(C, N, nl):
         assert int(err.item()) == 0
         for y, r in zip(ys, refs):
             assert torch.equal(y, r)
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pool", [(1, 32, 32, 256, 0, 512, False), (1, 16, 16, 512, 0, 512, True),
+                                                   (2, 64, 64, 128, 128, 128, False)])
+def test_conv_rowband_frag_weights(C, N, H, W, C1, C2, Cout, pool):
+    """conv_rowband on fragment-major weights == on OHWI weights, bitwise (same loads, other addresses)."""
+    from robotic_discovery_platform_amd.models.unet import rowband_frag_weights
+    torch.manual_seed(14)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, 9 * (C1 + C2), device=dev) / math.sqrt(9 * (C1 + C2)))
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev) * 0.1,
+                   torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev), 1e-5, coef)
+    outs = []
+    for wk, fr in ((w, 0), (rowband_frag_weights(w), 1)):
+        y = torch.full((N, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+        p = torch.full((N, H // 2, W // 2, Cout), float("nan"), dtype=torch.bfloat16, device=dev) if pool else None
+        assert C.conv_rowband(x1, x2, wk, y, coef, p, fr) == (1 if pool else 0)
+        outs.append((y, p))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if pool:
+        assert torch.equal(outs[0][1], outs[1][1])
