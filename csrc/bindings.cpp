@@ -609,15 +609,16 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     // the fused pool / upsample result flag: a heap cell owned by the launch (kept alive in a plan)
     auto pooled = std::make_shared<int>(0);
     // eval with the fragment-major weight copy (wfrag): the row-band kernel wherever its traffic model picks it
-    const bool frag = wfrag && esc && !sp && !y2 && taps == 9 && !packed && bm_pref == 0 &&
-                      rdp_conv_rowband_frag_auto(nn, a1.H, a1.W, a1.C + C2, Cout);
+    const int fmode = wfrag && esc && !sp && !y2 && taps == 9 && !packed && bm_pref == 0
+                          ? rdp_conv_rowband_frag_auto(nn, a1.H, a1.W, a1.C + C2, Cout) : 0;
+    const bool frag = fmode > 0;
     int r;
     if (frag) {
       void* const wfp = wfrag->data_ptr();
       const long wfb = wfrag->numel() * 2;
       const long pbytes = pool ? ((long)nn * po.H * po.W - 1) * ppit * 2 + (long)po.C * 2 : 0;
       const int rb = RDP_PLAN(rdp_conv_rowband_ex(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wfp, wfb, 0, py1, by1,
-                                                  o1.pitch, nn, a1.H, a1.W, Cout, esc, esh, relu, ppo, pbytes, ppit, 1,
+                                                  o1.pitch, nn, a1.H, a1.W, Cout, esc, esh, relu, ppo, pbytes, ppit, fmode,
                                                   st));
       TORCH_CHECK(rb >= 0, "conv_fwd: row-band kernel rejected a shape its model picked");
       *pooled = rb == 1 ? 1 : 0;

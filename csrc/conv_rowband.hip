@@ -47,6 +47,7 @@ struct RowbandArgs {
   int cshift;  // log2(Cin / 32): k-step -> tap
   int T;       // k-steps = 9 * Cin / 32
   int wfrag;   // 1: w is fragment-major (rdp_rowband_frag_weights): one k-step of 16 couts = 1 KiB contiguous
+  int segs;    // activation-staged variant: row segments of WB pixels per image row
 };
 
 // tap (0..8) -> (dr, ds) without division
@@ -223,6 +224,187 @@ __global__ __launch_bounds__(512, 4) void conv_rowband_kernel(const RowbandArgs 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Activation-staged variant (fragment-major weights only): the direct kernel reads every activation once
+// per tap (9x per 32-channel output slice) as 16 half cache lines per load. Here wave w owns the 32-channel
+// input chunks [w CC / 8, (w + 1) CC / 8) of all 9 taps; per chunk it stages the (R + 2) x (WB + 2) input
+// pixels x 32 channels of its tile ONCE into its own LDS region (zero halo from out-of-range offsets), and
+// the 9 taps read their shifted B fragments from there (16-B chunks XOR-swizzled by region column: the 16
+// pixels of a fragment hit 16 distinct 4-bank groups). Only this wave writes and reads its region, so no
+// block barrier is needed until the partial-tile exchange, which reuses the regions' LDS. A block owns
+// R image rows x WB (<= 32) pixels of one row segment x 32 output channels.
+template <int NPG, int R>
+__global__ __launch_bounds__(512, 2) void conv_rowband_x_kernel(const RowbandArgs a) {
+  constexpr int NF = 2, NWV = 8, NC = 32, PB = NPG * 16, WB = PB / R;
+  constexpr int RW = WB + 2, RR = R + 2;
+  constexpr int RBYTES = RR * RW * 64;
+  constexpr int NIT = RR * RW * 4;            // 16-B staging items per region
+  constexpr int NLD = (NIT + 63) / 64;        // per lane
+  constexpr int REDB = NWV * NF * NPG * 64 * 16;
+  constexpr int SMEM = NWV * RBYTES > REDB ? NWV * RBYTES : REDB;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ uint2 ytile[PB][NC / 4];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = a.N * a.bands * a.segs;  // tiles of one 32-channel output slice (consecutive: one XCD)
+  const int ct = (int)lid / nb;
+  int rem = (int)lid - ct * nb;
+  const int seg = rem % a.segs;
+  rem /= a.segs;
+  const int band = rem % a.bands, img = rem / a.bands;
+  const int h0 = band * R, w0 = seg * WB, cout0 = ct * NC;
+
+  const auto rx1 = make_rsrc(a.x1, a.xbytes1);
+  const auto rx2 = make_rsrc(a.x2 ? a.x2 : a.x1, a.x2 ? a.xbytes2 : 0u);
+  const auto rw = make_rsrc(a.w, a.wbytes);
+  char* const reg = smem + wave * RBYTES;
+  typedef __attribute__((address_space(3))) void lds_t;
+
+  // staging items of this lane: region pixel q = i >> 2 (row q / RW, column q % RW), 16-B part i & 3
+  int spix[NLD], sdst[NLD];
+#pragma unroll
+  for (int t = 0; t < NLD; ++t) {
+    const int i = lane + 64 * t, q = i >> 2, j = i & 3;
+    const int rr = q / RW, cc = q - rr * RW;
+    const int hh = h0 - 1 + rr, ww = w0 - 1 + cc;
+    const bool ok = i < NIT && inb(hh, a.H) && inb(ww, a.W);
+    spix[t] = ok ? ((img * a.H + hh) << a.wshift) + ww : -1;
+    sdst[t] = i < NIT ? q * 64 + 16 * (j ^ ((cc >> 2) & 3)) : -1;
+  }
+  uint4 xr[NLD];
+  auto load_x = [&](int chunk) {
+    const int cb = chunk * 32;
+    const bool s2 = cb >= a.C1;  // wave-uniform
+    const int pitch = s2 ? a.pitch2 : a.pitch1;
+    const int ch = s2 ? cb - a.C1 : cb;
+#pragma unroll
+    for (int t = 0; t < NLD; ++t) {
+      const int j = (lane + 64 * t) & 3;
+      const uint32_t off = spix[t] >= 0 ? (uint32_t)(spix[t] * pitch + ch + 8 * j) * 2u : RDP_OOB;
+      xr[t] = bload16(s2 ? rx2 : rx1, off);
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int t = 0; t < NLD; ++t)
+      if (sdst[t] >= 0) *(uint4*)(reg + sdst[t]) = xr[t];
+  };
+  // B fragment geometry: block pixel p = 16 g + (lane & 15) -> tile row p / WB, column p % WB
+  int brow[NPG], bcol[NPG];
+#pragma unroll
+  for (int g = 0; g < NPG; ++g) {
+    const int p = 16 * g + (lane & 15);
+    brow[g] = p / WB;
+    bcol[g] = p - brow[g] * WB;
+  }
+  const int gq = lane >> 4;
+  const int CC = a.T / 9;
+  uint32_t wbase[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) wbase[f] = (uint32_t)((cout0 / 16 + f) * a.T) * 1024u + (uint32_t)lane * 16u;
+
+  f32x4 acc[NF][NPG];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int g = 0; g < NPG; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int c0 = wave * CC / NWV, c1 = (wave + 1) * CC / NWV;
+  if (c0 < c1) {
+    load_x(c0);
+    store_x();
+  }
+  for (int chunk = c0; chunk < c1; ++chunk) {
+    if (chunk + 1 < c1) load_x(chunk + 1);  // lands under this chunk's taps
+    bf16x8 wa[2][3][NF];
+    auto load_w = [&](int tg, bf16x8 (&dst)[3][NF]) {
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const int ks = (3 * tg + tt) * CC + chunk;  // tap-major k-step of the fragment-major layout
+          dst[tt][f] = __builtin_bit_cast(bf16x8, bload16(rw, wbase[f] + (uint32_t)ks * 1024u));
+        }
+    };
+    load_w(0, wa[0]);
+#pragma unroll
+    for (int tg = 0; tg < 3; ++tg) {  // dr = tg - 1
+      if (tg < 2) load_w(tg + 1, wa[(tg + 1) & 1]);
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) {  // ds = tt - 1
+        bf16x8 fb[NPG];
+#pragma unroll
+        for (int g = 0; g < NPG; ++g) {
+          const int rr = brow[g] + tg, cc = bcol[g] + tt;
+          fb[g] = *(const bf16x8*)(reg + (rr * RW + cc) * 64 + 16 * (gq ^ ((cc >> 2) & 3)));
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+          for (int g = 0; g < NPG; ++g)
+            acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[tg & 1][tt][f], fb[g], acc[f][g], 0, 0, 0);
+      }
+    }
+    if (chunk + 1 < c1) store_x();  // after this wave's reads of the region (LDS ops of a wave stay in order)
+  }
+
+  // partial tiles of the 8 waves -> LDS (the regions' bytes: every wave is past its reads)
+  __syncthreads();
+  f32x4* red = (f32x4*)smem;  // [NWV][NF * NPG][64]
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int g = 0; g < NPG; ++g) red[(wave * NF * NPG + f * NPG + g) * 64 + lane] = acc[f][g];
+  __syncthreads();
+  const auto ry = make_rsrc(a.y, a.ybytes);
+  for (int u = threadIdx.x; u < NF * NPG * 64; u += NWV * 64) {
+    const int q = u >> 6, l = u & 63;
+    f32x4 v = red[q * 64 + l];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) v += red[(w * NF * NPG + q) * 64 + l];
+    const int f = q / NPG, g = q - f * NPG;
+    const int cl = 16 * f + 4 * (l >> 4);
+    const int c = cout0 + cl;
+    const float4 sc = *(const float4*)(a.escale + c), sh = *(const float4*)(a.eshift + c);
+    float o[4] = {fmaf(v[0], sc.x, sh.x), fmaf(v[1], sc.y, sh.y), fmaf(v[2], sc.z, sh.z), fmaf(v[3], sc.w, sh.w)};
+    if (a.erelu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+    }
+    const uint2 pk = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+    const int p = 16 * g + (l & 15);
+    const int pr = p / WB, pc = p - pr * WB;
+    const int m = ((img * a.H + h0 + pr) << a.wshift) + w0 + pc;
+    bstore8(ry, (uint32_t)(m * a.ypitch + c) * 2u, pk);
+    if (a.pool) ytile[p][cl >> 2] = pk;
+  }
+  if (!a.pool) return;  // block-uniform; R == 2 here
+  __syncthreads();
+  const auto rp = make_rsrc(a.pool, a.pbytes);
+  for (int u = threadIdx.x; u < (WB / 2) * (NC / 4); u += NWV * 64) {
+    const int wo = u / (NC / 4), cq = u - wo * (NC / 4);
+    const int p00 = 2 * wo, p10 = WB + 2 * wo;
+    const uint2 qv[4] = {ytile[p00][cq], ytile[p00 + 1][cq], ytile[p10][cq], ytile[p10 + 1][cq]};
+    float mx[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t wd = e < 2 ? qv[0].x : qv[0].y;
+      mx[e] = __uint_as_float((e & 1) ? (wd & 0xffff0000u) : (wd << 16));
+    }
+#pragma unroll
+    for (int t = 1; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t wd = e < 2 ? qv[t].x : qv[t].y;
+        mx[e] = fmaxf(mx[e], __uint_as_float((e & 1) ? (wd & 0xffff0000u) : (wd << 16)));
+      }
+    const int mo = (img * (a.H >> 1) + (h0 >> 1)) * (a.W >> 1) + (w0 >> 1) + wo;
+    bstore8(rp, (uint32_t)(mo * a.ppitch + cout0 + 4 * cq) * 2u, make_uint2(pack2bf(mx[0], mx[1]), pack2bf(mx[2], mx[3])));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Persistent chain of row-band layers of one map size (layer l + 1's input = layer l's output) in ONE
 // launch with row-level readiness counters instead of kernel boundaries (measured
 // against the per-layer launches by scripts/rowband_bench.py --chain, profiles/dead_ends.md).
@@ -329,7 +511,12 @@ extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int Cin, int Cout
   }();
   if (!on || (long)N * H * W > 4096 || W > 64 || W < 16 || Cin < 128 || Cout < 64 || Cout % 32) return 0;
   const long wb = (long)Cout * 9 * Cin * 2, xb = (long)N * H * W * Cin * 2;
-  return wb * ((long)N * H) / 2 + xb * 9 * (Cout / 32) <= 250000000L;
+  static const int xon = [] {
+    const char* e = getenv("RDP_ROWBAND_X");
+    return e ? atoi(e) : 1;
+  }();
+  if (xon && (Cin / 32) % 8 == 0) return 2;  // the activation-staged kernel (x read ~3x instead of 9x)
+  return wb * ((long)N * H) / 2 + xb * 9 * (Cout / 32) <= 250000000L ? 1 : 0;
 }
 
 static int ilog2_exact(long v) {
@@ -365,6 +552,30 @@ extern "C" int rdp_conv_rowband_ex(const void* x1, const void* x2, long xbytes1,
   if (xbytes1 >= (1L << 31) || xbytes2 >= (1L << 31) || wbytes >= (1L << 31) || ybytes >= (1L << 31) ||
       pbytes >= (1L << 31))
     return -1;
+  if (wfrag == 2) {  // the activation-staged kernel: 32-channel chunks, 8 per wave at least one
+    if ((Cin / 32) % 8) return -1;
+    const int WB = W < 32 ? W : 32;
+    const bool plx = pool != nullptr && H % 2 == 0 && ppitch % 4 == 0;
+    const int Rx = plx ? 2 : 1;
+    RowbandArgs a;
+    a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
+    a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
+    a.C1 = C1; a.C2 = C2; a.pitch1 = pitch1; a.pitch2 = pitch2;
+    a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
+    a.y = (u16*)y; a.ybytes = (uint32_t)ybytes; a.ypitch = ypitch;
+    a.pool = plx ? (u16*)pool : nullptr; a.pbytes = plx ? (uint32_t)pbytes : 0u; a.ppitch = ppitch;
+    a.escale = escale; a.eshift = eshift; a.erelu = erelu;
+    a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.wshift = ws;
+    a.R = Rx; a.bands = H / Rx; a.cshift = cs; a.T = 9 * Cin / 32; a.wfrag = 1; a.segs = W / WB;
+    const int grid = N * a.bands * a.segs * (Cout / 32);
+    const int PBx = Rx * WB;
+    if (PBx == 16) hipLaunchKernelGGL((conv_rowband_x_kernel<1, 1>), dim3(grid), dim3(512), 0, s, a);
+    else if (PBx == 32 && Rx == 1) hipLaunchKernelGGL((conv_rowband_x_kernel<2, 1>), dim3(grid), dim3(512), 0, s, a);
+    else if (PBx == 32) hipLaunchKernelGGL((conv_rowband_x_kernel<2, 2>), dim3(grid), dim3(512), 0, s, a);
+    else if (PBx == 64) hipLaunchKernelGGL((conv_rowband_x_kernel<4, 2>), dim3(grid), dim3(512), 0, s, a);
+    else return -1;
+    return plx ? 1 : 0;
+  }
   // the pool needs two rows per block: only where that block is <= 64 pixels (else the caller pools)
   const bool pl = pool != nullptr && H % 2 == 0 && ppitch % 4 == 0 && 2 * W <= 64;
   const int R = pl ? 2 : 1;

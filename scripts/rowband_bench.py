@@ -24,7 +24,8 @@ SHAPES = [("down2.conv1", 64, 128, 0, 256, None), ("down2.conv2", 64, 256, 0, 25
           ("down3.conv1", 32, 256, 0, 512, None), ("down3.conv2", 32, 512, 0, 512, "pool"),
           ("down4.conv1", 16, 512, 0, 512, None), ("down4.conv2", 16, 512, 0, 512, "up"),
           ("up1.conv1", 32, 512, 512, 512, None), ("up1.conv2", 32, 512, 0, 256, "up"),
-          ("up2.conv1", 64, 256, 256, 256, None), ("up2.conv2", 64, 256, 0, 128, "up")]
+          ("up2.conv1", 64, 256, 256, 256, None), ("up2.conv2", 64, 256, 0, 128, "up"),
+          ("up3.conv1", 128, 128, 128, 128, None)]
 
 
 def frag_weights(w):
@@ -127,14 +128,16 @@ def main():
         y = torch.empty(N, H, H, Co, dtype=torch.bfloat16, device=dev)
         pool = torch.empty(N, H // 2, H // 2, Co, dtype=torch.bfloat16, device=dev) if fuse == "pool" else None
         up = torch.empty(N, 2 * H, 2 * H, Co, dtype=torch.bfloat16, device=dev) if fuse == "up" else None
-        n_ws = max(C.conv_ws_elems(N, H, H, C1, C2, Co, 9, 0, v) for v in variants if v != 17)
+        n_ws = max(C.conv_ws_elems(N, H, H, C1, C2, Co, 9, 0, v) for v in variants if v < 17)
         ws = torch.zeros(max(n_ws, 1), device=dev)
         graphs = {}
         wf = frag_weights(w)
         for v in variants:
+            if v == 18 and (Cin // 32) % 8:  # the activation-staged kernel needs >= 8 chunks of 32 channels
+                continue
             def run(v=v):
-                if v == 17:  # the row-band kernel on fragment-major weights
-                    if C.conv_rowband(x1, x2, wf, y, coef, pool, 1) < 0:
+                if v in (17, 18):  # the row-band kernel on fragment-major weights (18: activation-staged)
+                    if C.conv_rowband(x1, x2, wf, y, coef, pool, v - 16) < 0:
                         raise RuntimeError("conv_rowband: shape not taken")
                     return
                 C.conv_fwd(x1, x2, w, 9, 0, y, None, None, v, coef, 1, ws, pool, up, 0, 0)
@@ -146,9 +149,9 @@ def main():
                 for _ in range(a.reps):
                     run()
             graphs[v] = g
-        times = {v: [] for v in variants}
+        times = {v: [] for v in graphs}
         for _ in range(a.rounds):
-            for v in variants:
+            for v in graphs:
                 graphs[v].replay()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -158,7 +161,7 @@ def main():
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1) * 1000.0 / a.reps)
         row = {"layer": name, "H": H, "cin": Cin, "cout": Co, "fused": fuse}
-        for v in variants:
+        for v in graphs:
             t = statistics.median(times[v])
             row[f"us_v{v}"] = round(t, 2)
             total[v] += t

@@ -1454,3 +1454,36 @@ def test_conv_rowband_frag_weights(C, N, H, W, C1, C2, Cout, pool):
     assert torch.equal(outs[0][0], outs[1][0])
     if pool:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,pool", [
+    (1, 32, 32, 256, 0, 512, False), (1, 32, 32, 512, 0, 512, True), (1, 16, 16, 512, 0, 512, True),
+    (1, 32, 32, 512, 512, 512, False), (1, 64, 64, 256, 0, 256, True), (1, 64, 64, 256, 256, 256, False),
+    (2, 16, 32, 256, 0, 96, True)])
+def test_conv_rowband_staged(C, N, H, W, C1, C2, Cout, pool):
+    """Activation-staged row-band conv (conv_rowband mode 2, fragment-major weights): vs fp32 torch, the
+    pool bitwise the 2x2 max of the output, the unpooled call bitwise the pooled one's output, and
+    deterministic."""
+    from robotic_discovery_platform_amd.models.unet import rowband_frag_weights
+    torch.manual_seed(15)
+    dev = "cuda"
+    x1 = bf(torch.randn(N, H, W, C1, device=dev))
+    x2 = bf(torch.randn(N, H, W, C2, device=dev)) if C2 else None
+    w = bf(torch.randn(Cout, C1 + C2, 3, 3, device=dev) / math.sqrt(9 * (C1 + C2)))
+    wf = rowband_frag_weights(ohwi(w).contiguous())
+    g, b = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    coef = torch.zeros(4 * Cout, device=dev)
+    C.bn_eval_coef(g, b, rm, rv, 1e-5, coef)
+    a = torch.full((N, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    p = torch.full((N, H // 2, W // 2, Cout), float("nan"), dtype=torch.bfloat16, device=dev) if pool else None
+    assert C.conv_rowband(x1, x2, wf, a, coef, p, 2) == (1 if pool else 0)
+    xin = nchw(x1).float() if x2 is None else torch.cat([nchw(x1), nchw(x2)], 1).float()
+    ref = F.relu(F.batch_norm(F.conv2d(xin, w.float(), padding=1), rm, rv, g, b, False, 0.0, 1e-5))
+    assert not torch.isnan(a.float()).any()
+    assert relerr(nchw(a), ref) < 1e-2
+    if pool:
+        assert torch.equal(p, F.max_pool2d(nchw(a).float(), 2).to(torch.bfloat16).permute(0, 2, 3, 1))
+    a2 = torch.empty_like(a)
+    assert C.conv_rowband(x1, x2, wf, a2, coef, None, 2) == 0
+    assert torch.equal(a, a2)
