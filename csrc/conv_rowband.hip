@@ -509,13 +509,15 @@ extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int Cin, int Cout
     const char* e = getenv("RDP_ROWBAND");
     return e ? atoi(e) : 1;
   }();
-  if (!on || (long)N * H * W > 4096 || W > 64 || W < 16 || Cin < 128 || Cout < 64 || Cout % 32) return 0;
-  const long wb = (long)Cout * 9 * Cin * 2, xb = (long)N * H * W * Cin * 2;
-  static const int xon = [] {
-    const char* e = getenv("RDP_ROWBAND_X");
-    return e ? atoi(e) : 1;
+  if (!on || W < 16 || Cin < 128 || Cout < 64 || Cout % 32) return 0;
+  const long M = (long)N * H * W;
+  const long wb = (long)Cout * 9 * Cin * 2, xb = M * Cin * 2;
+  static const long xmax = [] {
+    const char* e = getenv("RDP_ROWBAND_X_MAXPIX");  // 0 turns the activation-staged kernel off
+    return e ? atol(e) : 16384L;  // up3.conv1 at 128^2: 29.6 -> 22.6 us (scripts/rowband_bench.py)
   }();
-  if (xon && (Cin / 32) % 8 == 0) return 2;  // the activation-staged kernel (x read ~3x instead of 9x)
+  if ((Cin / 32) % 8 == 0 && M <= xmax && W <= 256) return 2;  // activation-staged (x read ~3x instead of 9x)
+  if (M > 4096 || W > 64) return 0;
   return wb * ((long)N * H) / 2 + xb * 9 * (Cout / 32) <= 250000000L ? 1 : 0;
 }
 
@@ -545,7 +547,8 @@ extern "C" int rdp_conv_rowband_ex(const void* x1, const void* x2, long xbytes1,
                                    int erelu, void* pool, long pbytes, int ppitch, int wfrag, hipStream_t s) {
   const int Cin = C1 + C2;
   const int cs = ilog2_exact(Cin / 32), ws = ilog2_exact(W);
-  if (C1 % 32 || C2 % 32 || Cin < 64 || Cin % 32 || cs < 0 || ws < 4 || W > 64 || Cout % 32) return -1;
+  if (C1 % 32 || C2 % 32 || Cin < 64 || Cin % 32 || cs < 0 || ws < 4 || W > (wfrag == 2 ? 256 : 64) || Cout % 32)
+    return -1;
   if (!escale || !eshift || (!wfrag && ldw < 9 * Cin) || (wfrag && wbytes < (long)Cout * 9 * Cin * 2) || (C2 && !x2))
     return -1;
   if (pitch1 % 8 || (C2 && pitch2 % 8) || ypitch % 4) return -1;

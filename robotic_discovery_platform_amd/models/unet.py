@@ -763,8 +763,10 @@ class UNetExecutor:
     def _rowband_candidate(self, L: "_Layer") -> bool:
         sp = L.spec
         n, h, w, _ = L.x1.shape
-        return (not sp.packed and sp.taps == 9 and sp.cout % 32 == 0 and n * h * w <= 4096 and w <= 64
-                and (sp.taps * sp.cin) % 32 == 0)
+        if sp.packed or sp.taps != 9 or sp.cout % 32 or (sp.taps * sp.cin) % 32:
+            return False
+        # the direct kernel up to 64^2 maps; the activation-staged one (>= 256 input channels) up to 128^2
+        return (n * h * w <= 4096 and w <= 64) or (sp.cin % 256 == 0 and n * h * w <= 16384)
 
     def forward(self, head: bool = True, refresh_eval: bool = True, mask_head: Optional[tuple] = None):
         """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead).
