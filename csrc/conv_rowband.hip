@@ -19,6 +19,14 @@
 // Block -> tile: consecutive logical ids (one XCD after xcd_remap) are consecutive row bands of ONE
 // 32-channel output slice, so that slice's weights (32 x 9 Cin bf16) are fetched into that XCD's L2
 // once and re-read there by every band.
+//
+// Three forms live here:
+//   * conv_rowband_kernel: the direct form above (OHWI or fragment-major weights);
+//   * conv_rowband_x_kernel: fragment-major weights + each wave's 32-channel input chunk staged once per
+//     tile in LDS for all 9 taps (the serving default wherever the input has 64, 128 or 256k channels);
+//   * conv_rowband_chain_kernel: the persistent multi-layer experiment (measured slower, kept tested).
+// The eval dispatch is rdp_conv_rowband_frag_auto (bindings conv_fwd with the executor's fragment-major
+// weights); rdp_conv_rowband_bytes is the OHWI form's traffic model used by rdp_conv_igemm.
 #include "common.h"
 #include <algorithm>
 #include <stdlib.h>
@@ -310,7 +318,19 @@ __global__ __launch_bounds__(512, 2) void conv_rowband_x_kernel(const RowbandArg
 #pragma unroll
     for (int g = 0; g < NPG; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int c0 = wave * CC / NWV, c1 = (wave + 1) * CC / NWV;
+  // K split over the waves: >= 8 chunks -> whole chunks (all 9 taps) per wave; 2 or 4 chunks (64 / 128 input
+  // channels) -> 8 / CC waves per chunk, each staging it and taking a range of its taps
+  int c0, c1, t0 = 0, t1 = 9;
+  if (CC >= NWV) {
+    c0 = wave * CC / NWV;
+    c1 = (wave + 1) * CC / NWV;
+  } else {
+    const int G = NWV / CC, part = wave % G;
+    c0 = wave / G;
+    c1 = c0 + 1;
+    t0 = part * 9 / G;
+    t1 = (part + 1) * 9 / G;
+  }
   if (c0 < c1) {
     load_x(c0);
     store_x();
@@ -320,12 +340,15 @@ __global__ __launch_bounds__(512, 2) void conv_rowband_x_kernel(const RowbandArg
     bf16x8 wa[2][3][NF];
     auto load_w = [&](int tg, bf16x8 (&dst)[3][NF]) {
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt)
+      for (int tt = 0; tt < 3; ++tt) {
+        const int tap = 3 * tg + tt;
+        if (tap < t0 || tap >= t1) continue;  // wave-uniform
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          const int ks = (3 * tg + tt) * CC + chunk;  // tap-major k-step of the fragment-major layout
+          const int ks = tap * CC + chunk;  // tap-major k-step of the fragment-major layout
           dst[tt][f] = __builtin_bit_cast(bf16x8, bload16(rw, wbase[f] + (uint32_t)ks * 1024u));
         }
+      }
     };
     load_w(0, wa[0]);
 #pragma unroll
@@ -333,6 +356,7 @@ __global__ __launch_bounds__(512, 2) void conv_rowband_x_kernel(const RowbandArg
       if (tg < 2) load_w(tg + 1, wa[(tg + 1) & 1]);
 #pragma unroll
       for (int tt = 0; tt < 3; ++tt) {  // ds = tt - 1
+        if (3 * tg + tt < t0 || 3 * tg + tt >= t1) continue;  // wave-uniform
         bf16x8 fb[NPG];
 #pragma unroll
         for (int g = 0; g < NPG; ++g) {
@@ -509,14 +533,16 @@ extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int Cin, int Cout
     const char* e = getenv("RDP_ROWBAND");
     return e ? atoi(e) : 1;
   }();
-  if (!on || W < 16 || Cin < 128 || Cout < 64 || Cout % 32) return 0;
+  if (!on || W < 16 || Cin < 64 || Cout < 64 || Cout % 32) return 0;
   const long M = (long)N * H * W;
   const long wb = (long)Cout * 9 * Cin * 2, xb = M * Cin * 2;
   static const long xmax = [] {
     const char* e = getenv("RDP_ROWBAND_X_MAXPIX");  // 0 turns the activation-staged kernel off
     return e ? atol(e) : 16384L;  // up3.conv1 at 128^2: 29.6 -> 22.6 us (scripts/rowband_bench.py)
   }();
-  if ((Cin / 32) % 8 == 0 && M <= xmax && W <= 256) return 2;  // activation-staged (x read ~3x instead of 9x)
+  // (64 input channels stay on the split-K GEMM: 128^2 64 -> 128 18.0 vs 11.5 us, four waves staging one chunk)
+  const bool xch = (Cin / 32) % 8 == 0 || Cin == 128;
+  if (xch && M <= xmax && W <= 256) return 2;  // activation-staged (x read ~3x instead of 9x)
   if (M > 4096 || W > 64) return 0;
   return wb * ((long)N * H) / 2 + xb * 9 * (Cout / 32) <= 250000000L ? 1 : 0;
 }
@@ -555,8 +581,8 @@ extern "C" int rdp_conv_rowband_ex(const void* x1, const void* x2, long xbytes1,
   if (xbytes1 >= (1L << 31) || xbytes2 >= (1L << 31) || wbytes >= (1L << 31) || ybytes >= (1L << 31) ||
       pbytes >= (1L << 31))
     return -1;
-  if (wfrag == 2) {  // the activation-staged kernel: 32-channel chunks, 8 per wave at least one
-    if ((Cin / 32) % 8) return -1;
+  if (wfrag == 2) {  // the activation-staged kernel: 32-channel chunks (a multiple of 8, or 2 / 4)
+    if ((Cin / 32) % 8 && Cin != 64 && Cin != 128) return -1;
     const int WB = W < 32 ? W : 32;
     const bool plx = pool != nullptr && H % 2 == 0 && ppitch % 4 == 0;
     const int Rx = plx ? 2 : 1;

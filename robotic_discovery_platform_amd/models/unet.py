@@ -766,7 +766,8 @@ class UNetExecutor:
         if sp.packed or sp.taps != 9 or sp.cout % 32 or (sp.taps * sp.cin) % 32:
             return False
         # the direct kernel up to 64^2 maps; the activation-staged one (>= 256 input channels) up to 128^2
-        return (n * h * w <= 4096 and w <= 64) or (sp.cin % 256 == 0 and n * h * w <= 16384)
+        staged = sp.cin % 256 == 0 or sp.cin == 128
+        return (n * h * w <= 4096 and w <= 64) or (staged and n * h * w <= 16384)
 
     def forward(self, head: bool = True, refresh_eval: bool = True, mask_head: Optional[tuple] = None):
         """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead).

@@ -25,7 +25,8 @@ SHAPES = [("down2.conv1", 64, 128, 0, 256, None), ("down2.conv2", 64, 256, 0, 25
           ("down4.conv1", 16, 512, 0, 512, None), ("down4.conv2", 16, 512, 0, 512, "up"),
           ("up1.conv1", 32, 512, 512, 512, None), ("up1.conv2", 32, 512, 0, 256, "up"),
           ("up2.conv1", 64, 256, 256, 256, None), ("up2.conv2", 64, 256, 0, 128, "up"),
-          ("up3.conv1", 128, 128, 128, 128, None)]
+          ("up3.conv1", 128, 128, 128, 128, None), ("down1.conv1", 128, 64, 0, 128, None),
+          ("down1.conv2", 128, 128, 0, 128, "pool"), ("up3.conv2", 128, 128, 0, 64, "up")]
 
 
 def frag_weights(w):
@@ -133,7 +134,7 @@ def main():
         graphs = {}
         wf = frag_weights(w)
         for v in variants:
-            if v == 18 and (Cin // 32) % 8:  # the activation-staged kernel needs >= 8 chunks of 32 channels
+            if v == 18 and (Cin // 32) % 8 and Cin not in (64, 128):  # staged: 2, 4 or 8k chunks of 32 channels
                 continue
             def run(v=v):
                 if v in (17, 18):  # the row-band kernel on fragment-major weights (18: activation-staged)

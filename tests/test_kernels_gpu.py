@@ -1459,7 +1459,8 @@ def test_conv_rowband_frag_weights(C, N, H, W, C1, C2, Cout, pool):
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pool", [
     (1, 32, 32, 256, 0, 512, False), (1, 32, 32, 512, 0, 512, True), (1, 16, 16, 512, 0, 512, True),
     (1, 32, 32, 512, 512, 512, False), (1, 64, 64, 256, 0, 256, True), (1, 64, 64, 256, 256, 256, False),
-    (2, 16, 32, 256, 0, 96, True)])
+    (2, 16, 32, 256, 0, 96, True), (1, 128, 128, 128, 0, 128, True), (1, 128, 128, 64, 0, 128, False),
+    (1, 64, 64, 64, 64, 64, False), (2, 32, 32, 128, 0, 256, True)])
 def test_conv_rowband_staged(C, N, H, W, C1, C2, Cout, pool):
     """Activation-staged row-band conv (conv_rowband mode 2, fragment-major weights): vs fp32 torch, the
     pool bitwise the 2x2 max of the output, the unpooled call bitwise the pooled one's output, and
