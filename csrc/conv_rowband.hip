@@ -1,4 +1,4 @@
-// Row-band convolution for small eval feature maps (serving at N = 1..4: the 64^2 .. 16^2 levels),
+// Row-band convolution for small eval feature maps (serving at N = 1: the 128^2 .. 16^2 levels),
 // NHWC bf16, 3x3, BN folded into the epilogue + ReLU, optional fused MaxPool2d(2).
 //
 // Replaces, at these sizes, the implicit GEMM + split-K slab + reduce launch pair
@@ -9,7 +9,7 @@
 // The LDS-staged GEMM tile needs split-K to fill 256 CUs, then pays a per-K-step block barrier on a
 // two-deep DMA pipeline (~0.75 us per step at 1 block / CU), an fp32 slab round trip and a second
 // launch. Here a block owns R image rows x 32 output channels with the WHOLE K, split over its 8 waves
-// by input channel (wave w: channels [w Cin / 8, (w + 1) Cin / 8) of all 9 taps). Both MFMA operands are
+// (wave w: the w-th eighth of the tap-major k-steps, 32 channels of one tap each). Both MFMA operands are
 // read straight from global memory into registers -- a 16x16x32 bf16 fragment row is 8 consecutive
 // channels, i.e. 16 contiguous bytes of NHWC activations or OHWI weights -- so a wave issues its loads
 // G k-steps ahead with no barrier and no LDS until the end, where the 8 partial tiles are summed in LDS
@@ -23,7 +23,7 @@
 // Three forms live here:
 //   * conv_rowband_kernel: the direct form above (OHWI or fragment-major weights);
 //   * conv_rowband_x_kernel: fragment-major weights + each wave's 32-channel input chunk staged once per
-//     tile in LDS for all 9 taps (the serving default wherever the input has 64, 128 or 256k channels);
+//     tile in LDS for all 9 taps (the serving default wherever the input has 128 or 256k channels);
 //   * conv_rowband_chain_kernel: the persistent multi-layer experiment (measured slower, kept tested).
 // The eval dispatch is rdp_conv_rowband_frag_auto (bindings conv_fwd with the executor's fragment-major
 // weights); rdp_conv_rowband_bytes is the OHWI form's traffic model used by rdp_conv_igemm.
@@ -54,7 +54,7 @@ struct RowbandArgs {
   int bands;   // H / R
   int cshift;  // log2(Cin / 32): k-step -> tap
   int T;       // k-steps = 9 * Cin / 32
-  int wfrag;   // 1: w is fragment-major (rdp_rowband_frag_weights): one k-step of 16 couts = 1 KiB contiguous
+  int wfrag;   // 1: w is fragment-major (models/unet.py rowband_frag_weights): 16 couts x 1 k-step = 1 KiB
   int segs;    // activation-staged variant: row segments of WB pixels per image row
 };
 
