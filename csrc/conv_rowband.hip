@@ -585,7 +585,15 @@ extern "C" int rdp_conv_rowband_ex(const void* x1, const void* x2, long xbytes1,
     if ((Cin / 32) % 8 && Cin != 64 && Cin != 128) return -1;
     const int WB = W < 32 ? W : 32;
     const bool plx = pool != nullptr && H % 2 == 0 && ppitch % 4 == 0;
-    const int Rx = plx ? 2 : 1;
+    // two-row tiles (each block's weight slice serves twice the pixels) wherever that grid still has >= 256
+    // blocks: up1.conv1 22.4 -> 18.2 us, up2.conv1 24.5 -> 21.9, down3.conv1 7.8 -> 6.9 (at 128 blocks, the
+    // 16^2 and 32^2 -> 256 convs, one-row tiles stay faster); RDP_ROWBAND_R2=0 keeps one-row tiles (A/B)
+    static const int r2_on = [] {
+      const char* e = getenv("RDP_ROWBAND_R2");
+      return e ? atoi(e) : 1;
+    }();
+    const bool r2 = r2_on && H % 2 == 0 && (long)N * (H / 2) * (W / (W < 32 ? W : 32)) * (Cout / 32) >= 256;
+    const int Rx = plx || r2 ? 2 : 1;
     RowbandArgs a;
     a.x1 = (const u16*)x1; a.x2 = (const u16*)x2;
     a.xbytes1 = (uint32_t)xbytes1; a.xbytes2 = (uint32_t)xbytes2;
