@@ -90,7 +90,7 @@ int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_comm_emulate(double, int, hipStream_t);
 int rdp_rows_fold(const float*, int, int, double*, hipStream_t);
 int rdp_rows_hilo(const double*, float*, int, hipStream_t);
-int rdp_wprep(const float*, void*, const void*, int, int*, int, hipStream_t);
+int rdp_wprep(const float*, void*, const void*, int, int*, int, int, hipStream_t);
 int rdp_wseg_size();
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
 double rdp_splev1(const double*, int, const double*, int, double, int);
@@ -1199,7 +1199,7 @@ void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg
     TORCH_CHECK(step->scalar_type() == torch::kInt32 && step->is_cuda(), "step int32");
     sp = (int*)step->data_ptr();
   }
-  RDP_PLAN(rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, sp, blocks, st));
+  RDP_PLAN(rdp_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), nseg, sp, blocks, 0, st));
 }
 
 void check_cpu_f64(const torch::Tensor& t, const char* name) {

@@ -67,50 +67,96 @@ struct WSeg {
   long src;  // element offset in the fp32 master
   long dst;  // element offset in the bf16 derived buffer
   int kind, cout, cin, taps;
+  int tile0;  // first work tile of this segment in the table's flat tile range
+  int pad;
 };
 
-// kind 0 is a per-tap 2-D transpose ([cout][cin] -> [cin][cout]); it goes through a 64x64 LDS tile
-// so both the fp32 reads (along cin) and the bf16 writes (along cout) are coalesced. (The direct
-// element-wise gather read the masters with a stride of taps*cin floats: ~130 us per step.)
+// Work tiles of a segment: kind 0 = one 64 x 64 (cout x cin) block of one tap, kind 1 = 256 threads x 8
+// packed elements. The table carries each segment's first tile (tile0), so the launch is ONE flat range
+// of real tiles (grid-strided) instead of a [max tiles] x [segments] grid that was mostly early-exit
+// blocks.
+RDP_DEV int wseg_tiles(const WSeg& sg) {
+  return sg.kind == 0 ? sg.taps * ((sg.cout + 63) >> 6) * ((sg.cin + 63) >> 6) : (sg.cout * 128 + 2047) >> 11;
+}
+
+// kind 0 is a per-tap 2-D transpose ([cout][cin] -> [cin][cout]) through a 64 x 64 bf16 LDS tile:
+// fp32 masters read as 16-B vectors along cin (a 64-float row = one full 256-B line per 16 lanes),
+// converted to bf16 and scattered transposed into LDS ([cin][cout]); the bf16 rows go out as 16-B
+// vectors along cout (128 B per cin row). The first form moved 4-B loads / 2-B stores per element
+// through a [cout][cin] tile (430 us of shared CU time per bs-64 step beside the forward, 67 us alone
+// at bs 4: profiles/train_step_kernels.md). Segments with cin % 4, cout % 8 or unaligned offsets take the
+// scalar path (the model's 64-element parameter alignment never does).
 // step != nullptr: also advance Adam's device step counter (the optimizer step just ran on the
 // same stream, so every Adam block has read it) -- one launch fewer than a separate increment
 __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ master, u16* __restrict__ out,
-                                                    const WSeg* __restrict__ segs, int* __restrict__ step) {
-  const WSeg sg = segs[blockIdx.y];
+                                                    const WSeg* __restrict__ segs, int nseg, int total,
+                                                    int* __restrict__ step) {
+  __shared__ __attribute__((aligned(16))) u16 tile[64][72];  // [cin][cout], 144-B rows (16-B aligned)
   const int tid = threadIdx.x;
-  if (step && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) step[0] += 1;
-  if (sg.kind == 0) {
-    __shared__ u16 tile[64][66];
-    const int tco = (sg.cout + 63) >> 6, tci = (sg.cin + 63) >> 6;
-    const int ntiles = sg.taps * tco * tci;
-    const int lc = tid & 63, lr = tid >> 6;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-      const int tap = t % sg.taps, r = t / sg.taps;
+  if (step && blockIdx.x == 0 && tid == 0) step[0] += 1;
+  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    int si = 0;  // segment of tile t (tables hold a few dozen segments: linear scan, uniform)
+    while (si + 1 < nseg && segs[si + 1].tile0 <= t) ++si;
+    const WSeg sg = segs[si];
+    const int lt = t - sg.tile0;
+    if (sg.kind == 0) {
+      const int tco = (sg.cout + 63) >> 6;
+      const int tap = lt % sg.taps, r = lt / sg.taps;
       const int co0 = (r % tco) << 6, ci0 = (r / tco) << 6;
-      const int ci = ci0 + lc;
+      const int tp = sg.taps - 1 - tap;
+      if ((sg.cin & 3) == 0 && (sg.cout & 7) == 0 && (sg.src & 3) == 0 && (sg.dst & 7) == 0) {
+        // read: thread -> (cout row co0 + (tid >> 4) + 16 j, cin quad 4 (tid & 15))
+        const int cq = 4 * (tid & 15);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int co = co0 + lr + 4 * j;
-        float v = 0.f;
-        if (co < sg.cout && ci < sg.cin) v = master[sg.src + ((long)co * sg.taps + tap) * sg.cin + ci];
-        tile[lr + 4 * j][lc] = f2bf(v);
-      }
-      __syncthreads();
-      const int tp = sg.taps - 1 - tap, co = co0 + lc;
+        for (int j = 0; j < 4; ++j) {
+          const int rco = (tid >> 4) + 16 * j, co = co0 + rco, ci = ci0 + cq;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (co < sg.cout && ci < sg.cin)
+            v = *(const float4*)(master + sg.src + ((long)co * sg.taps + tap) * sg.cin + ci);
+          tile[cq + 0][rco] = f2bf(v.x);
+          tile[cq + 1][rco] = f2bf(v.y);
+          tile[cq + 2][rco] = f2bf(v.z);
+          tile[cq + 3][rco] = f2bf(v.w);
+        }
+        __syncthreads();
+        // write: thread -> (cin row ci0 + (tid >> 3) + 32 j, 8 couts 8 (tid & 7))
+        const int c8 = 8 * (tid & 7);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int ci2 = ci0 + lr + 4 * j;
-        if (co < sg.cout && ci2 < sg.cin) out[sg.dst + ((long)ci2 * sg.taps + tp) * sg.cout + co] = tile[lc][lr + 4 * j];
+        for (int j = 0; j < 2; ++j) {
+          const int rci = (tid >> 3) + 32 * j, ci2 = ci0 + rci, co = co0 + c8;
+          if (ci2 < sg.cin && co < sg.cout)
+            *(uint4*)(out + sg.dst + ((long)ci2 * sg.taps + tp) * sg.cout + co) = *(const uint4*)&tile[rci][c8];
+        }
+        __syncthreads();
+      } else {
+        const int lc = tid & 63, lr = tid >> 6;
+        for (int j = 0; j < 16; ++j) {
+          const int co = co0 + lr + 4 * j, ci = ci0 + lc;
+          float v = 0.f;
+          if (co < sg.cout && ci < sg.cin) v = master[sg.src + ((long)co * sg.taps + tap) * sg.cin + ci];
+          tile[lc][lr + 4 * j] = f2bf(v);
+        }
+        __syncthreads();
+        for (int j = 0; j < 16; ++j) {
+          const int ci2 = ci0 + lr + 4 * j, co = co0 + lc;
+          if (co < sg.cout && ci2 < sg.cin) out[sg.dst + ((long)ci2 * sg.taps + tp) * sg.cout + co] = tile[lr + 4 * j][lc];
+        }
+        __syncthreads();
       }
-      __syncthreads();
-    }
-  } else {
-    const long n = (long)sg.cout * 128;
-    for (long i = blockIdx.x * (long)blockDim.x + tid; i < n; i += (long)gridDim.x * blockDim.x) {
-      const int c = i % 8, tap = (i / 8) % 16, co = i / 128;
-      float val = 0.f;
-      if (tap < sg.taps && c < sg.cin) val = master[sg.src + ((long)co * sg.taps + tap) * sg.cin + c];
-      out[sg.dst + i] = f2bf(val);
+    } else {  // packed first layer: 8 consecutive elements (one tap's channel slots) per thread
+      const long e0 = ((long)lt * 256 + tid) * 8, n = (long)sg.cout * 128;
+      if (e0 < n) {
+        const int tap = (int)((e0 >> 3) & 15), co = (int)(e0 >> 7);
+        float f[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          f[c] = (tap < sg.taps && c < sg.cin) ? master[sg.src + ((long)co * sg.taps + tap) * sg.cin + c] : 0.f;
+        if ((sg.dst & 7) == 0)
+          *(uint4*)(out + sg.dst + e0) =
+              make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+        else
+          for (int c = 0; c < 8; ++c) out[sg.dst + e0 + c] = f2bf(f[c]);
+      }
     }
   }
 }
@@ -142,19 +188,17 @@ int rdp_cast_bf16(const float* p, void* out, long n, hipStream_t s) {
   return 0;
 }
 
-// segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps} (32 bytes each);
-// blocks: blocks per segment (0: 1152, enough for the largest layer; the caller passes the table's own
-// need -- e.g. 32 for the packed first layer alone -- so a small table is not a 1152-block launch)
-int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* step, int blocks, hipStream_t s) {
-  if (nseg <= 0) {
+// segs: device array of nseg WSeg {long src, long dst, int kind, cout, cin, taps, tile0, pad} (40 bytes
+// each; tile0 = the running sum of wseg_tiles over the earlier segments); tiles = the table's total tile
+// count (the caller's sum), blocks = grid cap (0: one block per tile, at most 4096)
+int rdp_wprep(const float* master, void* out, const void* segs, int nseg, int* step, int tiles, int blocks,
+              hipStream_t s) {
+  if (nseg <= 0 || tiles <= 0) {
     if (step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
     return 0;
   }
-  // blocks per segment: the largest layer (512 x 1024 x 9) has 1152 64x64 tiles; at 128 blocks per
-  // segment every block of it walked 9 tiles back to back (latency-bound: 68 us per step, a fixed
-  // cost at every batch size). Blocks of smaller segments past their tile count exit at once.
-  const int gx = blocks > 0 ? std::min(blocks, 1152) : 1152;
-  hipLaunchKernelGGL(wprep_kernel, dim3(gx, nseg), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, step);
+  const int gx = std::max(1, std::min(tiles, blocks > 0 ? blocks : 4096));
+  hipLaunchKernelGGL(wprep_kernel, dim3(gx), dim3(256), 0, s, master, (u16*)out, (const WSeg*)segs, nseg, tiles, step);
   return 0;
 }
 int rdp_wseg_size() { return (int)sizeof(WSeg); }

@@ -280,17 +280,21 @@ class UNetNative(nn.Module):
         seg_size = C.wseg_size()
         import struct
 
-        def table(ss):
+        def tiles(s):  # wprep work tiles of a segment (csrc/optim.hip wseg_tiles)
+            _, _, kind, co, ci, taps = s
+            return (co * 128 + 2047) // 2048 if kind == 1 else taps * ((co + 63) // 64) * ((ci + 63) // 64)
+
+        def table(ss):  # records carry their first tile: the launch walks one flat range of real tiles
             raw = bytearray()
+            t0 = 0
             for s in ss:
-                rec = struct.pack("<qqiiii", *s)
+                rec = struct.pack("<qqiiiiii", *s, t0, 0)
                 raw += rec + b"\0" * (seg_size - len(rec))
+                t0 += tiles(s)
             return torch.tensor(list(raw) or [0], dtype=torch.uint8).to(st.device), len(ss)
 
-        def blocks(ss):  # wprep blocks per segment this table needs (64 x 64 tiles / 256-element chunks)
-            need = [(co * 128 + 255) // 256 if kind == 1 else taps * ((co + 63) // 64) * ((ci + 63) // 64)
-                    for _, _, kind, co, ci, taps in ss]
-            return min(max(need + [1]), 1152)
+        def blocks(ss):  # the table's total tile count (wprep's `blocks` argument)
+            return sum(tiles(s) for s in ss)
 
         self._segs, self._nseg = table(segs)
         self._wblk = blocks(segs)
