@@ -23,6 +23,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -32,6 +33,7 @@
 
 namespace py = pybind11;
 
+extern "C" int rdp_h2d_copy(const void*, void*, long, hipStream_t);
 extern "C" long rdp_png_encode_gray(const uint8_t*, int, int, int, int, int, uint8_t*, long);
 extern "C" long rdp_png_encode_bound(int, int, int, int);
 extern "C" long rdp_jpeg_info(const uint8_t*, long, int*);
@@ -110,6 +112,19 @@ class FrameRunner {
                    uintptr_t d_mask, uintptr_t h_mask, size_t mask_bytes, uintptr_t d_res, uintptr_t h_res,
                    size_t res_bytes) {
     d_color_ = P(d_color); h_color_ = P(h_color); color_bytes_ = color_bytes;
+    // the colour upload runs as a copy kernel on the frame stream (rdp_h2d_copy) where the staging
+    // buffer has a device mapping and RDP_COLOR_COPY != dma: the DMA-engine copy cost ~31 us + a ~10 us
+    // engine -> compute hand-off before the preprocess kernel (profiles/serve_experiments.md)
+    h_color_dev_ = nullptr;
+    const char* cc = getenv("RDP_COLOR_COPY");
+    if (h_color_ && !(cc && std::string(cc) == "dma")) {
+      DeviceScope g(dev_);
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, h_color_, 0) == hipSuccess && dp && !(((uintptr_t)dp | (uintptr_t)d_color_) & 15))
+        h_color_dev_ = dp;
+      else
+        (void)hipGetLastError();
+    }
     d_depth_ = P(d_depth); h_depth_ = P(h_depth); depth_bytes_ = depth_bytes;
     d_meta_ = P(d_meta); meta_bytes_ = meta_bytes; d_coef_ = P(d_coef); coef_cap_ = coef_cap;
     d_mask_ = P(d_mask); h_mask_ = P(h_mask); mask_bytes_ = mask_bytes;
@@ -127,7 +142,11 @@ class FrameRunner {
     DeviceScope g(dev_);
     std::memcpy(h_color_, cp, color_bytes_);  // host staging: the caller's "submit" stage, not device time
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
-    hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
+    if (h_color_dev_)
+      hip_check(rdp_h2d_copy(h_color_dev_, d_color_, (long)color_bytes_, s_) == 0 ? hipSuccess : hipErrorLaunchFailure,
+                "H2D colour kernel");
+    else
+      hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
     hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
   }
 
@@ -331,6 +350,7 @@ class FrameRunner {
   std::vector<void*> host_;
   hipGraphExec_t exec_[4] = {nullptr, nullptr, nullptr, nullptr};
   void *d_color_ = nullptr, *h_color_ = nullptr, *d_depth_ = nullptr, *h_depth_ = nullptr;
+  void* h_color_dev_ = nullptr;  // device mapping of the colour staging buffer (copy-kernel upload)
   void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
   void *d_res_ = nullptr, *h_res_ = nullptr;
   size_t color_bytes_ = 0, depth_bytes_ = 0, meta_bytes_ = 0, coef_cap_ = 0, mask_bytes_ = 0, res_bytes_ = 0;
