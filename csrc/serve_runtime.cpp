@@ -112,19 +112,7 @@ class FrameRunner {
                    uintptr_t d_mask, uintptr_t h_mask, size_t mask_bytes, uintptr_t d_res, uintptr_t h_res,
                    size_t res_bytes) {
     d_color_ = P(d_color); h_color_ = P(h_color); color_bytes_ = color_bytes;
-    // the colour upload runs as a copy kernel on the frame stream (rdp_h2d_copy) where the staging
-    // buffer has a device mapping and RDP_COLOR_COPY != dma: the DMA-engine copy cost ~31 us + a ~10 us
-    // engine -> compute hand-off before the preprocess kernel (profiles/serve_experiments.md)
-    h_color_dev_ = nullptr;
-    const char* cc = getenv("RDP_COLOR_COPY");
-    if (h_color_ && !(cc && std::string(cc) == "dma")) {
-      DeviceScope g(dev_);
-      void* dp = nullptr;
-      if (hipHostGetDevicePointer(&dp, h_color_, 0) == hipSuccess && dp && !(((uintptr_t)dp | (uintptr_t)d_color_) & 15))
-        h_color_dev_ = dp;
-      else
-        (void)hipGetLastError();
-    }
+    kernel_copy_ = !(getenv("RDP_COLOR_COPY") && std::string(getenv("RDP_COLOR_COPY")) == "dma");
     d_depth_ = P(d_depth); h_depth_ = P(h_depth); depth_bytes_ = depth_bytes;
     d_meta_ = P(d_meta); meta_bytes_ = meta_bytes; d_coef_ = P(d_coef); coef_cap_ = coef_cap;
     d_mask_ = P(d_mask); h_mask_ = P(h_mask); mask_bytes_ = mask_bytes;
@@ -142,11 +130,7 @@ class FrameRunner {
     DeviceScope g(dev_);
     std::memcpy(h_color_, cp, color_bytes_);  // host staging: the caller's "submit" stage, not device time
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
-    if (h_color_dev_)
-      hip_check(rdp_h2d_copy(h_color_dev_, d_color_, (long)color_bytes_, s_) == 0 ? hipSuccess : hipErrorLaunchFailure,
-                "H2D colour kernel");
-    else
-      hip_check(hipMemcpyAsync(d_color_, h_color_, color_bytes_, hipMemcpyHostToDevice, s_), "H2D colour");
+    upload(d_color_, h_color_, color_bytes_, "H2D colour");
     hip_check(hipGraphLaunch(exec_[src], s_), "hipGraphLaunch");
   }
 
@@ -158,8 +142,8 @@ class FrameRunner {
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
     hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
-    hip_check(hipMemcpyAsync(d_meta_, P(meta), meta_bytes, hipMemcpyHostToDevice, s_), "H2D meta");
-    hip_check(hipMemcpyAsync(d_coef_, P(coefs), coef_bytes, hipMemcpyHostToDevice, s_), "H2D coefs");
+    upload(d_meta_, P(meta), meta_bytes, "H2D meta", false);
+    upload(d_coef_, P(coefs), coef_bytes, "H2D coefs", false);
     hip_check(hipGraphLaunch(exec_[2], s_), "hipGraphLaunch");
   }
 
@@ -176,6 +160,33 @@ class FrameRunner {
   }
 
  private:
+  // Host -> device upload on the frame stream: a copy kernel reading the pinned source through its device
+  // mapping (rdp_h2d_copy) where it has one and RDP_COLOR_COPY != dma -- the DMA-engine copy costs an
+  // engine -> compute hand-off (~10 us) before the next kernel (profiles/serve_experiments.md) -- else
+  // hipMemcpyAsync. Device mappings of the (few, long-lived) staging buffers are cached.
+  void upload(void* dst, const void* src, size_t bytes, const char* what, bool cache = true) {
+    if (kernel_copy_ && bytes && !((uintptr_t)dst & 15)) {
+      void* dp = nullptr;
+      bool known = false;
+      if (cache)
+        for (auto& m : hmap_)
+          if (m.first == src) { dp = m.second; known = true; }
+      if (!known) {  // (with unified addressing the mapping is often the host address itself)
+        if (hipHostGetDevicePointer(&dp, const_cast<void*>(src), 0) != hipSuccess) {
+          (void)hipGetLastError();
+          dp = nullptr;
+        }
+        if (cache) {  // runner-owned staging only: a caller's buffer may be freed and its address reused
+          if (hmap_.size() >= 16) hmap_.erase(hmap_.begin());
+          hmap_.emplace_back(src, dp);  // nullptr: no mapping, the DMA copy below
+        }
+      }
+      if (dp && !((uintptr_t)dp & 15) && rdp_h2d_copy(dp, dst, (long)bytes, s_) == 0) return;
+      (void)hipGetLastError();
+    }
+    hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s_), what);
+  }
+
   void launch_depth_half() {  // h_depth_ staged; the device is current
     if (depth_stream_) {
       hip_check(hipMemcpyAsync(d_depth_, h_depth_, depth_bytes_, hipMemcpyHostToDevice, cs_), "H2D depth");
@@ -266,8 +277,8 @@ class FrameRunner {
         for (int i = 0; i < 3 * 64; ++i) meta[32 + i] = qt[i];
         DeviceScope gk(dev_);
         hip_check(hipEventRecord(ev0_, s_), "hipEventRecord");
-        hip_check(hipMemcpyAsync(d_meta_, h_meta_, meta_bytes_, hipMemcpyHostToDevice, s_), "H2D meta");
-        hip_check(hipMemcpyAsync(d_coef_, h_coef_, (size_t)nco * 2, hipMemcpyHostToDevice, s_), "H2D coefs");
+        upload(d_meta_, h_meta_, meta_bytes_, "H2D meta");
+        upload(d_coef_, h_coef_, (size_t)nco * 2, "H2D coefs");
         hip_check(hipGraphLaunch(exec_[2], s_), "hipGraphLaunch");
       } else {  // depth: 16-bit PNG straight into the pinned staging buffer
         if (rdp_png_decode(d, dn, (uint8_t*)h_depth_, (long)depth_bytes_, 1) != 0) rc[1] = kCorrupt;
@@ -350,7 +361,8 @@ class FrameRunner {
   std::vector<void*> host_;
   hipGraphExec_t exec_[4] = {nullptr, nullptr, nullptr, nullptr};
   void *d_color_ = nullptr, *h_color_ = nullptr, *d_depth_ = nullptr, *h_depth_ = nullptr;
-  void* h_color_dev_ = nullptr;  // device mapping of the colour staging buffer (copy-kernel upload)
+  bool kernel_copy_ = true;  // uploads by copy kernel (upload())
+  std::vector<std::pair<const void*, void*>> hmap_;  // host staging pointer -> device mapping
   void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
   void *d_res_ = nullptr, *h_res_ = nullptr;
   size_t color_bytes_ = 0, depth_bytes_ = 0, meta_bytes_ = 0, coef_cap_ = 0, mask_bytes_ = 0, res_bytes_ = 0;
