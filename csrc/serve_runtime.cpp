@@ -165,6 +165,7 @@ class FrameRunner {
   // engine -> compute hand-off (~10 us) before the next kernel (profiles/serve_experiments.md) -- else
   // hipMemcpyAsync. Device mappings of the (few, long-lived) staging buffers are cached.
   void upload(void* dst, const void* src, size_t bytes, const char* what, bool cache = true) {
+    const hipStream_t st = s_;
     if (kernel_copy_ && bytes && !((uintptr_t)dst & 15)) {
       void* dp = nullptr;
       bool known = false;
@@ -181,10 +182,10 @@ class FrameRunner {
           hmap_.emplace_back(src, dp);  // nullptr: no mapping, the DMA copy below
         }
       }
-      if (dp && !((uintptr_t)dp & 15) && rdp_h2d_copy(dp, dst, (long)bytes, s_) == 0) return;
+      if (dp && !((uintptr_t)dp & 15) && rdp_h2d_copy(dp, dst, (long)bytes, st) == 0) return;
       (void)hipGetLastError();
     }
-    hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s_), what);
+    hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st), what);
   }
 
   void launch_depth_half() {  // h_depth_ staged; the device is current
