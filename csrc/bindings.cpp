@@ -92,6 +92,7 @@ int rdp_rows_fold(const float*, int, int, double*, hipStream_t);
 int rdp_rows_hilo(const double*, float*, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, int, hipStream_t);
 int rdp_wseg_size();
+int rdp_h2d_copy(const void*, void*, long, hipStream_t);
 int rdp_parcur(int, int, const double*, const double*, double, int, int, double*, double*, int*, double*);
 double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
@@ -1189,6 +1190,22 @@ void cast_bf16(torch::Tensor p, torch::Tensor out) {
   RDP_PLAN(rdp_cast_bf16(p.data_ptr<float>(), out.data_ptr(), p.numel(), st));
 }
 
+// The serving runtime's frame upload kernel (csrc/serve_kernels.hip), for tests: a pinned CPU tensor ->
+// a device tensor of the same byte size through the host buffer's device mapping. Returns 0, or -1 when
+// the kernel does not take the pair (unaligned) or the buffer has no mapping.
+int h2d_copy(torch::Tensor src, torch::Tensor dst) {
+  TORCH_CHECK(!src.is_cuda() && src.is_pinned() && src.is_contiguous(), "h2d_copy: src must be a pinned CPU tensor");
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "h2d_copy: dst must be a contiguous device tensor");
+  const long bytes = (long)(src.numel() * src.element_size());
+  TORCH_CHECK(bytes == (long)(dst.numel() * dst.element_size()), "h2d_copy: byte sizes differ");
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, src.data_ptr(), 0) != hipSuccess || !dp) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return rdp_h2d_copy(dp, dst.data_ptr(), bytes, c10::hip::getCurrentHIPStream().stream());
+}
+
 void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int nseg, c10::optional<torch::Tensor> step,
            int blocks) {
   check_f32(master, "master");
@@ -1566,6 +1583,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
         py::arg("inc") = true, py::arg("max_blocks") = 0);
   m.def("cast_bf16", on_device(&cast_bf16));
+  m.def("h2d_copy", &h2d_copy, py::arg("src"), py::arg("dst"));
   m.def("wprep", on_device(&wprep), py::arg("master"), py::arg("out"), py::arg("segs"), py::arg("nseg"),
         py::arg("step") = py::none(), py::arg("blocks") = 0);
   m.def("wseg_size", &rdp_wseg_size);

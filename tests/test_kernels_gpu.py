@@ -1176,6 +1176,16 @@ def test_conv_ring_cout128(C, N, H, W, split):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4096 + 7, 640 * 480 * 3, 640 * 480 * 2 + 3])
+def test_h2d_copy_kernel(C, nbytes):
+    """The serving frame upload kernel (rdp_h2d_copy): pinned host bytes -> device, 16-B chunks + tail."""
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8).pin_memory()
+    dst = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    assert C.h2d_copy(src, dst) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dst.cpu(), src)
+
+
 @pytest.mark.parametrize("decoder", ["bilinear", "transposed"])
 def test_wprep_derived_layouts(C, decoder):
     """wprep (LDS-tiled transpose) rebuilds every derived bf16 weight layout from the fp32 masters."""
