@@ -111,7 +111,7 @@ int rdp_area_maxtap();
 int rdp_resize_area_u8(const void*, int, int, int, const int*, const int*, const double*, const int*, const int*,
                        const double*, int, int, int, void*, hipStream_t);
 int rdp_geo_spline(const double*, int, int, const int*, const int*, double*, int*, double*, int, double, int, int,
-                   double, int, int, const int*, int, double*, double*, int, hipStream_t);
+                   double, int, int, const int*, int, double*, double*, int, const void*, void*, long, hipStream_t);
 }
 
 namespace {
@@ -1339,7 +1339,8 @@ long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 // fit + nsamp-point evaluation and curvature into res (rdp_geo_spline_res_len(nsamp) doubles)
 void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch::Tensor sorted, torch::Tensor gperm,
                 torch::Tensor u, torch::Tensor res, double s, int k, int nsamp, double eps, int min_points,
-                int min_edge, c10::optional<torch::Tensor> cov, c10::optional<torch::Tensor> dbg, bool presorted) {
+                int min_edge, c10::optional<torch::Tensor> cov, c10::optional<torch::Tensor> dbg, bool presorted,
+                c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> mask_host) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat64 && out.dim() == 3 && out.size(2) == 4 &&
               out.is_contiguous(), "out [nbins][kcap][4] f64");
   TORCH_CHECK(kout.scalar_type() == torch::kInt32 && kout.numel() >= out.size(0), "kout");
@@ -1362,10 +1363,24 @@ void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch
     TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kFloat64 && dbg->numel() >= 20, "dbg: >= 20 f64");
     dbgp = dbg->data_ptr<double>();
   }
+  // mask + mask_host (serving): the frame mask's host copy, written by blocks beside the fit block
+  const void* mp = nullptr;
+  void* mh = nullptr;
+  long mbytes = 0;
+  if (mask_host && mask_host->defined()) {
+    TORCH_CHECK(mask && mask->defined() && mask->is_cuda() && mask->scalar_type() == torch::kUInt8 &&
+                    mask->is_contiguous(), "geo_spline: mask_host needs the device mask (u8, contiguous)");
+    TORCH_CHECK(!mask_host->is_cuda() && mask_host->scalar_type() == torch::kUInt8 && mask_host->is_contiguous() &&
+                    mask_host->numel() == mask->numel(), "geo_spline: mask_host: host u8 tensor of the mask's size");
+    mp = mask->data_ptr();
+    mh = mask_host->data_ptr();
+    mbytes = mask->numel();
+  }
   const int r = rdp_geo_spline(out.data_ptr<double>(), out.size(0), out.size(1), kout.data_ptr<int>(),
                                npts.data_ptr<int>(), sorted.data_ptr<double>(), gperm.data_ptr<int>(),
                                u.data_ptr<double>(), ecap, s, k, nsamp, eps, min_points, min_edge, covp, ncov,
-                               res.data_ptr<double>(), dbgp, presorted ? 1 : 0, unplanned_stream());
+                               res.data_ptr<double>(), dbgp, presorted ? 1 : 0, mp, mh, mbytes, unplanned_stream());
+  TORCH_CHECK(r != -2, "geo_spline: mask copy needs 4-byte aligned buffers and a size multiple of 4");
   TORCH_CHECK(r == 0, "geo_spline: k must be in [1, 5], nsamp in [1, 256]");
 }
 
@@ -1598,7 +1613,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("geo_spline", on_device(&geo_spline), py::arg("out"), py::arg("kout"), py::arg("npts"), py::arg("sorted"),
         py::arg("gperm"), py::arg("u"), py::arg("res"), py::arg("s"), py::arg("k"), py::arg("nsamp"), py::arg("eps"),
         py::arg("min_points"), py::arg("min_edge"), py::arg("cov") = py::none(), py::arg("dbg") = py::none(),
-        py::arg("presorted") = false);
+        py::arg("presorted") = false, py::arg("mask") = py::none(), py::arg("mask_host") = py::none());
   m.def("png_decode", &png_decode, py::arg("data"), py::arg("parallel") = 1,
         "parallel: 0 serial inflate, 1 banded (rdPs index) with serial fallback, 2 banded only (tests)");
   m.def("jpeg_decode", &jpeg_decode, py::arg("data"), py::arg("parallel") = true, py::arg("pin") = false);

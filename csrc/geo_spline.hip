@@ -468,7 +468,16 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
                                                               const int* __restrict__ npts_p, int ecap, double s,
                                                               int nsamp, double eps, int min_points, int min_edge,
                                                               const int* __restrict__ cov, int ncov,
-                                                              double* __restrict__ res, double* __restrict__ dbg) {
+                                                              double* __restrict__ res, double* __restrict__ dbg,
+                                                              const uint32_t* __restrict__ hsrc,
+                                                              uint32_t* __restrict__ hdst, int hwords) {
+  if (blockIdx.x > 0) {
+    // blocks 1.. (serving): the frame mask's copy into host memory (4-B words) beside the one fit block,
+    // on CUs it leaves idle -- written by geo_count it lengthened that kernel by ~4.5 us of its 9.4
+    const int i = ((int)blockIdx.x - 1) * SPL_THREADS + (int)threadIdx.x;
+    if (i < hwords) hdst[i] = hsrc[i];
+    return;
+  }
   constexpr int K1 = K + 1, K2 = K + 2, nmin = 2 * K1;
   constexpr int NCAP = SPL_NK + K1;  // max knots: nk1 = n - K1 <= SPL_NK coefficients
   __shared__ SplSh S;
@@ -855,14 +864,19 @@ int rdp_geo_spline_res_len(int nsamp) { return 9 + 3 * nsamp; }
 int rdp_geo_spline(const double* out, int nbins, int kcap, const int* kout, const int* npts, double* sorted,
                    int* gperm, double* u, int ecap, double s, int k, int nsamp, double eps, int min_points,
                    int min_edge, const int* cov, int ncov, double* res, double* dbg, int presorted,
-                   hipStream_t st) {
+                   const void* mask, void* mask_host, long mask_bytes, hipStream_t st) {
   if (k < 1 || k > SPL_KMAX || nsamp < 1 || nsamp > SPL_THREADS) return -1;
   // presorted: rdp_geo_edges already wrote `sorted` (fused select + sort)
   if (!presorted)
     hipLaunchKernelGGL(geo_sort_kernel, dim3(nbins), dim3(256), 0, st, out, kcap, kout, sorted, gperm, ecap);
-#define RDP_FIT(KK)                                                                                                \
-  hipLaunchKernelGGL(geo_fit_kernel<KK>, dim3(1), dim3(SPL_THREADS), 0, st, sorted, u, kout, nbins, kcap, npts, \
-                     ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res, dbg)
+  // mask_host: copy `mask` (device) into it with blocks beside the fit (4-B words; mask_bytes % 4 == 0)
+  if (mask_host && (mask_bytes % 4 || (((uintptr_t)mask | (uintptr_t)mask_host) & 3))) return -2;
+  const int hwords = mask_host ? (int)(mask_bytes / 4) : 0;
+  const int grid = 1 + (hwords + SPL_THREADS - 1) / SPL_THREADS;
+#define RDP_FIT(KK)                                                                                                 \
+  hipLaunchKernelGGL(geo_fit_kernel<KK>, dim3(grid), dim3(SPL_THREADS), 0, st, sorted, u, kout, nbins, kcap, npts, \
+                     ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res, dbg, (const uint32_t*)mask,        \
+                     (uint32_t*)mask_host, hwords)
   switch (k) {
     case 1: RDP_FIT(1); break;
     case 2: RDP_FIT(2); break;

@@ -152,16 +152,20 @@ class GeometryEngine:
         self._serving_form = False
 
     def launch_frame(self, m256_dev: torch.Tensor, mask_out: torch.Tensor, depth_dev: torch.Tensor, K: np.ndarray,
-                     scale: float, mask_host: Optional[torch.Tensor] = None):
+                     scale: float, mask_host: Optional[torch.Tensor] = None, host_copy_in_spline: bool = False):
         """Serving form: ``mask_out`` (H x W) is produced here by nearest-upsampling the model-resolution
         mask ``m256_dev`` (no separate upsample kernel), with the coverage count per row block, and no
         packed edge list; follow with ``launch_spline()`` (its result then carries the coverage).
-        ``mask_host``: a host-memory copy of the mask written by the same kernel (no read-back copy)."""
+        ``mask_host``: a host-memory copy of the mask (no read-back copy), written by the mask kernel, or
+        with ``host_copy_in_spline`` by blocks of the next ``launch_spline()`` beside its single fit block
+        (off the critical path: in the mask kernel the PCIe writes lengthened it by ~4.5 us)."""
         c = self.cfg
+        defer = host_copy_in_spline and mask_host is not None and mask_out.numel() % 4 == 0
         self.C.geo_edges(mask_out, depth_dev, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]),
                          float(scale), self.work_i, self.work_d, self.pts, self.npts, self.out, self.kout, c.num_bins,
                          c.top_k_percent, c.min_points, None, None, m256_dev, self.cov, self.sorted, self.gperm,
-                         mask_host)
+                         None if defer else mask_host)
+        self._host_copy = (mask_out, mask_host) if defer else None
         self._serving_form = True  # the select kernel also wrote the x-sorted edge points
 
     def launch_spline(self, res_out: Optional[torch.Tensor] = None):
@@ -173,7 +177,9 @@ class GeometryEngine:
         self.C.geo_spline(self.out, self.kout, self.npts, self.sorted, self.gperm, self.u,
                           self.res if res_out is None else res_out, c.smoothing,
                           c.spline_degree, c.num_samples, c.deriv_eps, c.min_points, c.min_edge_points,
-                          self.cov if serving else None, presorted=serving)
+                          self.cov if serving else None, presorted=serving,
+                          **({"mask": hc[0], "mask_host": hc[1]} if (hc := getattr(self, "_host_copy", None)) else {}))
+        self._host_copy = None
 
     def finish_device(self, res_host: np.ndarray) -> CurvatureResult:
         """Result of ``launch_spline`` (``res`` read back); a fit beyond the device capacity is redone

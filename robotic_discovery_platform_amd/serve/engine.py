@@ -230,7 +230,7 @@ class FramePipeline:
     def _geo_program(self):
         zc = self.zero_copy
         self.geo.launch_frame(self.m256.view(self.S, self.S), self.mask, self.d_depth, self.K, self.scale,
-                              mask_host=self.h_mask if zc else None)
+                              mask_host=self.h_mask if zc else None, host_copy_in_spline=True)
         self.geo.launch_spline(res_out=self.h_res if zc else None)
 
     def refresh_weights(self):
