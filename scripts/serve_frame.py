@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernel timeline of one serving-engine frame from a rocprofv3 kernel trace.
 
-Frames are delimited by ``preprocess_kernel`` (one per frame). Prints, per kernel position of the
+Frames are delimited by ``h2d_copy_kernel`` (the colour upload) or, without it, ``preprocess_kernel``. Prints, per kernel position of the
 frame, the start offset and duration of the second-to-last complete frame plus the median duration
 over the last (up to) 50 frames with the same kernel sequence, and the summed kernel time.
 usage: serve_frame.py <kernel_trace.csv> [first_frame]
@@ -15,7 +15,9 @@ import sys
 
 def main(path, first=None):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("preprocess_kernel")]
+    # a frame starts at its colour upload kernel where the runner uploads by kernel, else at the preprocess
+    start_k = "h2d_copy_kernel" if any(r["Kernel_Name"].startswith("h2d_copy_kernel") for r in rows) else "preprocess_kernel"
+    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(start_k)]
     if len(idx) < 3:
         print("fewer than 3 frames in the trace")
         return
