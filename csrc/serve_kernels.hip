@@ -10,6 +10,7 @@
 //   (server.py:124-125,133): u8 {0,1} mask at the camera resolution + coverage count (atomics).
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 #define AA_MAXTAP 16
 
@@ -275,13 +276,39 @@ __global__ __launch_bounds__(256) void h2d_copy_kernel(const uint4* __restrict__
   if (i < ntail) tdst[i] = tsrc[i];
 }
 
+// U chunks per lane, strided by the grid (each load instruction of a wave still covers 1 KiB contiguous)
+__global__ __launch_bounds__(256) void h2d_copy4_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        long n16, const uint8_t* __restrict__ tsrc,
+                                                        uint8_t* __restrict__ tdst, int ntail) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x, str = (long)gridDim.x * 256;
+  uint4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (i + u * str < n16) v[u] = src[i + u * str];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (i + u * str < n16) dst[i + u * str] = v[u];
+  if (i < ntail) tdst[i] = tsrc[i];
+}
+
 extern "C" int rdp_h2d_copy(const void* src, void* dst, long bytes, hipStream_t s) {
   if (bytes <= 0) return 0;
   if (((uintptr_t)src | (uintptr_t)dst) & 15) return -1;
   const long n16 = bytes / 16;
   const int ntail = (int)(bytes - n16 * 16);
-  const long blocks = std::max<long>(1, (std::max<long>(n16, ntail) + 255) / 256);
-  hipLaunchKernelGGL(h2d_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, n16,
-                     (const uint8_t*)src + n16 * 16, (uint8_t*)dst + n16 * 16, ntail);
+  // 4 chunks per lane by default (engine GPU p50 0.385 vs 0.387 ms in two interleaved rounds,
+  // profiles/serve_experiments.md); RDP_H2D_VEC=1: one chunk per lane
+  static const int vec = [] {
+    const char* e = getenv("RDP_H2D_VEC");
+    return e && atoi(e) == 1 ? 1 : 4;
+  }();
+  const long lanes = vec == 4 ? std::max<long>((n16 + 3) / 4, ntail) : std::max<long>(n16, ntail);
+  const long blocks = std::max<long>(1, (lanes + 255) / 256);
+  if (vec == 4)
+    hipLaunchKernelGGL(h2d_copy4_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, n16,
+                       (const uint8_t*)src + n16 * 16, (uint8_t*)dst + n16 * 16, ntail);
+  else
+    hipLaunchKernelGGL(h2d_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, n16,
+                       (const uint8_t*)src + n16 * 16, (uint8_t*)dst + n16 * 16, ntail);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
