@@ -254,6 +254,19 @@ def main():
     if rc is not None:
         sys.exit(rc)
     rank, world, dev = setup_dist(args)
+    comm = {}
+    if dist.is_initialized():
+        # the first real multi-rank run of the native collective path checks itself before anything is
+        # timed: RCCL's rank count, a rank-sum probe through the buckets' exact call, fallback to
+        # torch.distributed issue if it fails, measured all-reduce bus bandwidth (parallel/selfcheck.py)
+        from robotic_discovery_platform_amd.parallel.selfcheck import CommMismatch, comm_selfcheck
+        from robotic_discovery_platform_amd.train.engine import NativeTrainer
+        want_native = args.impl == "native" and dev.type == "cuda" and NativeTrainer.native_comm_wanted_env()
+        try:
+            comm = comm_selfcheck(dev, want_native)
+        except CommMismatch as e:
+            print(f"bench.py: {e}", file=sys.stderr, flush=True)
+            sys.exit(3)
     step = make_eager_step(args, dev, world) if args.impl == "eager" else make_native_step(args, dev, world)
     tr = getattr(step, "trainer", None)
     used_graph = bool(tr.use_graph) if tr is not None else False
@@ -268,11 +281,19 @@ def main():
         step()
     barrier(world, dev)
     dt = time.perf_counter() - t0
+    dt_own = dt
     t = torch.tensor([dt], dtype=torch.float64, device=dev if world > 1 and dev.type == "cuda" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     ms = dt / args.steps * 1e3
+    rank_ms = [ms]
+    if world > 1:  # every rank's own timed-region length (the headline uses the max)
+        own = torch.tensor([dt_own / args.steps * 1e3], dtype=torch.float64,
+                           device=dev if dev.type == "cuda" and dist.get_backend() == "nccl" else "cpu")
+        allt = [torch.zeros_like(own) for _ in range(world)]
+        dist.all_gather(allt, own)
+        rank_ms = [float(x.item()) for x in allt]
     imgs = args.batch * world * args.steps / dt
     extra = {}
     extras = args.extras if args.extras >= 0 else int(world == 1 and args.impl == "native" and dev.type == "cuda")
@@ -326,6 +347,10 @@ def main():
             "baseline_note": "vs_baseline = value / 2.14 img/s (BASELINE.md: reference bs4 fp32 on CPU; "
                              "no published GPU number exists)",
         }
+        if world > 1:
+            out["rank_ms_per_step_min"] = round(min(rank_ms), 3)
+            out["rank_ms_per_step_max"] = round(max(rank_ms), 3)
+        out.update(comm)
         out.update(extra)
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

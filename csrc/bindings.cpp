@@ -24,7 +24,7 @@ int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, con
                    float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
 int rdp_conv_rowband_ex(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, long, int,
                         int, int, int, int, const float*, const float*, int, void*, long, int, int, hipStream_t);
-int rdp_conv_rowband_frag_auto(int, int, int, int, int);
+int rdp_conv_rowband_frag_auto(int, int, int, int, int, int);
 int rdp_conv_rowband_chain(int, const void*, long, int, int, const void* const*, const long*, const int*, void* const*,
                            const long*, const int*, const int*, const float* const*, const float* const*, int, int, int,
                            int*, int*, hipStream_t);
@@ -326,6 +326,14 @@ int plan_size(int id) {
   return (int)g_plans[id]->ops.size();
 }
 
+// the op kinds of a recorded plan, in order (tests: which cross-stream waits a plan holds)
+std::vector<int> plan_kinds(int id) {
+  TORCH_CHECK(id >= 0 && id < (int)g_plans.size() && g_plans[id], "plan_kinds: bad plan id");
+  std::vector<int> k;
+  for (auto& op : g_plans[id]->ops) k.push_back(op.kind);
+  return k;
+}
+
 void plan_free(int id) {
   if (id < 0 || id >= (int)g_plans.size() || !g_plans[id]) return;
   for (auto& op : g_plans[id]->ops) if (op.ev && op.kind == 1) hipEventDestroy(op.ev);
@@ -343,11 +351,13 @@ typedef int (*NcclAllReduceFn)(const void*, void*, size_t, int, int, void*, hipS
 typedef int (*NcclAsyncErrFn)(void*, int*);
 typedef const char* (*NcclErrStrFn)(int);
 typedef int (*NcclAbortFn)(void*);
+typedef int (*NcclCommIntFn)(const void*, int*);
 struct RcclApi {
   NcclAllReduceFn all_reduce = nullptr;
   NcclAsyncErrFn async_err = nullptr;
   NcclErrStrFn err_str = nullptr;
   NcclAbortFn abort = nullptr;
+  NcclCommIntFn count = nullptr, user_rank = nullptr, device = nullptr;
   std::string path;
 } g_rccl;
 
@@ -370,7 +380,11 @@ std::string comm_bind() {
   g_rccl.async_err = (NcclAsyncErrFn)dlsym(h, "ncclCommGetAsyncError");
   g_rccl.err_str = (NcclErrStrFn)dlsym(h, "ncclGetErrorString");
   g_rccl.abort = (NcclAbortFn)dlsym(h, "ncclCommAbort");
-  TORCH_CHECK(g_rccl.all_reduce && g_rccl.async_err && g_rccl.err_str && g_rccl.abort, "comm_bind: RCCL symbols in ",
+  g_rccl.count = (NcclCommIntFn)dlsym(h, "ncclCommCount");
+  g_rccl.user_rank = (NcclCommIntFn)dlsym(h, "ncclCommUserRank");
+  g_rccl.device = (NcclCommIntFn)dlsym(h, "ncclCommCuDevice");
+  TORCH_CHECK(g_rccl.count && g_rccl.user_rank && g_rccl.device &&
+              g_rccl.all_reduce && g_rccl.async_err && g_rccl.err_str && g_rccl.abort, "comm_bind: RCCL symbols in ",
               path);
   g_rccl.path = path;
   return path;
@@ -446,6 +460,17 @@ py::tuple comm_async_error(long comm) {
   const int r = g_rccl.async_err((void*)comm, &e);
   const int code = r != 0 ? r : e;
   return py::make_tuple(code, std::string(code ? g_rccl.err_str(code) : ""));
+}
+
+// (ranks, this rank, device) of `comm` as RCCL itself sees them (ncclCommCount / ncclCommUserRank /
+// ncclCommCuDevice): bench.py's self-check that the gradient communicator spans WORLD_SIZE ranks
+py::tuple comm_info(long comm) {
+  TORCH_CHECK(g_rccl.count != nullptr && comm != 0, "comm_info: call comm_bind() first");
+  int n = -1, r = -1, d = -1;
+  TORCH_CHECK(g_rccl.count((void*)comm, &n) == 0, "ncclCommCount failed");
+  TORCH_CHECK(g_rccl.user_rank((void*)comm, &r) == 0, "ncclCommUserRank failed");
+  TORCH_CHECK(g_rccl.device((void*)comm, &d) == 0, "ncclCommCuDevice failed");
+  return py::make_tuple(n, r, d);
 }
 
 // ncclCommAbort: unblocks every kernel of the communicator still waiting on a dead peer (the watchdog's
@@ -611,20 +636,23 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
     auto pooled = std::make_shared<int>(0);
     // eval with the fragment-major weight copy (wfrag): the row-band kernel wherever its traffic model picks it
     const int fmode = wfrag && esc && !sp && !y2 && taps == 9 && !packed && bm_pref == 0
-                          ? rdp_conv_rowband_frag_auto(nn, a1.H, a1.W, a1.C + C2, Cout) : 0;
-    const bool frag = fmode > 0;
-    int r;
-    if (frag) {
+                          ? rdp_conv_rowband_frag_auto(nn, a1.H, a1.W, a1.C, C2, Cout) : 0;
+    int r = -1;
+    if (fmode > 0) {
       void* const wfp = wfrag->data_ptr();
       const long wfb = wfrag->numel() * 2;
       const long pbytes = pool ? ((long)nn * po.H * po.W - 1) * ppit * 2 + (long)po.C * 2 : 0;
       const int rb = RDP_PLAN(rdp_conv_rowband_ex(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wfp, wfb, 0, py1, by1,
                                                   o1.pitch, nn, a1.H, a1.W, Cout, esc, esh, relu, ppo, pbytes, ppit, fmode,
                                                   st));
-      TORCH_CHECK(rb >= 0, "conv_fwd: row-band kernel rejected a shape its model picked");
-      *pooled = rb == 1 ? 1 : 0;
-      r = 0;
-    } else {
+      // the selector checks every predicate of the launch; should one still reject (rb < 0: nothing was
+      // launched), the layer runs on the implicit GEMM below instead of failing the eval
+      if (rb >= 0) {
+        *pooled = rb == 1 ? 1 : 0;
+        r = 0;
+      }
+    }
+    if (r < 0) {
       r = RDP_PLAN(rdp_conv_igemm(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wp, wb, (int)ldw, py1, py2, by1, by2, o1.C,
                                   o1.pitch, yp2, spc, nn, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu, wsp,
                                   wsn, ppo, ppit, want_fused ? pooled.get() : nullptr, pup, upit, uH, uW, up_oy, up_ox,
@@ -1528,6 +1556,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_end", &plan_end);
   m.def("plan_abort", &plan_abort);
   m.def("plan_replay", &plan_replay, py::arg("id"), py::arg("host_call") = py::none());
+  m.def("plan_kinds", &plan_kinds);
   m.def("plan_recording", &plan_recording);
   m.def("comm_bind", &comm_bind, "resolve RCCL from the library torch loaded; returns its path");
   m.def("comm_all_reduce", on_device(&comm_all_reduce), py::arg("buf"), py::arg("comm"),
@@ -1536,6 +1565,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rows_hilo", on_device(&rows_hilo), py::arg("sums"), py::arg("buf"), py::arg("width"));
   m.def("comm_async_error", &comm_async_error, py::arg("comm"), "(code, message) of ncclCommGetAsyncError");
   m.def("comm_abort", &comm_abort, py::arg("comm"), "ncclCommAbort");
+  m.def("comm_info", &comm_info, py::arg("comm"), "(ncclCommCount, ncclCommUserRank, ncclCommCuDevice)");
   m.def("comm_emulate", &comm_emulate, py::arg("us"), py::arg("blocks"),
         "modelled collective on the current stream (RDP_DDP_EMULATE; recorded in plans)");
   m.def("plan_mark", &plan_mark, "record a host call point (replay calls host_call(tag) there)");
@@ -1594,6 +1624,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_head_mask", on_device(&conv_head_mask));
   m.def("conv_rowband_chain", on_device(&conv_rowband_chain));
   m.def("conv_rowband", on_device(&conv_rowband));
+  // host-only: the eval conv's row-band mode for a shape (0 = implicit GEMM), the same decision conv_fwd takes
+  m.def("rowband_frag_mode", &rdp_conv_rowband_frag_auto, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c1"),
+        py::arg("c2"), py::arg("cout"));
   m.def("adam", on_device(&adam), py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("gscale"), py::arg("step"),
         py::arg("inc") = true, py::arg("max_blocks") = 0);

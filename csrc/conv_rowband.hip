@@ -528,12 +528,20 @@ extern "C" long rdp_conv_rowband_bytes(int N, int H, int W, int Cin, int Cout, i
 // 16^2 512 -> 512 8.8 vs 14.6 us on OHWI weights, 32^2 256 -> 512 13.2 vs 18.9). The eval dispatch
 // (bindings conv_fwd with wfrag) takes the row-band kernel up to 250 MB of weighted operand bytes: every
 // <= 64^2 layer of the U-Net but the two long-K decoder convs (32^2 1024 -> 512, 64^2 512 -> 256).
-extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int Cin, int Cout) {
+static int ilog2_exact(long v);
+
+// C1 / C2: the two sources' channels (C2 = 0 for one source). Every shape predicate rdp_conv_rowband_ex
+// applies is checked here too, so a mode this returns is never rejected by the launch (W and Cin / 32
+// powers of two, each source a multiple of 32 channels); the Python executor asks this same function
+// (binding rowband_frag_mode) which layers need a fragment-major weight copy.
+extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int C1, int C2, int Cout) {
   static const int on = [] {
     const char* e = getenv("RDP_ROWBAND");
     return e ? atoi(e) : 1;
   }();
-  if (!on || W < 16 || Cin < 64 || Cout < 64 || Cout % 32) return 0;
+  const int Cin = C1 + C2;
+  if (!on || W < 16 || Cin < 64 || Cout < 64 || Cout % 32 || C1 % 32 || C2 % 32) return 0;
+  if (ilog2_exact(W) < 0 || ilog2_exact(Cin / 32) < 0) return 0;
   const long M = (long)N * H * W;
   const long wb = (long)Cout * 9 * Cin * 2, xb = M * Cin * 2;
   static const long xmax = [] {

@@ -19,6 +19,7 @@ execution model is MI355X-first:
 from __future__ import annotations
 
 import contextlib
+import math
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -221,9 +222,15 @@ class UNetNative(nn.Module):
 
     def _join_adam(self):
         """Order the current stream after the side stream's Adam group B only (not the re-layouts queued
-        behind it): the next forward's join before its first group-B layer."""
-        if self.__dict__.pop("_adam_ev_pending", False):
-            _native().stream_wait_event(torch.cuda.current_stream().cuda_stream, self._adam_ev)
+        behind it): the next forward's join before its first group-B layer. While a launch plan is
+        recorded the wait is unconditional once the overlap has ever run: an eval or state_dict between
+        steps clears the pending flag, but every replay of the plan follows a replayed overlapped Adam
+        (a wait on a completed event costs almost nothing)."""
+        C = _native()
+        pending = self.__dict__.pop("_adam_ev_pending", False)
+        ev = self.__dict__.get("_adam_ev")
+        if ev is not None and (pending or C.plan_recording()):
+            C.stream_wait_event(torch.cuda.current_stream().cuda_stream, ev)
 
     def state_dict(self, *args, **kwargs):
         # the masters of the Adam update's group B may still be written on the side stream
@@ -316,8 +323,15 @@ class UNetNative(nn.Module):
             split = st.offsets[self.specs[4].name + ".weight"]
             names_a = [n for n in st.names if st.offsets[n] < split]
             own_a = {sp.name for sp in self.specs[:4]}
-            if all(n.rsplit(".", 1)[0] in own_a or any(n.startswith(sp.bn + ".") for sp in self.specs[:4])
-                   for n in names_a):
+            def in_a(n):
+                return n.rsplit(".", 1)[0] in own_a or any(n.startswith(sp.bn + ".") for sp in self.specs[:4])
+
+            def end(n):
+                return st.offsets[n] + math.prod(st.shapes[n])
+
+            # both directions: group A holds only specs[:4]'s parameters, and ALL of them (else the side
+            # stream's group B would update one the next forward's first layers read before the join)
+            if all(in_a(n) for n in names_a) and all(end(n) <= split for n in st.names if in_a(n)):
                 self._adam_split = split
         fwd_a = [s for i, s in enumerate(segs) if i < n_conv and self.specs[i].packed and i < 4]
         fwd_b = [s for s in fwd if s not in fwd_a]
@@ -601,6 +615,7 @@ class UNetExecutor:
             if training:
                 ws = max(ws, C.conv_ws_elems(n, h, w, 4 * us.cout, 0, us.cin, 1, 0, 0))
         self.kws = torch.zeros(ws, dtype=torch.float32, device=dev) if ws else None
+        self._frag_names = frozenset()  # layers whose fragment-major eval weights prepare_eval refreshed
         if training:
             self._alloc_backward(C)
         else:
@@ -721,7 +736,8 @@ class UNetExecutor:
         if not self.training:  # eval: BN folded into the conv epilogue, ReLU fused, writes a directly
             # with ``pool`` / ``up``: MaxPool2d(2) / the upsample too (fused into the split-K reduce or
             # the row-ring epilogue where those run, else separate launches)
-            wf = m.eval_frag_weight(sp)
+            # only a copy this executor's own prepare_eval refreshed (another executor's may be stale)
+            wf = m.eval_frag_weight(sp) if sp.name in self._frag_names else None
             if up is not None:
                 oy = (up.shape[1] - 2 * L.a.shape[1]) // 2
                 ox = (up.shape[2] - 2 * L.a.shape[2]) // 2
@@ -762,16 +778,19 @@ class UNetExecutor:
         # the row-band eval conv's fragment-major weights for the small-map 3x3 layers (csrc/conv_rowband.hip;
         # conv_fwd picks the kernel per layer from its traffic model)
         if self.dev.type == "cuda":
-            m.refresh_eval_frag([L.spec for L in self.layers if self._rowband_candidate(L)])
+            specs = [L.spec for L in self.layers if self._rowband_candidate(C, L)]
+            m.refresh_eval_frag(specs)
+            self._frag_names = frozenset(sp.name for sp in specs)
 
-    def _rowband_candidate(self, L: "_Layer") -> bool:
+    def _rowband_candidate(self, C, L: "_Layer") -> bool:
+        """Whether conv_fwd will run ``L`` on the row-band kernel: asked of the native selector itself
+        (rdp_conv_rowband_frag_auto, csrc/conv_rowband.hip), so the two can never disagree."""
         sp = L.spec
-        n, h, w, _ = L.x1.shape
-        if sp.packed or sp.taps != 9 or sp.cout % 32 or (sp.taps * sp.cin) % 32:
+        if sp.packed or sp.taps != 9:
             return False
-        # the direct kernel up to 64^2 maps; the activation-staged one (>= 256 input channels) up to 128^2
-        staged = sp.cin % 256 == 0 or sp.cin == 128
-        return (n * h * w <= 4096 and w <= 64) or (staged and n * h * w <= 16384)
+        n, h, w, c1 = L.x1.shape
+        c2 = L.x2.shape[3] if L.x2 is not None else 0
+        return C.rowband_frag_mode(n, h, w, c1, c2, sp.cout) > 0
 
     def forward(self, head: bool = True, refresh_eval: bool = True, mask_head: Optional[tuple] = None):
         """Run the network; ``head=False`` stops after up4 (serving applies ``head_mask`` instead).
@@ -1101,6 +1120,10 @@ class UNetExecutor:
         st = self.m.store
         main = torch.cuda.current_stream() if self.overlap_wgrad else None
         pend = self.m.__dict__.pop("_wprep_pending", None)
+        if pend is None and self.overlap_wgrad and C.plan_recording():
+            # recorded plans always join the side stream here: a replay follows a replayed Adam whose
+            # dgrad re-layout runs there, even if an eval / checkpoint cleared the flag before recording
+            pend = self.side
         if pend is not None:  # the dgrad weights rebuilt on a side stream after the last Adam step
             _stream_wait(torch.cuda.current_stream(), pend)
         try:

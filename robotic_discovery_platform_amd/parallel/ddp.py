@@ -306,6 +306,11 @@ def native_comm_group(device: torch.device, tag: str = "grad"):
     return _GRAD_GROUPS[key]
 
 
+def native_comm_ptrs() -> List[int]:
+    """Every natively used RCCL communicator of this process (the comm watchdog polls and aborts all)."""
+    return [ptr for _, ptr in _GRAD_GROUPS.values()]
+
+
 def broadcast_module_state(tensors: Iterable[torch.Tensor], src: int = 0, group=None):
     """Broadcast parameters/buffers from ``src`` so every replica starts identical."""
     for t in tensors:

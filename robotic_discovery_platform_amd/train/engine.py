@@ -147,12 +147,29 @@ class NativeTrainer:
 
     def _make_watchdog(self, comm_ptr: int):
         """Host watchdog over the natively issued collectives (parallel/watchdog.py): they bypass
-        ProcessGroupNCCL's work objects, so its timeout would not see a dead peer."""
+        ProcessGroupNCCL's work objects, so its timeout would not see a dead peer. It polls EVERY native
+        communicator of the process (the gradient buckets' and, with SyncBN, the statistics'), read at
+        each poll so a communicator created later is covered, and aborts all of them on a failure."""
         from ..ops import native
+        from ..parallel.ddp import native_comm_ptrs
         from ..parallel.watchdog import CommWatchdog
         C = native(build_if_missing=False)
-        return CommWatchdog(poll=lambda: tuple(C.comm_async_error(comm_ptr)), abort=lambda: C.comm_abort(comm_ptr),
-                            rank=self.rank)
+
+        def comms():
+            return native_comm_ptrs() or [comm_ptr]
+
+        def poll():
+            for p in comms():
+                code, text = C.comm_async_error(p)
+                if code:
+                    return code, text
+            return 0, ""
+
+        def abort():
+            for p in comms():
+                C.comm_abort(p)
+
+        return CommWatchdog(poll=poll, abort=abort, rank=self.rank)
 
     def _arm_watchdog(self):
         if self.watchdog is not None:
@@ -161,15 +178,19 @@ class NativeTrainer:
             self.watchdog.arm(ev)
 
     @staticmethod
-    def _native_comm_wanted(model) -> bool:
-        """RCCL issued natively (parallel.ddp native_comm_group) unless RDP_DDP_COMM=torch: nccl backend,
-        GPU parameters and the executor's wgrad side stream to issue from."""
+    def native_comm_wanted_env() -> bool:
+        """RCCL issued natively (parallel.ddp native_comm_group) unless RDP_DDP_COMM=torch: nccl backend
+        and the executor's wgrad side stream to issue from (the device is checked by the caller)."""
         import torch.distributed as dist
         mode = os.environ.get("RDP_DDP_COMM", "native")
         if mode not in ("native", "torch"):
             raise ValueError(f"RDP_DDP_COMM must be 'native' or 'torch', got {mode!r}")
-        return (mode == "native" and model.store.device.type == "cuda" and dist.get_backend() == "nccl"
+        return (mode == "native" and dist.is_initialized() and dist.get_backend() == "nccl"
                 and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0")
+
+    @classmethod
+    def _native_comm_wanted(cls, model) -> bool:
+        return model.store.device.type == "cuda" and cls.native_comm_wanted_env()
 
     def _host_call(self, fn):
         """Run ``fn`` (torch.distributed work); while a plan is being recorded, also make it a host call

@@ -265,3 +265,72 @@ def test_side_stream_wprep_matches_inline(bilinear):
     fresh.load_state_dict(sd)
     torch.cuda.synchronize()
     assert torch.equal(nat.derived, fresh.derived)
+
+
+@pytest.mark.parametrize("h,w", [(64, 96), (224, 224), (48, 80)])
+def test_eval_non_power_of_two_widths_match_reference(h, w):
+    """Eval (BN folded, row-band convs where the native selector picks them) at map widths that are not
+    powers of two: the selector must never pick a kernel the launch rejects (down1 at 64 x 96 has W = 48),
+    and every layer it does not pick runs on the implicit GEMM. Compared with UNetRef in eval mode."""
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    torch.manual_seed(11)
+    dev = torch.device("cuda")
+    ref = UNetRef(3, 1).to(dev)
+    with torch.no_grad():  # non-trivial running statistics
+        for name, b in ref.named_buffers():
+            if name.endswith("running_mean"):
+                b.uniform_(-0.2, 0.2)
+            elif name.endswith("running_var"):
+                b.uniform_(0.5, 2.0)
+    ref.eval()
+    nat = UNetNative(3, 1, device=dev, init_from=ref)
+    x = torch.rand(1, 3, h, w, device=dev)
+    with torch.no_grad():
+        want = ref(x.to(torch.bfloat16).float())
+    got = nat.forward(x)
+    torch.cuda.synchronize()
+    assert got.shape == want.shape
+    assert _rel(got, want) < 0.08, _rel(got, want)
+    ex = nat.executor(1, h, w, training=False)
+    from robotic_discovery_platform_amd.ops import native
+    C = native()
+    for L in ex.layers:  # the executor's fragment copies are exactly the selector's picks
+        n_, h_, w_, c1 = L.x1.shape
+        c2 = L.x2.shape[3] if L.x2 is not None else 0
+        picked = (not L.spec.packed and L.spec.taps == 9
+                  and C.rowband_frag_mode(n_, h_, w_, c1, c2, L.spec.cout) > 0)
+        assert (L.spec.name in ex._frag_names) == picked, L.spec.name
+
+
+def test_plan_recorded_after_eval_keeps_adam_joins():
+    """An eval (or checkpoint) between steps 2 and 3 clears the overlapped Adam's pending flags; the plan
+    recorded at step 3 must still hold the forward's wait on the side-stream update (kind 4) and the
+    backward's join of the side stream -- the same op kinds as a plan recorded without the eval."""
+    from robotic_discovery_platform_amd.models.unet import UNetNative
+    from robotic_discovery_platform_amd.models.unet_ref import UNetRef
+    from robotic_discovery_platform_amd.ops import native
+    from robotic_discovery_platform_amd.train.engine import NativeTrainer
+    torch.manual_seed(12)
+    dev = torch.device("cuda")
+    ref = UNetRef(3, 1)
+    x = torch.rand(2, 3, 64, 64, device=dev)
+    y = (torch.rand(2, 1, 64, 64, device=dev) > 0.5).float()
+    C = native()
+    kinds, states = [], []
+    for interrupt in (False, True):
+        nat = UNetNative(3, 1, device=dev, init_from=ref)
+        tr = NativeTrainer(nat, 2, 64, 64, lr=1e-3, plan=True)
+        tr.set_batch(x, y)
+        for i in range(5):
+            if interrupt and i == 2:
+                tr.eval_loss()
+                nat.state_dict()
+            tr.step()
+        torch.cuda.synchronize()
+        k = C.plan_kinds(tr.plan_id)
+        assert k.count(4) >= 1
+        kinds.append(k)
+        states.append(nat.store.flat.clone())
+    assert kinds[0] == kinds[1]
+    assert torch.equal(states[0], states[1])
