@@ -173,8 +173,11 @@ def comm_selfcheck(dev: torch.device, want_native: bool, measure_bw: bool = True
         ok, why = probe_all_reduce(native_ar, dev, rank, world, timeout_s=timeout_s, poll_err=poll,
                                    inject=os.environ.get("RDP_COMM_PROBE_FAIL", "0") == "1")
     ok = agree(ok)
-    if native_ar is not None and not ok:
-        try:  # release any probe collective still waiting on a peer; the buckets go through c10d now
+    if native_ar is not None and not ok and why.startswith(("TimeoutError", "RuntimeError: RCCL async error")):
+        # a probe collective may still wait on a peer: release it (the buckets go through c10d now; the
+        # aborted communicator's group then fails its own teardown, which bench.py tolerates). A probe
+        # that completed with wrong sums leaves the communicator intact.
+        try:
             nat.abort()
         except Exception:
             pass

@@ -44,7 +44,7 @@ def _entry(rank, world, port, kind, out):
 
             def all_reduce(self, t):
                 if kind == "raises":
-                    raise RuntimeError("ncclAllReduce: unhandled system error")
+                    raise TimeoutError("probe all-reduce incomplete after 120 s")
                 dist.all_reduce(t)
                 if kind == "wrong" and rank == 1:  # one rank sees a broken sum: both must fall back
                     t += 1
@@ -87,10 +87,11 @@ def test_failed_native_probe_falls_back_on_every_rank(kind, tmp_path):
     res = _run(kind, tmp_path)
     for r in res:
         assert r["ddp_comm"].startswith("torch (native probe failed: "), r
-        assert r["env_comm"] == "torch" and r["aborted"] == 1
+        # a hung probe aborts the communicator; one that returned wrong sums leaves it alone
+        assert r["env_comm"] == "torch" and r["aborted"] == (1 if kind == "raises" else 0)
         assert r["comm_probe"] == "ok (torch.distributed)"
     if kind == "raises":
-        assert "unhandled system error" in res[0]["ddp_comm"]
+        assert "incomplete after" in res[0]["ddp_comm"]
     else:  # rank 0's own probe passed; it still falls back because rank 1's failed
         assert "elements wrong" in res[1]["ddp_comm"]
 
