@@ -88,6 +88,7 @@ int rdp_adam(float*, const void*, int, float*, float*, void*, long, float, float
              int, hipStream_t);
 int rdp_cast_bf16(const float*, void*, long, hipStream_t);
 int rdp_comm_emulate(double, int, hipStream_t);
+int rdp_comm_emulate_traffic(double, int, void*, long, long, hipStream_t);
 int rdp_rows_fold(const float*, int, int, double*, hipStream_t);
 int rdp_rows_hilo(const double*, float*, int, hipStream_t);
 int rdp_wprep(const float*, void*, const void*, int, int*, int, int, hipStream_t);
@@ -483,8 +484,19 @@ int comm_abort(long comm) {
 
 // RDP_DDP_EMULATE: the modelled all-reduce (`us` microseconds, `blocks` resident workgroups) on the current
 // stream in place of ncclAllReduce (csrc/comm.hip), recorded into plans like the real call
-void comm_emulate(double us, int blocks) {
+// with `scratch` and traffic_bytes > 0: the modelled collective's HBM traffic too (traffic_bytes read from
+// the scratch's first half and written to its second, paced over the duration)
+void comm_emulate(double us, int blocks, c10::optional<torch::Tensor> scratch, long traffic_bytes) {
   TORCH_CHECK(us >= 0 && blocks >= 1 && blocks <= 4096, "comm_emulate: bad duration / block count");
+  if (scratch && traffic_bytes > 0) {
+    TORCH_CHECK(scratch->is_cuda() && scratch->is_contiguous() &&
+                    scratch->numel() * scratch->element_size() >= 2 * traffic_bytes,
+                "comm_emulate: scratch must hold 2 x traffic_bytes");
+    void* const p = scratch->data_ptr();
+    const long nb = scratch->numel() * scratch->element_size();
+    TORCH_CHECK(RDP_PLAN(rdp_comm_emulate_traffic(us, blocks, p, nb, traffic_bytes, st)) == 0, "comm_emulate_traffic");
+    return;
+  }
   RDP_PLAN(rdp_comm_emulate(us, blocks, st));
 }
 
@@ -1566,8 +1578,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_async_error", &comm_async_error, py::arg("comm"), "(code, message) of ncclCommGetAsyncError");
   m.def("comm_abort", &comm_abort, py::arg("comm"), "ncclCommAbort");
   m.def("comm_info", &comm_info, py::arg("comm"), "(ncclCommCount, ncclCommUserRank, ncclCommCuDevice)");
-  m.def("comm_emulate", &comm_emulate, py::arg("us"), py::arg("blocks"),
-        "modelled collective on the current stream (RDP_DDP_EMULATE; recorded in plans)");
+  m.def("comm_emulate", &comm_emulate, py::arg("us"), py::arg("blocks"), py::arg("scratch") = py::none(),
+        py::arg("traffic_bytes") = 0, "RDP_DDP_EMULATE: the modelled all-reduce on the current stream (recorded in plans)");
   m.def("plan_mark", &plan_mark, "record a host call point (replay calls host_call(tag) there)");
   m.def("plan_pause", &plan_pause);
   m.def("plan_resume", &plan_resume);

@@ -312,3 +312,51 @@ extern "C" int rdp_h2d_copy(const void* src, void* dst, long bytes, hipStream_t 
                        (const uint8_t*)src + n16 * 16, (uint8_t*)dst + n16 * 16, ntail);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Several host -> device uploads in ONE launch (the batched serving path: every frame of a batch has its
+// colour / JPEG coefficients, metadata and depth staged in pinned memory): blockIdx.y = segment, each
+// lane moves 4 16-byte chunks strided by the segment's grid row, plus the segment's byte tail.
+struct CopySegs {
+  const uint8_t* src[16];
+  uint8_t* dst[16];
+  long bytes[16];
+};
+
+__global__ __launch_bounds__(256) void h2d_copy_multi_kernel(CopySegs g) {
+  const int sg = blockIdx.y;
+  const long bytes = g.bytes[sg];
+  const long n16 = bytes / 16;
+  const uint4* __restrict__ src = (const uint4*)g.src[sg];
+  uint4* __restrict__ dst = (uint4*)g.dst[sg];
+  const long i = (long)blockIdx.x * 256 + threadIdx.x, str = (long)gridDim.x * 256;
+  for (long b = i; b < n16; b += 4 * str) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (b + u * str < n16) v[u] = src[b + u * str];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (b + u * str < n16) dst[b + u * str] = v[u];
+  }
+  const long t = n16 * 16 + i;
+  if (i < 16 && t < bytes) g.dst[sg][t] = g.src[sg][t];
+}
+
+// n <= 16 segments, every src / dst 16-byte aligned (returns -1, nothing launched, otherwise)
+extern "C" int rdp_h2d_copy_multi(const void* const* src, void* const* dst, const long* bytes, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > 16) return -1;
+  CopySegs g;
+  long most = 0;
+  for (int k = 0; k < n; ++k) {
+    if ((((uintptr_t)src[k] | (uintptr_t)dst[k]) & 15) || bytes[k] < 0) return -1;
+    g.src[k] = (const uint8_t*)src[k];
+    g.dst[k] = (uint8_t*)dst[k];
+    g.bytes[k] = bytes[k];
+    most = std::max(most, bytes[k]);
+  }
+  const long lanes = std::max<long>((most / 16 + 3) / 4, 16);
+  const long bx = std::max<long>(1, (lanes + 255) / 256);
+  hipLaunchKernelGGL(h2d_copy_multi_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, s, g);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

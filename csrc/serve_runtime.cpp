@@ -34,6 +34,7 @@
 namespace py = pybind11;
 
 extern "C" int rdp_h2d_copy(const void*, void*, long, hipStream_t);
+extern "C" int rdp_h2d_copy_multi(const void* const*, void* const*, const long*, int, hipStream_t);
 extern "C" long rdp_png_encode_gray(const uint8_t*, int, int, int, int, int, uint8_t*, long);
 extern "C" long rdp_png_encode_bound(int, int, int, int);
 extern "C" long rdp_jpeg_info(const uint8_t*, long, int*);
@@ -297,7 +298,7 @@ class FrameRunner {
     {
       py::gil_scoped_release nogil;
       DeviceScope g(dev_);
-      hip_check(hipEventSynchronize(ev1_), "hipEventSynchronize");
+      sync_end();
       hip_check(hipEventElapsedTime(&gpu_ms, ev0_, ev1_), "hipEventElapsedTime");
       const double* r = (const double*)h_res_;
       st = (int)r[0];
@@ -329,11 +330,29 @@ class FrameRunner {
     if (!recorded_) return 0.f;  // nothing submitted yet
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
-    hip_check(hipEventSynchronize(ev1_), "hipEventSynchronize");
+    sync_end();
     float ms = 0.f;
     hip_check(hipEventElapsedTime(&ms, ev0_, ev1_), "hipEventElapsedTime");
     return ms;
   }
+
+  // Wait for the frame's end event: poll it for up to spin_us_ microseconds (a frame is ~0.4 ms of GPU
+  // time, so a waiter that polls sees the result as soon as it lands instead of paying a blocking
+  // wait's wake-up), then block. RDP_SERVE_SPIN_US (default 0: block at once) / set_spin_us.
+  void sync_end() {
+    if (spin_us_ > 0) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t q = hipEventQuery(ev1_);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) hip_check(q, "hipEventQuery");
+        if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us_)
+          break;
+      }
+    }
+    hip_check(hipEventSynchronize(ev1_), "hipEventSynchronize");
+  }
+  void set_spin_us(double us) { spin_us_ = us; }
 
  private:
   static void check_contig(const py::buffer_info& b, size_t bytes, const char* what) {
@@ -350,6 +369,10 @@ class FrameRunner {
     if (!exec_[slot]) throw std::runtime_error("FrameRunner: graph slot " + std::to_string(slot) + " not set");
   }
 
+  double spin_us_ = [] {
+    const char* e = getenv("RDP_SERVE_SPIN_US");
+    return e ? atof(e) : 0.0;
+  }();
   bool recorded_ = false;
   bool depth_stream_ = true;
   int H_ = 0, W_ = 0, ns_ = 0;
@@ -367,6 +390,274 @@ class FrameRunner {
   void *d_meta_ = nullptr, *d_coef_ = nullptr, *d_mask_ = nullptr, *h_mask_ = nullptr;
   void *d_res_ = nullptr, *h_res_ = nullptr;
   size_t color_bytes_ = 0, depth_bytes_ = 0, meta_bytes_ = 0, coef_cap_ = 0, mask_bytes_ = 0, res_bytes_ = 0;
+};
+
+// ---- batched frames across streams ----------------------------------------------------------------------
+// BatchRunner: the host side of serve/engine.py BatchEngine. Frames of several client streams are gathered
+// into a batch of n <= P positions and run as ONE captured graph -- the U-Net at batch n (the network costs
+// 0.379 / 0.476 / 0.700 ms at n = 1 / 2 / 4, so four frames need 46 % of the GPU time of four n = 1
+// frames) plus every frame's geometry -- instead of n graphs that time-slice the GPU. K batch frames
+// rotate (one open for new frames, the others in flight or being collected); each (frame k, position j)
+// owns its pinned staging and the host memory its results land in, the device inputs belong to position
+// j (uploads are stream-ordered after the previous batch's graph). Everything here runs without the GIL:
+// decoding a request into its position, the batch's uploads (one multi-segment copy kernel) and graph
+// launch, the wait and the response encoding.
+class BatchRunner {
+ public:
+  BatchRunner(int device, uintptr_t stream, int frames, int positions, int H, int W, int num_samples, int src,
+              size_t coef_cap, size_t res_doubles)
+      : dev_(device), s_((hipStream_t)stream), K_(frames), P_(positions), H_(H), W_(W), ns_(num_samples), src_(src),
+        coef_cap_(coef_cap), res_len_(res_doubles) {
+    if (K_ < 1 || P_ < 1 || P_ > 4 || src_ < 0 || src_ > 2) throw std::invalid_argument("BatchRunner: frames / positions / src");
+    DeviceScope g(dev_);
+    ev0_.resize(K_);
+    ev1_.resize(K_);
+    for (int k = 0; k < K_; ++k) {
+      hip_check(hipEventCreate(&ev0_[k]), "hipEventCreate");
+      hip_check(hipEventCreate(&ev1_[k]), "hipEventCreate");
+    }
+    const size_t npos = (size_t)K_ * P_;
+    slots_.resize(npos);
+    for (auto& sl : slots_) {
+      if (src_ == 2) {
+        sl.color = pinned(coef_cap_ ? coef_cap_ : 16);
+        sl.meta = pinned(224 * 4);
+      } else {
+        sl.color = pinned((size_t)H_ * W_ * 3);
+      }
+      sl.depth = pinned((size_t)H_ * W_ * 2);
+      sl.mask = coherent((size_t)H_ * W_);
+      sl.res = coherent(res_len_ * 8);
+    }
+    dcol_.assign(P_, nullptr);
+    dmeta_.assign(P_, nullptr);
+    ddep_.assign(P_, nullptr);
+    exec_.assign((size_t)K_ * (P_ + 1), nullptr);
+    spin_us_ = getenv("RDP_SERVE_SPIN_US") ? atof(getenv("RDP_SERVE_SPIN_US")) : 1000.0;
+  }
+  ~BatchRunner() {
+    for (auto e : ev0_) (void)hipEventDestroy(e);
+    for (auto e : ev1_) (void)hipEventDestroy(e);
+    for (void* p : pinned_) (void)hipHostFree(p);
+  }
+  // host buffers of (k, j): 0 colour (arrays) / JPEG coefficients, 1 JPEG meta, 2 depth, 3 mask, 4 result
+  uintptr_t host_ptr(int kind, int k, int j) {
+    Slot& sl = slot(k, j);
+    void* p = kind == 0 ? sl.color : kind == 1 ? sl.meta : kind == 2 ? sl.depth : kind == 3 ? sl.mask : kind == 4 ? sl.res
+                                                                                                        : nullptr;
+    if (!p) throw std::invalid_argument("BatchRunner.host_ptr: kind");
+    return (uintptr_t)p;
+  }
+  // device inputs of position j (the captured graphs read them)
+  void set_device(int j, uintptr_t color, uintptr_t meta, uintptr_t depth) {
+    if (j < 0 || j >= P_) throw std::invalid_argument("position");
+    dcol_[j] = P(color);
+    dmeta_[j] = P(meta);
+    ddep_[j] = P(depth);
+  }
+  void set_graph(int k, int n, uintptr_t exec) {
+    if (k < 0 || k >= K_ || n < 1 || n > P_) throw std::invalid_argument("BatchRunner.set_graph");
+    exec_[(size_t)k * (P_ + 1) + n] = (hipGraphExec_t)exec;
+  }
+  void set_spin_us(double us) { spin_us_ = us; }
+
+  // a request's colour JPEG + 16-bit depth PNG decoded into (k, j): 0 ok, 1 not a frame this path takes,
+  // 2 other frame size, 3 corrupt
+  int decode(int k, int j, py::bytes color, py::bytes depth) {
+    if (src_ != 2) throw std::runtime_error("BatchRunner.decode: not a JPEG batch runner");
+    char *cp = nullptr, *dp = nullptr;
+    Py_ssize_t cn = 0, dn = 0;
+    if (PyBytes_AsStringAndSize(color.ptr(), &cp, &cn) != 0 || PyBytes_AsStringAndSize(depth.ptr(), &dp, &dn) != 0)
+      throw py::error_already_set();
+    Slot& sl = slot(k, j);
+    py::gil_scoped_release nogil;
+    sl.t0 = std::chrono::steady_clock::now();
+    const uint8_t* c = (const uint8_t*)cp;
+    const uint8_t* d = (const uint8_t*)dp;
+    int hi[24];
+    const long nco = rdp_jpeg_info(c, (long)cn, hi);
+    if (nco == -1) return 3;
+    if (nco <= 0) return 1;
+    int pw = 0, ph = 0, bd = 0;
+    if (rdp_png_info(d, (long)dn, &pw, &ph, &bd) != 0 || bd != 16) return 1;
+    if (hi[0] != W_ || hi[1] != H_ || pw != W_ || ph != H_) return 2;
+    if ((size_t)nco * 2 > coef_cap_) return 1;
+    int rc[2] = {0, 0};
+    rdp::host_pool().parallel_for(2, [&](int h) {
+      if (h == 0) {
+        int* meta = (int*)sl.meta;
+        rdp_jpeg_meta(hi, meta);
+        uint16_t qt[3 * 64];
+        if (rdp_jpeg_decode(c, (long)cn, (int16_t*)sl.color, nco, qt, 1) != 0) {
+          rc[0] = 3;
+          return;
+        }
+        for (int i = 0; i < 3 * 64; ++i) meta[32 + i] = qt[i];
+      } else if (rdp_png_decode(d, (long)dn, (uint8_t*)sl.depth, (long)H_ * W_ * 2, 1) != 0) {
+        rc[1] = 3;
+      }
+    });
+    if (rc[0] || rc[1]) return 3;
+    sl.bytes = (size_t)nco * 2;
+    return 0;
+  }
+
+  // (arrays source) an HxWx3 u8 colour frame and HxW 16-bit depth frame staged into (k, j)
+  void stage(int k, int j, py::buffer color, py::buffer depth) {
+    if (src_ == 2) throw std::runtime_error("BatchRunner.stage: a JPEG batch runner");
+    py::buffer_info c = color.request(), d = depth.request();
+    contig(c, (size_t)H_ * W_ * 3, "colour");
+    contig(d, (size_t)H_ * W_ * 2, "depth");
+    Slot& sl = slot(k, j);
+    const void *cp = c.ptr, *dp = d.ptr;
+    py::gil_scoped_release nogil;
+    sl.t0 = std::chrono::steady_clock::now();
+    std::memcpy(sl.color, cp, (size_t)H_ * W_ * 3);
+    std::memcpy(sl.depth, dp, (size_t)H_ * W_ * 2);
+    sl.bytes = (size_t)H_ * W_ * 3;
+  }
+
+  // batch frame k with its first n positions: every upload in one copy kernel, the graph, the end event
+  void launch(int k, int n) {
+    if (k < 0 || k >= K_ || n < 1 || n > P_) throw std::invalid_argument("BatchRunner.launch");
+    hipGraphExec_t ex = exec_[(size_t)k * (P_ + 1) + n];
+    if (!ex) throw std::runtime_error("BatchRunner: graph (" + std::to_string(k) + ", " + std::to_string(n) + ") not set");
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    const void* src[16];
+    void* dst[16];
+    long bytes[16];
+    int m = 0;
+    for (int j = 0; j < n; ++j) {
+      Slot& sl = slot(k, j);
+      src[m] = devptr(sl.color); dst[m] = dcol_[j]; bytes[m++] = (long)sl.bytes;
+      if (src_ == 2) { src[m] = devptr(sl.meta); dst[m] = dmeta_[j]; bytes[m++] = 224 * 4; }
+      src[m] = devptr(sl.depth); dst[m] = ddep_[j]; bytes[m++] = (long)H_ * W_ * 2;
+    }
+    hip_check(hipEventRecord(ev0_[k], s_), "hipEventRecord");
+    if (rdp_h2d_copy_multi(src, dst, bytes, m, s_) != 0) {
+      (void)hipGetLastError();
+      for (int i = 0; i < m; ++i)
+        hip_check(hipMemcpyAsync(dst[i], src[i], (size_t)bytes[i], hipMemcpyHostToDevice, s_), "H2D batch");
+    }
+    hip_check(hipGraphLaunch(ex, s_), "hipGraphLaunch");
+    hip_check(hipEventRecord(ev1_[k], s_), "hipEventRecord");
+  }
+
+  // block until batch k's results are on the host; its device time (ms)
+  float wait(int k) {
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    return sync(k);
+  }
+
+  // (payload, mean, max, coverage %, status, gpu ms) of (k, j) after its batch ran (status 4: host fit needed)
+  py::tuple collect_encoded(int k, int j, int level, int bands) {
+    float gpu_ms = 0.f;
+    double mean = 0, maxc = 0, cov = 0;
+    int st = 0;
+    std::string out;
+    {
+      py::gil_scoped_release nogil;
+      DeviceScope g(dev_);
+      gpu_ms = sync(k);
+      Slot& sl = slot(k, j);
+      const double* r = (const double*)sl.res;
+      st = (int)r[0];
+      cov = 100.0 * r[8 + 3 * ns_] / ((double)H_ * W_);
+      if (st != 4) {
+        static const char* names[4] = {"ok", "too_few_points", "too_few_edge_points", "fit_failed"};
+        const std::string status = (st >= 0 && st < 4) ? names[st] : "fit_failed";
+        if (st == 0) { mean = r[4]; maxc = r[5]; }
+        const float proc = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - sl.t0).count();
+        out = encode_wire(mean, maxc, st == 0 ? r + 8 : nullptr, st == 0 ? (size_t)ns_ : 0, status,
+                          (const uint8_t*)sl.mask, H_, W_, (float)cov, proc, level, bands);
+      }
+    }
+    return py::make_tuple(py::bytes(out), mean, maxc, cov, st, gpu_ms);
+  }
+
+  void drain() {
+    py::gil_scoped_release nogil;
+    DeviceScope g(dev_);
+    hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
+  }
+
+ private:
+  struct Slot {
+    void *color = nullptr, *meta = nullptr, *depth = nullptr, *mask = nullptr, *res = nullptr;
+    size_t bytes = 0;
+    std::chrono::steady_clock::time_point t0;
+  };
+  Slot& slot(int k, int j) {
+    if (k < 0 || k >= K_ || j < 0 || j >= P_) throw std::invalid_argument("BatchRunner: (frame, position)");
+    return slots_[(size_t)k * P_ + j];
+  }
+  float sync(int k) {
+    if (k < 0 || k >= K_) throw std::invalid_argument("BatchRunner: frame");
+    if (spin_us_ > 0) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t q = hipEventQuery(ev1_[k]);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) hip_check(q, "hipEventQuery");
+        if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us_) {
+          hip_check(hipEventSynchronize(ev1_[k]), "hipEventSynchronize");
+          break;
+        }
+      }
+    } else {
+      hip_check(hipEventSynchronize(ev1_[k]), "hipEventSynchronize");
+    }
+    float ms = 0.f;
+    hip_check(hipEventElapsedTime(&ms, ev0_[k], ev1_[k]), "hipEventElapsedTime");
+    return ms;
+  }
+  void* pinned(size_t bytes) {
+    DeviceScope g(dev_);
+    void* p = nullptr;
+    hip_check(hipHostMalloc(&p, (bytes + 15) / 16 * 16, hipHostMallocDefault), "hipHostMalloc");
+    std::memset(p, 0, bytes);
+    pinned_.push_back(p);
+    return p;
+  }
+  void* coherent(size_t bytes) {
+    DeviceScope g(dev_);
+    void* p = nullptr;
+    hip_check(hipHostMalloc(&p, (bytes + 15) / 16 * 16, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
+    std::memset(p, 0, bytes);
+    pinned_.push_back(p);
+    return p;
+  }
+  void* devptr(void* host) {  // the device mapping of a pinned buffer (the copy kernel reads through it)
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, host, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return host;
+    }
+    return dp;
+  }
+  static void contig(const py::buffer_info& b, size_t bytes, const char* what) {
+    size_t n = (size_t)b.itemsize;
+    for (auto sh : b.shape) n *= (size_t)sh;
+    ssize_t expect = b.itemsize;
+    for (ssize_t i = b.ndim - 1; i >= 0; --i) {
+      if (b.shape[i] > 1 && b.strides[i] != expect) throw std::invalid_argument(std::string(what) + ": not C-contiguous");
+      expect *= b.shape[i];
+    }
+    if (n != bytes) throw std::invalid_argument(std::string(what) + ": size does not match the batch runner");
+  }
+
+  int dev_;
+  hipStream_t s_;
+  int K_, P_, H_, W_, ns_, src_;
+  size_t coef_cap_, res_len_;
+  double spin_us_ = 1000.0;
+  std::vector<hipEvent_t> ev0_, ev1_;
+  std::vector<Slot> slots_;
+  std::vector<void*> dcol_, dmeta_, ddep_;
+  std::vector<hipGraphExec_t> exec_;
+  std::vector<void*> pinned_;
 };
 
 // ---- protobuf wire format (proto3)
@@ -478,7 +769,24 @@ void register_serve_runtime(py::module_& m) {
            "0 launched, 1 not a native frame, 2 other frame size, 3 corrupt (nothing in flight)")
       .def("collect_encoded", &FrameRunner::collect_encoded, py::arg("level") = 1, py::arg("bands") = 4)
       .def("abort", &FrameRunner::abort)
+      .def("set_spin_us", &FrameRunner::set_spin_us, py::arg("us"),
+           "poll the frame's end event for up to `us` microseconds before blocking")
       .def("wait", &FrameRunner::wait);
+  py::class_<BatchRunner>(m, "BatchRunner")
+      .def(py::init<int, uintptr_t, int, int, int, int, int, int, size_t, size_t>(), py::arg("device"),
+           py::arg("stream"), py::arg("frames"), py::arg("positions"), py::arg("H"), py::arg("W"),
+           py::arg("num_samples"), py::arg("src"), py::arg("coef_cap"), py::arg("res_doubles"))
+      .def("host_ptr", &BatchRunner::host_ptr)
+      .def("set_device", &BatchRunner::set_device)
+      .def("set_graph", &BatchRunner::set_graph)
+      .def("set_spin_us", &BatchRunner::set_spin_us)
+      .def("decode", &BatchRunner::decode, "0 ok, 1 not a native frame, 2 other frame size, 3 corrupt")
+      .def("stage", &BatchRunner::stage)
+      .def("launch", &BatchRunner::launch)
+      .def("wait", &BatchRunner::wait)
+      .def("collect_encoded", &BatchRunner::collect_encoded, py::arg("k"), py::arg("j"), py::arg("level") = 1,
+           py::arg("bands") = 4)
+      .def("drain", &BatchRunner::drain);
   m.def("encode_response", &encode_response, py::arg("mean"), py::arg("max"), py::arg("points"), py::arg("status"),
         py::arg("mask"), py::arg("coverage"), py::arg("proc_ms"), py::arg("level") = 1, py::arg("bands") = 4);
 }

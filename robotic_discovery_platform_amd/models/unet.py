@@ -977,7 +977,7 @@ class UNetExecutor:
             emu = getattr(self, "sync_emulate", None)
             if emu is not None:  # RDP_DDP_EMULATE: the modelled collective instead (one-GPU A/B)
                 from ..parallel.ddp import ring_allreduce_us
-                n, bw, blocks, alpha = emu
+                n, bw, blocks, alpha, _traffic = emu  # (16 c bytes: traffic is negligible)
                 C.comm_emulate(ring_allreduce_us(16 * c, n, bw, alpha), 1)
             else:
                 C.comm_all_reduce(ws[: 2 * c], self.sync_comm)

@@ -52,23 +52,26 @@ import torch
 import torch.distributed as dist
 
 
-def emulate_spec(spec: Optional[str] = None) -> Optional[Tuple[int, float, int, float]]:
-    """Parse ``RDP_DDP_EMULATE`` = ``<n>:<GB/s>[:<blocks>[:<alpha_us>]]`` -> (n, GB/s, blocks, alpha_us), or
-    None. ``blocks`` resident workgroups (default 16, RCCL's channel count order on xGMI), ``alpha_us``
-    the fixed latency of one ring all-reduce (default 15 us: 2 (n - 1) hops of ~1 us)."""
+def emulate_spec(spec: Optional[str] = None) -> Optional[Tuple[int, float, int, float, float]]:
+    """Parse ``RDP_DDP_EMULATE`` = ``<n>:<GB/s>[:<blocks>[:<alpha_us>[:<traffic_x>]]]`` -> (n, GB/s, blocks,
+    alpha_us, traffic_x), or None. ``blocks`` resident workgroups (default 16, RCCL's channel count order on
+    xGMI), ``alpha_us`` the fixed latency of one ring all-reduce (default 15 us: 2 (n - 1) hops of ~1 us),
+    ``traffic_x`` the HBM traffic the emulated collective streams, in multiples of the bucket read AND
+    written over its duration (default 0: residency only; a ring all-reduce moves ~3x the bucket)."""
     import os
     spec = os.environ.get("RDP_DDP_EMULATE", "") if spec is None else spec
     if not spec:
         return None
     parts = spec.split(":")
     if len(parts) < 2:
-        raise ValueError(f"RDP_DDP_EMULATE must be <n>:<GB/s>[:<blocks>[:<alpha_us>]], got {spec!r}")
+        raise ValueError(f"RDP_DDP_EMULATE must be <n>:<GB/s>[:<blocks>[:<alpha_us>[:<traffic_x>]]], got {spec!r}")
     n, bw = int(parts[0]), float(parts[1])
     blocks = int(parts[2]) if len(parts) > 2 and parts[2] else 16
     alpha = float(parts[3]) if len(parts) > 3 and parts[3] else 15.0
-    if n < 2 or bw <= 0 or not 1 <= blocks <= 4096 or alpha < 0:
+    traffic = float(parts[4]) if len(parts) > 4 and parts[4] else 0.0
+    if n < 2 or bw <= 0 or not 1 <= blocks <= 4096 or alpha < 0 or not 0 <= traffic <= 16:
         raise ValueError(f"RDP_DDP_EMULATE out of range: {spec!r}")
-    return n, bw, blocks, alpha
+    return n, bw, blocks, alpha, traffic
 
 
 def ring_allreduce_us(nbytes: int, n: int, gbps: float, alpha_us: float) -> float:
@@ -89,10 +92,11 @@ class FlatBucketer:
                  bucket_mb: float = 16.0, group=None, comm_dtype: Optional[torch.dtype] = None,
                  launch_ctx: Optional[Callable[[], ContextManager]] = None, native_comm: Optional[int] = None,
                  join: Optional[Callable[[], None]] = None,
-                 emulate: Optional[Tuple[int, float, int, float]] = None):
+                 emulate: Optional[Tuple[int, float, int, float, float]] = None):
         self.grad = grad_flat
         # (n, GB/s, blocks, alpha_us): a modelled collective instead of ncclAllReduce (native issue only)
         self.emulate = emulate
+        self._emu_scratch: Optional[torch.Tensor] = None  # the emulated collectives' HBM traffic buffer
         # RCCL communicator (ncclComm_t as int) for native issue, and the callable that orders the
         # caller's stream after the issuing stream once every bucket is out (native mode has no handles)
         self.native_comm = native_comm
@@ -173,8 +177,13 @@ class FlatBucketer:
                     buf = self.comm[lo:hi]
                     C.cast_bf16(self.grad[lo:hi], buf)  # narrowing cast, ordered after every producer
                 if self.emulate is not None:
-                    n, bw, blocks, alpha = self.emulate
-                    C.comm_emulate(ring_allreduce_us(buf.numel() * buf.element_size(), n, bw, alpha), blocks)
+                    n, bw, blocks, alpha, traffic = self.emulate
+                    nbytes = buf.numel() * buf.element_size()
+                    tb = int(traffic * nbytes) // 16 * 16
+                    if tb > 0 and (self._emu_scratch is None or self._emu_scratch.numel() < 2 * tb):
+                        self._emu_scratch = torch.zeros(2 * tb, dtype=torch.uint8, device=buf.device)
+                    C.comm_emulate(ring_allreduce_us(nbytes, n, bw, alpha), blocks,
+                                   self._emu_scratch if tb > 0 else None, tb)
                 else:
                     C.comm_all_reduce(buf, self.native_comm)
                 self.handles.append((b, None))

@@ -30,6 +30,26 @@ def _pct(v, q):
     return float(np.percentile(np.asarray(v), q)) if len(v) else float("nan")
 
 
+def _freeze():
+    """gc.freeze() once the long-lived objects exist, as the server does (server.freeze_heap)."""
+    import gc
+    gc.collect()
+    gc.freeze()
+
+
+def slow_frames(lat, parts: dict) -> dict:
+    """Frames slower than 2x the median and, per frame, the part (of ``parts``: name -> per-frame ms) that
+    exceeded its own median by the most: {"count": n, "<part>": frames, ...}."""
+    lat = np.asarray(lat)
+    med = {k: float(np.median(v)) for k, v in parts.items()}
+    out = {"count": 0}
+    for i in np.nonzero(lat > 2 * np.median(lat))[0]:
+        k = max(parts, key=lambda k: parts[k][i] - med[k])
+        out[k] = out.get(k, 0) + 1
+        out["count"] += 1
+    return out
+
+
 def prepare_model(dev, train_steps: int = 200, batch: int = 16, n_scenes: int = 48, seed: int = 0):
     from ..data.image_io import bgr2rgb, resize_area, resize_nearest
     from ..data.synthetic import make_scene
@@ -61,6 +81,8 @@ def measure_engine(model, scenes, frames: int = 200, warmup: int = 20):
     ok = 0
     for i in range(warmup + frames):
         s = scenes[i % len(scenes)]
+        if i == warmup:
+            _freeze()
         t0 = time.perf_counter()
         r = p.process(s.color, s.depth)
         dt = (time.perf_counter() - t0) * 1e3
@@ -69,9 +91,12 @@ def measure_engine(model, scenes, frames: int = 200, warmup: int = 20):
             gpu.append(r.timings["gpu_ms"])
             fit.append(r.timings["fit_ms"])
             ok += r.curvature.status == "ok"
+    host = [a - b - c for a, b, c in zip(lat, gpu, fit)]
     out = {"engine_fps": round(1e3 * len(lat) / sum(lat), 1), "engine_p50_ms": round(_pct(lat, 50), 3),
            "engine_p99_ms": round(_pct(lat, 99), 3), "engine_gpu_p50_ms": round(_pct(gpu, 50), 3),
-           "engine_fit_p50_ms": round(_pct(fit, 50), 3), "engine_ok_frac": ok / max(1, len(lat))}
+           "engine_gpu_p99_ms": round(_pct(gpu, 99), 3), "engine_frames": len(lat),
+           "engine_fit_p50_ms": round(_pct(fit, 50), 3), "engine_ok_frac": ok / max(1, len(lat)),
+           "engine_slow_frames": slow_frames(lat, {"gpu": gpu, "fit": fit, "host": host})}
     out.update(measure_engine_pipelined(model, scenes, frames, warmup))
     return out
 
@@ -114,6 +139,7 @@ def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8, lock
     from ..proto import vision as pb
     from .client import make_request
     reqs = [make_request(sc.color, sc.depth) for sc in (make_scene(i) for i in range(n_scenes))]
+    _freeze()
     if go is not None:
         go()
     out = {}
@@ -147,14 +173,21 @@ def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8, lock
                 yield reqs[i % len(reqs)]
                 q.get()
 
-        rtt = []
+        rtt, sproc = [], []
         for i, resp in enumerate(stub.AnalyzeActuatorPerformance(gen_ls())):
             now = time.perf_counter()
             if i >= warmup:
                 rtt.append((now - sent[i]) * 1e3)
+                sproc.append(resp.proc_time_ms)
             q.put(1)
         out["e2e_p50_ms"] = round(_pct(rtt, 50), 3)
         out["e2e_p99_ms"] = round(_pct(rtt, 99), 3)
+        out["e2e_p999_ms"] = round(_pct(rtt, 99.9), 3)
+        out["e2e_lockstep_frames"] = len(rtt)
+        # each slow round trip: the server's processing (the response's proc_time_ms) or everything
+        # around it (transport, gRPC threads, the client)
+        out["e2e_slow_frames"] = slow_frames(rtt, {"server_proc": sproc,
+                                                   "transport": [a - b for a, b in zip(rtt, sproc)]})
     return out
 
 
@@ -328,6 +361,7 @@ def _server_child(wpath: str, pool: int) -> None:
     pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
     port = server.add_insecure_port("127.0.0.1:0")
     server.start()
+    _freeze()
     print(f"port {port}", flush=True)
     sys.stdin.read()
     server.stop(0).wait()
@@ -364,6 +398,7 @@ def measure_e2e(model, scenes, frames: int = 200, warmup: int = 20, pool: int = 
     pb.add_VisionAnalysisServiceServicer_to_server(svc, server)
     port = server.add_insecure_port("127.0.0.1:0")
     server.start()
+    _freeze()  # as build_server does
     out = {}
     sfx = "" if streams == 1 else f"_{streams}streams"
     try:
@@ -404,7 +439,7 @@ def _progress(msg):
     print(f"[bench_serve] {msg}", file=sys.stderr, flush=True)
 
 
-def measure_serving(dev: Optional[torch.device] = None, frames: int = 200, warmup: int = 20,
+def measure_serving(dev: Optional[torch.device] = None, frames: int = 2000, warmup: int = 50,
                     train_steps: int = 200, e2e: bool = True, multi: bool = True) -> dict:
     dev = dev or torch.device("cuda")
     model, scenes = prepare_model(dev, train_steps)
@@ -428,8 +463,8 @@ if __name__ == "__main__":
     import argparse
     import json
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--frames", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--train-steps", type=int, default=200)
     ap.add_argument("--e2e", type=int, default=1)
     ap.add_argument("--multi", type=int, default=1, help="also the 4-thread engine rate")

@@ -186,6 +186,9 @@ class FramePipeline:
             self.h_res = _host_tensor(r, (self.geo.res.numel(),), np.float64)
             self.zero_copy = True
             nb = lambda t: t.numel() * t.element_size()  # noqa: E731
+            # poll the frame's end event before blocking (FrameRunner.sync_end): a frame is ~0.4 ms of GPU
+            # time and a blocking wait's wake-up put 0.05-0.4 ms on the slow frames (profiles/serve_tail.md)
+            r.set_spin_us(float(os.environ.get("RDP_SERVE_SPIN_US", "1000")))
             r.set_buffers(self.d_color.data_ptr(), self.h_color.data_ptr(), nb(self.d_color),
                           self.d_depth.data_ptr(), self.h_depth.data_ptr(), nb(self.d_depth),
                           self.d_meta.data_ptr(), nb(self.d_meta), self.d_coef.data_ptr(), nb(self.d_coef),
@@ -406,6 +409,317 @@ class FramePipeline:
             return self.collect()
 
 
+class BatchEngine:
+    """Frames of several client streams run as ONE batched device program (one replica, one GPU).
+
+    The network is latency-bound at N = 1 (0.379 ms; 0.476 at N = 2, 0.700 at N = 4), and N = 1 graphs of
+    concurrent streams time-slice the GPU instead of sharing its width: four streams served 3,179 frames/s
+    against 3,410 for one (driver, round 5). Here a frame takes a position j of the open batch frame k
+    (K frames rotate, P positions each), is decoded / staged straight into that position's pinned buffers
+    (natively, no interpreter lock: csrc/serve_runtime.cpp BatchRunner), and a launcher thread closes the
+    batch and launches it as one captured graph -- per position the JPEG pixel stage and preprocess into
+    slice j of the batch-n input, the U-Net at batch n with the head + threshold fused, then per position
+    the geometry (mask upsample, back-projection, edge bins, spline fit) writing that position's host
+    result memory. Launch policy: at once when the batch is full or the GPU has nothing of this engine in
+    flight; otherwise the batch keeps filling until the GPU drains or ``window_us`` passed since its first
+    frame -- under load batches grow, when idle a frame never waits.
+
+    Reference per-frame body: ``/root/reference/services/vision_analysis/server.py:116-152`` (10 worker
+    threads sharing one model, ``:172``)."""
+
+    def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, threshold: float = 0.5,
+                 geo_cfg: Optional[GeometryConfig] = None, device: Optional[torch.device] = None, src: int = SRC_JPEG,
+                 frames: int = 3, positions: int = 4, window_us: float = 300.0):
+        dev = _norm_device(device if device is not None else model.store.device)
+        with torch.cuda.device(dev):
+            self._init(model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, frames, positions, window_us)
+
+    def _init(self, model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, frames, positions, window_us):
+        from ..models.unet import UNetExecutor
+        from ..ops import native
+        C = self.C = native()
+        self.model, self.dev, self.src = model, dev, src
+        self.H, self.W, self.S = H, W, size
+        self.K = np.asarray(K, np.float64)
+        self.scale = float(depth_scale)
+        self.thr_logit = _logit(threshold)
+        self.cfg = geo_cfg or GeometryConfig()
+        self.nf, self.P = int(frames), int(positions)
+        self.window = window_us * 1e-6
+        self.stream = torch.cuda.Stream(dev)
+        ys, yn, yw = aa_tables(H, size)
+        xs, xn, xw = aa_tables(W, size)
+        self.tab = [torch.from_numpy(a).to(dev) for a in (ys, yn, yw, xs, xn, xw)]
+        jpeg = src == SRC_JPEG
+        coef_cap = C.jpeg_max_coefs(H, W) if jpeg else 0
+        ecap = self.cfg.num_bins + int(H * W * self.cfg.top_k_percent) + 1
+        self.geo = [[GeometryEngine(H, W, dev, self.cfg, ecap=ecap) for _ in range(self.P)] for _ in range(self.nf)]
+        self.masks = [[torch.empty(H, W, dtype=torch.uint8, device=dev) for _ in range(self.P)] for _ in range(self.nf)]
+        res_len = self.geo[0][0].res.numel()
+        self.runner = C.BatchRunner(dev.index, self.stream.cuda_stream, self.nf, self.P, H, W, self.cfg.num_samples,
+                                    src, coef_cap * 2, res_len)
+        self.runner.set_spin_us(float(os.environ.get("RDP_SERVE_SPIN_US", "1000")))
+        # position inputs on the device (uploads are ordered after the previous batch on the one stream)
+        self.d_color = [torch.empty(H, W, 3, dtype=torch.uint8, device=dev) for _ in range(self.P)]
+        self.d_depth = [torch.empty(H, W, dtype=torch.int16, device=dev) for _ in range(self.P)]
+        if jpeg:
+            self.d_coef = [torch.empty(coef_cap, dtype=torch.int16, device=dev) for _ in range(self.P)]
+            self.d_meta = [torch.zeros(32 + 192, dtype=torch.int32, device=dev) for _ in range(self.P)]
+            self.d_planes = [torch.empty(C.jpeg_plane_bytes(H, W), dtype=torch.uint8, device=dev)
+                             for _ in range(self.P)]
+        for j in range(self.P):
+            up = self.d_coef[j] if jpeg else self.d_color[j]
+            self.runner.set_device(j, up.data_ptr(), self.d_meta[j].data_ptr() if jpeg else 0, self.d_depth[j].data_ptr())
+        # host results of (k, j): mask + result vector in the runner's fine-grained host memory
+        def host(kind, k, j, shape, dtype):
+            import ctypes
+            n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+            buf = (ctypes.c_uint8 * n).from_address(self.runner.host_ptr(kind, k, j))
+            return torch.from_numpy(np.frombuffer(buf, dtype=dtype).reshape(shape))
+        self.h_mask = [[host(3, k, j, (H, W), np.uint8) for j in range(self.P)] for k in range(self.nf)]
+        self.h_res = [[host(4, k, j, (res_len,), np.float64) for j in range(self.P)] for k in range(self.nf)]
+        # one eval executor per batch size (activations shared by every batch frame: one stream)
+        self.ex = {n: UNetExecutor(model, n, size, size, False, "bce", 1.0) for n in range(1, self.P + 1)}
+        self.m256 = {n: torch.empty(n * size * size, dtype=torch.uint8, device=dev) for n in range(1, self.P + 1)}
+        self.graphs = {}
+        self.refresh_weights()
+        for k in range(self.nf):
+            for n in range(1, self.P + 1):
+                self._capture(k, n)
+        # batching state (under _cv)
+        self._cv = threading.Condition()
+        self._free = collections.deque(range(self.nf))
+        self._open = None        # batch frame taking new frames
+        self._acq = 0            # positions handed out in the open frame
+        self._ready = 0          # of those, staged
+        self._void = set()       # positions of the open frame whose staging failed (run, result dropped)
+        self._t_first = 0.0
+        self._refs = [0] * self.nf  # results of a launched frame not yet collected
+        self._gen = [0] * self.nf  # times each frame was opened
+        self._launched_gen = [0] * self.nf  # ... and launched (a collect waits for its frame's launch)
+        self._launched = collections.deque()  # launched frames, oldest first (GPU occupancy)
+        self._done_evs = {}
+        self.batch_sizes = collections.Counter()
+        self._stop = False
+        self._th = threading.Thread(target=self._launcher, name="rdp-batch-launcher", daemon=True)
+        self._th.start()
+
+    # ------------------------------------------------------------------ device program
+    def _program(self, k: int, n: int):
+        C, m = self.C, self.model
+        ex = self.ex[n]
+        for j in range(n):
+            if self.src == SRC_JPEG:
+                C.jpeg_to_rgb(self.d_coef[j], self.d_meta[j][:32], self.d_meta[j][32:], self.d_planes[j], self.d_color[j])
+            C.preprocess(self.d_color[j], *self.tab, ex.x_in[j:j + 1], int(self.src != SRC_BGR))
+        ex.forward(head=False, refresh_eval=False,
+                   mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
+                              self.thr_logit, self.m256[n]))
+        S2 = self.S * self.S
+        for j in range(n):
+            g = self.geo[k][j]
+            g.launch_frame(self.m256[n][j * S2:(j + 1) * S2].view(self.S, self.S), self.masks[k][j], self.d_depth[j],
+                           self.K, self.scale, mask_host=self.h_mask[k][j], host_copy_in_spline=True)
+            g.launch_spline(res_out=self.h_res[k][j])
+
+    def _capture(self, k: int, n: int):
+        with torch.cuda.device(self.dev):
+            with torch.cuda.stream(self.stream):
+                self._program(k, n)  # warm-up (lazy allocations, kernel loading)
+            self.stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+                self._program(k, n)
+        self.graphs[(k, n)] = g
+        self.runner.set_graph(k, n, g.raw_cuda_graph_exec())
+
+    def refresh_weights(self):
+        """BN-fold coefficients (and fragment-major eval weights) of every batch executor from the current
+        weights; the graphs read them from buffers rewritten in place."""
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            for ex in self.ex.values():
+                ex.prepare_eval()
+        self.stream.synchronize()
+
+    def wait_idle(self):
+        self.runner.drain()
+
+    # ------------------------------------------------------------------ batching
+    def _acquire(self, block: bool = True):
+        """(k, j, generation) of a position in the open batch frame; None if ``block`` is False and none is
+        free."""
+        with self._cv:
+            while True:
+                if self._stop:
+                    raise RuntimeError("BatchEngine closed")
+                if self._open is None and self._free:
+                    self._open = self._free.popleft()
+                    self._acq = self._ready = 0
+                    self._void = set()
+                    self._gen[self._open] += 1
+                if self._open is not None and self._acq < self.P:
+                    j = self._acq
+                    self._acq += 1
+                    return self._open, j, self._gen[self._open]
+                if not block:
+                    return None
+                self._cv.wait()
+
+    def _staged(self, k: int, j: int, ok: bool):
+        with self._cv:
+            if not ok:
+                self._void.add(j)
+            if self._ready == 0:
+                self._t_first = time.perf_counter()
+            self._ready += 1
+            self._cv.notify_all()
+
+    def _gpu_pending(self) -> int:
+        """Launched frames whose device work has not finished (polled, no blocking)."""
+        while self._launched and self._done(self._launched[0]):
+            self._launched.popleft()
+        return len(self._launched)
+
+    def _done(self, k: int) -> bool:
+        ev = self._done_evs.get(k)
+        return ev is None or ev.query()
+
+    def _launcher(self):
+        with torch.cuda.device(self.dev):
+            while True:
+                with self._cv:
+                    while True:
+                        if self._stop:
+                            return
+                        k, acq, ready = self._open, self._acq, self._ready
+                        if k is not None and ready > 0 and ready == acq:
+                            if acq == self.P or self._gpu_pending() == 0 or \
+                                    time.perf_counter() - self._t_first >= self.window:
+                                break
+                            self._cv.wait(timeout=50e-6)
+                            continue
+                        self._cv.wait(timeout=1e-3 if k is not None and ready > 0 else None)
+                    n, void = acq, self._void
+                    self._open = None  # the next acquire opens a new frame
+                    self._refs[k] = n - len(void)
+                    if self._refs[k] == 0:
+                        self._free.append(k)
+                    self._cv.notify_all()
+                self.runner.launch(k, n)  # uploads + graph + end event (no GIL)
+                ev = self._done_evs.get(k)
+                if ev is None:
+                    ev = self._done_evs[k] = torch.cuda.Event()
+                ev.record(self.stream)
+                with self._cv:
+                    self._launched.append(k)
+                    self._launched_gen[k] = self._gen[k]
+                    self.batch_sizes[n] += 1
+                    self._cv.notify_all()
+
+    def _await_launch(self, k: int, gen: int):
+        with self._cv:
+            while self._launched_gen[k] != gen:
+                if self._stop:
+                    raise RuntimeError("BatchEngine closed")
+                self._cv.wait()
+
+    def _release(self, k: int):
+        with self._cv:
+            self._refs[k] -= 1
+            if self._refs[k] == 0:
+                self._free.append(k)
+                self._cv.notify_all()
+
+    def submit_encoded(self, color: bytes, depth: bytes, pos=None):
+        """(code, ticket): 0 and the frame's (k, j) when it is staged for the next batch; otherwise nothing
+        of it runs (1 / 2 / 3 as FramePipeline.submit_encoded: the caller decodes it itself). ``pos``: a
+        position already taken with ``_acquire``."""
+        k, j, gen = pos if pos is not None else self._acquire()
+        try:
+            code = self.runner.decode(k, j, color, depth)
+        except BaseException:
+            self._staged(k, j, False)
+            raise
+        self._staged(k, j, code == 0)
+        return code, (k, j, gen)
+
+    def submit(self, color, depth: np.ndarray, pos=None):
+        """An HxWx3 u8 colour array (this engine's channel order) + HxW depth frame; returns the ticket."""
+        if self.src == SRC_JPEG:
+            raise ValueError("BatchEngine(src=JPEG) takes encoded requests")
+        d = depth.view(np.int16) if depth.dtype == np.uint16 else depth
+        k, j, gen = pos if pos is not None else self._acquire()
+        try:
+            self.runner.stage(k, j, np.ascontiguousarray(color), np.ascontiguousarray(d))
+        except BaseException:
+            self._staged(k, j, False)
+            raise
+        self._staged(k, j, True)
+        return k, j, gen
+
+    def collect_encoded(self, ticket):
+        k, j, gen = ticket
+        try:
+            self._await_launch(k, gen)
+            payload, mean, maxc, cov, st, gpu_ms = self.runner.collect_encoded(k, j, 1, 4)
+            if st == 4:  # the fit needs the host (device capacity exceeded): from this position's edge buffers
+                r = self._frame_result(k, j, gpu_ms)
+                return r
+            return WireResult(payload, mean, maxc, cov, gpu_ms)
+        finally:
+            self._release(k)
+
+    def collect(self, ticket) -> FrameResult:
+        k, j, gen = ticket
+        try:
+            self._await_launch(k, gen)
+            gpu_ms = self.runner.wait(k)
+            return self._frame_result(k, j, gpu_ms)
+        finally:
+            self._release(k)
+
+    def _frame_result(self, k, j, gpu_ms) -> FrameResult:
+        from ..geometry.curvature import coverage_from_device
+        h_res = self.h_res[k][j].numpy()
+        count = coverage_from_device(h_res, self.cfg)
+        with torch.cuda.device(self.dev):
+            res = self.geo[k][j].finish_device(h_res)
+        pts = None
+        if int(h_res[0]) == 0 and res.status == "ok":
+            pts = h_res[8:8 + 3 * self.cfg.num_samples].reshape(-1, 3).copy()
+        return FrameResult(self.h_mask[k][j].numpy().copy(), 100.0 * count / (self.H * self.W), res,
+                           {"gpu_ms": gpu_ms}, pts)
+
+    def hold(self):
+        """Take every batch frame (waits until each is free: nothing in flight or uncollected), so the
+        weights can be swapped; ``unhold`` gives them back."""
+        got = []
+        with self._cv:
+            while len(got) < self.nf:
+                if self._open is not None and self._acq == 0:  # an open frame nobody took a position in
+                    self._free.append(self._open)
+                    self._open = None
+                if self._free:
+                    got.append(self._free.popleft())
+                    continue
+                self._cv.wait()
+        self._held = got
+        self.runner.drain()
+
+    def unhold(self):
+        with self._cv:
+            self._free.extend(getattr(self, "_held", []))
+            self._held = []
+            self._cv.notify_all()
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        self._th.join(timeout=5.0)
+        self.runner.drain()
+
+
 class CpuFramePipeline:
     """Same contract on the CPU: torch (any UNet module) + numpy geometry + native C++ spline."""
 
@@ -513,7 +827,7 @@ class EnginePool:
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, n: int = 2,
                  threshold: float = 0.5, graph: bool = True, geo_cfg: Optional[GeometryConfig] = None,
-                 devices=None, rgb: bool = False, jpeg: bool = False, max_sizes: int = 3):
+                 devices=None, rgb: bool = False, jpeg: bool = False, max_sizes: int = 3, batch: Optional[int] = None):
         self.model = model
         self.home_size = (H, W)
         self.max_sizes = max(0, max_sizes)
@@ -534,6 +848,33 @@ class EnginePool:
         self.sessions_opened = [0] * len(self.replicas)
         for r in range(len(self.replicas)):
             self._get(r, H, W)
+        # cross-stream batching (BatchEngine): positions per batch (0: off; RDP_SERVE_BATCH). Frames of the
+        # configured size from sessions of a replica that is serving >= 2 active streams go through it;
+        # a lone stream keeps its double-buffered pipelines (no batching wait on its latency).
+        if batch is None:
+            batch = int(os.environ.get("RDP_SERVE_BATCH", "4"))
+        self.batch_positions = batch if (self.gpu and graph and batch >= 2) else 0
+        self.batchers = []
+        if self.batch_positions:
+            src = SRC_JPEG if self.jpeg else (SRC_RGB if rgb else SRC_BGR)
+            self.batchers = [BatchEngine(self.replicas[r], H=H, W=W, device=self.devices[r], src=src,
+                                         positions=self.batch_positions, **self.args) for r in range(len(self.replicas))]
+        self._recent = [dict() for _ in self.replicas]  # replica -> {session id: last submit time}
+        self.batch_active_s = 0.005
+
+    def _batcher(self, r: int, sid: int, shape) -> "Optional[BatchEngine]":
+        """The replica's BatchEngine if this frame should be batched: configured frame size and at least two
+        sessions of the replica submitted within the last ``batch_active_s``."""
+        if not self.batchers or tuple(shape) != self.home_size:
+            return None
+        now = time.perf_counter()
+        rec = self._recent[r]
+        rec[sid] = now
+        if len(rec) > 64:
+            for k in [k for k, t in rec.items() if now - t > self.batch_active_s]:
+                rec.pop(k, None)
+        active = sum(1 for t in list(rec.values()) if now - t <= self.batch_active_s)
+        return self.batchers[r] if active >= 2 else None
 
     def _new(self, r: int, H, W):
         m = self.replicas[r]
@@ -575,12 +916,15 @@ class EnginePool:
     @contextlib.contextmanager
     def exclusive(self):
         """Hold every pipeline of every replica (no frame in flight), e.g. while weights are swapped
-        in place; yields the held pipelines."""
+        in place; yields the held pipelines and batch engines (all of them drained)."""
         with self._mk_lock:
             held = [(q, q.get()) for q in self._pools.values() for _ in range(self.n)]
+            held_b = [b.hold() for b in self.batchers]
             try:
-                yield [p for _, p in held]
+                yield [p for _, p in held] + list(self.batchers)
             finally:
+                for b in self.batchers:
+                    b.unhold()
                 for q, p in held:
                     q.put(p)
 
@@ -615,6 +959,16 @@ class EngineSession:
     def __init__(self, pool: EnginePool, replica: int, depth: int = 2):
         self.pool, self.replica, self.depth = pool, replica, max(1, depth)
         self.inflight: "collections.deque" = collections.deque()
+        self.sid = id(self)
+
+    def _batch_pos(self, b: "BatchEngine", out: list):
+        """A position in ``b``'s open batch: without blocking if one is free, else after collecting this
+        session's own frames (a session never waits on the pool while holding positions others wait on)."""
+        pos = b._acquire(block=False)
+        if pos is None:
+            out += self.drain()
+            pos = b._acquire()
+        return pos
 
     def submit(self, color_bgr, depth, tag=None, rgb: bool = False) -> list:
         """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect.
@@ -632,6 +986,17 @@ class EngineSession:
             return out
         while len(self.inflight) >= self.depth:
             out.append(self._collect_one())
+        b = None if split or isinstance(color_bgr, JpegCoefs) else self.pool._batcher(self.replica, self.sid,
+                                                                                         color_bgr.shape[:2])
+        if b is not None and b.src == (SRC_RGB if rgb else SRC_BGR):
+            try:
+                t = b.submit(color_bgr, depth, pos=self._batch_pos(b, out))
+            except Exception as e:
+                out += self.drain()
+                out.append((tag, e))
+                return out
+            self.inflight.append((tag, b, t, "array"))
+            return out
         try:
             q = self.pool._get(self.replica, *color_bgr.shape[:2])
         except RuntimeError as e:  # too many frame sizes in flight: this frame fails, the stream goes on
@@ -677,6 +1042,17 @@ class EngineSession:
         out = []
         while len(self.inflight) >= self.depth:
             out.append(self._collect_one())
+        b = self.pool._batcher(self.replica, self.sid, self.pool.home_size)
+        if b is not None and b.src == SRC_JPEG:
+            try:
+                code, t = b.submit_encoded(color, depth, pos=self._batch_pos(b, out))
+            except Exception as e:
+                out += self.drain()
+                out.append((tag, e))
+                return out, 0
+            if code == 0:
+                self.inflight.append((tag, b, t, "encoded"))
+            return out, code
         q = self.pool._get(self.replica, *self.pool.home_size)
         try:
             p = q.get_nowait()
@@ -701,6 +1077,11 @@ class EngineSession:
 
     def _collect_one(self):
         tag, p, q, *enc = self.inflight.popleft()
+        if isinstance(p, BatchEngine):  # q: the frame's ticket, enc: its kind
+            try:
+                return tag, (p.collect_encoded(q) if enc[0] == "encoded" else p.collect(q))
+            except Exception as e:
+                return tag, e
         try:
             return tag, (p.collect_encoded() if enc else p.collect())
         except Exception as e:  # a failed frame must not take the pipeline with it
@@ -722,6 +1103,12 @@ class EngineSession:
         that ended early: client cancel, transport error, abort). Idempotent."""
         while self.inflight:
             _, p, q, *_enc = self.inflight.popleft()
+            if isinstance(p, BatchEngine):
+                try:
+                    p.collect(q)  # waits for its batch, releases the position
+                except Exception:
+                    pass
+                continue
             try:
                 p.wait_idle()
             except Exception:  # the pipeline goes back either way

@@ -488,7 +488,19 @@ def build_server(cfg: ServeConfig, device: Optional[torch.device] = None, pool_s
     watcher = None
     if cfg.hot_reload_alias:
         watcher = ModelWatcher(cfg, model, engine, version)
+    freeze_heap()
     return server, service, watcher, bound
+
+
+def freeze_heap() -> None:
+    """Once the long-lived objects exist (model, engine, graphs, gRPC server): move them out of the
+    cyclic collector's generations (``gc.freeze``), so a collection triggered by per-frame allocations
+    walks only the young objects instead of the whole torch / gRPC heap -- a full pass over it stalled
+    the handler threads for milliseconds, the largest single source of slow frames
+    (profiles/serve_tail.md)."""
+    import gc
+    gc.collect()
+    gc.freeze()
 
 
 def serve(cfg: Optional[ServeConfig] = None, block: bool = True):

@@ -106,9 +106,10 @@ def test_default_failure_exits_process_nonzero():
 def test_emulate_spec_and_model():
     from robotic_discovery_platform_amd.parallel.ddp import emulate_spec, ring_allreduce_us
     assert emulate_spec("") is None
-    assert emulate_spec("8:150") == (8, 150.0, 16, 15.0)
-    assert emulate_spec("4:300:32:5") == (4, 300.0, 32, 5.0)
-    for bad in ("8", "1:100", "8:0", "8:100:0"):
+    assert emulate_spec("8:150") == (8, 150.0, 16, 15.0, 0.0)
+    assert emulate_spec("4:300:32:5") == (4, 300.0, 32, 5.0, 0.0)
+    assert emulate_spec("8:150:16:15:3") == (8, 150.0, 16, 15.0, 3.0)
+    for bad in ("8", "1:100", "8:0", "8:100:0", "8:150:16:15:-1"):
         with pytest.raises(ValueError):
             emulate_spec(bad)
     # 69 MB fp32 gradients over 8 ranks at 150 GB/s: 2 * 7/8 * 69e6 / 150e9 s = 805 us (+ alpha)
