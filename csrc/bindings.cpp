@@ -98,6 +98,13 @@ int rdp_parcur(int, int, const double*, const double*, double, int, int, double*
 double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
 int rdp_geo_spline_res_len(int);
+int rdp_geo_edges_batch(int, const void* const*, const void* const*, int, int, double, double, double, double, double,
+                        int* const*, double* const*, double* const*, double* const*, int, int* const*, double* const*,
+                        int, int* const*, int, double, int, const void* const*, int, int, int* const*, double* const*,
+                        int* const*, int, void* const*, hipStream_t);
+int rdp_geo_spline_batch(int, int, int, const int* const*, const int* const*, double* const*, double* const*, int,
+                         double, int, int, double, int, int, const int* const*, int, double* const*, const void* const*,
+                         void* const*, long, hipStream_t);
 int rdp_png_info(const uint8_t*, long, int*, int*, int*);
 long rdp_jpeg_info(const uint8_t*, long, int*);
 void rdp_jpeg_meta(const int*, int*);
@@ -132,6 +139,9 @@ void note_device(int& dev, const torch::Tensor& t) {
 }
 void note_device(int& dev, const c10::optional<torch::Tensor>& t) {
   if (t) note_device(dev, *t);
+}
+void note_device(int& dev, const std::vector<torch::Tensor>& ts) {
+  for (const auto& t : ts) note_device(dev, t);
 }
 template <class T>
 void note_device(int&, const T&) {}
@@ -1375,6 +1385,82 @@ void geo_edges(torch::Tensor mask, torch::Tensor depth, double fx, double fy, do
 int geo_nblocks(int H) { return rdp_geo_nblocks(H); }
 long geo_work_ints(int H, int W) { return rdp_geo_work_ints(H, W); }
 
+// The serving geometry of n <= 4 frames of one camera (BatchEngine): the edge stage (mask upsample +
+// coverage, deprojection, bins, per-bin top-k + x-sort) and the spline fit, each ONE launch over the frames
+// (csrc/geometry.hip rdp_geo_edges_batch, csrc/geo_spline.hip rdp_geo_spline_batch). Per-frame lists of
+// the buffers GeometryEngine.launch_frame / launch_spline pass; the results (and the mask copies) go to
+// host memory (res / mask_host).
+void geo_frames_batch(std::vector<torch::Tensor> mask, std::vector<torch::Tensor> depth,
+                      std::vector<torch::Tensor> m256, std::vector<torch::Tensor> work_i,
+                      std::vector<torch::Tensor> work_d, std::vector<torch::Tensor> pts,
+                      std::vector<torch::Tensor> npts, std::vector<torch::Tensor> out, std::vector<torch::Tensor> kout,
+                      std::vector<torch::Tensor> cov, std::vector<torch::Tensor> sorted,
+                      std::vector<torch::Tensor> gperm, std::vector<torch::Tensor> u, std::vector<torch::Tensor> res,
+                      std::vector<torch::Tensor> mask_host, double fx, double fy, double cx, double cy, double scale,
+                      int nbins, double top, int min_points, double smooth, int k, int nsamp, double eps,
+                      int min_edge) {
+  const int n = (int)mask.size();
+  TORCH_CHECK(n >= 1 && n <= 4, "geo_frames_batch: 1..4 frames");
+  for (auto* v : {&depth, &m256, &work_i, &work_d, &pts, &npts, &out, &kout, &cov, &sorted, &gperm, &u, &res})
+    TORCH_CHECK((int)v->size() == n, "geo_frames_batch: every list needs one tensor per frame");
+  TORCH_CHECK(mask_host.empty() || (int)mask_host.size() == n, "geo_frames_batch: mask_host: none or one per frame");
+  const int H = mask[0].size(0), W = mask[0].size(1);
+  const int nblk = rdp_geo_nblocks(H);
+  const int mh = m256[0].size(0), mw = m256[0].size(1);
+  const int cap = H * W, kcap = out[0].size(1), secap = sorted[0].size(0);
+  std::vector<const void*> pm(n), pd(n), pm256(n);
+  std::vector<int*> pcnt(n), pnpts(n), pkout(n), pcov(n), pgp(n);
+  std::vector<double*> pxmin(n), pxmax(n), ppts(n), pout(n), psort(n), pu(n), pres(n);
+  std::vector<void*> pmh(n);
+  std::vector<const int*> ckout(n), cnpts(n), ccov(n);
+  std::vector<const void*> cmask(n);
+  for (int i = 0; i < n; ++i) {
+    TORCH_CHECK(mask[i].is_cuda() && mask[i].scalar_type() == torch::kUInt8 && mask[i].dim() == 2 &&
+                    mask[i].is_contiguous() && mask[i].size(0) == H && mask[i].size(1) == W, "mask: u8 HxW, one camera");
+    TORCH_CHECK(depth[i].is_cuda() && depth[i].element_size() == 2 && depth[i].sizes() == mask[i].sizes() &&
+                    depth[i].is_contiguous(), "depth u16 HxW");
+    TORCH_CHECK(m256[i].is_cuda() && m256[i].scalar_type() == torch::kUInt8 && m256[i].dim() == 2 &&
+                    m256[i].is_contiguous() && m256[i].size(0) == mh && m256[i].size(1) == mw, "m256 u8 2-D");
+    TORCH_CHECK(work_i[i].numel() >= rdp_geo_work_ints(H, W) && work_i[i].scalar_type() == torch::kInt32, "work_i");
+    TORCH_CHECK(work_d[i].numel() >= 2 * nblk && work_d[i].scalar_type() == torch::kFloat64, "work_d");
+    TORCH_CHECK(pts[i].scalar_type() == torch::kFloat64 && pts[i].numel() >= (long)H * W * 4, "pts cap");
+    TORCH_CHECK(out[i].scalar_type() == torch::kFloat64 && out[i].dim() == 3 && out[i].size(0) >= nbins &&
+                    out[i].size(1) == kcap && out[i].size(2) == 4 && out[i].is_contiguous(), "out");
+    TORCH_CHECK(kout[i].scalar_type() == torch::kInt32 && kout[i].numel() >= nbins, "kout");
+    TORCH_CHECK(npts[i].scalar_type() == torch::kInt32, "npts");
+    TORCH_CHECK(cov[i].scalar_type() == torch::kInt32 && cov[i].numel() >= nblk, "cov");
+    TORCH_CHECK(sorted[i].scalar_type() == torch::kFloat64 && sorted[i].dim() == 2 && sorted[i].size(1) == 3 &&
+                    sorted[i].size(0) == secap, "sorted");
+    TORCH_CHECK(gperm[i].scalar_type() == torch::kInt32 && gperm[i].numel() >= 2L * secap, "gperm");
+    TORCH_CHECK(u[i].scalar_type() == torch::kFloat64 && u[i].numel() >= secap, "u");
+    TORCH_CHECK(res[i].scalar_type() == torch::kFloat64 && res[i].numel() >= rdp_geo_spline_res_len(nsamp) &&
+                    res[i].is_contiguous(), "res");
+    pm[i] = mask[i].data_ptr(); pd[i] = depth[i].data_ptr(); pm256[i] = m256[i].data_ptr();
+    pcnt[i] = work_i[i].data_ptr<int>();
+    pxmin[i] = work_d[i].data_ptr<double>(); pxmax[i] = pxmin[i] + nblk;
+    ppts[i] = pts[i].data_ptr<double>(); pnpts[i] = npts[i].data_ptr<int>(); pout[i] = out[i].data_ptr<double>();
+    pkout[i] = kout[i].data_ptr<int>(); pcov[i] = cov[i].data_ptr<int>(); psort[i] = sorted[i].data_ptr<double>();
+    pgp[i] = gperm[i].data_ptr<int>(); pu[i] = u[i].data_ptr<double>(); pres[i] = res[i].data_ptr<double>();
+    ckout[i] = pkout[i]; cnpts[i] = pnpts[i]; ccov[i] = pcov[i]; cmask[i] = pm[i];
+    if (!mask_host.empty()) {
+      TORCH_CHECK(!mask_host[i].is_cuda() && mask_host[i].scalar_type() == torch::kUInt8 &&
+                      mask_host[i].is_contiguous() && mask_host[i].numel() == mask[i].numel(), "mask_host");
+      pmh[i] = mask_host[i].data_ptr();
+    }
+  }
+  const hipStream_t st = unplanned_stream();
+  TORCH_CHECK(rdp_geo_edges_batch(n, pm.data(), pd.data(), H, W, fx, fy, cx, cy, scale, pcnt.data(), pxmin.data(),
+                                  pxmax.data(), ppts.data(), cap, pnpts.data(), pout.data(), kcap, pkout.data(), nbins,
+                                  top, min_points, pm256.data(), mh, mw, pcov.data(), psort.data(), pgp.data(), secap,
+                                  nullptr, st) >= 0, "geo_frames_batch: nbins must be in [1, 128]");
+  const int r = rdp_geo_spline_batch(n, nbins, kcap, ckout.data(), cnpts.data(), psort.data(), pu.data(), secap,
+                                     smooth, k, nsamp, eps, min_points, min_edge, ccov.data(), nblk, pres.data(),
+                                     cmask.data(), mask_host.empty() ? nullptr : pmh.data(),
+                                     (long)H * W, st);
+  TORCH_CHECK(r != -2, "geo_frames_batch: mask copy needs 4-byte aligned buffers and a size multiple of 4");
+  TORCH_CHECK(r == 0, "geo_frames_batch: k must be in [1, 5], nsamp in [1, 256]");
+}
+
 // on-device spline stage: per-bin sort of the edge points (out/kout from geo_edges) + FITPACK-equivalent
 // fit + nsamp-point evaluation and curvature into res (rdp_geo_spline_res_len(nsamp) doubles)
 void geo_spline(torch::Tensor out, torch::Tensor kout, torch::Tensor npts, torch::Tensor sorted, torch::Tensor gperm,
@@ -1648,6 +1734,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("step") = py::none(), py::arg("blocks") = 0);
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
+  m.def("geo_frames_batch", on_device(&geo_frames_batch));
   m.def("geo_edges", on_device(&geo_edges), py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),
         py::arg("cy"), py::arg("scale"), py::arg("work_i"), py::arg("work_d"), py::arg("pts"), py::arg("npts"),
         py::arg("out"), py::arg("kout"), py::arg("nbins"), py::arg("top"), py::arg("min_points"),

@@ -546,11 +546,22 @@ extern "C" int rdp_conv_rowband_frag_auto(int N, int H, int W, int C1, int C2, i
   const long wb = (long)Cout * 9 * Cin * 2, xb = M * Cin * 2;
   static const long xmax = [] {
     const char* e = getenv("RDP_ROWBAND_X_MAXPIX");  // 0 turns the activation-staged kernel off
-    return e ? atol(e) : 16384L;  // up3.conv1 at 128^2: 29.6 -> 22.6 us (scripts/rowband_bench.py)
+    return e ? atol(e) : 65536L;  // (the work bound below decides; up3.conv2 at N = 2: 20.0 vs 32.5 us)
   }();
   // (64 input channels stay on the split-K GEMM: 128^2 64 -> 128 18.0 vs 11.5 us, four waves staging one chunk)
   const bool xch = (Cin / 32) % 8 == 0 || Cin == 128;
-  if (xch && M <= xmax && W <= 256) return 2;  // activation-staged (x read ~3x instead of 9x)
+  if (xch && M <= xmax && W <= 256) {  // activation-staged (x read ~3x instead of 9x)
+    // ... while its work (blocks x K, the launch's own tiling below) stays within about two waves of 512
+    // blocks: past that the GEMM wins (scripts/rowband_bench.py --batch 1 / 2 / 4, every <= 128^2 layer of
+    // the U-Net: e.g. up1.conv1 17.9 vs 26.9 us at N = 1 but 44.9 vs 38.8 at N = 2, down2.conv1 20.9 vs
+    // 25.3 at N = 2 but 38.9 vs 20.2 at N = 4; 128-channel inputs, staged in 4 chunks, cross over earlier)
+    const int WB = W < 32 ? W : 32, segs = W / WB;
+    const bool r2 = H % 2 == 0 && (long)N * (H / 2) * segs * (Cout / 32) >= 256;
+    const long blocks = (long)N * (H / (r2 ? 2 : 1)) * segs * (Cout / 32);
+    const long work = blocks * 9 * Cin;
+    if (work <= ((Cin / 32) % 8 == 0 ? 2500000L : 1300000L)) return 2;
+    return 0;
+  }
   if (M > 4096 || W > 64) return 0;
   return wb * ((long)N * H) / 2 + xb * 9 * (Cout / 32) <= 250000000L ? 1 : 0;
 }

@@ -463,7 +463,7 @@ RDP_DEV void splev3_dev(const double* t1, int lo, int nn, const double (*cd)[SPL
 }
 
 template <int K>
-__global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __restrict__ P, double* __restrict__ U,
+RDP_DEV void geo_fit_body(const double* __restrict__ P, double* __restrict__ U,
                                                               const int* __restrict__ kout, int nbins, int kcap,
                                                               const int* __restrict__ npts_p, int ecap, double s,
                                                               int nsamp, double eps, int min_points, int min_edge,
@@ -857,8 +857,74 @@ __global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __re
   prof_flush();
 }
 
+template <int K>
+__global__ __launch_bounds__(SPL_THREADS) void geo_fit_kernel(const double* __restrict__ P, double* __restrict__ U,
+                                                              const int* __restrict__ kout, int nbins, int kcap,
+                                                              const int* __restrict__ npts_p, int ecap, double s,
+                                                              int nsamp, double eps, int min_points, int min_edge,
+                                                              const int* __restrict__ cov, int ncov,
+                                                              double* __restrict__ res, double* __restrict__ dbg,
+                                                              const uint32_t* __restrict__ hsrc,
+                                                              uint32_t* __restrict__ hdst, int hwords) {
+  geo_fit_body<K>(P, U, kout, nbins, kcap, npts_p, ecap, s, nsamp, eps, min_points, min_edge, cov, ncov, res, dbg,
+                  hsrc, hdst, hwords);
+}
+
+// up to 4 frames' fits in one launch (blockIdx.y = frame; blocks 1.. of each row copy that frame's mask)
+struct FitFrame {
+  const double* P;
+  double* U;
+  const int* kout;
+  const int* npts;
+  const int* cov;
+  double* res;
+  const uint32_t* hsrc;
+  uint32_t* hdst;
+};
+struct FitFrames {
+  FitFrame f[4];
+  int nbins, kcap, ecap, nsamp, min_points, min_edge, ncov, hwords;
+  double s, eps;
+};
+template <int K>
+__global__ __launch_bounds__(SPL_THREADS) void geo_fit_batch_kernel(const FitFrames g) {
+  const FitFrame& a = g.f[blockIdx.y];
+  geo_fit_body<K>(a.P, a.U, a.kout, g.nbins, g.kcap, a.npts, g.ecap, g.s, g.nsamp, g.eps, g.min_points, g.min_edge,
+                  a.cov, g.ncov, a.res, nullptr, a.hsrc, a.hdst, g.hwords);
+}
+
 extern "C" {
 int rdp_geo_spline_res_len(int nsamp) { return 9 + 3 * nsamp; }
+
+// rdp_geo_spline (presorted, serving) for n <= 4 frames in one launch: per-frame arrays of its buffers
+int rdp_geo_spline_batch(int n, int nbins, int kcap, const int* const* kout, const int* const* npts,
+                         double* const* sorted, double* const* u, int ecap, double s, int k, int nsamp, double eps,
+                         int min_points, int min_edge, const int* const* cov, int ncov, double* const* res,
+                         const void* const* mask, void* const* mask_host, long mask_bytes, hipStream_t st) {
+  if (k < 1 || k > SPL_KMAX || nsamp < 1 || nsamp > SPL_THREADS || n < 1 || n > 4) return -1;
+  if (mask_host && mask_bytes % 4) return -2;
+  FitFrames g;
+  g.nbins = nbins; g.kcap = kcap; g.ecap = ecap; g.nsamp = nsamp; g.min_points = min_points; g.min_edge = min_edge;
+  g.ncov = ncov; g.s = s; g.eps = eps;
+  g.hwords = mask_host ? (int)(mask_bytes / 4) : 0;
+  for (int i = 0; i < 4; ++i) {
+    const int j = i < n ? i : 0;
+    FitFrame& f = g.f[i];
+    f.P = sorted[j]; f.U = u[j]; f.kout = kout[j]; f.npts = npts[j]; f.cov = cov[j]; f.res = res[j];
+    f.hsrc = mask_host ? (const uint32_t*)mask[j] : nullptr;
+    f.hdst = mask_host ? (uint32_t*)mask_host[j] : nullptr;
+    if (mask_host && ((((uintptr_t)mask[j]) | ((uintptr_t)mask_host[j])) & 3)) return -2;
+  }
+  const int grid = 1 + (g.hwords + SPL_THREADS - 1) / SPL_THREADS;
+  switch (k) {
+    case 1: hipLaunchKernelGGL(geo_fit_batch_kernel<1>, dim3(grid, n), dim3(SPL_THREADS), 0, st, g); break;
+    case 2: hipLaunchKernelGGL(geo_fit_batch_kernel<2>, dim3(grid, n), dim3(SPL_THREADS), 0, st, g); break;
+    case 3: hipLaunchKernelGGL(geo_fit_batch_kernel<3>, dim3(grid, n), dim3(SPL_THREADS), 0, st, g); break;
+    case 4: hipLaunchKernelGGL(geo_fit_batch_kernel<4>, dim3(grid, n), dim3(SPL_THREADS), 0, st, g); break;
+    default: hipLaunchKernelGGL(geo_fit_batch_kernel<5>, dim3(grid, n), dim3(SPL_THREADS), 0, st, g); break;
+  }
+  return 0;
+}
 
 // sort the per-bin edge points (out [nbins][kcap][4], kout) into sorted [ecap][3] and fit/evaluate.
 int rdp_geo_spline(const double* out, int nbins, int kcap, const int* kout, const int* npts, double* sorted,

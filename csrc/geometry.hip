@@ -72,7 +72,7 @@ RDP_DEV uint8_t src_mask(const GeoSrc& g, const uint8_t* mask, int p, int W) {
   return g.m256[iy * g.mw + ix];
 }
 
-__global__ __launch_bounds__(GEO_THREADS) void geo_count_kernel(const uint8_t* __restrict__ mask,
+RDP_DEV void geo_count_body(const uint8_t* __restrict__ mask,
                                                                 const uint16_t* __restrict__ depth, int H, int W,
                                                                 GeoCam cam, int* __restrict__ counts,
                                                                 double* __restrict__ xmin, double* __restrict__ xmax,
@@ -137,7 +137,7 @@ struct GeoBins {
 // pts: [cap][4] doubles (x, y, z, index) ; npts[0] = total count (written by the last block's thread 0)
 // The x-bin of every written point and the per-bin counts are produced here too (the global x range
 // is reduced from geo_count's per-block partials by every block): no separate counting launch.
-__global__ __launch_bounds__(GEO_THREADS) void geo_write_kernel(const uint8_t* __restrict__ mask,
+RDP_DEV void geo_write_body(const uint8_t* __restrict__ mask,
                                                                 const uint16_t* __restrict__ depth, int H, int W,
                                                                 GeoCam cam, const int* __restrict__ counts,
                                                                 int nblocks, double* __restrict__ pts, int cap,
@@ -223,7 +223,7 @@ RDP_DEV void geo_range(const double* bxmin, const double* bxmax, int nblk, doubl
   *s_hi = rhi[0];
 }
 
-__global__ __launch_bounds__(GEO_THREADS) void geo_bin_scatter_kernel(const int* __restrict__ npts_p, int nbins,
+RDP_DEV void geo_bin_scatter_body(const int* __restrict__ npts_p, int nbins,
                                                                       GeoBins gb) {
   __shared__ int base[128];
   __shared__ unsigned lc[128], lbase[128];
@@ -341,7 +341,7 @@ RDP_DEV void wave_pick_digit(const unsigned* hist, int need, int lane, int& digi
   eq = __shfl(e, owner, 64);
 }
 
-__global__ __launch_bounds__(256) void geo_select_wave_kernel(const double* __restrict__ pts,
+RDP_DEV void geo_select_wave_body(const double* __restrict__ pts,
                                                               const int* __restrict__ npts_p, int nbins, double top,
                                                               GeoBins gb, double* __restrict__ out, int kcap,
                                                               int* __restrict__ kout, int min_points,
@@ -543,6 +543,73 @@ __global__ void geo_zero_kernel(int* p, int n) {
   if (i < n) p[i] = 0;
 }
 
+// ---- kernels: one frame (the bodies above), or up to GEO_BATCH frames per launch (blockIdx.y = frame) ----
+__global__ __launch_bounds__(GEO_THREADS) void geo_count_kernel(const uint8_t* __restrict__ mask,
+                                                                const uint16_t* __restrict__ depth, int H, int W,
+                                                                GeoCam cam, int* __restrict__ counts,
+                                                                double* __restrict__ xmin, double* __restrict__ xmax,
+                                                                GeoSrc gs) {
+  geo_count_body(mask, depth, H, W, cam, counts, xmin, xmax, gs);
+}
+__global__ __launch_bounds__(GEO_THREADS) void geo_write_kernel(const uint8_t* __restrict__ mask,
+                                                                const uint16_t* __restrict__ depth, int H, int W,
+                                                                GeoCam cam, const int* __restrict__ counts, int nblocks,
+                                                                double* __restrict__ pts, int cap, int* __restrict__ npts,
+                                                                const double* __restrict__ bxmin,
+                                                                const double* __restrict__ bxmax, int nbins, GeoBins gb) {
+  geo_write_body(mask, depth, H, W, cam, counts, nblocks, pts, cap, npts, bxmin, bxmax, nbins, gb);
+}
+__global__ __launch_bounds__(GEO_THREADS) void geo_bin_scatter_kernel(const int* __restrict__ npts_p, int nbins,
+                                                                      GeoBins gb) {
+  geo_bin_scatter_body(npts_p, nbins, gb);
+}
+__global__ __launch_bounds__(256) void geo_select_wave_kernel(const double* __restrict__ pts,
+                                                              const int* __restrict__ npts_p, int nbins, double top,
+                                                              GeoBins gb, double* __restrict__ out, int kcap,
+                                                              int* __restrict__ kout, int min_points,
+                                                              double* __restrict__ sorted, int* __restrict__ gperm,
+                                                              int ecap) {
+  geo_select_wave_body(pts, npts_p, nbins, top, gb, out, kcap, kout, min_points, sorted, gperm, ecap);
+}
+
+// One frame's edge-stage arguments (rdp_geo_edges' launches, serving form: no packed edge list).
+struct GeoFrame {
+  const uint8_t* mask;
+  const uint16_t* depth;
+  int* counts;
+  double *xmin, *xmax, *pts, *out, *sorted;
+  int *npts, *kout, *gperm;
+  int cap, kcap, secap;
+  GeoSrc gs;
+  GeoBins gb;
+};
+#define GEO_BATCH 4
+struct GeoFrames {
+  GeoFrame f[GEO_BATCH];
+  GeoCam cam;
+  int H, W, nblk, nbins, min_points;
+  double top;
+};
+// (the frame index is wave-uniform: kernel-argument loads through it stay scalar)
+__global__ __launch_bounds__(GEO_THREADS) void geo_count_batch_kernel(const GeoFrames g) {
+  const GeoFrame& a = g.f[blockIdx.y];
+  geo_count_body(a.mask, a.depth, g.H, g.W, g.cam, a.counts, a.xmin, a.xmax, a.gs);
+}
+__global__ __launch_bounds__(GEO_THREADS) void geo_write_batch_kernel(const GeoFrames g) {
+  const GeoFrame& a = g.f[blockIdx.y];
+  geo_write_body(a.mask, a.depth, g.H, g.W, g.cam, a.counts, g.nblk, a.pts, a.cap, a.npts, a.xmin, a.xmax, g.nbins,
+                 a.gb);
+}
+__global__ __launch_bounds__(GEO_THREADS) void geo_bin_scatter_batch_kernel(const GeoFrames g) {
+  const GeoFrame& a = g.f[blockIdx.y];
+  geo_bin_scatter_body(a.npts, g.nbins, a.gb);
+}
+__global__ __launch_bounds__(256) void geo_select_wave_batch_kernel(const GeoFrames g) {
+  const GeoFrame& a = g.f[blockIdx.y];
+  geo_select_wave_body(a.pts, a.npts, g.nbins, g.top, a.gb, a.out, a.kcap, a.kout, g.min_points, a.sorted, a.gperm,
+                       a.secap);
+}
+
 extern "C" {
 int rdp_geo_nblocks(int H) { return (H + GEO_ROWS_PER_BLOCK - 1) / GEO_ROWS_PER_BLOCK; }
 
@@ -590,5 +657,49 @@ int rdp_geo_edges(const void* mask, const void* depth, int H, int W, double fx, 
                        kcap, kout, min_points, sorted, gperm, secap);
   if (edges) hipLaunchKernelGGL(geo_pack_kernel, dim3(nbins), dim3(256), 0, s, out, kcap, kout, nbins, edges, ecap, hdr);
   return nblk;
+}
+
+// The serving form of rdp_geo_edges for n <= GEO_BATCH frames of one camera in ONE launch per stage
+// (blockIdx.y = frame): each frame's buffers as rdp_geo_edges takes them (array of n per field). The
+// stages are latency-bound small grids, so n frames cost about what one does (a batch of 4 served frames:
+// 4 x 48 us of geometry as per-frame launches, profiles/serve_batch.md).
+int rdp_geo_edges_batch(int n, const void* const* mask, const void* const* depth, int H, int W, double fx, double fy,
+                        double cx, double cy, double scale, int* const* counts, double* const* xmin,
+                        double* const* xmax, double* const* pts, int cap, int* const* npts, double* const* out,
+                        int kcap, int* const* kout, int nbins, double top, int min_points, const void* const* m256,
+                        int mh, int mw, int* const* cov, double* const* sorted, int* const* gperm, int secap,
+                        void* const* mask_host, hipStream_t s) {
+  if (nbins > 128 || nbins < 1 || n < 1 || n > GEO_BATCH) return -1;
+  GeoFrames g;
+  g.cam = GeoCam{fx, fy, cx, cy, scale};
+  g.H = H; g.W = W; g.nblk = rdp_geo_nblocks(H); g.nbins = nbins; g.min_points = min_points; g.top = top;
+  for (int i = 0; i < GEO_BATCH; ++i) {
+    const int j = i < n ? i : 0;  // (unused slots: a copy of frame 0's, never launched)
+    GeoFrame& f = g.f[i];
+    f.mask = (const uint8_t*)mask[j];
+    f.depth = (const uint16_t*)depth[j];
+    f.counts = counts[j]; f.xmin = xmin[j]; f.xmax = xmax[j]; f.pts = pts[j]; f.out = out[j]; f.sorted = sorted[j];
+    f.npts = npts[j]; f.kout = kout[j]; f.gperm = gperm[j];
+    f.cap = cap; f.kcap = kcap; f.secap = secap;
+    f.gb.bin_of = counts[j] + g.nblk;
+    f.gb.bidx = f.gb.bin_of + cap;
+    f.gb.cnt = f.gb.bidx + cap;
+    f.gb.cursor = f.gb.cnt + 128;
+    f.gs.m256 = (const uint8_t*)m256[j];
+    f.gs.mh = mh; f.gs.mw = mw;
+    f.gs.sy = 1.0 / ((double)H / (double)mh);
+    f.gs.sx = 1.0 / ((double)W / (double)mw);
+    f.gs.mask_out = (uint8_t*)mask[j];
+    f.gs.mask_host = mask_host ? (uint8_t*)mask_host[j] : nullptr;
+    f.gs.cov = cov[j];
+    f.gs.zero = f.gb.cnt;
+    f.gs.nzero = 256;
+  }
+  const int pblocks = (cap + GEO_THREADS * 4 - 1) / (GEO_THREADS * 4);
+  hipLaunchKernelGGL(geo_count_batch_kernel, dim3(g.nblk, n), dim3(GEO_THREADS), 0, s, g);
+  hipLaunchKernelGGL(geo_write_batch_kernel, dim3(g.nblk, n), dim3(GEO_THREADS), 0, s, g);
+  hipLaunchKernelGGL(geo_bin_scatter_batch_kernel, dim3(pblocks, n), dim3(GEO_THREADS), 0, s, g);
+  hipLaunchKernelGGL(geo_select_wave_batch_kernel, dim3((nbins + 3) / 4, n), dim3(256), 0, s, g);
+  return g.nblk;
 }
 }

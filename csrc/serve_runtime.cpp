@@ -412,10 +412,15 @@ class BatchRunner {
     DeviceScope g(dev_);
     ev0_.resize(K_);
     ev1_.resize(K_);
+    evup_.resize(K_);
     for (int k = 0; k < K_; ++k) {
       hip_check(hipEventCreate(&ev0_[k]), "hipEventCreate");
       hip_check(hipEventCreate(&ev1_[k]), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&evup_[k], hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate");
     }
+    // uploads run on the copy engine, on a stream of their own: batch k + 1's frames cross PCIe while batch
+    // k computes (131 us of a 4-frame batch as a copy kernel in front of its graph; profiles/serve_batch.md)
+    hip_check(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking), "hipStreamCreate");
     const size_t npos = (size_t)K_ * P_;
     slots_.resize(npos);
     for (auto& sl : slots_) {
@@ -429,15 +434,18 @@ class BatchRunner {
       sl.mask = coherent((size_t)H_ * W_);
       sl.res = coherent(res_len_ * 8);
     }
-    dcol_.assign(P_, nullptr);
-    dmeta_.assign(P_, nullptr);
-    ddep_.assign(P_, nullptr);
+    dcol_.assign(npos, nullptr);
+    dmeta_.assign(npos, nullptr);
+    ddep_.assign(npos, nullptr);
     exec_.assign((size_t)K_ * (P_ + 1), nullptr);
+    fs_.assign(K_, s_);  // every batch frame on the engine's stream unless set_frame_stream says otherwise
     spin_us_ = getenv("RDP_SERVE_SPIN_US") ? atof(getenv("RDP_SERVE_SPIN_US")) : 1000.0;
   }
   ~BatchRunner() {
     for (auto e : ev0_) (void)hipEventDestroy(e);
     for (auto e : ev1_) (void)hipEventDestroy(e);
+    for (auto e : evup_) (void)hipEventDestroy(e);
+    if (cs_) (void)hipStreamDestroy(cs_);
     for (void* p : pinned_) (void)hipHostFree(p);
   }
   // host buffers of (k, j): 0 colour (arrays) / JPEG coefficients, 1 JPEG meta, 2 depth, 3 mask, 4 result
@@ -448,12 +456,20 @@ class BatchRunner {
     if (!p) throw std::invalid_argument("BatchRunner.host_ptr: kind");
     return (uintptr_t)p;
   }
-  // device inputs of position j (the captured graphs read them)
-  void set_device(int j, uintptr_t color, uintptr_t meta, uintptr_t depth) {
-    if (j < 0 || j >= P_) throw std::invalid_argument("position");
-    dcol_[j] = P(color);
-    dmeta_[j] = P(meta);
-    ddep_[j] = P(depth);
+  // device inputs of (k, j) (the captured graphs of frame k read them): per batch frame, so that frame
+  // k + 1's uploads never wait for frame k's graph
+  void set_device(int k, int j, uintptr_t color, uintptr_t meta, uintptr_t depth) {
+    slot(k, j);
+    const size_t i = (size_t)k * P_ + j;
+    dcol_[i] = P(color);
+    dmeta_[i] = P(meta);
+    ddep_[i] = P(depth);
+  }
+  void set_upload_kernel(bool on) { upload_kernel_ = on; }
+  // the stream batch frame k runs on (BatchEngine lanes: frames of different lanes run concurrently)
+  void set_frame_stream(int k, uintptr_t stream) {
+    if (k < 0 || k >= K_) throw std::invalid_argument("BatchRunner.set_frame_stream");
+    fs_[k] = (hipStream_t)stream;
   }
   void set_graph(int k, int n, uintptr_t exec) {
     if (k < 0 || k >= K_ || n < 1 || n > P_) throw std::invalid_argument("BatchRunner.set_graph");
@@ -530,18 +546,28 @@ class BatchRunner {
     int m = 0;
     for (int j = 0; j < n; ++j) {
       Slot& sl = slot(k, j);
-      src[m] = devptr(sl.color); dst[m] = dcol_[j]; bytes[m++] = (long)sl.bytes;
-      if (src_ == 2) { src[m] = devptr(sl.meta); dst[m] = dmeta_[j]; bytes[m++] = 224 * 4; }
-      src[m] = devptr(sl.depth); dst[m] = ddep_[j]; bytes[m++] = (long)H_ * W_ * 2;
+      const size_t i = (size_t)k * P_ + j;
+      src[m] = sl.color; dst[m] = dcol_[i]; bytes[m++] = (long)sl.bytes;
+      if (src_ == 2) { src[m] = sl.meta; dst[m] = dmeta_[i]; bytes[m++] = 224 * 4; }
+      src[m] = sl.depth; dst[m] = ddep_[i]; bytes[m++] = (long)H_ * W_ * 2;
     }
-    hip_check(hipEventRecord(ev0_[k], s_), "hipEventRecord");
-    if (rdp_h2d_copy_multi(src, dst, bytes, m, s_) != 0) {
-      (void)hipGetLastError();
+    const hipStream_t fs = fs_[k];
+    if (upload_kernel_) {  // one copy kernel on the frame's stream, in front of the graph
+      hip_check(hipEventRecord(ev0_[k], fs), "hipEventRecord");
+      for (int i = 0; i < m; ++i) src[i] = devptr(const_cast<void*>(src[i]));
+      if (rdp_h2d_copy_multi(src, dst, bytes, m, fs) != 0) {
+        (void)hipGetLastError();
+        throw std::runtime_error("BatchRunner: upload kernel rejected the segments");
+      }
+    } else {  // DMA on the copy stream; the frame stream waits for it (GPU-side)
+      hip_check(hipEventRecord(ev0_[k], cs_), "hipEventRecord");
       for (int i = 0; i < m; ++i)
-        hip_check(hipMemcpyAsync(dst[i], src[i], (size_t)bytes[i], hipMemcpyHostToDevice, s_), "H2D batch");
+        hip_check(hipMemcpyAsync(dst[i], src[i], (size_t)bytes[i], hipMemcpyHostToDevice, cs_), "H2D batch");
+      hip_check(hipEventRecord(evup_[k], cs_), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(fs, evup_[k], 0), "hipStreamWaitEvent");
     }
-    hip_check(hipGraphLaunch(ex, s_), "hipGraphLaunch");
-    hip_check(hipEventRecord(ev1_[k], s_), "hipEventRecord");
+    hip_check(hipGraphLaunch(ex, fs), "hipGraphLaunch");
+    hip_check(hipEventRecord(ev1_[k], fs), "hipEventRecord");
   }
 
   // block until batch k's results are on the host; its device time (ms)
@@ -580,7 +606,8 @@ class BatchRunner {
   void drain() {
     py::gil_scoped_release nogil;
     DeviceScope g(dev_);
-    hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
+    hip_check(hipStreamSynchronize(cs_), "hipStreamSynchronize");
+    for (auto fs : fs_) hip_check(hipStreamSynchronize(fs), "hipStreamSynchronize");
   }
 
  private:
@@ -653,7 +680,10 @@ class BatchRunner {
   int K_, P_, H_, W_, ns_, src_;
   size_t coef_cap_, res_len_;
   double spin_us_ = 1000.0;
-  std::vector<hipEvent_t> ev0_, ev1_;
+  std::vector<hipEvent_t> ev0_, ev1_, evup_;
+  hipStream_t cs_ = nullptr;
+  std::vector<hipStream_t> fs_;
+  bool upload_kernel_ = getenv("RDP_BATCH_UPLOAD") && std::string(getenv("RDP_BATCH_UPLOAD")) == "kernel";
   std::vector<Slot> slots_;
   std::vector<void*> dcol_, dmeta_, ddep_;
   std::vector<hipGraphExec_t> exec_;
@@ -780,6 +810,8 @@ void register_serve_runtime(py::module_& m) {
       .def("set_device", &BatchRunner::set_device)
       .def("set_graph", &BatchRunner::set_graph)
       .def("set_spin_us", &BatchRunner::set_spin_us)
+      .def("set_upload_kernel", &BatchRunner::set_upload_kernel)
+      .def("set_frame_stream", &BatchRunner::set_frame_stream)
       .def("decode", &BatchRunner::decode, "0 ok, 1 not a native frame, 2 other frame size, 3 corrupt")
       .def("stage", &BatchRunner::stage)
       .def("launch", &BatchRunner::launch)

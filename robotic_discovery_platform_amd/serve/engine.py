@@ -429,12 +429,20 @@ class BatchEngine:
 
     def __init__(self, model, K, depth_scale, H: int = 480, W: int = 640, size: int = 256, threshold: float = 0.5,
                  geo_cfg: Optional[GeometryConfig] = None, device: Optional[torch.device] = None, src: int = SRC_JPEG,
-                 frames: int = 3, positions: int = 4, window_us: float = 300.0):
+                 frames: Optional[int] = None, positions: int = 4, window_us: float = 300.0,
+                 lanes: Optional[int] = None):
         dev = _norm_device(device if device is not None else model.store.device)
+        if lanes is None:
+            lanes = int(os.environ.get("RDP_BATCH_LANES", "2"))
+        lanes = max(1, int(lanes))
+        if frames is None:
+            frames = 2 * lanes + 1
         with torch.cuda.device(dev):
-            self._init(model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, frames, positions, window_us)
+            self._init(model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, max(frames, lanes), positions,
+                       window_us, lanes)
 
-    def _init(self, model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, frames, positions, window_us):
+    def _init(self, model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, frames, positions, window_us,
+              lanes):
         from ..models.unet import UNetExecutor
         from ..ops import native
         C = self.C = native()
@@ -446,7 +454,12 @@ class BatchEngine:
         self.cfg = geo_cfg or GeometryConfig()
         self.nf, self.P = int(frames), int(positions)
         self.window = window_us * 1e-6
-        self.stream = torch.cuda.Stream(dev)
+        # lanes: batch frame k runs on lane k % lanes (its own stream and executor activations), so two
+        # batches can be on the GPU at once -- concurrent streams overlap one batch's latency-bound stages
+        # with the other's work, as concurrent N = 1 graphs do
+        self.lanes = lanes
+        self.lane_stream = [torch.cuda.Stream(dev) for _ in range(lanes)]
+        self.stream = self.lane_stream[0]
         ys, yn, yw = aa_tables(H, size)
         xs, xn, xw = aa_tables(W, size)
         self.tab = [torch.from_numpy(a).to(dev) for a in (ys, yn, yw, xs, xn, xw)]
@@ -459,17 +472,29 @@ class BatchEngine:
         self.runner = C.BatchRunner(dev.index, self.stream.cuda_stream, self.nf, self.P, H, W, self.cfg.num_samples,
                                     src, coef_cap * 2, res_len)
         self.runner.set_spin_us(float(os.environ.get("RDP_SERVE_SPIN_US", "1000")))
-        # position inputs on the device (uploads are ordered after the previous batch on the one stream)
-        self.d_color = [torch.empty(H, W, 3, dtype=torch.uint8, device=dev) for _ in range(self.P)]
-        self.d_depth = [torch.empty(H, W, dtype=torch.int16, device=dev) for _ in range(self.P)]
+        for k in range(self.nf):
+            self.runner.set_frame_stream(k, self.lane_stream[k % lanes].cuda_stream)
+        # inputs of (batch frame k, position j) on the device: frame k + 1's uploads (copy engine, copy
+        # stream) run while frame k computes; the JPEG pixel stage's planes / colour are per position
+        nk, P = self.nf, self.P
+        up_u8 = (lambda: torch.empty(H, W, 3, dtype=torch.uint8, device=dev))  # noqa: E731
+        self.d_depth = [[torch.empty(H, W, dtype=torch.int16, device=dev) for _ in range(P)] for _ in range(nk)]
         if jpeg:
-            self.d_coef = [torch.empty(coef_cap, dtype=torch.int16, device=dev) for _ in range(self.P)]
-            self.d_meta = [torch.zeros(32 + 192, dtype=torch.int32, device=dev) for _ in range(self.P)]
-            self.d_planes = [torch.empty(C.jpeg_plane_bytes(H, W), dtype=torch.uint8, device=dev)
-                             for _ in range(self.P)]
-        for j in range(self.P):
-            up = self.d_coef[j] if jpeg else self.d_color[j]
-            self.runner.set_device(j, up.data_ptr(), self.d_meta[j].data_ptr() if jpeg else 0, self.d_depth[j].data_ptr())
+            self.d_coef = [[torch.empty(coef_cap, dtype=torch.int16, device=dev) for _ in range(P)] for _ in range(nk)]
+            self.d_meta = [[torch.zeros(32 + 192, dtype=torch.int32, device=dev) for _ in range(P)] for _ in range(nk)]
+            self.d_planes = [torch.empty(C.jpeg_plane_bytes(H, W), dtype=torch.uint8, device=dev) for _ in range(P)]
+            col = [up_u8() for _ in range(P)]
+            self.d_color = [col for _ in range(nk)]
+        else:
+            self.d_color = [[up_u8() for _ in range(P)] for _ in range(nk)]
+        for k in range(nk):
+            for j in range(P):
+                up = self.d_coef[k][j] if jpeg else self.d_color[k][j]
+                self.runner.set_device(k, j, up.data_ptr(), self.d_meta[k][j].data_ptr() if jpeg else 0,
+                                       self.d_depth[k][j].data_ptr())
+        # the per-frame stages of a batch (JPEG pixel stage + preprocess, geometry) run as parallel branches
+        # of its graph, each frame's on a capture stream of its own
+        self.branch = [torch.cuda.Stream(dev) for _ in range(P)]
         # host results of (k, j): mask + result vector in the runner's fine-grained host memory
         def host(kind, k, j, shape, dtype):
             import ctypes
@@ -478,9 +503,12 @@ class BatchEngine:
             return torch.from_numpy(np.frombuffer(buf, dtype=dtype).reshape(shape))
         self.h_mask = [[host(3, k, j, (H, W), np.uint8) for j in range(self.P)] for k in range(self.nf)]
         self.h_res = [[host(4, k, j, (res_len,), np.float64) for j in range(self.P)] for k in range(self.nf)]
-        # one eval executor per batch size (activations shared by every batch frame: one stream)
-        self.ex = {n: UNetExecutor(model, n, size, size, False, "bce", 1.0) for n in range(1, self.P + 1)}
-        self.m256 = {n: torch.empty(n * size * size, dtype=torch.uint8, device=dev) for n in range(1, self.P + 1)}
+        # one eval executor per (lane, batch size): activations shared by the batch frames of a lane (one stream)
+        self.exl = [{n: UNetExecutor(model, n, size, size, False, "bce", 1.0) for n in range(1, self.P + 1)}
+                    for _ in range(lanes)]
+        self.m256l = [{n: torch.empty(n * size * size, dtype=torch.uint8, device=dev) for n in range(1, self.P + 1)}
+                      for _ in range(lanes)]
+        self.ex, self.m256 = self.exl[0], self.m256l[0]
         self.graphs = {}
         self.refresh_weights()
         for k in range(self.nf):
@@ -505,30 +533,72 @@ class BatchEngine:
         self._th.start()
 
     # ------------------------------------------------------------------ device program
+    def _fork(self, n: int, body):
+        """Run ``body(j)`` for j < n, frame j's work on branch stream j (forked from and joined back into the
+        current stream: parallel branches of a captured graph) with ``RDP_BATCH_BRANCHES=1``; by default in
+        order (the branches measured 0.06 ms slower per 4-frame batch: profiles/serve_batch.md)."""
+        if n == 1 or os.environ.get("RDP_BATCH_BRANCHES", "0") == "0":
+            for j in range(n):
+                body(j)
+            return
+        main = torch.cuda.current_stream()
+        for j in range(n):
+            b = self.branch[j]
+            b.wait_stream(main)
+            with torch.cuda.stream(b):
+                body(j)
+        for j in range(n):
+            main.wait_stream(self.branch[j])
+
     def _program(self, k: int, n: int):
         C, m = self.C, self.model
-        ex = self.ex[n]
-        for j in range(n):
+        lane = k % self.lanes
+        ex = self.exl[lane][n]
+        m256 = self.m256l[lane][n]
+
+        def pre(j):
             if self.src == SRC_JPEG:
-                C.jpeg_to_rgb(self.d_coef[j], self.d_meta[j][:32], self.d_meta[j][32:], self.d_planes[j], self.d_color[j])
-            C.preprocess(self.d_color[j], *self.tab, ex.x_in[j:j + 1], int(self.src != SRC_BGR))
+                C.jpeg_to_rgb(self.d_coef[k][j], self.d_meta[k][j][:32], self.d_meta[k][j][32:], self.d_planes[j],
+                              self.d_color[k][j])
+            C.preprocess(self.d_color[k][j], *self.tab, ex.x_in[j:j + 1], int(self.src != SRC_BGR))
+
+        self._fork(n, pre)
         ex.forward(head=False, refresh_eval=False,
                    mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
-                              self.thr_logit, self.m256[n]))
+                              self.thr_logit, m256))
         S2 = self.S * self.S
-        for j in range(n):
+
+        if os.environ.get("RDP_BATCH_GEO", "1") != "0":
+            # every frame's geometry in one launch per stage (csrc/geometry.hip / geo_spline.hip batch forms)
+            gs = [self.geo[k][j] for j in range(n)]
+            c, Kc = self.cfg, self.K
+            C.geo_frames_batch([self.masks[k][j] for j in range(n)], [self.d_depth[k][j] for j in range(n)],
+                               [m256[j * S2:(j + 1) * S2].view(self.S, self.S) for j in range(n)],
+                               [g.work_i for g in gs], [g.work_d for g in gs], [g.pts for g in gs],
+                               [g.npts for g in gs], [g.out for g in gs], [g.kout for g in gs], [g.cov for g in gs],
+                               [g.sorted for g in gs], [g.gperm for g in gs], [g.u for g in gs],
+                               [self.h_res[k][j] for j in range(n)], [self.h_mask[k][j] for j in range(n)],
+                               float(Kc[0, 0]), float(Kc[1, 1]), float(Kc[0, 2]), float(Kc[1, 2]), self.scale,
+                               c.num_bins, c.top_k_percent, c.min_points, c.smoothing, c.spline_degree,
+                               c.num_samples, c.deriv_eps, c.min_edge_points)
+            return
+
+        def geo(j):
             g = self.geo[k][j]
-            g.launch_frame(self.m256[n][j * S2:(j + 1) * S2].view(self.S, self.S), self.masks[k][j], self.d_depth[j],
-                           self.K, self.scale, mask_host=self.h_mask[k][j], host_copy_in_spline=True)
+            g.launch_frame(m256[j * S2:(j + 1) * S2].view(self.S, self.S), self.masks[k][j],
+                           self.d_depth[k][j], self.K, self.scale, mask_host=self.h_mask[k][j], host_copy_in_spline=True)
             g.launch_spline(res_out=self.h_res[k][j])
 
+        self._fork(n, geo)
+
     def _capture(self, k: int, n: int):
+        st = self.lane_stream[k % self.lanes]
         with torch.cuda.device(self.dev):
-            with torch.cuda.stream(self.stream):
+            with torch.cuda.stream(st):
                 self._program(k, n)  # warm-up (lazy allocations, kernel loading)
-            self.stream.synchronize()
+            st.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
                 self._program(k, n)
         self.graphs[(k, n)] = g
         self.runner.set_graph(k, n, g.raw_cuda_graph_exec())
@@ -537,8 +607,9 @@ class BatchEngine:
         """BN-fold coefficients (and fragment-major eval weights) of every batch executor from the current
         weights; the graphs read them from buffers rewritten in place."""
         with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
-            for ex in self.ex.values():
-                ex.prepare_eval()
+            for exs in self.exl:
+                for ex in exs.values():
+                    ex.prepare_eval()
         self.stream.synchronize()
 
     def wait_idle(self):
@@ -593,7 +664,7 @@ class BatchEngine:
                             return
                         k, acq, ready = self._open, self._acq, self._ready
                         if k is not None and ready > 0 and ready == acq:
-                            if acq == self.P or self._gpu_pending() == 0 or \
+                            if acq == self.P or self._gpu_pending() < self.lanes or \
                                     time.perf_counter() - self._t_first >= self.window:
                                 break
                             self._cv.wait(timeout=50e-6)
@@ -609,7 +680,7 @@ class BatchEngine:
                 ev = self._done_evs.get(k)
                 if ev is None:
                     ev = self._done_evs[k] = torch.cuda.Event()
-                ev.record(self.stream)
+                ev.record(self.lane_stream[k % self.lanes])
                 with self._cv:
                     self._launched.append(k)
                     self._launched_gen[k] = self._gen[k]
