@@ -1322,7 +1322,9 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   // 1024->512 63.5 -> 53.2 us, 512->512 39.9 -> 36.7, 512+512->256 39.0 -> 36.7, 64^2 256->128 31.5 ->
   // 29.4; where the 128 x 128 grid needs no split (64^2 256->256) the unsplit kernel wins, 32.9 vs 39.5,
   // and at M = 1024 (16^2 512->1024: 29.5 vs 31.0 us) the 128 x 128 split does)
-  if (bm_pref == 0 && !packed && escale == nullptr && Cout % 128 == 0 && Cy1 % 32 == 0 && C1 + C2 >= 128 &&
+  // (eval too, BN fold in the shared reduce: the batched serving network at N = 4, scripts/rowband_bench.py
+  // --batch 4 --variants 0,7: 32^2 1024->512 63.2 -> 52.3 us, 512->512 + pool 39.3 -> 36.4)
+  if (bm_pref == 0 && !packed && Cout % 128 == 0 && Cy1 % 32 == 0 && C1 + C2 >= 128 &&
       a.M >= 4096 && (long)(a.M + 127) / 128 * (Cout / 128) < 192 && pp_split_enabled()) {
     const int d = pp_split_plan(a.M, Cout, 128, a.nks, wse);
     if (d > 1) return launch_pp<128>(a, s, d, pooled);

@@ -125,8 +125,13 @@ def measure_engine_pipelined(model, scenes, frames: int = 200, warmup: int = 20,
     ths = [threading.Thread(target=run, args=(k,)) for k in range(streams)]
     [t.start() for t in ths]
     [t.join() for t in ths]
-    return {f"engine_pipelined_fps{'' if streams == 1 else f'_{streams}streams'}":
-            round(frames * streams / max(res.values()), 1)}
+    sfx = '' if streams == 1 else f'_{streams}streams'
+    out = {f"engine_pipelined_fps{sfx}": round(frames * streams / max(res.values()), 1)}
+    if streams > 1 and getattr(pool, "batchers", None):  # batched serving: how the frames were grouped
+        out[f"engine_batch_sizes{sfx}"] = {str(k): v for k, v in sorted(pool.batchers[0].batch_sizes.items())}
+        for b in pool.batchers:
+            b.close()
+    return out
 
 
 def run_client_load(port: int, frames: int, warmup: int, n_scenes: int = 8, lockstep: bool = True,

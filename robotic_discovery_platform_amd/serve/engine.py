@@ -433,10 +433,10 @@ class BatchEngine:
                  lanes: Optional[int] = None):
         dev = _norm_device(device if device is not None else model.store.device)
         if lanes is None:
-            lanes = int(os.environ.get("RDP_BATCH_LANES", "2"))
+            lanes = int(os.environ.get("RDP_BATCH_LANES", "1"))
         lanes = max(1, int(lanes))
-        if frames is None:
-            frames = 2 * lanes + 1
+        if frames is None:  # per lane: one running, one queued, one filling, one being collected
+            frames = 4 * lanes
         with torch.cuda.device(dev):
             self._init(model, K, depth_scale, H, W, size, threshold, geo_cfg, dev, src, max(frames, lanes), positions,
                        window_us, lanes)
@@ -454,6 +454,7 @@ class BatchEngine:
         self.cfg = geo_cfg or GeometryConfig()
         self.nf, self.P = int(frames), int(positions)
         self.window = window_us * 1e-6
+        self.max_wait = float(os.environ.get("RDP_BATCH_MAX_WAIT_US", "2000")) * 1e-6
         # lanes: batch frame k runs on lane k % lanes (its own stream and executor activations), so two
         # batches can be on the GPU at once -- concurrent streams overlap one batch's latency-bound stages
         # with the other's work, as concurrent N = 1 graphs do
@@ -528,6 +529,9 @@ class BatchEngine:
         self._launched = collections.deque()  # launched frames, oldest first (GPU occupancy)
         self._done_evs = {}
         self.batch_sizes = collections.Counter()
+        # callable -> how many client streams feed this engine now (EnginePool: sessions active in the last
+        # few ms), the batch size to wait for; None: launch as the GPU frees up
+        self.target = None
         self._stop = False
         self._th = threading.Thread(target=self._launcher, name="rdp-batch-launcher", daemon=True)
         self._th.start()
@@ -664,8 +668,22 @@ class BatchEngine:
                             return
                         k, acq, ready = self._open, self._acq, self._ready
                         if k is not None and ready > 0 and ready == acq:
-                            if acq == self.P or self._gpu_pending() < self.lanes or \
-                                    time.perf_counter() - self._t_first >= self.window:
+                            # every active stream's frame is in (each stream has one frame waiting at a time
+                            # in steady state), or the batch is full, or the window since its first frame
+                            # passed; with no stream count (target None) a lone batch also goes when the GPU
+                            # has nothing of this engine in flight
+                            tgt = self.target() if self.target is not None else None
+                            waited = time.perf_counter() - self._t_first
+                            if tgt is None:  # no stream count: launch as a lane frees up
+                                go = acq >= self.P or self._gpu_pending() < self.lanes or waited >= self.window
+                            else:
+                                # a partial batch goes early only onto an idle GPU (after the window) or after
+                                # max_wait: while a batch runs, launching would only queue it behind -- it
+                                # keeps filling instead (frames of a stream that was preempted still join)
+                                go = (acq >= min(self.P, max(tgt, 1)) or
+                                      (waited >= self.window and self._gpu_pending() < self.lanes) or
+                                      waited >= self.max_wait)
+                            if go:
                                 break
                             self._cv.wait(timeout=50e-6)
                             continue
@@ -932,6 +950,13 @@ class EnginePool:
                                          positions=self.batch_positions, **self.args) for r in range(len(self.replicas))]
         self._recent = [dict() for _ in self.replicas]  # replica -> {session id: last submit time}
         self.batch_active_s = 0.005
+        for r, b in enumerate(self.batchers):
+            b.target = (lambda r=r: self._active(r))
+
+    def _active(self, r: int) -> int:
+        """Sessions of replica ``r`` that submitted within the last ``batch_active_s``."""
+        now = time.perf_counter()
+        return sum(1 for t in list(self._recent[r].values()) if now - t <= self.batch_active_s)
 
     def _batcher(self, r: int, sid: int, shape) -> "Optional[BatchEngine]":
         """The replica's BatchEngine if this frame should be batched: configured frame size and at least two
@@ -944,8 +969,7 @@ class EnginePool:
         if len(rec) > 64:
             for k in [k for k, t in rec.items() if now - t > self.batch_active_s]:
                 rec.pop(k, None)
-        active = sum(1 for t in list(rec.values()) if now - t <= self.batch_active_s)
-        return self.batchers[r] if active >= 2 else None
+        return self.batchers[r] if self._active(r) >= 2 else None
 
     def _new(self, r: int, H, W):
         m = self.replicas[r]
@@ -1036,10 +1060,10 @@ class EngineSession:
         """A position in ``b``'s open batch: without blocking if one is free, else after collecting this
         session's own frames (a session never waits on the pool while holding positions others wait on)."""
         pos = b._acquire(block=False)
-        if pos is None:
-            out += self.drain()
-            pos = b._acquire()
-        return pos
+        while pos is None and self.inflight:  # oldest first, only as many as needed
+            out.append(self._collect_one())
+            pos = b._acquire(block=False)
+        return pos if pos is not None else b._acquire()
 
     def submit(self, color_bgr, depth, tag=None, rgb: bool = False) -> list:
         """Stage + enqueue a frame; returns [(tag, FrameResult | Exception)] of frames it had to collect.

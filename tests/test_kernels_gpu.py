@@ -760,7 +760,9 @@ def _splitk_case(C, N, H, W, C1, C2, Cout):
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(1, 64, 64, 256, 0, 256), (1, 32, 32, 512, 0, 512),
                                               (1, 128, 128, 128, 0, 128), (2, 16, 16, 256, 256, 512),
                                               (1, 256, 256, 64, 0, 128), (1, 256, 256, 64, 0, 64),
-                                              (2, 64, 128, 64, 0, 64), (1, 24, 40, 64, 0, 64)])
+                                              (2, 64, 128, 64, 0, 64), (1, 24, 40, 64, 0, 64),
+                                              # batched serving (N = 4): split-K ping-pong + eval reduce
+                                              (4, 32, 32, 512, 0, 512)])
 def test_conv_eval_fused_pool(C, N, H, W, C1, C2, Cout):
     """Eval conv (BN fold + ReLU) with ``pool=``: MaxPool2d(2) fused into the split-K reduce (deep
     serving shapes), into the row-ring epilogue (64 -> 64, W % 64 == 0) or launched after the conv
@@ -791,7 +793,7 @@ def test_conv_eval_fused_pool(C, N, H, W, C1, C2, Cout):
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,pad", [(1, 16, 16, 512, 0, 512, 0), (1, 32, 32, 512, 512, 256, 0),
                                                    (1, 64, 64, 256, 256, 128, 1), (2, 16, 16, 256, 0, 256, 1),
-                                                   (1, 128, 128, 128, 128, 64, 0)])
+                                                   (1, 128, 128, 128, 128, 64, 0), (4, 32, 32, 512, 512, 512, 0)])
 def test_conv_eval_fused_upsample(C, N, H, W, C1, C2, Cout, pad):
     """Eval conv (BN fold + ReLU) with ``up=``: the decoder's bilinear x2 upsample (align_corners,
     centred pad) fused into the split-K reduce (maps of <= 16^2 pixels; larger ones take the separate

@@ -122,3 +122,47 @@ def test_batch_encoded_matches_pipeline_wire(setup):
         if pa[:-5] != pb[:-5]:  # masks may differ in a handful of threshold pixels between batch sizes
             assert abs(a.coverage - b.coverage) < 0.1 and abs(a.mean_curvature - b.mean_curvature) <= \
                 0.05 * abs(b.mean_curvature) + 1e-6
+
+
+@pytest.mark.parametrize("n", [1, 3, 4])
+def test_batched_geometry_bitwise_equals_per_frame(setup, n):
+    """geo_frames_batch (one launch per stage for n frames, csrc/geometry.hip rdp_geo_edges_batch +
+    csrc/geo_spline.hip rdp_geo_spline_batch) on the same model masks and depth frames gives bit-identical
+    result vectors and masks as each frame's own GeometryEngine launches."""
+    from robotic_discovery_platform_amd.config import GeometryConfig
+    from robotic_discovery_platform_amd.data.image_io import resize_nearest
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
+    from robotic_discovery_platform_amd.geometry.curvature import GeometryEngine
+    from robotic_discovery_platform_amd.ops import native
+    _, scenes = setup
+    C = native()
+    dev = torch.device("cuda")
+    cfg = GeometryConfig()
+    H, W = 480, 640
+    m256 = [torch.from_numpy(resize_nearest(sc.mask, (256, 256))).to(dev).contiguous() for sc in scenes[:n]]
+    m256 = [(m > 0).to(torch.uint8) for m in m256]
+    depth = [torch.from_numpy(sc.depth.view(np.int16)).to(dev) for sc in scenes[:n]]
+    K = DEFAULT_K
+    single = []
+    ge = [GeometryEngine(H, W, dev, cfg) for _ in range(n)]
+    for j in range(n):
+        mask = torch.empty(H, W, dtype=torch.uint8, device=dev)
+        mh = torch.zeros(H, W, dtype=torch.uint8).pin_memory()
+        ge[j].launch_frame(m256[j], mask, depth[j], K, 0.001, mask_host=mh, host_copy_in_spline=True)
+        ge[j].launch_spline(res_out=ge[j].res)
+        torch.cuda.synchronize()
+        single.append((ge[j].res.cpu().clone(), mask.cpu().clone(), mh.clone()))
+    gb = [GeometryEngine(H, W, dev, cfg) for _ in range(n)]
+    masks = [torch.empty(H, W, dtype=torch.uint8, device=dev) for _ in range(n)]
+    mhs = [torch.zeros(H, W, dtype=torch.uint8).pin_memory() for _ in range(n)]
+    C.geo_frames_batch(masks, depth, m256, [g.work_i for g in gb], [g.work_d for g in gb], [g.pts for g in gb],
+                       [g.npts for g in gb], [g.out for g in gb], [g.kout for g in gb], [g.cov for g in gb],
+                       [g.sorted for g in gb], [g.gperm for g in gb], [g.u for g in gb], [g.res for g in gb], mhs,
+                       float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]), 0.001, cfg.num_bins,
+                       cfg.top_k_percent, cfg.min_points, cfg.smoothing, cfg.spline_degree, cfg.num_samples,
+                       cfg.deriv_eps, cfg.min_edge_points)
+    torch.cuda.synchronize()
+    for j in range(n):
+        r, m, mh = single[j]
+        assert torch.equal(gb[j].res.cpu(), r), j
+        assert torch.equal(masks[j].cpu(), m) and torch.equal(mhs[j], mh), j
