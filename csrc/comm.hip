@@ -26,19 +26,26 @@ __global__ __launch_bounds__(256) void comm_emulate_traffic_kernel(uint64_t tick
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const long per = (n4 + gridDim.x - 1) / gridDim.x;
   const long lo = (long)blockIdx.x * per, hi = lo + per < n4 ? lo + per : n4;
-  constexpr int kChunk = 256 * 4;  // float4 elements per chunk (16 KiB read + 16 KiB written)
+  // 16 loads in flight per lane (64 KiB read + 64 KiB written per chunk and block): a few resident blocks
+  // sustain the modelled rate (scripts/comm_emulate_check.py: the kernel must not outlast its modelled time)
+  constexpr int U = 16, kChunk = 256 * U;
   const long chunks = hi > lo ? (hi - lo + kChunk - 1) / kChunk : 0;
   for (long c = 0; c < chunks; ++c) {
     const uint64_t due = (uint64_t)((double)ticks * c / chunks);
     while (__builtin_amdgcn_s_memrealtime() - t0 < due) __builtin_amdgcn_s_sleep(2);
     const long base = lo + c * kChunk;
+    float4 v[U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < U; ++k) {
+      const long i = base + k * 256 + threadIdx.x;
+      if (i < hi) v[k] = buf[i];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
       const long i = base + k * 256 + threadIdx.x;
       if (i < hi) {
-        float4 v = buf[i];
-        v.x += 1.0f;
-        buf[n4 + i] = v;
+        v[k].x += 1.0f;
+        buf[n4 + i] = v[k];
       }
     }
   }

@@ -685,7 +685,11 @@ class BatchEngine:
                                       waited >= self.max_wait)
                             if go:
                                 break
-                            self._cv.wait(timeout=50e-6)
+                            # sleep until the window ends (a new frame notifies earlier), then poll the GPU
+                            # every 100 us: a short fixed poll woke this thread ~20k times a second, each
+                            # wake-up taking the interpreter lock from the stream threads
+                            t = self.window - waited if waited < self.window else 100e-6
+                            self._cv.wait(timeout=max(20e-6, min(t, self.max_wait - waited)))
                             continue
                         self._cv.wait(timeout=1e-3 if k is not None and ready > 0 else None)
                     n, void = acq, self._void
