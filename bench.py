@@ -255,7 +255,7 @@ def main():
         sys.exit(rc)
     rank, world, dev = setup_dist(args)
     comm = {}
-    if dist.is_initialized():
+    if dist.is_initialized() and os.environ.get("RDP_COMM_SELFCHECK", "1") != "0":
         # the first real multi-rank run of the native collective path checks itself before anything is
         # timed: RCCL's rank count, a rank-sum probe through the buckets' exact call, fallback to
         # torch.distributed issue if it fails, measured all-reduce bus bandwidth (parallel/selfcheck.py)

@@ -467,6 +467,54 @@ class _Layer:
 _STREAM_OBSERVERS: List = []
 
 
+_CONCURRENT_CACHE: Dict[tuple, bool] = {}
+
+
+def _runs_concurrently(a: "torch.cuda.Stream", b: "torch.cuda.Stream") -> bool:
+    """Whether kernels of streams ``a`` and ``b`` overlap on the GPU: a 300 us single-block resident kernel
+    (csrc/comm.hip, the collective emulator's spin) on each; on one hardware queue they serialize (~600 us).
+    The GPU must be idle (called while an executor is set up, never inside a step or a plan)."""
+    key = (a.cuda_stream, b.cuda_stream)
+    if key in _CONCURRENT_CACHE:
+        return _CONCURRENT_CACHE[key]
+    import time
+    C = _native()
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(2):
+        t0 = time.perf_counter()
+        with torch.cuda.stream(a):
+            C.comm_emulate(300.0, 1)
+        with torch.cuda.stream(b):
+            C.comm_emulate(300.0, 1)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    ok = best < 450e-6
+    _CONCURRENT_CACHE[key] = _CONCURRENT_CACHE[(key[1], key[0])] = ok
+    return ok
+
+
+def concurrent_stream(dev, others, tries: int = 8) -> "torch.cuda.Stream":
+    """A new stream whose kernels run concurrently with every stream of ``others``. HIP gives streams hardware
+    queues round-robin in creation order (GPU_MAX_HW_QUEUES, 4 by default; torch.cuda.Stream draws from a
+    pre-created pool), so a plain new stream may share a queue with the main or the weight-gradient stream --
+    and then everything issued on it waits behind their work. Measured under emulated n = 8 collectives
+    (profiles/ddp_emulated.md, round 6): the same dedicated collective stream gave 19.2 or 21.9 ms per bs-64
+    step depending only on how many streams the process had drawn before it (a high-priority stream did not
+    help: 22.1 ms). Draws up to ``tries`` streams and returns the first that overlaps every stream of
+    ``others`` in a timed probe (``RDP_STREAM_PROBE=0``: no probe, the next pool stream)."""
+    others = [o for o in others if o is not None]
+    if os.environ.get("RDP_STREAM_PROBE", "1") == "0" or torch.device(dev).type != "cuda":
+        return torch.cuda.Stream(dev)
+    s = None
+    with torch.cuda.device(dev):
+        for _ in range(tries):
+            s = torch.cuda.Stream(dev)
+            if all(_runs_concurrently(s, o) for o in others):
+                return s
+    return s
+
+
 def _stream_wait(waiter: "torch.cuda.Stream", waitee: "torch.cuda.Stream"):
     """``waiter.wait_stream(waitee)`` through the native runtime, so that a launch plan being recorded
     (NativeTrainer plan mode, csrc/bindings.cpp) also holds the cross-stream dependency."""
@@ -626,7 +674,8 @@ class UNetExecutor:
         dev, bf = self.dev, torch.bfloat16
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
-        self.side = torch.cuda.Stream(dev) if self.overlap_wgrad else None
+        # a stream whose kernels overlap the main stream's (concurrent_stream: not on its hardware queue)
+        self.side = concurrent_stream(dev, [torch.cuda.current_stream(dev)]) if self.overlap_wgrad else None
         # split-K grid target of the generic / packed weight-gradient kernels. Fewer splits = less fp32
         # slab traffic, more = more parallelism; 512 measured best at bs 4 .. 64 (the side stream's wgrads
         # overlap the main stream, so a lighter slab wins over the serialised optimum).
@@ -1034,7 +1083,9 @@ class UNetExecutor:
             yield
             return
         if getattr(self, "comm_side", None) is None:
-            self.comm_side = torch.cuda.Stream(self.dev)
+            # the main stream here is the caller's current one; the collective stream must not share a
+            # hardware queue with it or with the weight-gradient stream
+            self.comm_side = concurrent_stream(self.dev, [torch.cuda.current_stream(self.dev), self.side])
         cur = torch.cuda.current_stream()
         _stream_wait(self.comm_side, self.side)
         if cur != self.side and (producer is None or producer != self.side):

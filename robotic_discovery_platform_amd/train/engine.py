@@ -131,10 +131,13 @@ class NativeTrainer:
     # Issue stream of the natively issued bucket all-reduces by (emulated) world size, from the A/B in
     # profiles/ddp_emulated.md (RDP_DDP_EMULATE on one MI355X); RDP_DDP_STREAM=side|dedicated overrides.
     # World 1 (forced DDP): RCCL launches nothing, an extra stream wait would only cost (ddp_world1.md).
-    # Measured: the side stream wins at every emulated point (n = 8 at 150 GB/s x 16 CUs and 300 GB/s x 32
-    # CUs; bs 64: 20.34 / 20.04 ms vs 22.33 / 21.96 ms dedicated; bs 4: 3.26 / 2.87 vs 3.62 / 3.21 ms).
+    # World > 1: a dedicated collective stream on a hardware queue of its own (models.unet.concurrent_stream)
+    # -- round 6, n = 8 emulated: bs 64 19.16-19.22 vs 19.94-19.98 ms on the side stream, bs 4 2.68 vs 3.19-3.20
+    # (150 GB/s, 16 CUs); 19.39-19.59 vs 19.56-19.62 and 2.45 vs 2.80 at 300 GB/s, 32 CUs. Round 5 measured the
+    # opposite (22.3 vs 20.3 ms) with a dedicated stream that shared a queue with the main or side stream:
+    # the same stream placed by creation order alone gave 21.8-22.2 ms this round.
     DDP_STREAM_BY_WORLD = {1: "side"}
-    DDP_STREAM_DEFAULT = "side"
+    DDP_STREAM_DEFAULT = "dedicated"
 
     @classmethod
     def ddp_stream_mode(cls, world: int) -> str:

@@ -15,6 +15,7 @@ from robotic_discovery_platform_amd.parallel.ddp import ring_allreduce_us  # noq
 
 
 def main():
+    blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     C = native()
     dev = torch.device("cuda")
     rows = []
@@ -28,12 +29,12 @@ def main():
             for _ in range(12):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                C.comm_emulate(us, 16, scratch if tb else None, tb)
+                C.comm_emulate(us, blocks, scratch if tb else None, tb)
                 e1.record()
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3)
             t = sorted(ts[2:])[len(ts[2:]) // 2]
-            rows.append({"bucket_mb": mb, "traffic_x": traffic, "modelled_us": round(us, 1), "measured_us": round(t, 1),
+            rows.append({"blocks": blocks, "bucket_mb": mb, "traffic_x": traffic, "modelled_us": round(us, 1), "measured_us": round(t, 1),
                          "hbm_gbps": round(2 * tb / (t * 1e3), 1) if tb else 0.0})
             print(json.dumps(rows[-1]), flush=True)
 
