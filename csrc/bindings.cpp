@@ -98,6 +98,10 @@ int rdp_parcur(int, int, const double*, const double*, double, int, int, double*
 double rdp_splev1(const double*, int, const double*, int, double, int);
 int rdp_fit_curvature(const double*, int, double, int, int, double, double*, double*);
 int rdp_geo_spline_res_len(int);
+int rdp_preprocess_batch(int, const void* const*, int, int, const int*, const int*, const float*, const int*,
+                         const int*, const float*, int, int, int, void* const*, hipStream_t);
+int rdp_jpeg_gpu_batch(int, const void* const*, const int* const*, const int* const*, void* const*, int, int, int,
+                       void* const*, hipStream_t);
 int rdp_geo_edges_batch(int, const void* const*, const void* const*, int, int, double, double, double, double, double,
                         int* const*, double* const*, double* const*, double* const*, int, int* const*, double* const*,
                         int, int* const*, int, double, int, const void* const*, int, int, int* const*, double* const*,
@@ -1581,6 +1585,51 @@ py::object jpeg_decode(py::bytes data, bool parallel, bool pin) {
 // geo / coefs / qt: jpeg_decode's outputs, on the device. Launch sizes come from the pipeline's
 // frame size (H, W) so one captured graph serves every JPEG of that size; the kernels read the
 // actual geometry from `geo`.
+// the pixel stage + preprocess of n <= 4 frames of a serving batch in 2 + 1 launches (BatchEngine): per-frame
+// lists; coefs / meta / planes empty for array sources (rgb: HxWx3 u8 colour frames, the preprocess input)
+void batch_preprocess(std::vector<torch::Tensor> coefs, std::vector<torch::Tensor> meta,
+                      std::vector<torch::Tensor> planes, std::vector<torch::Tensor> rgb, torch::Tensor ystart,
+                      torch::Tensor ysize, torch::Tensor yw, torch::Tensor xstart, torch::Tensor xsize,
+                      torch::Tensor xw, torch::Tensor out, int rgb_order) {
+  const int n = (int)rgb.size();
+  TORCH_CHECK(n >= 1 && n <= 4, "batch_preprocess: 1..4 frames");
+  const int H = rgb[0].size(0), W = rgb[0].size(1);
+  Act o = act(out, "out");
+  TORCH_CHECK(o.N >= n && o.C == 8 && o.pitch == 8, "out must be [>= n, OH, OW, 8] contiguous");
+  TORCH_CHECK(ystart.numel() == o.H && xstart.numel() == o.W && yw.numel() == (long)o.H * 16 &&
+              xw.numel() == (long)o.W * 16, "aa tables");
+  const bool jpeg = !coefs.empty();
+  TORCH_CHECK(!jpeg || ((int)coefs.size() == n && (int)meta.size() == n && (int)planes.size() == n),
+              "batch_preprocess: coefs / meta / planes: one per frame or none");
+  std::vector<const void*> pc(n), pr(n);
+  std::vector<const int*> pg(n), pq(n);
+  std::vector<void*> pp(n), prw(n), po(n);
+  for (int i = 0; i < n; ++i) {
+    TORCH_CHECK(rgb[i].is_cuda() && rgb[i].scalar_type() == torch::kUInt8 && rgb[i].dim() == 3 && rgb[i].size(2) == 3 &&
+                    rgb[i].is_contiguous() && rgb[i].size(0) == H && rgb[i].size(1) == W, "rgb u8 HxWx3, one size");
+    pr[i] = rgb[i].data_ptr();
+    prw[i] = rgb[i].data_ptr();
+    po[i] = (char*)o.ptr + (long)i * o.H * o.W * 8 * 2;
+    if (jpeg) {
+      TORCH_CHECK(coefs[i].is_cuda() && coefs[i].scalar_type() == torch::kInt16 &&
+                      coefs[i].numel() >= rdp_jpeg_max_coefs(H, W), "coefs");
+      TORCH_CHECK(meta[i].is_cuda() && meta[i].scalar_type() == torch::kInt32 && meta[i].numel() >= 224, "meta");
+      TORCH_CHECK(planes[i].is_cuda() && planes[i].numel() >= rdp_jpeg_plane_bytes(H, W), "planes");
+      pc[i] = coefs[i].data_ptr();
+      pg[i] = meta[i].data_ptr<int>();
+      pq[i] = meta[i].data_ptr<int>() + 32;
+      pp[i] = planes[i].data_ptr();
+    }
+  }
+  const hipStream_t st = unplanned_stream();
+  if (jpeg)
+    TORCH_CHECK(rdp_jpeg_gpu_batch(n, pc.data(), pg.data(), pq.data(), pp.data(), H, W,
+                                   (int)(coefs[0].numel() / 64), prw.data(), st) == 0, "jpeg batch");
+  TORCH_CHECK(rdp_preprocess_batch(n, pr.data(), H, W, ystart.data_ptr<int>(), ysize.data_ptr<int>(),
+                                   yw.data_ptr<float>(), xstart.data_ptr<int>(), xsize.data_ptr<int>(),
+                                   xw.data_ptr<float>(), o.H, o.W, rgb_order, po.data(), st) == 0, "preprocess batch");
+}
+
 void jpeg_to_rgb(torch::Tensor coefs, torch::Tensor geo, torch::Tensor qt, torch::Tensor planes, torch::Tensor rgb) {
   TORCH_CHECK(coefs.is_cuda() && coefs.scalar_type() == torch::kInt16 && coefs.is_contiguous(), "coefs int16");
   TORCH_CHECK(geo.is_cuda() && geo.scalar_type() == torch::kInt32 && geo.numel() >= 32, "geo int32[32]");
@@ -1734,6 +1783,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("step") = py::none(), py::arg("blocks") = 0);
   m.def("wseg_size", &rdp_wseg_size);
   m.def("parcur", &parcur);
+  m.def("batch_preprocess", on_device(&batch_preprocess));
   m.def("geo_frames_batch", on_device(&geo_frames_batch));
   m.def("geo_edges", on_device(&geo_edges), py::arg("mask"), py::arg("depth"), py::arg("fx"), py::arg("fy"), py::arg("cx"),
         py::arg("cy"), py::arg("scale"), py::arg("work_i"), py::arg("work_d"), py::arg("pts"), py::arg("npts"),

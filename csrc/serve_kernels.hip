@@ -20,10 +20,10 @@ struct AATable {  // per output index: first input index, number of taps, weight
   float w[256][AA_MAXTAP];
 };
 
-__global__ void preprocess_kernel(const uint8_t* __restrict__ bgr, int H, int W, const int* __restrict__ ystart,
-                                  const int* __restrict__ ysize, const float* __restrict__ yw,
-                                  const int* __restrict__ xstart, const int* __restrict__ xsize,
-                                  const float* __restrict__ xw, int OH, int OW, int rgb, u16* __restrict__ out) {
+RDP_DEV void preprocess_body(const uint8_t* __restrict__ bgr, int H, int W, const int* __restrict__ ystart,
+                             const int* __restrict__ ysize, const float* __restrict__ yw,
+                             const int* __restrict__ xstart, const int* __restrict__ xsize,
+                             const float* __restrict__ xw, int OH, int OW, int rgb, u16* __restrict__ out) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= OH * OW) return;
   const int oy = o / OW, ox = o - oy * OW;
@@ -55,6 +55,25 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ bgr, int H, int W,
   v.z = 0u;
   v.w = 0u;
   *(uint4*)(out + (size_t)o * 8) = v;
+}
+
+__global__ void preprocess_kernel(const uint8_t* __restrict__ bgr, int H, int W, const int* __restrict__ ystart,
+                                  const int* __restrict__ ysize, const float* __restrict__ yw,
+                                  const int* __restrict__ xstart, const int* __restrict__ xsize,
+                                  const float* __restrict__ xw, int OH, int OW, int rgb, u16* __restrict__ out) {
+  preprocess_body(bgr, H, W, ystart, ysize, yw, xstart, xsize, xw, OH, OW, rgb, out);
+}
+
+// up to 4 frames of a serving batch in one launch (blockIdx.y = frame; serve/engine.py BatchEngine)
+struct PreFrames {
+  const uint8_t* bgr[4];
+  u16* out[4];
+};
+__global__ void preprocess_batch_kernel(const PreFrames f, int H, int W, const int* __restrict__ ystart,
+                                        const int* __restrict__ ysize, const float* __restrict__ yw,
+                                        const int* __restrict__ xstart, const int* __restrict__ xsize,
+                                        const float* __restrict__ xw, int OH, int OW, int rgb) {
+  preprocess_body(f.bgr[blockIdx.y], H, W, ystart, ysize, yw, xstart, xsize, xw, OH, OW, rgb, f.out[blockIdx.y]);
 }
 
 // nearest upsample of the model-resolution mask to (H, W) + coverage count.
@@ -91,6 +110,21 @@ int rdp_preprocess(const void* bgr, int H, int W, const int* ystart, const int* 
   const int n = OH * OW;
   hipLaunchKernelGGL(preprocess_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)bgr, H, W, ystart,
                      ysize, yw, xstart, xsize, xw, OH, OW, rgb, (u16*)out);
+  return 0;
+}
+
+int rdp_preprocess_batch(int n, const void* const* bgr, int H, int W, const int* ystart, const int* ysize,
+                         const float* yw, const int* xstart, const int* xsize, const float* xw, int OH, int OW, int rgb,
+                         void* const* out, hipStream_t s) {
+  if (n < 1 || n > 4) return -1;
+  PreFrames f;
+  for (int i = 0; i < 4; ++i) {
+    f.bgr[i] = (const uint8_t*)bgr[i < n ? i : 0];
+    f.out[i] = (u16*)out[i < n ? i : 0];
+  }
+  const int np = OH * OW;
+  hipLaunchKernelGGL(preprocess_batch_kernel, dim3((np + 255) / 256, n), dim3(256), 0, s, f, H, W, ystart, ysize, yw,
+                     xstart, xsize, xw, OH, OW, rgb);
   return 0;
 }
 
@@ -158,8 +192,8 @@ RDP_DEV void jidct_1d(const int* v, int& e0, int& e1, int& e2, int& e3, int& o0,
   o3 = a3 + z1 + z4;  // tmp3
 }
 
-__global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restrict__ coefs, const int* __restrict__ geo,
-                                                        const int* __restrict__ qt, uint8_t* __restrict__ planes) {
+RDP_DEV void jpeg_idct_body(const int16_t* __restrict__ coefs, const int* __restrict__ geo,
+                            const int* __restrict__ qt, uint8_t* __restrict__ planes) {
   __shared__ int ws[32][64];
   const int lb = threadIdx.x >> 3, k = threadIdx.x & 7;
   const int jb = blockIdx.x * 32 + lb;
@@ -226,8 +260,8 @@ RDP_DEV int jpeg_chroma(const uint8_t* __restrict__ planes, const int* g, int hm
   return base[(y / vr) * stride + x / hr];
 }
 
-__global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restrict__ planes, const int* __restrict__ geo,
-                                                         int H, int W, uint8_t* __restrict__ rgb) {
+RDP_DEV void jpeg_color_body(const uint8_t* __restrict__ planes, const int* __restrict__ geo, int H, int W,
+                             uint8_t* __restrict__ rgb) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= H * W) return;
   const int y = p / W, x = p - y * W;
@@ -247,7 +281,49 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
   o[2] = (uint8_t)min(max(b, 0), 255);
 }
 
+__global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restrict__ coefs, const int* __restrict__ geo,
+                                                        const int* __restrict__ qt, uint8_t* __restrict__ planes) {
+  jpeg_idct_body(coefs, geo, qt, planes);
+}
+__global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restrict__ planes, const int* __restrict__ geo,
+                                                         int H, int W, uint8_t* __restrict__ rgb) {
+  jpeg_color_body(planes, geo, H, W, rgb);
+}
+struct JpegFrames {
+  const int16_t* coefs[4];
+  const int* geo[4];
+  const int* qt[4];
+  uint8_t* planes[4];
+  uint8_t* rgb[4];
+};
+__global__ __launch_bounds__(256) void jpeg_idct_batch_kernel(const JpegFrames f) {
+  const int i = blockIdx.y;
+  jpeg_idct_body(f.coefs[i], f.geo[i], f.qt[i], f.planes[i]);
+}
+__global__ __launch_bounds__(256) void jpeg_color_batch_kernel(const JpegFrames f, int H, int W) {
+  const int i = blockIdx.y;
+  jpeg_color_body(f.planes[i], f.geo[i], H, W, f.rgb[i]);
+}
+
 extern "C" {
+// the JPEG pixel stage of n <= 4 frames (each its coefficient / meta / planes / RGB buffers) in 2 launches
+int rdp_jpeg_gpu_batch(int n, const void* const* coefs, const int* const* geo, const int* const* qt,
+                       void* const* planes, int H, int W, int max_blocks, void* const* rgb, hipStream_t s) {
+  if (n < 1 || n > 4) return -1;
+  JpegFrames f;
+  for (int i = 0; i < 4; ++i) {
+    const int j = i < n ? i : 0;
+    f.coefs[i] = (const int16_t*)coefs[j];
+    f.geo[i] = geo[j];
+    f.qt[i] = qt[j];
+    f.planes[i] = (uint8_t*)planes[j];
+    f.rgb[i] = (uint8_t*)rgb[j];
+  }
+  hipLaunchKernelGGL(jpeg_idct_batch_kernel, dim3((max_blocks + 31) / 32, n), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(jpeg_color_batch_kernel, dim3((H * W + 255) / 256, n), dim3(256), 0, s, f, H, W);
+  return 0;
+}
+
 // coefficient / plane capacity for frames of H x W (any supported sampling: Y and chroma planes at most
 // MCU-padded to 16 x 16)
 long rdp_jpeg_max_coefs(int H, int W) { return 3L * ((W + 15) / 16 * 16) * ((H + 15) / 16 * 16); }

@@ -566,7 +566,15 @@ class BatchEngine:
                               self.d_color[k][j])
             C.preprocess(self.d_color[k][j], *self.tab, ex.x_in[j:j + 1], int(self.src != SRC_BGR))
 
-        self._fork(n, pre)
+        if os.environ.get("RDP_BATCH_PRE", "1") != "0":
+            # every frame's JPEG pixel stage (2 launches) and preprocess (1 launch), blockIdx.y = frame
+            jp = self.src == SRC_JPEG
+            C.batch_preprocess([self.d_coef[k][j] for j in range(n)] if jp else [],
+                               [self.d_meta[k][j] for j in range(n)] if jp else [],
+                               [self.d_planes[j] for j in range(n)] if jp else [],
+                               [self.d_color[k][j] for j in range(n)], *self.tab, ex.x_in, int(self.src != SRC_BGR))
+        else:
+            self._fork(n, pre)
         ex.forward(head=False, refresh_eval=False,
                    mask_head=(m.store.view("outc.conv.weight").reshape(-1), m.store.view("outc.conv.bias"),
                               self.thr_logit, m256))
