@@ -66,6 +66,69 @@ inline void* P(uintptr_t v) { return reinterpret_cast<void*>(v); }
 std::string encode_wire(double mean, double maxc, const double* pts, size_t npts, const std::string& status,
                         const uint8_t* mask01, int h, int w, float coverage, float proc_ms, int level, int bands);
 
+// evofab.vision.AnalysisRequest wire bytes -> its two Image.data payloads (/root/reference/protos/
+// vision.proto:14-24: Image{bytes data = 1; int32 width = 2; int32 height = 3}, AnalysisRequest{Image
+// color_image = 1; Image depth_image = 2}). The server registers its handler with the raw request bytes
+// (proto/vision.py) and the native path reads the payloads in place: no protobuf parse, no bytes copies
+// under the interpreter lock. false: not a message this parser takes (the caller parses it in Python).
+bool read_varint(const uint8_t*& p, const uint8_t* e, uint64_t& v) {
+  v = 0;
+  for (int sh = 0; sh < 64 && p < e; sh += 7) {
+    const uint8_t b = *p++;
+    v |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) return true;
+  }
+  return false;
+}
+bool skip_field(const uint8_t*& p, const uint8_t* e, int wt) {
+  uint64_t v;
+  switch (wt) {
+    case 0: return read_varint(p, e, v);
+    case 1: if (e - p < 8) return false; p += 8; return true;
+    case 2: if (!read_varint(p, e, v) || (uint64_t)(e - p) < v) return false; p += v; return true;
+    case 5: if (e - p < 4) return false; p += 4; return true;
+    default: return false;
+  }
+}
+bool image_data(const uint8_t* p, const uint8_t* e, const uint8_t*& d, size_t& n) {
+  d = nullptr;
+  n = 0;
+  while (p < e) {
+    uint64_t key;
+    if (!read_varint(p, e, key)) return false;
+    const int f = (int)(key >> 3), wt = (int)(key & 7);
+    if (f == 1 && wt == 2) {
+      uint64_t len;
+      if (!read_varint(p, e, len) || (uint64_t)(e - p) < len) return false;
+      d = p;  // proto3: the last occurrence wins
+      n = (size_t)len;
+      p += len;
+    } else if (!skip_field(p, e, wt)) {
+      return false;
+    }
+  }
+  return true;
+}
+bool parse_request(const uint8_t* p, size_t size, const uint8_t*& c, size_t& cn, const uint8_t*& d, size_t& dn) {
+  const uint8_t* e = p + size;
+  c = d = nullptr;
+  cn = dn = 0;
+  while (p < e) {
+    uint64_t key;
+    if (!read_varint(p, e, key)) return false;
+    const int f = (int)(key >> 3), wt = (int)(key & 7);
+    if ((f == 1 || f == 2) && wt == 2) {
+      uint64_t len;
+      if (!read_varint(p, e, len) || (uint64_t)(e - p) < len) return false;
+      if (!image_data(p, p + len, f == 1 ? c : d, f == 1 ? cn : dn)) return false;
+      p += len;
+    } else if (!skip_field(p, e, wt)) {
+      return false;
+    }
+  }
+  return c != nullptr && d != nullptr && cn > 0 && dn > 0;
+}
+
 class FrameRunner {
  public:
   FrameRunner(int device, uintptr_t stream) : dev_(device), s_((hipStream_t)stream) {
@@ -231,9 +294,25 @@ class FrameRunner {
       throw py::error_already_set();
     if (!h_meta_ || !h_coef_ || !exec_[2] || !exec_[3]) throw std::runtime_error("FrameRunner: configure_encoded first");
     py::gil_scoped_release nogil;
+    return submit_encoded_ptr((const uint8_t*)cp, (long)cn, (const uint8_t*)dp, (long)dn);
+  }
+
+  // the whole serialized AnalysisRequest (the server's raw-bytes handler): parsed here, without the GIL;
+  // 1 (and nothing launched) when it is not a message this parser takes
+  int submit_request(py::bytes raw) {
+    char* rp = nullptr;
+    Py_ssize_t rn = 0;
+    if (PyBytes_AsStringAndSize(raw.ptr(), &rp, &rn) != 0) throw py::error_already_set();
+    if (!h_meta_ || !h_coef_ || !exec_[2] || !exec_[3]) throw std::runtime_error("FrameRunner: configure_encoded first");
+    py::gil_scoped_release nogil;
+    const uint8_t *c, *d;
+    size_t cn, dn;
+    if (!parse_request((const uint8_t*)rp, (size_t)rn, c, cn, d, dn)) return kNotNative;
+    return submit_encoded_ptr(c, (long)cn, d, (long)dn);
+  }
+
+  int submit_encoded_ptr(const uint8_t* c, long cn, const uint8_t* d, long dn) {  // GIL released
     t0_ = std::chrono::steady_clock::now();
-    const uint8_t* c = (const uint8_t*)cp;
-    const uint8_t* d = (const uint8_t*)dp;
     // headers first: nothing is launched unless both halves are native frames of this pipeline's size
     int hi[24];
     const long nco = rdp_jpeg_info(c, (long)cn, hi);
@@ -485,11 +564,28 @@ class BatchRunner {
     Py_ssize_t cn = 0, dn = 0;
     if (PyBytes_AsStringAndSize(color.ptr(), &cp, &cn) != 0 || PyBytes_AsStringAndSize(depth.ptr(), &dp, &dn) != 0)
       throw py::error_already_set();
-    Slot& sl = slot(k, j);
+    slot(k, j);
     py::gil_scoped_release nogil;
+    return decode_ptr(k, j, (const uint8_t*)cp, (long)cn, (const uint8_t*)dp, (long)dn);
+  }
+
+  // the whole serialized AnalysisRequest, parsed here (FrameRunner.submit_request)
+  int decode_request(int k, int j, py::bytes raw) {
+    if (src_ != 2) throw std::runtime_error("BatchRunner.decode_request: not a JPEG batch runner");
+    char* rp = nullptr;
+    Py_ssize_t rn = 0;
+    if (PyBytes_AsStringAndSize(raw.ptr(), &rp, &rn) != 0) throw py::error_already_set();
+    slot(k, j);
+    py::gil_scoped_release nogil;
+    const uint8_t *c, *d;
+    size_t cn, dn;
+    if (!parse_request((const uint8_t*)rp, (size_t)rn, c, cn, d, dn)) return 1;
+    return decode_ptr(k, j, c, (long)cn, d, (long)dn);
+  }
+
+  int decode_ptr(int k, int j, const uint8_t* c, long cn, const uint8_t* d, long dn) {  // GIL released
+    Slot& sl = slot(k, j);
     sl.t0 = std::chrono::steady_clock::now();
-    const uint8_t* c = (const uint8_t*)cp;
-    const uint8_t* d = (const uint8_t*)dp;
     int hi[24];
     const long nco = rdp_jpeg_info(c, (long)cn, hi);
     if (nco == -1) return 3;
@@ -797,6 +893,8 @@ void register_serve_runtime(py::module_& m) {
       .def("configure_encoded", &FrameRunner::configure_encoded, py::arg("H"), py::arg("W"), py::arg("num_samples"))
       .def("submit_encoded", &FrameRunner::submit_encoded, py::arg("color"), py::arg("depth"),
            "0 launched, 1 not a native frame, 2 other frame size, 3 corrupt (nothing in flight)")
+      .def("submit_request", &FrameRunner::submit_request, py::arg("raw"),
+           "a serialized AnalysisRequest: codes as submit_encoded")
       .def("collect_encoded", &FrameRunner::collect_encoded, py::arg("level") = 1, py::arg("bands") = 4)
       .def("abort", &FrameRunner::abort)
       .def("set_spin_us", &FrameRunner::set_spin_us, py::arg("us"),
@@ -813,12 +911,22 @@ void register_serve_runtime(py::module_& m) {
       .def("set_upload_kernel", &BatchRunner::set_upload_kernel)
       .def("set_frame_stream", &BatchRunner::set_frame_stream)
       .def("decode", &BatchRunner::decode, "0 ok, 1 not a native frame, 2 other frame size, 3 corrupt")
+      .def("decode_request", &BatchRunner::decode_request)
       .def("stage", &BatchRunner::stage)
       .def("launch", &BatchRunner::launch)
       .def("wait", &BatchRunner::wait)
       .def("collect_encoded", &BatchRunner::collect_encoded, py::arg("k"), py::arg("j"), py::arg("level") = 1,
            py::arg("bands") = 4)
       .def("drain", &BatchRunner::drain);
+  m.def("parse_request", [](py::bytes raw) -> py::object {  // (colour bytes, depth bytes) or None (tests)
+    char* rp = nullptr;
+    Py_ssize_t rn = 0;
+    if (PyBytes_AsStringAndSize(raw.ptr(), &rp, &rn) != 0) throw py::error_already_set();
+    const uint8_t *c, *d;
+    size_t cn, dn;
+    if (!parse_request((const uint8_t*)rp, (size_t)rn, c, cn, d, dn)) return py::none();
+    return py::make_tuple(py::bytes((const char*)c, cn), py::bytes((const char*)d, dn));
+  });
   m.def("encode_response", &encode_response, py::arg("mean"), py::arg("max"), py::arg("points"), py::arg("status"),
         py::arg("mask"), py::arg("coverage"), py::arg("proc_ms"), py::arg("level") = 1, py::arg("bands") = 4);
 }

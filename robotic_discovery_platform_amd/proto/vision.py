@@ -90,10 +90,14 @@ def _serialize_response(m) -> bytes:
 
 
 def add_VisionAnalysisServiceServicer_to_server(servicer, server) -> None:
+    """A servicer with ``raw_requests`` true receives each request as its serialized bytes (the native
+    serving path reads the two image payloads in place, csrc/serve_runtime.cpp parse_request, and parses
+    with AnalysisRequest.FromString only the frames it hands back); otherwise AnalysisRequest messages."""
     import grpc
+    raw = bool(getattr(servicer, "raw_requests", False))
     handlers = {
         METHOD: grpc.stream_stream_rpc_method_handler(
-            servicer.AnalyzeActuatorPerformance, request_deserializer=AnalysisRequest.FromString,
+            servicer.AnalyzeActuatorPerformance, request_deserializer=None if raw else AnalysisRequest.FromString,
             response_serializer=_serialize_response),
     }
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(FULL_SERVICE, handlers),))

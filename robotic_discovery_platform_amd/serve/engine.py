@@ -362,6 +362,15 @@ class FramePipeline:
         with trace.range("serve.frame.submit_encoded"):
             return self.runner.submit_encoded(color, depth)
 
+    def submit_request(self, raw: bytes) -> int:
+        """A whole serialized AnalysisRequest, its image payloads read in place natively
+        (csrc/serve_runtime.cpp parse_request); codes as ``submit_encoded`` (1 also for a message the native
+        parser does not take)."""
+        if not self.encoded:
+            return 1
+        with trace.range("serve.frame.submit_request"):
+            return self.runner.submit_request(raw)
+
     def collect_encoded(self):
         """WireResult of the frame ``submit_encoded`` launched, or a FrameResult when its spline fit
         must finish on the host (the device's capacity was exceeded: rare)."""
@@ -738,6 +747,17 @@ class BatchEngine:
         k, j, gen = pos if pos is not None else self._acquire()
         try:
             code = self.runner.decode(k, j, color, depth)
+        except BaseException:
+            self._staged(k, j, False)
+            raise
+        self._staged(k, j, code == 0)
+        return code, (k, j, gen)
+
+    def submit_request(self, raw: bytes, pos=None):
+        """``submit_encoded`` from a whole serialized AnalysisRequest (payloads read in place natively)."""
+        k, j, gen = pos if pos is not None else self._acquire()
+        try:
+            code = self.runner.decode_request(k, j, raw)
         except BaseException:
             self._staged(k, j, False)
             raise
@@ -1141,7 +1161,11 @@ class EngineSession:
         self.inflight.append((tag, p, q))
         return out
 
-    def submit_encoded(self, color: bytes, depth: bytes, tag=None):
+    def submit_request(self, raw: bytes, tag=None):
+        """``submit_encoded`` from a whole serialized AnalysisRequest (the server's raw-bytes handler)."""
+        return self.submit_encoded(None, None, tag, raw=raw)
+
+    def submit_encoded(self, color: bytes, depth: bytes, tag=None, raw: Optional[bytes] = None):
         """A request's encoded colour / depth bytes straight to a pipeline of the pool's configured size
         (FramePipeline.submit_encoded: decode + launch natively, no interpreter lock). Returns
         (collected, code): the frames it had to collect, and 0 when this frame is in flight -- else
@@ -1152,7 +1176,9 @@ class EngineSession:
         b = self.pool._batcher(self.replica, self.sid, self.pool.home_size)
         if b is not None and b.src == SRC_JPEG:
             try:
-                code, t = b.submit_encoded(color, depth, pos=self._batch_pos(b, out))
+                pos = self._batch_pos(b, out)
+                code, t = (b.submit_request(raw, pos=pos) if raw is not None
+                           else b.submit_encoded(color, depth, pos=pos))
             except Exception as e:
                 out += self.drain()
                 out.append((tag, e))
@@ -1168,7 +1194,10 @@ class EngineSession:
                 out.append(self._collect_one())
             p = q.get()
         try:
-            code = p.submit_encoded(color, depth) if getattr(p, "encoded", False) else 1
+            if not getattr(p, "encoded", False):
+                code = 1
+            else:
+                code = p.submit_request(raw) if raw is not None else p.submit_encoded(color, depth)
         except BaseException as e:
             q.put(p)
             if not isinstance(e, Exception):

@@ -151,6 +151,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         # decodes, launches, waits and encodes the response without the interpreter lock; this thread
         # only moves bytes. Frames that path declines take the decode path below.
         self._encoded = self._gpu_jpeg and self._pin and hasattr(engine, "home_size")
+        # with the native path, requests arrive as their serialized bytes (proto/vision.py registers the
+        # handler without a deserializer): the two image payloads are read in place natively, no protobuf
+        # parse or bytes copies under the interpreter lock (fault injection needs the parsed fields)
+        self.raw_requests = self._encoded and faults is None and os.environ.get("RDP_SERVE_RAW", "1") != "0"
         try:
             from ..ops import native
             self._encode = getattr(native(build_if_missing=False), "encode_response", None)
@@ -195,6 +199,10 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             try:
                 for i, req in enumerate(request_iterator):
                     t = time.perf_counter()
+                    if isinstance(req, (bytes, bytearray)):  # raw_requests: the serialized message
+                        if not put((t, _Raw(req), None, None)):
+                            return
+                        continue
                     cb, db = req.color_image.data, req.depth_image.data
                     if self.faults is not None:
                         cb, db = self.faults.corrupt_request(i, cb, db)
@@ -220,7 +228,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                 if item[3] is not None:
                     raise item[3]
                 t, fc, fd, _ = item
-                if isinstance(fc, bytes):  # encoded frame: (colour bytes, depth bytes)
+                if isinstance(fc, (bytes, _Raw)):  # encoded frame: (colour bytes, depth bytes) / raw request
                     yield t, fc, fd, None, lambda: q.qsize() > 0
                     continue
                 try:
@@ -363,9 +371,15 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             for i, (t_read, color, depth, err, more) in enumerate(frames):
                 t_start = time.perf_counter()
                 times[i] = (t_read, t_start)
-                if isinstance(color, bytes):  # encoded frame: natively decoded + launched by a pipeline
+                if isinstance(color, (bytes, _Raw)):  # encoded frame: natively decoded + launched by a pipeline
                     with trace.range("serve.rpc.frame"):
-                        done, code = sess.submit_encoded(color, depth, tag=i)
+                        if isinstance(color, _Raw):
+                            done, code = sess.submit_request(color.raw, tag=i)
+                            if code != 0:  # not taken natively: the message's fields for the paths below
+                                req = pb.AnalysisRequest.FromString(color.raw)
+                                color, depth = req.color_image.data, req.depth_image.data
+                        else:
+                            done, code = sess.submit_encoded(color, depth, tag=i)
                         encode(done)
                         if code != 0:  # a frame that path declines: decode here, then the array path
                             try:
@@ -402,6 +416,14 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             # error, abort), the session's in-flight pipelines go back to the pool and the reader stops
             sess.close()
             frames.close()
+
+
+class _Raw:
+    """A request still in its serialized form (the native path parses it itself)."""
+    __slots__ = ("raw",)
+
+    def __init__(self, raw):
+        self.raw = bytes(raw)
 
 
 class _Ready:

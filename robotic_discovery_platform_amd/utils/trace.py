@@ -43,12 +43,20 @@ def enabled() -> bool:
     return _enabled and _load() is not None
 
 
-@contextlib.contextmanager
+_NULL = contextlib.nullcontext()
+
+
 def range(name: str):  # noqa: A001 - mirrors roctxRange naming
+    """A roctx range context; markers off: one shared no-op context (no generator per call -- several
+    ranges sit on every served frame's path)."""
     lib = _load() if _enabled else None
     if lib is None:
-        yield
-        return
+        return _NULL
+    return _roctx_range(lib, name)
+
+
+@contextlib.contextmanager
+def _roctx_range(lib, name: str):
     lib.roctxRangePushA(name.encode())
     try:
         yield

@@ -17,7 +17,7 @@ for st in (2, 4, 8):
 print(json.dumps(out), flush=True)
 import os; os._exit(0)
 PY
-for r in 1 2 3; do for v in "X=1" "RDP_SERVE_BATCH=0"; do
+for r in 1 2; do for v in "X=1" "RDP_BATCH_PRE=0"; do
   env $v timeout -k 10 300 python /tmp/pipe.py > gpurun_out/pipe.json 2>> gpurun_out/sb.err || exit 1
   echo "r$r $v $(cat gpurun_out/pipe.json)" | tee -a gpurun_out/batch_check.txt
 done; done

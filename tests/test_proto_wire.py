@@ -36,3 +36,32 @@ def test_service_shape():
     assert meth.client_streaming and meth.server_streaming
     assert pb.METHOD_PATH == "/evofab.vision.VisionAnalysisService/AnalyzeActuatorPerformance"
     assert pb.DESCRIPTOR.package == "evofab.vision"
+
+
+def test_native_request_parser_matches_protobuf():
+    """csrc/serve_runtime.cpp parse_request (the server's raw-bytes fast path) extracts the same image
+    payloads protobuf does -- field order, unknown fields, repeated fields (last wins) -- and declines
+    what it does not take (missing image, truncated bytes) so the server falls back to protobuf."""
+    import random
+    from robotic_discovery_platform_amd.ops import native
+    from robotic_discovery_platform_amd.proto import vision as pb
+    C = native(build_if_missing=False)
+    rng = random.Random(3)
+    for trial in range(50):
+        c = bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 3000)))
+        d = bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 5000)))
+        req = pb.AnalysisRequest(color_image=pb.Image(data=c, width=rng.randint(0, 9999), height=640),
+                                 depth_image=pb.Image(data=d, width=640, height=rng.randint(0, 9999)))
+        raw = req.SerializeToString()
+        if trial % 3 == 1:  # depth first on the wire
+            raw = (pb.AnalysisRequest(depth_image=req.depth_image).SerializeToString() +
+                   pb.AnalysisRequest(color_image=req.color_image).SerializeToString())
+        if trial % 3 == 2:  # an unknown field (number 9, varint) and a stale colour payload before the real one
+            raw = b"\x48\x07" + pb.AnalysisRequest(color_image=pb.Image(data=b"old")).SerializeToString() + raw
+        got = C.parse_request(raw)
+        msg = pb.AnalysisRequest.FromString(raw)
+        assert got == (msg.color_image.data, msg.depth_image.data)
+    only_color = pb.AnalysisRequest(color_image=pb.Image(data=b"x")).SerializeToString()
+    assert C.parse_request(only_color) is None
+    full = pb.AnalysisRequest(color_image=pb.Image(data=b"abc"), depth_image=pb.Image(data=b"def")).SerializeToString()
+    assert C.parse_request(full[:-2]) is None
