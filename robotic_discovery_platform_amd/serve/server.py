@@ -151,10 +151,11 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         # decodes, launches, waits and encodes the response without the interpreter lock; this thread
         # only moves bytes. Frames that path declines take the decode path below.
         self._encoded = self._gpu_jpeg and self._pin and hasattr(engine, "home_size")
-        # with the native path, requests arrive as their serialized bytes (proto/vision.py registers the
-        # handler without a deserializer): the two image payloads are read in place natively, no protobuf
-        # parse or bytes copies under the interpreter lock (fault injection needs the parsed fields)
-        self.raw_requests = self._encoded and faults is None and os.environ.get("RDP_SERVE_RAW", "1") != "0"
+        # RDP_SERVE_RAW=1: requests arrive as their serialized bytes (proto/vision.py registers the handler
+        # without a deserializer) and the native path reads the two image payloads in place. Measured slower
+        # than gRPC's own parse (e2e 1 stream 1,932 / 2,034 vs 2,193 / 2,230 FPS, 4 streams 3,645 / 3,333 vs
+        # 3,729 / 3,566; profiles/serve_e2e.md round 6), so off by default (fault injection needs the fields)
+        self.raw_requests = self._encoded and faults is None and os.environ.get("RDP_SERVE_RAW", "0") == "1"
         try:
             from ..ops import native
             self._encode = getattr(native(build_if_missing=False), "encode_response", None)
