@@ -542,6 +542,7 @@ class BatchEngine:
         # few ms), the batch size to wait for; None: launch as the GPU frees up
         self.target = None
         self._stop = False
+        self._error = None       # what ended the launcher, if a launch raised
         self._th = threading.Thread(target=self._launcher, name="rdp-batch-launcher", daemon=True)
         self._th.start()
 
@@ -643,7 +644,8 @@ class BatchEngine:
         with self._cv:
             while True:
                 if self._stop:
-                    raise RuntimeError("BatchEngine closed")
+                    raise RuntimeError("BatchEngine closed" if self._error is None
+                                       else f"BatchEngine launch failed: {self._error!r}")
                 if self._open is None and self._free:
                     self._open = self._free.popleft()
                     self._acq = self._ready = 0
@@ -710,19 +712,29 @@ class BatchEngine:
                             continue
                         self._cv.wait(timeout=1e-3 if k is not None and ready > 0 else None)
                     n, void = acq, self._void
+                    gen = self._gen[k]  # k may be reopened (a new generation) as soon as it is freed
                     self._open = None  # the next acquire opens a new frame
                     self._refs[k] = n - len(void)
-                    if self._refs[k] == 0:
+                    if self._refs[k] == 0:  # every position failed staging: nothing to run or collect
                         self._free.append(k)
+                        self._cv.notify_all()
+                        continue
                     self._cv.notify_all()
-                self.runner.launch(k, n)  # uploads + graph + end event (no GIL)
-                ev = self._done_evs.get(k)
-                if ev is None:
-                    ev = self._done_evs[k] = torch.cuda.Event()
-                ev.record(self.lane_stream[k % self.lanes])
+                try:
+                    self.runner.launch(k, n)  # uploads + graph + end event (no GIL)
+                    ev = self._done_evs.get(k)
+                    if ev is None:
+                        ev = self._done_evs[k] = torch.cuda.Event()
+                    ev.record(self.lane_stream[k % self.lanes])
+                except BaseException as e:  # collectors must not wait for a launch that never comes
+                    with self._cv:
+                        self._error = e
+                        self._stop = True
+                        self._cv.notify_all()
+                    return
                 with self._cv:
                     self._launched.append(k)
-                    self._launched_gen[k] = self._gen[k]
+                    self._launched_gen[k] = gen
                     self.batch_sizes[n] += 1
                     self._cv.notify_all()
 
@@ -730,7 +742,8 @@ class BatchEngine:
         with self._cv:
             while self._launched_gen[k] != gen:
                 if self._stop:
-                    raise RuntimeError("BatchEngine closed")
+                    raise RuntimeError("BatchEngine closed" if self._error is None
+                                       else f"BatchEngine launch failed: {self._error!r}") from self._error
                 self._cv.wait()
 
     def _release(self, k: int):
@@ -823,6 +836,9 @@ class BatchEngine:
                 if self._free:
                     got.append(self._free.popleft())
                     continue
+                if self._stop:  # the launcher is gone: a half-filled frame would never free
+                    self._free.extend(got)
+                    raise RuntimeError("BatchEngine closed")
                 self._cv.wait()
         self._held = got
         self.runner.drain()

@@ -124,6 +124,42 @@ def test_batch_encoded_matches_pipeline_wire(setup):
                 0.05 * abs(b.mean_curvature) + 1e-6
 
 
+def test_batch_all_void_frame_is_skipped_and_reused(setup):
+    """A batch whose every position failed staging (undecodable requests) is not launched; its frame goes
+    straight back to the rotation and the next batch on it (one frame: the same k, a new generation)
+    returns its own results, not a stale launch's."""
+    from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
+    from robotic_discovery_platform_amd.serve.client import make_request
+    from robotic_discovery_platform_amd.serve.engine import SRC_JPEG, BatchEngine, FramePipeline
+    model, scenes = setup
+    single = FramePipeline(model, DEFAULT_K, 0.001, graph=True, rgb=True, jpeg=True)
+    reqs = [make_request(sc.color, sc.depth) for sc in scenes[:4]]
+    want = []
+    for rq in reqs:
+        assert single.submit_encoded(rq.color_image.data, rq.depth_image.data) == 0
+        want.append(single.collect_encoded())
+    be = BatchEngine(model, DEFAULT_K, 0.001, src=SRC_JPEG, frames=1, positions=4, window_us=200000.0)
+    try:
+        def batch(pairs):
+            pos = [be._acquire() for _ in pairs]
+            out = [be.submit_encoded(c, d, pos=p) for (c, d), p in zip(pairs, pos)]
+            return out
+        first = batch([(rq.color_image.data, rq.depth_image.data) for rq in reqs[:2]])
+        got_a = [be.collect_encoded(t) for code, t in first if code == 0]
+        assert len(got_a) == 2
+        void = batch([(b"\xff\xd8not a jpeg", b"junk")] * 3)
+        assert all(code != 0 for code, _ in void)
+        second = batch([(rq.color_image.data, rq.depth_image.data) for rq in reqs[2:]])
+        assert all(code == 0 for code, _ in second)
+        got_b = [be.collect_encoded(t) for _, t in second]
+        assert sum(be.batch_sizes.values()) == 2, dict(be.batch_sizes)  # the void batch never ran
+    finally:
+        be.close()
+    for a, b in zip(got_a + got_b, want):
+        assert abs(a.coverage - b.coverage) < 0.1
+        assert abs(a.mean_curvature - b.mean_curvature) <= 0.05 * abs(b.mean_curvature) + 1e-6
+
+
 @pytest.mark.parametrize("n", [1, 3, 4])
 def test_batched_geometry_bitwise_equals_per_frame(setup, n):
     """geo_frames_batch (one launch per stage for n frames, csrc/geometry.hip rdp_geo_edges_batch +
