@@ -293,7 +293,14 @@ def native_comm_group(device: torch.device, tag: str = "grad"):
     """(process group, ncclComm_t as int) for natively issued all-reduces on ``device``: a dedicated
     nccl group per (device, ``tag``) -- "grad" for the gradient buckets (wgrad side stream), "syncbn" for
     the SyncBatchNorm statistics (main stream: a communicator of its own, so the two streams never
-    interleave operations of one communicator in a rank-dependent order) -- created once (collective:
+    interleave operations of one communicator in a rank-dependent order). The two communicators' kernels
+    run at once without a wait cycle: every rank issues both in the same host order (one executor / launch
+    plan); an RCCL kernel holds only its channel blocks, so one of each fits on the GPU beside the convs;
+    and the wait edges between the streams point one way per step (the side stream waits on backward
+    events of the same step, the main stream on the side stream's Adam event only at the next forward, by
+    when every bucket of this step is issued) -- so a SyncBN collective never waits, through its own
+    stream, on a bucket collective that waits on it. The watchdog polls and aborts both
+    (``native_comm_ptrs``). Created once (collective:
     every rank calls this in the same order) with BLOCKING communicators (eager-init groups default to
     non-blocking ones, whose calls may return ncclInProgress), initialised by one all-reduce before its
     communicator is taken."""
