@@ -147,7 +147,9 @@ def test_batch_all_void_frame_is_skipped_and_reused(setup):
         first = batch([(rq.color_image.data, rq.depth_image.data) for rq in reqs[:2]])
         got_a = [be.collect_encoded(t) for code, t in first if code == 0]
         assert len(got_a) == 2
-        void = batch([(b"\xff\xd8not a jpeg", b"junk")] * 3)
+        # all P positions, so the frame is full: the next acquire waits for the launcher to close it
+        # (acquiring several positions before staging any is safe only from a fresh frame)
+        void = batch([(b"\xff\xd8not a jpeg", b"junk")] * 4)
         assert all(code != 0 for code, _ in void)
         second = batch([(rq.color_image.data, rq.depth_image.data) for rq in reqs[2:]])
         assert all(code == 0 for code, _ in second)
