@@ -21,7 +21,8 @@
 extern "C" {
 int rdp_conv_igemm(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, void*, long,
                    long, int, int, int, float*, int, int, int, int, int, int, int, const float*, const float*, int,
-                   float*, long, void*, int, int*, void*, int, int, int, int, int, hipStream_t);
+                   float*, long, void*, int, int*, void*, int, int, int, int, int, const void*, int, const float*,
+                   float*, int*, hipStream_t);
 int rdp_conv_rowband_ex(const void*, const void*, long, long, int, int, int, int, const void*, long, int, void*, long, int,
                         int, int, int, int, const float*, const float*, int, void*, long, int, int, hipStream_t);
 int rdp_conv_rowband_frag_auto(int, int, int, int, int, int);
@@ -682,7 +683,7 @@ int conv_fwd(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
       r = RDP_PLAN(rdp_conv_igemm(px1, px2, bx1, bx2, a1.C, C2, a1.pitch, p2, wp, wb, (int)ldw, py1, py2, by1, by2, o1.C,
                                   o1.pitch, yp2, spc, nn, a1.H, a1.W, Cout, taps, packed, bm_pref, esc, esh, relu, wsp,
                                   wsn, ppo, ppit, want_fused ? pooled.get() : nullptr, pup, upit, uH, uW, up_oy, up_ox,
-                                  st));
+                                  nullptr, 0, nullptr, nullptr, nullptr, st));
     }
     TORCH_CHECK(r >= 0, "conv_fwd: unsupported shape (C1=", a1.C, ", C2=", C2, ", Cout=", Cout, ")");
     const int oN = nn, oH = o1.H, oW = o1.W, oC = o1.C, op1 = o1.pitch;
@@ -811,6 +812,45 @@ int conv_dgrad_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch:
   return RDP_PLAN(rdp_conv_ring_ex(a.ptr, a.bytes, a.C, a.pitch, w.data_ptr(), w.numel() * 2, w.size(1), o.ptr, o.bytes,
                           o.pitch, nullptr, 0, 0, o.C, o.C, partial.data_ptr<float>(), a.N, a.H, a.W, nullptr, nullptr,
                           0, 256, b.ptr, b.pitch, coef.data_ptr<float>(), nullptr, nullptr, nullptr, 0, 0, st));
+}
+
+// 3x3 dgrad into one BN + ReLU layer's activation gradient (dx, one destination) through the implicit-GEMM
+// dispatch: where it runs split-K (small M x long K: the reference batch's deep layers), the split-K
+// reduce also writes that layer's BN-backward partial rows (y_bn: its pre-BN output, coef: its
+// [mean|invstd|scale|shift]) and this returns their count; 0 when the conv ran on another path (the
+// caller runs bn_relu_bwd_reduce); -1 when nothing was launched (batches past the 2 GiB reach: the
+// caller's chunked conv_fwd).
+int conv_dgrad_splitk_bnred(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, torch::Tensor y_bn,
+                            torch::Tensor coef, torch::Tensor partial, c10::optional<torch::Tensor> ws) {
+  Act a = act(dy, "dy"), o = act(dx, "dx"), b = act(y_bn, "y_bn");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.is_contiguous() && w.dim() == 2, "w: bf16 [Cout][K]");
+  TORCH_CHECK(o.N == a.N && o.H == a.H && o.W == a.W && b.N == a.N && b.H == a.H && b.W == a.W && b.C == o.C,
+              "conv_dgrad_splitk_bnred: shape mismatch");
+  TORCH_CHECK(w.size(0) == o.C && w.size(1) >= 9l * a.C, "conv_dgrad_splitk_bnred: w must be [Cout][9 * Cin]");
+  check_f32(coef, "coef");
+  check_f32(partial, "partial");
+  TORCH_CHECK(coef.numel() >= 4l * o.C, "coef must hold 4*C floats");
+  TORCH_CHECK(partial.numel() >= 512l * 2 * o.C, "partial too small");  // the split-K reduce: <= 512 rows
+  if (ws) check_f32(*ws, "ws");
+  const long per_img = std::max(std::max((long)a.H * a.W * a.pitch, (long)o.H * o.W * o.pitch), (long)b.H * b.W * b.pitch) * 2;
+  if (chunk_images(per_img, a.N) < a.N) return -1;
+  auto rows = std::make_shared<int>(0);
+  void* const px = a.ptr;
+  void* const py = o.ptr;
+  void* const pyb = b.ptr;
+  void* const wp = w.data_ptr();
+  const long wb = w.numel() * 2, bx = a.bytes, by = o.bytes;
+  const int ldw = (int)w.size(1), C1 = a.C, p1 = a.pitch, Co = o.C, op = o.pitch, ypb = b.pitch, N = a.N, H = a.H,
+            W = a.W;
+  const float* const cf = coef.data_ptr<float>();
+  float* const pp = partial.data_ptr<float>();
+  float* const wsp = ws ? ws->data_ptr<float>() : nullptr;
+  const long wsn = ws ? (long)ws->numel() : 0L;
+  const int r = RDP_PLAN(rdp_conv_igemm(px, nullptr, bx, 0, C1, 0, p1, 0, wp, wb, ldw, py, nullptr, by, 0, Co, op, 0,
+                                        nullptr, N, H, W, Co, 9, 0, 0, nullptr, nullptr, 0, wsp, wsn, nullptr, 0,
+                                        nullptr, nullptr, 0, 0, 0, 0, 0, pyb, ypb, cf, pp, rows.get(), st));
+  TORCH_CHECK(r >= 0, "conv_dgrad_splitk_bnred: unsupported shape (Cin=", C1, ", Cout=", Co, ")");
+  return *rows;
 }
 
 // Training forward of a 3x3 64 -> 64 conv whose input is the producer layer's PRE-BN output x_pre: the
@@ -1741,6 +1781,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_apply", on_device(&bn_relu_apply));
   m.def("bn_relu_bwd_reduce", on_device(&bn_relu_bwd_reduce));
   m.def("conv_dgrad_bnred", on_device(&conv_dgrad_bnred));
+  m.def("conv_dgrad_splitk_bnred", on_device(&conv_dgrad_splitk_bnred), py::arg("dy"), py::arg("w"), py::arg("dx"),
+        py::arg("y_bn"), py::arg("coef"), py::arg("partial"), py::arg("ws") = py::none());
   m.def("bn_bwd_finalize", on_device(&bn_bwd_finalize));
   m.def("bn_relu_bwd_apply", on_device(&bn_relu_bwd_apply));
   m.def("maxpool2_fwd", on_device(&maxpool2_fwd));

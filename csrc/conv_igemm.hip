@@ -65,6 +65,15 @@ struct ConvArgs {
   // 2w + sub%2 + tox) of a [N][tH2][tW2] map, channel c, + ubias[c]. tlc = 0: plain output.
   const float* ubias = nullptr;
   int tlc = 0, tH2 = 0, tW2 = 0, toy = 0, tox = 0;
+  // split-K reduce only (training dgrad, one destination): the BN-backward partial rows of the BN + ReLU
+  // layer whose activation gradient this conv writes, in bn_relu_bwd_reduce's layout -- bnpart[block][0][c]
+  // = sum g, [block][1][c] = sum g * xhat, g = out * (bny * scale + shift > 0), xhat = (bny - mean) * invstd
+  // -- so the standalone reduce pass (reading the output and bny back) disappears
+  const u16* bny = nullptr;       // that layer's pre-BN output
+  const float* bncoef = nullptr;  // its [mean | invstd | scale | shift]
+  float* bnpart = nullptr;
+  int bnypitch = 0;
+  int* bnrows = nullptr;  // host cell: the partial rows written (set when the split-K reduce ran)
 };
 
 // 128 -> 128 convs as two two-source-ring launches where the ring grid is at least this large. Measured
@@ -941,26 +950,47 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
     }
     return;  // eval: no statistics
   }
-  for (int m = blockIdx.x * RPB + r; m < a.M; m += nrow_blocks * RPB) {
-    const uint2 w = pixel(m);
-    if (a.stats) {
-      const float q0 = __uint_as_float(w.x << 16), q1 = __uint_as_float(w.x & 0xffff0000u);
-      const float q2 = __uint_as_float(w.y << 16), q3 = __uint_as_float(w.y & 0xffff0000u);
-      s1[0] += q0; s2[0] += q0 * q0;
-      s1[1] += q1; s2[1] += q1 * q1;
-      s1[2] += q2; s2[2] += q2 * q2;
-      s1[3] += q3; s2[3] += q3 * q3;
+  // BN-backward partials (a.bnpart): the owner layer's coefficients of this thread's 4 channels
+  const bool bnr = a.stats == nullptr && a.bnpart != nullptr;
+  float bmean[4], binv[4], bsc[4], bsh[4];
+  if (bnr) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bmean[k] = a.bncoef[n + k];
+      binv[k] = a.bncoef[a.Cout + n + k];
+      bsc[k] = a.bncoef[2 * a.Cout + n + k];
+      bsh[k] = a.bncoef[3 * a.Cout + n + k];
     }
   }
-  if (!a.stats) return;
+  for (int m = blockIdx.x * RPB + r; m < a.M; m += nrow_blocks * RPB) {
+    const uint2 w = pixel(m);
+    const float q[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                        __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+    if (a.stats) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s1[k] += q[k]; s2[k] += q[k] * q[k]; }
+    } else if (bnr) {  // q = dL/da (as stored, bf16) of the owner's post-ReLU activation
+      const uint2 yv = *(const uint2*)(a.bny + (long)m * a.bnypitch + n);
+      const float fy[4] = {__uint_as_float(yv.x << 16), __uint_as_float(yv.x & 0xffff0000u),
+                           __uint_as_float(yv.y << 16), __uint_as_float(yv.y & 0xffff0000u)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float g = fmaf(fy[k], bsc[k], bsh[k]) > 0.f ? q[k] : 0.f;
+        s1[k] += g;
+        s2[k] += g * (fy[k] - bmean[k]) * binv[k];
+      }
+    }
+  }
+  float* const rows_out = a.stats ? a.stats : (bnr ? a.bnpart : nullptr);
+  if (!rows_out) return;
   *(float4*)(sst + (r * 2 + 0) * a.Cout + n) = make_float4(s1[0], s1[1], s1[2], s1[3]);
   *(float4*)(sst + (r * 2 + 1) * a.Cout + n) = make_float4(s2[0], s2[1], s2[2], s2[3]);
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * a.Cout; c += 256) {
     const int half = c / a.Cout, ch = c - half * a.Cout;
     float acc = 0.f;
-    for (int q = 0; q < RPB; ++q) acc += sst[(q * 2 + half) * a.Cout + ch];
-    a.stats[(long)blockIdx.x * 2 * a.Cout + c] = acc;
+    for (int qq = 0; qq < RPB; ++qq) acc += sst[(qq * 2 + half) * a.Cout + ch];
+    rows_out[(long)blockIdx.x * 2 * a.Cout + c] = acc;
   }
 }
 
@@ -1076,8 +1106,10 @@ static int launch_split_reduce(const ConvArgs& a, hipStream_t s, int* pooled) {
     nblk = nblk < 2048 ? nblk : 2048;
     if (pooled) *pooled = 1;
   }
-  const size_t lds = a.stats ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
+  const bool bnr = !a.stats && a.bnpart && !a.pool;
+  const size_t lds = (a.stats || bnr) ? (size_t)rpb * 2 * a.Cout * sizeof(float) : 0;
   hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(nblk), dim3(256), lds, s, a, nblk);
+  if (bnr && a.bnrows) *a.bnrows = nblk;
   return nblk;
 }
 
@@ -1152,12 +1184,17 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
                               int N, int H, int W, int Cout, int taps, int packed, int bm_pref,
                               const float* escale, const float* eshift, int erelu, float* ws, long ws_elems,
                               void* pool, int ppitch, int* pooled, void* up, int upitch, int uH, int uW,
-                              int uoy, int uox, hipStream_t s) {
+                              int uoy, int uox, const void* bny, int bnypitch, const float* bncoef, float* bnpart,
+                              int* bnrows, hipStream_t s) {
   // pool (eval, optional): MaxPool2d(2) of y1 fused into the split-K reduce when that path runs;
   // up (eval, optional, exclusive with pool): bilinear x2 upsample of y1 into up [N][uH][uW] at
   // (uoy, uox), fused the same way; *pooled = 1 if the fused output was written (else the caller
   // launches the pool / upsample)
+  // bny / bncoef / bnpart (training dgrad into one BN + ReLU layer's activation gradient, optional): that
+  // layer's BN-backward partial rows, written by the split-K reduce when that path runs (ConvArgs);
+  // *bnrows = the rows written, else 0 (the caller runs bn_relu_bwd_reduce)
   if (pooled) *pooled = 0;
+  if (bnrows) *bnrows = 0;
   // first layer (3-channel input, packed K): conv_first.hip (auto, or bm_pref 13 = force; bm_pref 256
   // runs this file's packed implicit GEMM, the tests' second opinion)
   {
@@ -1274,6 +1311,10 @@ extern "C" int rdp_conv_igemm(const void* x1, const void* x2, long xbytes1, long
   a.w = (const u16*)w; a.wbytes = (uint32_t)wbytes; a.ldw = ldw;
   a.y1 = (u16*)y1; a.y2 = (u16*)y2; a.ybytes1 = (uint32_t)ybytes1; a.ybytes2 = (uint32_t)ybytes2;
   a.Cy1 = Cy1; a.ypitch1 = ypitch1; a.ypitch2 = ypitch2; a.stats = stats;
+  if (bnpart && bny && bncoef && !stats && !escale && y2 == nullptr && Cy1 == Cout && bnypitch % 4 == 0 &&
+      pool == nullptr && up == nullptr) {
+    a.bny = (const u16*)bny; a.bnypitch = bnypitch; a.bncoef = bncoef; a.bnpart = bnpart; a.bnrows = bnrows;
+  }
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.M = N * H * W;
   a.taps = taps; a.packed = packed;
   if (packed) {

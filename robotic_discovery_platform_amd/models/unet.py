@@ -674,6 +674,8 @@ class UNetExecutor:
         dev, bf = self.dev, torch.bfloat16
         # RDP_WGRAD_OVERLAP=0 serialises the wgrads on the main stream (clean per-kernel profiles)
         self.overlap_wgrad = dev.type == "cuda" and os.environ.get("RDP_WGRAD_OVERLAP", "1") != "0"
+        # BN-backward partial rows from the split-K dgrad reduce (RDP_SPLITK_BNRED=0: the separate pass, A/B)
+        self.splitk_bnred = os.environ.get("RDP_SPLITK_BNRED", "1") != "0"
         # a stream whose kernels overlap the main stream's (concurrent_stream: not on its hardware queue)
         self.side = concurrent_stream(dev, [torch.cuda.current_stream(dev)]) if self.overlap_wgrad else None
         # split-K grid target of the generic / packed weight-gradient kernels. Fewer splits = less fp32
@@ -1149,12 +1151,22 @@ class UNetExecutor:
         # dgrad into the da of a BN layer: where the row-ring kernel runs it (64 -> 64 channels), its
         # epilogue also produces that layer's BN-backward partial sums (no bn_relu_bwd_reduce pass)
         owner = L.dx1_owner
-        if owner is not None and L.dx2 is None and sp.taps == 9 and not owner.bwd_rows:
+        fusable = owner is not None and L.dx2 is None and sp.taps == 9 and not owner.bwd_rows
+        done = False
+        if fusable:
             rows = C.conv_dgrad_bnred(L.dy, self.m.dgrad_weight(sp), L.dx1, owner.y, owner.coef, self.bn_partial)
             if rows > 0:
                 owner.bwd_rows = rows
-                owner = True
-        if L.dx1 is not None and owner is not True:
+                done = True
+        if fusable and not done and self.splitk_bnred:
+            # where the dgrad runs split-K (the reference batch's deep layers), the split-K reduce writes the
+            # owner's BN-backward partial rows too: no bn_relu_bwd_reduce pass (0 rows: another path ran)
+            rows = C.conv_dgrad_splitk_bnred(L.dy, self.m.dgrad_weight(sp), L.dx1, owner.y, owner.coef,
+                                             self.bn_partial, self.kws)
+            if rows >= 0:
+                owner.bwd_rows = rows
+                done = True
+        if L.dx1 is not None and not done:
             C.conv_fwd(L.dy, None, self.m.dgrad_weight(sp), sp.taps, 0, L.dx1, L.dx2, None, 0, None, 0, self.kws)
         if hooks is not None:  # the weight gradient is final once its stream's work so far has run
             hooks(sp, wstream)

@@ -1252,6 +1252,41 @@ def test_bn_relu_pool_fusions(C, N, H, W, Ch):
     assert torch.allclose(got, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("N,H,Cdy,Cdx", [(4, 32, 512, 256), (4, 16, 512, 512), (2, 8, 128, 64)])
+def test_dgrad_splitk_bnred_matches_separate_reduce(C, N, H, Cdy, Cdx):
+    """Split-K dgrad whose reduce also writes the owner BN layer's backward partial rows
+    (conv_dgrad_splitk_bnred, csrc/conv_igemm.hip conv_splitk_reduce_kernel): dx bitwise the plain dgrad,
+    the row sums equal bn_relu_bwd_reduce's and the fp32 sums of the same g."""
+    torch.manual_seed(12)
+    dev = "cuda"
+    dy = bf(torch.randn(N, H, H, Cdy, device=dev))
+    w = bf(torch.randn(Cdx, 9 * Cdy, device=dev) * 0.02)
+    y = bf(torch.randn(N, H, H, Cdx, device=dev) * 2 + 0.3)
+    mean, inv = torch.randn(Cdx, device=dev) * 0.1, torch.rand(Cdx, device=dev) + 0.5
+    gamma, beta = torch.randn(Cdx, device=dev), torch.randn(Cdx, device=dev) * 0.2
+    ss = gamma * inv
+    coef = torch.cat([mean, inv, ss, beta - mean * ss]).contiguous()
+    n_ws = C.conv_ws_elems(N, H, H, Cdy, 0, Cdx, 9, 0, 0)
+    assert n_ws > 0  # these shapes run split-K
+    ws = torch.zeros(n_ws, device=dev)
+    dx = torch.empty(N, H, H, Cdx, dtype=torch.bfloat16, device=dev)
+    part = torch.zeros(1024 * 2 * Cdx, device=dev)
+    T = C.conv_dgrad_splitk_bnred(dy, w, dx, y, coef, part, ws)
+    assert T > 0
+    dx_ref = torch.empty_like(dx)
+    C.conv_fwd(dy, None, w, 9, 0, dx_ref, None, None, 0, None, 0, ws)
+    assert torch.equal(dx, dx_ref)
+    part_ref = torch.zeros(1024 * 2 * Cdx, device=dev)
+    T_ref = C.bn_relu_bwd_reduce(dx_ref, y, coef, 1, part_ref)
+    got = part[:T * 2 * Cdx].view(T, 2, Cdx).double().sum(0)
+    ref = part_ref[:T_ref * 2 * Cdx].view(T_ref, 2, Cdx).double().sum(0)
+    g = dx_ref.float() * ((y.float() * ss + (beta - mean * ss)) > 0)
+    exact = torch.stack([g.sum((0, 1, 2)), (g * (y.float() - mean) * inv).sum((0, 1, 2))]).double()
+    scale = exact.abs().max().item()
+    assert torch.allclose(got, exact, rtol=1e-3, atol=1e-4 * scale)
+    assert torch.allclose(got, ref, rtol=1e-3, atol=1e-4 * scale)
+
+
 @pytest.mark.parametrize("dice_w", [0.0, 1.0])
 def test_head_bn_fused(C, dice_w):
     """BN-fused head (training): forward on the pre-BN y == BN apply then head; backward partials
