@@ -524,8 +524,20 @@ class BatchEngine:
         for k in range(self.nf):
             for n in range(1, self.P + 1):
                 self._capture(k, n)
-        # batching state (under _cv)
-        self._cv = threading.Condition()
+        self._init_batching()
+
+    def _init_batching(self):
+        """Batching state, guarded by one lock with three conditions: the launcher waits on ``_cv`` (a
+        frame staged), collectors on ``_cv_launched`` (a batch launched), acquirers and ``hold`` on
+        ``_cv_free`` (a frame closed or freed) -- each event wakes only the threads that wait for it, not
+        every session thread of the replica (``RDP_BATCH_ONECV=1``: one condition for all, A/B)."""
+        self._lock = threading.Lock()
+        self._cv = threading.Condition(self._lock)
+        if os.environ.get("RDP_BATCH_ONECV", "0") == "1":
+            self._cv_launched = self._cv_free = self._cv
+        else:
+            self._cv_launched = threading.Condition(self._lock)
+            self._cv_free = threading.Condition(self._lock)
         self._free = collections.deque(range(self.nf))
         self._open = None        # batch frame taking new frames
         self._acq = 0            # positions handed out in the open frame
@@ -540,7 +552,7 @@ class BatchEngine:
         self.batch_sizes = collections.Counter()
         # callable -> how many client streams feed this engine now (EnginePool: sessions active in the last
         # few ms), the batch size to wait for; None: launch as the GPU frees up
-        self.target = None
+        self.target = getattr(self, "target", None)
         self._stop = False
         self._error = None       # what ended the launcher, if a launch raised
         self._th = threading.Thread(target=self._launcher, name="rdp-batch-launcher", daemon=True)
@@ -657,7 +669,7 @@ class BatchEngine:
                     return self._open, j, self._gen[self._open]
                 if not block:
                     return None
-                self._cv.wait()
+                self._cv_free.wait()
 
     def _staged(self, k: int, j: int, ok: bool):
         with self._cv:
@@ -717,9 +729,9 @@ class BatchEngine:
                     self._refs[k] = n - len(void)
                     if self._refs[k] == 0:  # every position failed staging: nothing to run or collect
                         self._free.append(k)
-                        self._cv.notify_all()
+                    self._cv_free.notify_all()  # the next acquire opens a frame
+                    if self._refs[k] == 0:
                         continue
-                    self._cv.notify_all()
                 try:
                     self.runner.launch(k, n)  # uploads + graph + end event (no GIL)
                     ev = self._done_evs.get(k)
@@ -730,13 +742,13 @@ class BatchEngine:
                     with self._cv:
                         self._error = e
                         self._stop = True
-                        self._cv.notify_all()
+                        self._notify_every()
                     return
                 with self._cv:
                     self._launched.append(k)
                     self._launched_gen[k] = gen
                     self.batch_sizes[n] += 1
-                    self._cv.notify_all()
+                    self._cv_launched.notify_all()
 
     def _await_launch(self, k: int, gen: int):
         with self._cv:
@@ -744,14 +756,14 @@ class BatchEngine:
                 if self._stop:
                     raise RuntimeError("BatchEngine closed" if self._error is None
                                        else f"BatchEngine launch failed: {self._error!r}") from self._error
-                self._cv.wait()
+                self._cv_launched.wait()
 
     def _release(self, k: int):
         with self._cv:
             self._refs[k] -= 1
             if self._refs[k] == 0:
                 self._free.append(k)
-                self._cv.notify_all()
+                self._cv_free.notify_all()
 
     def submit_encoded(self, color: bytes, depth: bytes, pos=None):
         """(code, ticket): 0 and the frame's (k, j) when it is staged for the next batch; otherwise nothing
@@ -839,7 +851,7 @@ class BatchEngine:
                 if self._stop:  # the launcher is gone: a half-filled frame would never free
                     self._free.extend(got)
                     raise RuntimeError("BatchEngine closed")
-                self._cv.wait()
+                self._cv_free.wait()
         self._held = got
         self.runner.drain()
 
@@ -847,13 +859,18 @@ class BatchEngine:
         with self._cv:
             self._free.extend(getattr(self, "_held", []))
             self._held = []
-            self._cv.notify_all()
+            self._cv_free.notify_all()
 
     def close(self):
         with self._cv:
             self._stop = True
-            self._cv.notify_all()
+            self._notify_every()
         self._th.join(timeout=5.0)
+
+    def _notify_every(self):  # (lock held) stop / failure: wake every waiter
+        self._cv.notify_all()
+        self._cv_launched.notify_all()
+        self._cv_free.notify_all()
         self.runner.drain()
 
 

@@ -74,17 +74,8 @@ def make(runner, frames=2, positions=4, window_us=200000.0, max_wait_us=5e6, tar
     be.window, be.max_wait = window_us * 1e-6, max_wait_us * 1e-6
     be.lane_stream = [None]
     be.dev = None
-    be._cv = threading.Condition()
-    be._free = collections.deque(range(frames))
-    be._open, be._acq, be._ready, be._void, be._t_first = None, 0, 0, set(), 0.0
-    be._refs, be._gen, be._launched_gen = [0] * frames, [0] * frames, [0] * frames
-    be._launched = collections.deque()
-    be._done_evs = {}
-    be.batch_sizes = collections.Counter()
     be.target = target
-    be._stop, be._error = False, None
-    be._th = threading.Thread(target=be._launcher, daemon=True)
-    be._th.start()
+    be._init_batching()  # batching state + the launcher thread
     return be
 
 
