@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "host_pool.h"
+#include "wire_parse.h"
 
 namespace py = pybind11;
 
@@ -66,68 +67,7 @@ inline void* P(uintptr_t v) { return reinterpret_cast<void*>(v); }
 std::string encode_wire(double mean, double maxc, const double* pts, size_t npts, const std::string& status,
                         const uint8_t* mask01, int h, int w, float coverage, float proc_ms, int level, int bands);
 
-// evofab.vision.AnalysisRequest wire bytes -> its two Image.data payloads (/root/reference/protos/
-// vision.proto:14-24: Image{bytes data = 1; int32 width = 2; int32 height = 3}, AnalysisRequest{Image
-// color_image = 1; Image depth_image = 2}). The server registers its handler with the raw request bytes
-// (proto/vision.py) and the native path reads the payloads in place: no protobuf parse, no bytes copies
-// under the interpreter lock. false: not a message this parser takes (the caller parses it in Python).
-bool read_varint(const uint8_t*& p, const uint8_t* e, uint64_t& v) {
-  v = 0;
-  for (int sh = 0; sh < 64 && p < e; sh += 7) {
-    const uint8_t b = *p++;
-    v |= (uint64_t)(b & 0x7f) << sh;
-    if (!(b & 0x80)) return true;
-  }
-  return false;
-}
-bool skip_field(const uint8_t*& p, const uint8_t* e, int wt) {
-  uint64_t v;
-  switch (wt) {
-    case 0: return read_varint(p, e, v);
-    case 1: if (e - p < 8) return false; p += 8; return true;
-    case 2: if (!read_varint(p, e, v) || (uint64_t)(e - p) < v) return false; p += v; return true;
-    case 5: if (e - p < 4) return false; p += 4; return true;
-    default: return false;
-  }
-}
-bool image_data(const uint8_t* p, const uint8_t* e, const uint8_t*& d, size_t& n) {
-  d = nullptr;
-  n = 0;
-  while (p < e) {
-    uint64_t key;
-    if (!read_varint(p, e, key)) return false;
-    const int f = (int)(key >> 3), wt = (int)(key & 7);
-    if (f == 1 && wt == 2) {
-      uint64_t len;
-      if (!read_varint(p, e, len) || (uint64_t)(e - p) < len) return false;
-      d = p;  // proto3: the last occurrence wins
-      n = (size_t)len;
-      p += len;
-    } else if (!skip_field(p, e, wt)) {
-      return false;
-    }
-  }
-  return true;
-}
-bool parse_request(const uint8_t* p, size_t size, const uint8_t*& c, size_t& cn, const uint8_t*& d, size_t& dn) {
-  const uint8_t* e = p + size;
-  c = d = nullptr;
-  cn = dn = 0;
-  while (p < e) {
-    uint64_t key;
-    if (!read_varint(p, e, key)) return false;
-    const int f = (int)(key >> 3), wt = (int)(key & 7);
-    if ((f == 1 || f == 2) && wt == 2) {
-      uint64_t len;
-      if (!read_varint(p, e, len) || (uint64_t)(e - p) < len) return false;
-      if (!image_data(p, p + len, f == 1 ? c : d, f == 1 ? cn : dn)) return false;
-      p += len;
-    } else if (!skip_field(p, e, wt)) {
-      return false;
-    }
-  }
-  return c != nullptr && d != nullptr && cn > 0 && dn > 0;
-}
+using rdp_wire::parse_request;  // wire_parse.h: the request's two payloads, read in place
 
 class FrameRunner {
  public:
