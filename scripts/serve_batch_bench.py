@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--src", choices=["bgr", "jpeg"], default="bgr")
     ap.add_argument("--sizes", default="1,2,3,4")
+    ap.add_argument("--single", type=int, default=1, help="0: skip the single-frame pipeline (PMC runs)")
     a = ap.parse_args()
     from robotic_discovery_platform_amd.data.synthetic import DEFAULT_K
     from robotic_discovery_platform_amd.serve.bench_serve import prepare_model
@@ -29,12 +30,13 @@ def main():
     dev = torch.device("cuda")
     model, scenes = prepare_model(dev, 30, n_scenes=8)
     out = {}
-    single = FramePipeline(model, DEFAULT_K, 0.001, graph=True)
-    g = []
-    for i in range(a.reps):
-        sc = scenes[i % 8]
-        g.append(single.process(sc.color, sc.depth).timings["gpu_ms"])
-    out["single_gpu_ms_p50"] = round(float(np.median(g)), 4)
+    if a.single:
+        single = FramePipeline(model, DEFAULT_K, 0.001, graph=True)
+        g = []
+        for i in range(a.reps):
+            sc = scenes[i % 8]
+            g.append(single.process(sc.color, sc.depth).timings["gpu_ms"])
+        out["single_gpu_ms_p50"] = round(float(np.median(g)), 4)
     src = SRC_JPEG if a.src == "jpeg" else SRC_BGR
     reqs = [make_request(sc.color, sc.depth) for sc in scenes] if src == SRC_JPEG else None
     be = BatchEngine(model, DEFAULT_K, 0.001, src=src, positions=4, window_us=1e6)
