@@ -1244,6 +1244,51 @@ class EngineSession:
         self.inflight.append((tag, p, q, True))
         return out, 0
 
+    def submit_encoded_handle(self, color: bytes, depth: bytes, stop=None):
+        """The server's reader-thread form of ``submit_encoded``: decode + launch one frame and return
+        ``("t", handle)`` for ``collect_handle``, or ``("d", code)`` when nothing of it runs (as
+        ``submit_encoded``'s codes). It never collects: it waits for a free pipeline / batch position
+        instead, which the stream's handler thread frees as it collects the handles in order -- so frame
+        i + 1 decodes while frame i is on the GPU or being collected. The caller bounds the handles it has
+        outstanding (<= ``depth``). ``stop``: an Event that ends the wait for a pipeline (returns
+        ``("d", 1)``)."""
+        b = self.pool._batcher(self.replica, self.sid, self.pool.home_size)
+        if b is not None and b.src == SRC_JPEG:
+            code, t = b.submit_encoded(color, depth)  # blocks for a position while the batch frames are full
+            return ("t", (b, t)) if code == 0 else ("d", code)
+        q = self.pool._get(self.replica, *self.pool.home_size)
+        while True:
+            try:
+                p = q.get(timeout=0.05)
+                break
+            except queue.Empty:
+                if stop is not None and stop.is_set():
+                    return ("d", 1)
+        try:
+            code = p.submit_encoded(color, depth) if getattr(p, "encoded", False) else 1
+        except BaseException:
+            q.put(p)
+            raise
+        if code != 0:
+            q.put(p)
+            return ("d", code)
+        return ("t", (p, q))
+
+    @staticmethod
+    def collect_handle(handle):
+        """The WireResult (or FrameResult / exception) of a ``submit_encoded_handle`` frame; its pipeline or
+        batch position is free afterwards."""
+        obj, x = handle
+        try:
+            if isinstance(obj, BatchEngine):
+                return obj.collect_encoded(x)
+            return obj.collect_encoded()
+        except Exception as e:
+            return e
+        finally:
+            if not isinstance(obj, BatchEngine):
+                x.put(obj)
+
     def _collect_one(self):
         tag, p, q, *enc = self.inflight.popleft()
         if isinstance(p, BatchEngine):  # q: the frame's ticket, enc: its kind

@@ -35,7 +35,7 @@ from ..data.image_io import decode_image, encode_png
 from ..data.jpeg import decode_coefs
 from ..proto import vision as pb
 from ..utils import trace
-from .engine import EnginePool, WireResult, _is_native
+from .engine import EnginePool, EngineSession, WireResult, _is_native
 
 log = logging.getLogger(__name__)
 
@@ -156,6 +156,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         # than gRPC's own parse (e2e 1 stream 1,932 / 2,034 vs 2,193 / 2,230 FPS, 4 streams 3,645 / 3,333 vs
         # 3,729 / 3,566; profiles/serve_e2e.md round 6), so off by default (fault injection needs the fields)
         self.raw_requests = self._encoded and faults is None and os.environ.get("RDP_SERVE_RAW", "0") == "1"
+        # encoded frames submitted by the stream's reader thread (decode + launch of frame i + 1 overlaps the
+        # collection of frame i: _analyze_pipelined); RDP_SERVE_READER_SUBMIT=0: the handler submits (A/B)
+        self.reader_submit = os.environ.get("RDP_SERVE_READER_SUBMIT", "0") != "0"
         try:
             from ..ops import native
             self._encode = getattr(native(build_if_missing=False), "encode_response", None)
@@ -343,6 +346,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         """Responses leave in request order; one that is ready -- or any, when the client has not
         sent the next frame yet (lock-step clients) -- is never held back."""
         import grpc
+        if self._encoded and self.reader_submit and self.faults is None and not self.raw_requests:
+            yield from self._analyze_pipelined(request_iterator, context)
+            return
         log.info("new analysis stream")
         inflight: "collections.deque" = collections.deque()  # encode futures, request order
         sess = self.engine.session()
@@ -417,6 +423,112 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             # error, abort), the session's in-flight pipelines go back to the pool and the reader stops
             sess.close()
             frames.close()
+
+
+    def _analyze_pipelined(self, request_iterator, context):
+        """The native whole-frame path with the submit on the stream's reader thread
+        (``EngineSession.submit_encoded_handle``): the reader decodes and launches frame i + 1 while this
+        thread collects frame i, at most ``depth`` frames between the two. Frames the native path declines
+        are decoded here and served through the array path, in order. Each response leaves as soon as its
+        frame is collected, in request order (lock-step and streaming clients alike)."""
+        import grpc
+        log.info("new analysis stream")
+        sess = self.engine.session()
+        items: "queue.Queue" = queue.Queue()
+        END = object()
+        lk = threading.Lock()
+        state = {"stopped": False}
+        stop = threading.Event()
+        slots = threading.Semaphore(max(1, sess.depth))
+
+        def hand_over(item) -> bool:  # False once the handler is gone (the caller then frees the frame)
+            with lk:
+                if not state["stopped"]:
+                    items.put(item)
+                    return True
+            return False
+
+        def reader():
+            try:
+                for i, req in enumerate(request_iterator):
+                    t_read = time.perf_counter()
+                    while not slots.acquire(timeout=0.05):
+                        if stop.is_set():
+                            return
+                    cb, db = req.color_image.data, req.depth_image.data
+                    t_start = time.perf_counter()
+                    try:
+                        kind, val = sess.submit_encoded_handle(cb, db, stop)
+                    except Exception as e:
+                        kind, val = "e", e
+                    self.stage_ms["submit"].append((time.perf_counter() - t_start) * 1e3)
+                    if not hand_over((i, t_read, t_start, kind, val, cb, db)):
+                        if kind == "t":
+                            EngineSession.collect_handle(val)
+                        return
+            except Exception as e:  # transport errors surface in the handler thread
+                hand_over((None, None, None, "x", e, None, None))
+            hand_over(END)
+
+        threading.Thread(target=reader, daemon=True, name="rdp-stream-reader").start()
+        try:
+            while True:
+                it = items.get()
+                if it is END:
+                    break
+                i, t_read, t_start, kind, val, cb, db = it
+                if kind == "x":
+                    raise val
+                try:
+                    if kind == "t":
+                        results = [(i, EngineSession.collect_handle(val))]
+                    elif kind == "e":
+                        results = [(i, val)]
+                    else:  # declined by the native path: decoded here, the array path
+                        try:
+                            c, d = self._decode_color(cb), self._decode_depth(db)
+                        except Exception as e:
+                            results = [(i, e)]
+                        else:
+                            results = sess.submit(c, d, tag=i, rgb=True) + sess.drain()
+                finally:
+                    slots.release()
+                for _, r in results:
+                    yield self._respond_one(r, (t_read, t_start))
+        except Exception as e:
+            log.error("unhandled exception during analysis: %s", e)
+            context.set_code(grpc.StatusCode.INTERNAL)
+            context.set_details(f"Internal error during analysis: {e}")
+            yield pb.AnalysisResponse()
+        finally:
+            # however the stream ends: the reader hands nothing over any more, and the frames it already
+            # handed over give their pipelines / batch positions back
+            stop.set()
+            with lk:
+                state["stopped"] = True
+            while True:
+                try:
+                    it = items.get_nowait()
+                except queue.Empty:
+                    break
+                if it is not END and it[3] == "t":
+                    EngineSession.collect_handle(it[4])
+            sess.close()
+
+    def _respond_one(self, r, t):
+        """One collected frame (WireResult, FrameResult or its exception) -> the response, logged."""
+        if isinstance(r, Exception):
+            if self.frame_errors == "abort":
+                raise r
+            self.frame_failures += 1
+            log.warning("frame failed (%s: %s): degraded response", type(r).__name__, r)
+        if isinstance(r, WireResult):
+            resp, r2, t_ready = self._wire_ready(r, t)
+        else:
+            resp, r2, t_ready = self._respond_timed(r, t)
+        self._log(r2)
+        self.stage_ms["hold"].append((time.perf_counter() - t_ready) * 1e3)
+        return resp
 
 
 class _Raw:
