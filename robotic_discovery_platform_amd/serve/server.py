@@ -427,17 +427,19 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
 
     def _analyze_pipelined(self, request_iterator, context):
         """The native whole-frame path with the submit on the stream's reader thread
-        (``EngineSession.submit_encoded_handle``): the reader decodes and launches frame i + 1 while this
-        thread collects frame i, at most ``depth`` frames between the two. Frames the native path declines
-        are decoded here and served through the array path, in order. Each response leaves as soon as its
-        frame is collected, in request order (lock-step and streaming clients alike)."""
+        (``EngineSession.submit_encoded_handle``) while the client streams: a frame that arrives while
+        earlier frames of the stream are still unanswered is decoded and launched by the reader, so frame
+        i + 1 decodes while this thread collects frame i (at most ``depth`` frames between the two). A frame
+        that arrives when every earlier one is answered (lock-step clients) is submitted by this thread, as
+        in the handler path. Frames the native path declines are decoded here and served through the array
+        path, in order. Each response leaves as soon as its frame is collected, in request order."""
         import grpc
         log.info("new analysis stream")
         sess = self.engine.session()
         items: "queue.Queue" = queue.Queue()
         END = object()
         lk = threading.Lock()
-        state = {"stopped": False}
+        state = {"stopped": False, "pending": 0}  # pending: frames handed over, not yet answered
         stop = threading.Event()
         slots = threading.Semaphore(max(1, sess.depth))
 
@@ -445,8 +447,17 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
             with lk:
                 if not state["stopped"]:
                     items.put(item)
+                    state["pending"] += 1
                     return True
             return False
+
+        def submit(cb, db, t_start):
+            try:
+                kv = sess.submit_encoded_handle(cb, db, stop)
+            except Exception as e:
+                kv = ("e", e)
+            self.stage_ms["submit"].append((time.perf_counter() - t_start) * 1e3)
+            return kv
 
         def reader():
             try:
@@ -457,11 +468,12 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                             return
                     cb, db = req.color_image.data, req.depth_image.data
                     t_start = time.perf_counter()
-                    try:
-                        kind, val = sess.submit_encoded_handle(cb, db, stop)
-                    except Exception as e:
-                        kind, val = "e", e
-                    self.stage_ms["submit"].append((time.perf_counter() - t_start) * 1e3)
+                    with lk:
+                        streaming = state["pending"] > 0
+                    if streaming:
+                        kind, val = submit(cb, db, t_start)
+                    else:
+                        kind, val = "r", None  # the handler submits it (no extra hop on a lock-step frame)
                     if not hand_over((i, t_read, t_start, kind, val, cb, db)):
                         if kind == "t":
                             EngineSession.collect_handle(val)
@@ -479,6 +491,8 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                 i, t_read, t_start, kind, val, cb, db = it
                 if kind == "x":
                     raise val
+                if kind == "r":
+                    kind, val = submit(cb, db, t_start)
                 try:
                     if kind == "t":
                         results = [(i, EngineSession.collect_handle(val))]
@@ -495,6 +509,8 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                     slots.release()
                 for _, r in results:
                     yield self._respond_one(r, (t_read, t_start))
+                with lk:  # answered (gRPC asks for the next response once this one is sent)
+                    state["pending"] -= 1
         except Exception as e:
             log.error("unhandled exception during analysis: %s", e)
             context.set_code(grpc.StatusCode.INTERNAL)
