@@ -158,7 +158,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         self.raw_requests = self._encoded and faults is None and os.environ.get("RDP_SERVE_RAW", "0") == "1"
         # encoded frames submitted by the stream's reader thread (decode + launch of frame i + 1 overlaps the
         # collection of frame i: _analyze_pipelined); RDP_SERVE_READER_SUBMIT=0: the handler submits (A/B)
-        self.reader_submit = os.environ.get("RDP_SERVE_READER_SUBMIT", "0") != "0"
+        self.reader_submit = os.environ.get("RDP_SERVE_READER_SUBMIT", "1") != "0"
         try:
             from ..ops import native
             self._encode = getattr(native(build_if_missing=False), "encode_response", None)
