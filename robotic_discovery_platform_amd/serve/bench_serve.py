@@ -312,6 +312,7 @@ def measure_e2e_procs(model, frames: int = 200, warmup: int = 20, procs: int = 2
             env.pop(k)
     if hw_queues > 0:  # hardware queues per server process (HIP default 4)
         env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
+    env.setdefault("RDP_SERVE_READER_SUBMIT", "0")  # as ServeConfig.workers > 1 sets it (serve/server.py)
     per = max(1, -(-streams // procs))
     servers = [subprocess.Popen([sys.executable, "-m", "robotic_discovery_platform_amd.serve.bench_serve",
                                  "--server-child", wpath, "--pool", str(2 * per)],

@@ -156,8 +156,9 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         # than gRPC's own parse (e2e 1 stream 1,932 / 2,034 vs 2,193 / 2,230 FPS, 4 streams 3,645 / 3,333 vs
         # 3,729 / 3,566; profiles/serve_e2e.md round 6), so off by default (fault injection needs the fields)
         self.raw_requests = self._encoded and faults is None and os.environ.get("RDP_SERVE_RAW", "0") == "1"
-        # encoded frames submitted by the stream's reader thread (decode + launch of frame i + 1 overlaps the
-        # collection of frame i: _analyze_pipelined); RDP_SERVE_READER_SUBMIT=0: the handler submits (A/B)
+        # encoded frames submitted by the stream's reader thread while the client streams (decode + launch of
+        # frame i + 1 overlaps the collection of frame i: _analyze_pipelined); RDP_SERVE_READER_SUBMIT=0: the
+        # handler submits -- the default of multi-process servers (_serve_workers)
         self.reader_submit = os.environ.get("RDP_SERVE_READER_SUBMIT", "1") != "0"
         try:
             from ..ops import native
@@ -688,6 +689,10 @@ def _serve_workers(cfg: ServeConfig, block: bool = True):
         raise ValueError("workers > 1 need a fixed port (every worker binds it with SO_REUSEPORT)")
     ctx = mp.get_context("spawn")  # fresh interpreters: the parent never initialises the GPU
     MetricsLog(cfg.metrics_log).close()  # the CSV and its header exist before any worker appends
+    # several server processes on one host: the handler submit (the reader-thread submit measured 8-22 %
+    # slower with 2 processes x 2 streams: more concurrent decodes oversubscribe the host's cores;
+    # profiles/serve_e2e.md round 6), unless set explicitly
+    os.environ.setdefault("RDP_SERVE_READER_SUBMIT", "0")
     procs = [ctx.Process(target=_worker_main, args=(cfg,), name=f"rdp-serve-{i}", daemon=False)
              for i in range(cfg.workers)]
     for p in procs:
