@@ -35,7 +35,7 @@ from ..data.image_io import decode_image, encode_png
 from ..data.jpeg import decode_coefs
 from ..proto import vision as pb
 from ..utils import trace
-from .engine import EnginePool, EngineSession, WireResult, _is_native
+from .engine import RESP_PNG_BANDS, RESP_PNG_LEVEL, EnginePool, EngineSession, WireResult, _is_native
 
 log = logging.getLogger(__name__)
 
@@ -303,7 +303,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
         t_read, t_start = t
         now = time.perf_counter()
         payload = self._encode(c.mean_curvature, c.max_curvature, pts, c.status, r.mask, r.coverage,
-                               (now - t_start) * 1e3, 1, 4)
+                               (now - t_start) * 1e3, RESP_PNG_LEVEL, RESP_PNG_BANDS)
         with self._stats_lock:
             self.queue_ms.append((t_start - t_read) * 1e3)
             self.proc_ms.append((now - t_start) * 1e3)
@@ -323,7 +323,7 @@ class VisionAnalysisService(pb.VisionAnalysisServiceServicer):
                                        status=c.status, mask_coverage=r.coverage)
             if c.spline_points:
                 resp.spline_points.extend([pb.Point3D(x=p.x, y=p.y, z=p.z) for p in c.spline_points])
-            resp.mask = encode_png(r.mask * np.uint8(255), compress_level=1, bands=4)
+            resp.mask = encode_png(r.mask * np.uint8(255), compress_level=RESP_PNG_LEVEL, bands=RESP_PNG_BANDS)
         now = time.perf_counter()
         resp.proc_time_ms = (now - t_start) * 1e3
         with self._stats_lock:
