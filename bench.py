@@ -170,14 +170,26 @@ def make_native_step(args, dev, world):
                             sync_bn=bool(args.sync_bn), grad_comm=args.grad_comm, ddp_force=bool(args.ddp_force))
 
 
-def measure_ref_batch(args, dev, steps: int = 50, warmup: int = 10) -> dict:
-    """The reference's batch (bs 4, train_segmenter.py:46) through the same native step."""
+def quiesce_gc() -> None:
+    """Collect once and move every object alive now out of the cyclic collector's reach (``gc.freeze``,
+    as the server does after start-up): a full collection of the framework's start-up heap landing inside
+    a short timed region shows up as a slow step."""
+    import gc
+    gc.collect()
+    gc.freeze()
+
+
+def measure_ref_batch(args, dev, steps: int = 200, warmup: int = 20) -> dict:
+    """The reference's batch (bs 4, train_segmenter.py:46) through the same native step. (200 timed steps,
+    ~0.5 s: 50 steps left the number at the mercy of a single host hiccup -- 1,342-1,384 vs 1,689-1,703 img/s
+    in otherwise equal runs, profiles/bench_recheck_r6.jsonl.)"""
     from robotic_discovery_platform_amd.train.engine import build_bench_step
     step = build_bench_step(batch=4, size=args.size, decoder=args.decoder, device=dev, world=1, graph="auto",
                             bucket_mb=args.bucket_mb, loss=args.loss)
     for _ in range(warmup):
         step()
     sync(dev)
+    quiesce_gc()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -198,6 +210,7 @@ def measure_transposed(args, dev, steps: int = 20, warmup: int = 5) -> dict:
     for _ in range(warmup):
         step()
     sync(dev)
+    quiesce_gc()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -275,6 +288,7 @@ def main():
         progress.phase = f"warmup step {i + 1}/{args.warmup}"
         step()
     progress.phase = "timed steps"
+    quiesce_gc()
     barrier(world, dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
